@@ -1,0 +1,285 @@
+"""Drop-in descriptor modules: ``HardNet`` and ``HardNetNAS``.
+
+Both keep the reference's ``nn.Module`` surface and state_dict layout so that the
+reference training / FPR95 loops and checkpoints work unchanged:
+
+* ``HardNet`` mirrors hardnet/HardNet.py:275-315 -- ``.features`` is an
+  ``nn.Sequential`` with the same 21 indices, ``.input_norm(x)`` and
+  ``.forward(x) -> [B,128]`` (L2-normalised, hardnet/Utils.py:15-22).
+* ``HardNetNAS(arch)`` is the sampled hardnetNAS descriptor: the supernet skeleton
+  (hardnetNAS/supernet_functions/model_supernet.py:53-85) with every MixedOperation
+  replaced by its arch op (fbnet_modeldef.py:30-95).  Sub-module names follow
+  ``ConvBNRelu`` / ``IRFBlock`` / ``Identity`` (fbnet_building_blocks/fbnet_builder.py)
+  so the keys of a supernet checkpoint map 1:1 (``load_supernet_state_dict``).
+
+Eval-mode forward on a HIP tensor (fp32, contiguous ``[B,1,32,32]``) runs the
+hand-written gfx950 kernels through the C ABI (``hardnetnas_amd._native``).  There
+is no silent fallback for that case: if the native library is missing the call
+raises.  Train mode (BatchNorm batch statistics, Dropout, autograd -- SURVEY.md
+8(f) row 4, out of scope for the HIP path) and CPU tensors run the module's own
+PyTorch layers, exactly like the reference module would.
+"""
+from __future__ import annotations
+
+from collections import OrderedDict
+from typing import List, Sequence
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import arch as A
+
+
+class L2Norm(nn.Module):
+    """hardnet/Utils.py:15-22: x / sqrt(sum(x^2) + 1e-10)."""
+
+    def __init__(self):
+        super().__init__()
+        self.eps = 1e-10
+
+    def forward(self, x):
+        norm = torch.sqrt(torch.sum(x * x, dim=1) + self.eps)
+        return x / norm.unsqueeze(-1).expand_as(x)
+
+
+class Flatten(nn.Module):
+    """fbnet_builder.py:194-199."""
+
+    def forward(self, x):
+        return x.reshape(x.size(0), -1)
+
+
+def _native_eligible(module: nn.Module, x: torch.Tensor) -> bool:
+    return (not module.training and x.is_cuda and x.dtype == torch.float32
+            and x.dim() == 4 and tuple(x.shape[1:]) == (1, 32, 32))
+
+
+class _NativeMixin:
+    """Owns the packed device model; re-packs when parameters/buffers change."""
+
+    def _native_key(self):
+        ts = list(self.parameters()) + list(self.buffers())
+        return tuple((t.data_ptr(), t._version) for t in ts)
+
+    def _native_forward(self, x: torch.Tensor) -> torch.Tensor:
+        from . import _native
+        key = (x.device.index, self._native_key())
+        h = getattr(self, "_hn_handle", None)
+        if h is None or self._hn_key != key:
+            self._hn_handle = None  # release the old one first
+            self._hn_handle = _native.NativeModel.from_module(self, x.device)
+            self._hn_key = key
+        return self._hn_handle.forward(x)
+
+    def __getstate__(self):
+        d = dict(self.__dict__)
+        d.pop("_hn_handle", None)
+        d.pop("_hn_key", None)
+        return d
+
+
+class HardNet(_NativeMixin, nn.Module):
+    """HardNet model definition (hardnet/HardNet.py:275-315)."""
+
+    def __init__(self):
+        super().__init__()
+        self.features = nn.Sequential(
+            nn.Conv2d(1, 32, kernel_size=3, padding=1, bias=False),
+            nn.BatchNorm2d(32, affine=False),
+            nn.ReLU(),
+            nn.Conv2d(32, 32, kernel_size=3, padding=1, bias=False),
+            nn.BatchNorm2d(32, affine=False),
+            nn.ReLU(),
+            nn.Conv2d(32, 64, kernel_size=3, stride=2, padding=1, bias=False),
+            nn.BatchNorm2d(64, affine=False),
+            nn.ReLU(),
+            nn.Conv2d(64, 64, kernel_size=3, padding=1, bias=False),
+            nn.BatchNorm2d(64, affine=False),
+            nn.ReLU(),
+            nn.Conv2d(64, 128, kernel_size=3, stride=2, padding=1, bias=False),
+            nn.BatchNorm2d(128, affine=False),
+            nn.ReLU(),
+            nn.Conv2d(128, 128, kernel_size=3, padding=1, bias=False),
+            nn.BatchNorm2d(128, affine=False),
+            nn.ReLU(),
+            nn.Dropout(0.3),
+            nn.Conv2d(128, 128, kernel_size=8, bias=False),
+            nn.BatchNorm2d(128, affine=False),
+        )
+        self.features.apply(weights_init)
+        # epsilons of this variant (HardNet.py:308, Utils.py:18); FDLNet clones use 1e-8 / none
+        self.input_norm_eps = 1e-7
+        self.l2_eps = 1e-10
+
+    def input_norm(self, x):
+        """HardNet.py:306-310: per-patch (x - mean) / (unbiased std + eps)."""
+        flat = x.view(x.size(0), -1)
+        mp = torch.mean(flat, dim=1)
+        sp = torch.std(flat, dim=1) + self.input_norm_eps
+        return (x - mp.detach().view(-1, 1, 1, 1)) / sp.detach().view(-1, 1, 1, 1)
+
+    def forward(self, input):
+        if _native_eligible(self, input):
+            return self._native_forward(input)
+        x_features = self.features(self.input_norm(input))
+        x = x_features.view(x_features.size(0), -1)
+        norm = torch.sqrt(torch.sum(x * x, dim=1) + self.l2_eps)
+        return x / norm.unsqueeze(-1)
+
+
+def weights_init(m):
+    """HardNet.py:317-324 (orthogonal, gain 0.6)."""
+    if isinstance(m, nn.Conv2d):
+        nn.init.orthogonal_(m.weight.data, gain=0.6)
+        if m.bias is not None:
+            nn.init.constant_(m.bias.data, 0.01)
+
+
+# ----------------------------------------------------------------------------------
+# hardnetNAS building blocks (fbnet_building_blocks/fbnet_builder.py)
+# ----------------------------------------------------------------------------------
+
+class ConvBNRelu(nn.Sequential):
+    """fbnet_builder.py:352-404 with bn_type="bn" (affine BN, eps 1e-5)."""
+
+    def __init__(self, c_in, c_out, kernel, stride, pad, relu=True, group=1):
+        super().__init__()
+        conv = nn.Conv2d(c_in, c_out, kernel_size=kernel, stride=stride, padding=pad,
+                         bias=False, groups=group)
+        nn.init.kaiming_normal_(conv.weight, mode="fan_out", nonlinearity="relu")
+        self.add_module("conv", conv)
+        self.add_module("bn", nn.BatchNorm2d(c_out))
+        if relu:
+            self.add_module("relu", nn.ReLU(inplace=True))
+
+
+class ChannelShuffle(nn.Module):
+    """fbnet_builder.py:332-349."""
+
+    def __init__(self, groups):
+        super().__init__()
+        self.groups = groups
+
+    def forward(self, x):
+        n, c, h, w = x.size()
+        g = self.groups
+        return x.view(n, g, c // g, h, w).permute(0, 2, 1, 3, 4).contiguous().view(n, c, h, w)
+
+
+class SEModule(nn.Module):
+    """fbnet_builder.py:407-421."""
+
+    def __init__(self, c):
+        super().__init__()
+        mid = A.se_mid(c)
+        self.op = nn.Sequential(nn.AdaptiveAvgPool2d(1), nn.Conv2d(c, mid, 1, 1, 0),
+                                nn.ReLU(inplace=True), nn.Conv2d(mid, c, 1, 1, 0), nn.Sigmoid())
+
+    def forward(self, x):
+        return x * self.op(x)
+
+
+class IRFBlock(nn.Module):
+    """fbnet_builder.py:455-570 (kernel 3/5, no cdw, no upsample)."""
+
+    def __init__(self, c_in, c_out, expansion, stride, kernel=3, pw_group=1,
+                 shuffle=False, se=False):
+        super().__init__()
+        self.use_res_connect = stride == 1 and c_in == c_out
+        mid = A.ir_mid(c_in, expansion)
+        self.pw = ConvBNRelu(c_in, mid, 1, 1, 0, relu=True, group=pw_group)
+        self.dw = ConvBNRelu(mid, mid, kernel, stride, kernel // 2, relu=True, group=mid)
+        self.pwl = ConvBNRelu(mid, c_out, 1, 1, 0, relu=False, group=pw_group)
+        self.shuffle_type = "mid" if shuffle else None
+        if shuffle:
+            self.shuffle = ChannelShuffle(pw_group)
+        self.se4 = SEModule(c_out) if se else nn.Sequential()
+
+    def forward(self, x):
+        y = self.pw(x)
+        if self.shuffle_type == "mid":
+            y = self.shuffle(y)
+        y = self.dw(y)
+        y = self.pwl(y)
+        if self.use_res_connect:
+            y = y + x
+        return self.se4(y)
+
+
+class Identity(nn.Module):
+    """The "skip" candidate, fbnet_builder.py:202-228."""
+
+    def __init__(self, c_in, c_out, stride):
+        super().__init__()
+        if c_in != c_out:
+            if stride == 1:
+                self.conv = ConvBNRelu(c_in, c_out, 1, 1, 0, relu=True)
+            else:
+                self.conv = nn.Sequential(nn.MaxPool2d(3, 2, 1), ConvBNRelu(c_in, c_out, 1, 1, 0))
+        else:
+            self.conv = None if stride == 1 else nn.Sequential(nn.MaxPool2d(3, 2, 1))
+
+    def forward(self, x):
+        return self.conv(x) if self.conv is not None else x
+
+
+def make_op(name: str, c_in: int, c_out: int, stride: int) -> nn.Module:
+    spec = A.OP_SPECS[name]
+    if spec.kind == "skip":
+        return Identity(c_in, c_out, stride)
+    return IRFBlock(c_in, c_out, spec.expansion, stride, kernel=spec.kernel,
+                    pw_group=spec.pw_group, shuffle=spec.shuffle, se=spec.se)
+
+
+class HardNetNAS(_NativeMixin, nn.Module):
+    """Sampled hardnetNAS descriptor (model_supernet.py:53-85, argmax op per layer).
+
+    ``arch`` is a MODEL_ARCH name ('wang2', 'wang3', 'wang4') or a list of six
+    CANDIDATE_BLOCKS op names.  There is no input_norm: the NAS loaders normalise
+    globally (general_functions/dataloader.py:118-122).  The final normalisation is
+    ``y / torch.norm(y)`` with no epsilon (model_supernet.py:84).
+    """
+
+    def __init__(self, arch="wang2", layers: Sequence = None):
+        super().__init__()
+        self.arch_ops: List[str] = A.arch_ops(arch)
+        self.layers = list(layers) if layers is not None else list(A.SEARCH_SPACE2)
+        self.first = ConvBNRelu(1, A.STEM_CHANNELS, 3, 1, 1, relu=True)
+        self.stages = nn.ModuleList([make_op(op, ci, co, s)
+                                     for op, (ci, co, s) in zip(self.arch_ops, self.layers)])
+        self.last_stages = nn.Sequential(OrderedDict([
+            ("conv_k1", nn.Conv2d(self.layers[-1][1], A.DESC_DIM, kernel_size=A.HEAD_KERNEL,
+                                  bias=False)),
+            ("batchnorm", nn.BatchNorm2d(A.DESC_DIM, affine=False)),
+            ("flatten", Flatten()),
+        ]))
+
+    def forward(self, x):
+        if _native_eligible(self, x):
+            return self._native_forward(x)
+        y = self.first(x)
+        for op in self.stages:
+            y = op(y)
+        y = self.last_stages(y)
+        return y / torch.norm(y, p=2, dim=-1, keepdim=True)
+
+    def load_supernet_state_dict(self, sd, strict: bool = True):
+        """Load a FBNet_Stochastic_SuperNet checkpoint (optionally DataParallel
+        ``module.``-prefixed, general_functions/utils.py:94-98): keys
+        ``stages_to_search.{i}.ops.{j}.*`` with j = CANDIDATE_BLOCKS.index(op_i)
+        become ``stages.{i}.*``; ``thetas`` and the other ops are dropped."""
+        out = OrderedDict()
+        want = {i: A.CANDIDATE_BLOCKS.index(op) for i, op in enumerate(self.arch_ops)}
+        for k, v in sd.items():
+            if k.startswith("module."):
+                k = k[len("module."):]
+            if k.startswith("stages_to_search."):
+                parts = k.split(".")
+                i = int(parts[1])
+                if parts[2] != "ops" or int(parts[3]) != want[i]:
+                    continue
+                out[".".join(["stages", str(i)] + parts[4:])] = v
+            elif k.startswith("first.") or k.startswith("last_stages."):
+                out[k] = v
+        return self.load_state_dict(out, strict=strict)
