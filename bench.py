@@ -1,0 +1,242 @@
+#!/usr/bin/env python3
+"""Throughput of the MI355X descriptor forward -- BASELINE.json metric
+"Mpatches/s (32x32 -> 128-D)".
+
+One step = one eval forward of B synthetic patches already resident in HBM (default:
+stock HardNet, B = 262,144 per GPU = BASELINE config 2) through the hand-written
+gfx950 kernels (C ABI), plus -- when N > 1 -- the RCCL all-gather of the [B,128]
+descriptors that reassembles the descriptor matrix (BASELINE config 4).  Per-GPU work
+is fixed (weak scaling); ``value`` = patches processed by all ranks / max-over-ranks
+wall time of the K timed steps.
+
+Extra objects on the JSON line:
+  roofline      dominant kernel's algorithmic FLOP per launch / its average launch
+                duration (hipEvents recorded by the library on the launch stream
+                during the timed region), against the bf16x3 effective peak.
+  cpu_baseline  the torch-CPU restatement of the same forward (oracle/), rank 0 at
+                N = 1 only, on a bounded sample.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--model hardnet|wang2|...]
+For N > 1 launch with torch.distributed.run (one process per GPU).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from hardnetnas_amd import arch as A  # noqa: E402
+from hardnetnas_amd import synth  # noqa: E402
+from hardnetnas_amd._native import NativeModel  # noqa: E402
+from hardnetnas_amd.model import HardNet, HardNetNAS  # noqa: E402
+
+METRIC = "Mpatches/s (32×32→128-D) at 1/2/4/8 MI355X; HPatches FPR95 parity"
+PEAK_MFMA_BF16 = 2500.0           # TFLOP/s dense bf16 (MI355X_MICROARCH.md)
+PEAK_BF16X3 = PEAK_MFMA_BF16 / 3  # fp32-equivalent: 3 bf16 MFMAs per fp32 product
+PEAK_FP32 = 157.3                 # TFLOP/s f32 (vector == f32 MFMA)
+PEAK_HBM = 8000.0                 # GB/s
+
+# algorithmic work per patch of each HardNet stage
+HARDNET_STAGE_MAC = {"stem": 294912, "conv1": 9437184, "conv2": 4718592, "conv3": 9437184,
+                     "conv4": 4718592, "conv5": 9437184, "head": 1048576}
+HARDNET_STAGE_BYTES = {"stem": 4096 + 131072, "conv1": 2 * 131072, "conv2": 131072 + 65536,
+                       "conv3": 2 * 65536, "conv4": 65536 + 32768, "conv5": 2 * 32768,
+                       "head": 32768 + 512}
+
+
+def build_model(name: str):
+    """Synthetic weights (splitmix64 seed 1234) + the calibrated BN statistics committed
+    with the golden fixtures (tests/golden/*.npz, data only)."""
+    m = HardNet() if name == "hardnet" else HardNetNAS(name)
+    fx = np.load(os.path.join(ROOT, "tests", "golden",
+                              ("hardnet" if name == "hardnet" else "nas_" + name) + ".npz"))
+    sd = m.state_dict()
+    tmpl = {k: tuple(v.shape) for k, v in sd.items()}
+    w = synth.synth_state_dict(tmpl, 1234)
+    for k in w:
+        sd[k] = torch.from_numpy(fx["bn/" + k] if "running" in k else w[k])
+    m.load_state_dict(sd)
+    return m.eval()
+
+
+def synth_input_on_device(b: int, device, seed: int) -> torch.Tensor:
+    g = torch.Generator(device=device).manual_seed(seed)
+    q = torch.randint(0, 256, (b, 1, 32, 32), device=device, generator=g, dtype=torch.int32)
+    x = q.float() / 255.0
+    return (x - synth.MEAN_IMAGE) / synth.STD_IMAGE
+
+
+def flop_per_patch(name: str) -> int:
+    return 2 * (A.hardnet_macs() if name == "hardnet" else A.nas_macs(name))
+
+
+def cpu_baseline(name: str, model, seconds: float = 12.0):
+    """Time the oracle (torch fp32 CPU restatement of the reference forward) on host cores."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from oracle import hardnet_oracle as O
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    p = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    b = 1024
+    x = torch.from_numpy(synth.synth_patches(b, seed=11))
+
+    def run():
+        with torch.no_grad():
+            if name == "hardnet":
+                O.hardnet_forward(p, x)
+            else:
+                O.nas_forward(p, model.arch_ops, x)
+
+    run()
+    run()
+    rates, t_start = [], time.perf_counter()
+    while time.perf_counter() - t_start < seconds or len(rates) < 3:
+        t0 = time.perf_counter()
+        run()
+        rates.append(b / (time.perf_counter() - t0))
+    return {"value": round(statistics.median(rates), 1), "unit": "patches/s", "cores": threads,
+            "kind": "port",
+            "sample": f"oracle/hardnet_oracle.py {name} fp32 torch-CPU forward, batch {b} x "
+                      f"{len(rates)} batches (~{seconds:.0f} s), {threads} threads, median"}
+
+
+def read_traffic(name: str, stage: str):
+    f = os.path.join(ROOT, "profiles", f"pmc_traffic_{name}.json")
+    if not os.path.exists(f):
+        return None
+    try:
+        d = json.load(open(f))
+        return d.get(stage)
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--model", default="hardnet")
+    ap.add_argument("--batch", type=int, default=262144, help="patches per GPU per step")
+    ap.add_argument("--no-allgather", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    model = build_model(args.model)
+    nm = NativeModel.from_module(model, dev)
+    b = args.batch
+    x = synth_input_on_device(b, dev, seed=1000 + rank)
+    out = torch.empty((b, 128), device=dev)
+    ws = torch.empty(nm.workspace_bytes(b), device=dev, dtype=torch.uint8)
+    gathered = torch.empty((b * world, 128), device=dev) if world > 1 else None
+
+    def step():
+        nm.forward(x, out=out, workspace=ws)
+        if world > 1 and not args.no_allgather:
+            dist.all_gather_into_tensor(gathered, out)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    nm.stage_times()  # clear
+    nm.set_profiling(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    nm.set_profiling(False)
+    stages = nm.stage_times()
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+
+    total = b * world * args.steps
+    value = total / elapsed / 1e6
+    result = None
+    if rank == 0:
+        # dominant kernel = stage with the largest summed device time
+        dom = max(stages, key=lambda k: stages[k][0])
+        dom_ms, dom_n = stages[dom]
+        avg_ms = dom_ms / max(dom_n, 1)
+        launches_per_step = dom_n / args.steps
+        patches_per_launch = b / launches_per_step
+        if args.model == "hardnet":
+            flop = 2 * HARDNET_STAGE_MAC[dom] * patches_per_launch
+            bound, peak = "mfma", PEAK_BF16X3
+            achieved = flop / (avg_ms * 1e-3) / 1e12
+            unit = "TFLOP/s"
+            alg = HARDNET_STAGE_BYTES[dom] * patches_per_launch
+        else:
+            alg = None
+            bound, peak, unit = "hbm", PEAK_HBM, "GB/s"
+            achieved = None
+        traffic = read_traffic(args.model, dom)
+        roof = {"bound": bound, "kernel": dom,
+                "achieved": round(achieved, 2) if achieved is not None else None,
+                "peak": round(peak, 1), "unit": unit,
+                "frac": round(achieved / peak, 4) if achieved is not None else None,
+                "traffic": traffic,
+                "avg_launch_ms": round(avg_ms, 4), "launches": dom_n,
+                "patches_per_launch": int(patches_per_launch),
+                "algorithmic_bytes_per_launch": int(alg) if alg else None,
+                "peak_basis": ("bf16 MFMA dense 2.5 PFLOP/s / 3 (bf16x3 split-precision fp32 "
+                               "products); algorithmic fp32 FLOP = 2*MAC") if bound == "mfma"
+                else "HBM3E 8 TB/s",
+                "stages_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in stages.items()}}
+        result = {
+            "metric": METRIC, "value": round(value, 4), "unit": "Mpatches/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": ("Stock HardNet forward" if args.model == "hardnet"
+                                    else f"hardnetNAS {args.model} forward")
+                       + f", {b} synthetic 32x32 patches per GPU"
+                       + (", RCCL all-gather of descriptors" if world > 1 and not args.no_allgather else ""),
+                       "model": args.model, "global_batch": b * world, "per_gpu_batch": b,
+                       "parallelism": f"dp{world}",
+                       "precision": "bf16x3 split-precision MFMA, fp32 accumulate" if args.model == "hardnet"
+                       else "fp32 VALU",
+                       "flop_per_patch": flop_per_patch(args.model)},
+            "roofline": roof,
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            result["cpu_baseline"] = cpu_baseline(args.model, model, args.cpu_seconds)
+            cb = result["cpu_baseline"]["value"]
+            result["gpu_vs_cpu"] = round(value * 1e6 / cb, 1)
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

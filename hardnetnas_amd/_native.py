@@ -1,0 +1,238 @@
+"""ctypes binding of the C ABI in include/hardnet_mi355x.h (libhardnet_mi355x.so).
+
+PyTorch is only plumbing here: it owns device memory (inputs, outputs, workspace via
+the caching allocator) and the current HIP stream; all arithmetic of the forward runs
+in the library's gfx950 kernels.  ``torch`` is imported before the library is loaded so
+that both share the one HIP runtime already mapped by torch (SONAME libamdhip64.so.7).
+
+There is no fallback: if the library cannot be loaded, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from . import arch as A
+
+_LIB_NAME = "libhardnet_mi355x.so"
+_lib = None
+_lib_lock = threading.Lock()
+
+HN_KIND_HARDNET = 0
+HN_KIND_NAS = 1
+HN_MAX_LAYERS = 8
+
+
+class HnArchDesc(ctypes.Structure):
+    _fields_ = [
+        ("kind", ctypes.c_int32),
+        ("n_layers", ctypes.c_int32),
+        ("op", ctypes.c_int32 * HN_MAX_LAYERS),
+        ("c_in", ctypes.c_int32 * HN_MAX_LAYERS),
+        ("c_out", ctypes.c_int32 * HN_MAX_LAYERS),
+        ("stride", ctypes.c_int32 * HN_MAX_LAYERS),
+        ("input_norm_eps", ctypes.c_float),
+        ("l2_eps", ctypes.c_float),
+        ("bn_eps", ctypes.c_float),
+    ]
+
+
+EXPORTED = ["hn_param_count", "hn_create", "hn_workspace_bytes", "hn_forward",
+            "hn_pairdist_workspace_bytes", "hn_pairdist_hardneg", "hn_set_profiling",
+            "hn_stage_times", "hn_destroy", "hn_last_error", "hn_abi_version"]
+
+
+def lib_path() -> str:
+    env = os.environ.get("HN_LIB")
+    if env:
+        return env
+    return os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", _LIB_NAME)
+
+
+def load_library():
+    """Load (once) and type the C ABI.  Raises if the library is missing."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None:
+            return _lib
+        path = lib_path()
+        if not os.path.exists(path):
+            raise RuntimeError(
+                f"hardnetnas_amd native library not found at {path}; build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (make -C hardnetnas_amd/csrc)")
+        lib = ctypes.CDLL(path)
+        P, S, I32, I64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int32, ctypes.c_int64
+        lib.hn_param_count.argtypes = [ctypes.POINTER(HnArchDesc), ctypes.POINTER(S)]
+        lib.hn_create.argtypes = [ctypes.POINTER(HnArchDesc), P, S, ctypes.POINTER(P)]
+        lib.hn_workspace_bytes.argtypes = [P, I64, ctypes.POINTER(S)]
+        lib.hn_forward.argtypes = [P, P, I64, P, P, S, P]
+        lib.hn_pairdist_workspace_bytes.argtypes = [I64, ctypes.POINTER(S)]
+        lib.hn_pairdist_hardneg.argtypes = [P, P, I64, I32, I32, P, P, P, S, P]
+        lib.hn_set_profiling.argtypes = [P, ctypes.c_int]
+        lib.hn_stage_times.argtypes = [P, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),
+                                       ctypes.POINTER(ctypes.c_double), ctypes.POINTER(I64)]
+        lib.hn_destroy.argtypes = [P]
+        lib.hn_destroy.restype = None
+        lib.hn_last_error.restype = ctypes.c_char_p
+        for name in ("hn_param_count", "hn_create", "hn_workspace_bytes", "hn_forward",
+                     "hn_pairdist_workspace_bytes", "hn_pairdist_hardneg", "hn_abi_version",
+                     "hn_set_profiling", "hn_stage_times"):
+            getattr(lib, name).restype = ctypes.c_int
+        _lib = lib
+        return lib
+
+
+def _check(rc: int, what: str):
+    if rc != 0:
+        msg = load_library().hn_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what} failed (status {rc}): {msg}")
+
+
+# ----------------------------------------------------------------------------------
+# descriptors and parameter blobs
+# ----------------------------------------------------------------------------------
+def hardnet_desc(input_norm_eps: float = 1e-7, l2_eps: float = 1e-10) -> HnArchDesc:
+    d = HnArchDesc()
+    d.kind = HN_KIND_HARDNET
+    d.input_norm_eps = input_norm_eps
+    d.l2_eps = l2_eps
+    d.bn_eps = 1e-5
+    return d
+
+
+def nas_desc(ops: List[str], layers=None, input_norm_eps: float = -1.0,
+             l2_eps: float = 0.0) -> HnArchDesc:
+    layers = layers or A.SEARCH_SPACE2
+    d = HnArchDesc()
+    d.kind = HN_KIND_NAS
+    d.n_layers = len(ops)
+    for i, (op, (ci, co, s)) in enumerate(zip(ops, layers)):
+        d.op[i] = A.CANDIDATE_BLOCKS.index(op)
+        d.c_in[i], d.c_out[i], d.stride[i] = ci, co, s
+    d.input_norm_eps = input_norm_eps
+    d.l2_eps = l2_eps
+    d.bn_eps = 1e-5
+    return d
+
+
+def state_dict_blob(sd: Dict[str, torch.Tensor]) -> np.ndarray:
+    """Concatenate every float tensor of a state_dict in state_dict order, skipping
+    ``num_batches_tracked``.  This is exactly the order hn_create parses:
+      HardNet: features.{0,3,...,19}.weight followed by the BN running_mean/var;
+      NAS:     first.conv/bn(w,b,mean,var), per block pw/dw/pwl ConvBNRelu (and
+               se4.op.{1,3}.{weight,bias}) or the skip's 1x1 ConvBNRelu, then
+               last_stages.conv_k1.weight + last_stages.batchnorm running stats."""
+    parts = [v.detach().to("cpu", torch.float32).contiguous().reshape(-1).numpy()
+             for k, v in sd.items() if not k.endswith("num_batches_tracked")]
+    return np.ascontiguousarray(np.concatenate(parts), dtype=np.float32)
+
+
+def desc_for_module(module) -> HnArchDesc:
+    from .model import HardNet, HardNetNAS
+    if isinstance(module, HardNet):
+        return hardnet_desc(module.input_norm_eps, module.l2_eps)
+    if isinstance(module, HardNetNAS):
+        return nas_desc(module.arch_ops, module.layers)
+    raise TypeError(type(module))
+
+
+class NativeModel:
+    """A device model (packed, BN-folded weights) created through hn_create."""
+
+    def __init__(self, desc: HnArchDesc, blob: np.ndarray, device: torch.device):
+        self.lib = load_library()
+        self.device = torch.device(device)
+        self.desc = desc
+        n = ctypes.c_size_t()
+        _check(self.lib.hn_param_count(ctypes.byref(desc), ctypes.byref(n)), "hn_param_count")
+        if n.value != blob.size:
+            raise ValueError(f"parameter blob has {blob.size} floats, library expects {n.value}")
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            _check(self.lib.hn_create(ctypes.byref(desc), blob.ctypes.data, blob.size,
+                                      ctypes.byref(h)), "hn_create")
+        self._h = h
+
+    @classmethod
+    def from_module(cls, module, device) -> "NativeModel":
+        return cls(desc_for_module(module), state_dict_blob(module.state_dict()), device)
+
+    def workspace_bytes(self, batch: int) -> int:
+        n = ctypes.c_size_t()
+        _check(self.lib.hn_workspace_bytes(self._h, batch, ctypes.byref(n)), "hn_workspace_bytes")
+        return n.value
+
+    def forward(self, x: torch.Tensor, out: Optional[torch.Tensor] = None,
+                workspace: Optional[torch.Tensor] = None) -> torch.Tensor:
+        if x.device != self.device:
+            raise ValueError(f"input on {x.device}, model on {self.device}")
+        if x.dtype != torch.float32 or x.dim() != 4 or tuple(x.shape[1:]) != (1, 32, 32):
+            raise ValueError(f"expected fp32 [B,1,32,32], got {x.dtype} {tuple(x.shape)}")
+        x = x.contiguous()
+        b = x.shape[0]
+        if out is None:
+            out = torch.empty((b, 128), device=self.device, dtype=torch.float32)
+        ws_bytes = self.workspace_bytes(b)
+        if workspace is None or workspace.numel() < ws_bytes:
+            workspace = torch.empty(max(ws_bytes, 16), device=self.device, dtype=torch.uint8)
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        with torch.cuda.device(self.device):
+            _check(self.lib.hn_forward(self._h, x.data_ptr(), b, out.data_ptr(),
+                                       workspace.data_ptr(), workspace.numel(), stream),
+                   "hn_forward")
+        return out
+
+    __call__ = forward
+
+    def set_profiling(self, on: bool):
+        _check(self.lib.hn_set_profiling(self._h, int(on)), "hn_set_profiling")
+
+    def stage_times(self) -> Dict[str, tuple]:
+        """{stage: (total_ms, launches)} accumulated since the last call (waits on the
+        recorded events; call after the stream has been synchronised)."""
+        n = 32
+        names = (ctypes.c_char_p * n)()
+        ms = (ctypes.c_double * n)()
+        cnt = (ctypes.c_int64 * n)()
+        k = self.lib.hn_stage_times(self._h, n, names, ms, cnt)
+        if k < 0:
+            _check(-k, "hn_stage_times")
+        return {names[i].decode(): (ms[i], cnt[i]) for i in range(k)}
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self.lib.hn_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def pairdist_hardneg(anchor: torch.Tensor, positive: torch.Tensor, anchor_swap: bool = False):
+    """(pos, min_neg) of loss_HardNet's 'min' batch_reduce (hardnet/Losses.py:87-110),
+    computed by the fused kernel without materialising the BxB distance matrix."""
+    lib = load_library()
+    if anchor.shape != positive.shape or anchor.dim() != 2:
+        raise ValueError("anchor/positive must be equal [B,D]")
+    a = anchor.contiguous().float()
+    p = positive.contiguous().float()
+    b, d = a.shape
+    n = ctypes.c_size_t()
+    _check(lib.hn_pairdist_workspace_bytes(b, ctypes.byref(n)), "hn_pairdist_workspace_bytes")
+    ws = torch.empty(max(n.value, 16), device=a.device, dtype=torch.uint8)
+    pos = torch.empty(b, device=a.device, dtype=torch.float32)
+    mn = torch.empty(b, device=a.device, dtype=torch.float32)
+    stream = torch.cuda.current_stream(a.device).cuda_stream
+    with torch.cuda.device(a.device):
+        _check(lib.hn_pairdist_hardneg(a.data_ptr(), p.data_ptr(), b, d, int(anchor_swap),
+                                       pos.data_ptr(), mn.data_ptr(), ws.data_ptr(), ws.numel(),
+                                       stream), "hn_pairdist_hardneg")
+    return pos, mn

@@ -1,0 +1,615 @@
+// C ABI of the MI355X descriptor forward (include/hardnet_mi355x.h).
+//
+// Host-side responsibilities: validate the architecture and the flat parameter blob,
+// fold eval-mode BatchNorm into conv weight + bias (in double), pack weights into the
+// device layouts the kernels consume, and sequence the kernel launches of one forward
+// on the caller's stream over fixed-size patch chunks.
+#include "hardnet_mi355x.h"
+#include "hn_internal.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+static thread_local std::string g_err;
+
+static int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIPCHK(x)                                                                          \
+  do {                                                                                     \
+    hipError_t e_ = (x);                                                                   \
+    if (e_ != hipSuccess)                                                                  \
+      return fail(HN_ERR_HIP, std::string(#x) + ": " + hipGetErrorString(e_));             \
+  } while (0)
+
+namespace {
+
+// candidate op table, restating hardnetNAS/fbnet_building_blocks/fbnet_builder.py:36-191
+// for CANDIDATE_BLOCKS (lookup_table_builder.py:18-20), in that index order.
+struct OpSpec {
+  const char* name;
+  int skip, e, k, g, se;
+};
+const OpSpec kOps[17] = {
+    {"skip", 1, 0, 0, 0, 0},        {"ir_k3_e1", 0, 1, 3, 1, 0},    {"ir_k3_e3", 0, 3, 3, 1, 0},
+    {"ir_k3_s4", 0, 4, 3, 4, 0},    {"ir_k5_e1", 0, 1, 5, 1, 0},    {"ir_k5_e3", 0, 3, 5, 1, 0},
+    {"ir_k5_s4", 0, 4, 5, 4, 0},    {"ir_k3_e1_se", 0, 1, 3, 1, 1}, {"ir_k3_e3_se", 0, 3, 3, 1, 1},
+    {"ir_k3_s4_se", 0, 4, 3, 4, 1}, {"ir_k5_e1_se", 0, 1, 5, 1, 1}, {"ir_k5_e3_se", 0, 3, 5, 1, 1},
+    {"ir_k5_s4_se", 0, 4, 5, 4, 1}, {"ir_k3_s2", 0, 1, 3, 2, 0},    {"ir_k5_s2", 0, 1, 5, 2, 0},
+    {"ir_k3_s2_se", 0, 1, 3, 2, 1}, {"ir_k5_s2_se", 0, 1, 5, 2, 1},
+};
+
+struct NasLayer {
+  int op = 0, cin = 0, cout = 0, stride = 1, hin = 0, hout = 0;
+  int skip = 0, e = 1, k = 3, g = 1, se = 0, mid = 0, semid = 0;
+  int skip_conv = 0;  // skip op with a 1x1 ConvBNRelu (C changes)
+  float *pw_w = nullptr, *pw_b = nullptr, *dw_w = nullptr, *dw_b = nullptr;
+  float *pwl_w = nullptr, *pwl_b = nullptr;
+  float *se_w1 = nullptr, *se_b1 = nullptr, *se_w2 = nullptr, *se_b2 = nullptr;
+};
+
+struct Cursor {
+  const float* p;
+  size_t n, i = 0;
+  bool ok = true;
+  const float* take(size_t k) {
+    if (i + k > n) {
+      ok = false;
+      return nullptr;
+    }
+    const float* r = p + i;
+    i += k;
+    return r;
+  }
+};
+
+uint16_t f2bf(float x) {  // round-to-nearest-even, as v_cvt_pk_bf16_f32
+  uint32_t u;
+  std::memcpy(&u, &x, 4);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+float bf2f(uint16_t b) {
+  uint32_t u = (uint32_t)b << 16;
+  float f;
+  std::memcpy(&f, &u, 4);
+  return f;
+}
+
+// eval BatchNorm folded into the preceding bias-free conv:
+//   y = (conv(x) - mean) * gamma / sqrt(var + eps) + beta
+struct Folded {
+  std::vector<float> w, b;
+};
+Folded fold(const float* w, size_t per_out, int cout, const float* gamma, const float* beta,
+            const float* mean, const float* var, float eps) {
+  Folded f;
+  f.w.resize((size_t)cout * per_out);
+  f.b.resize(cout);
+  for (int n = 0; n < cout; ++n) {
+    const double sc = (gamma ? (double)gamma[n] : 1.0) / std::sqrt((double)var[n] + (double)eps);
+    for (size_t j = 0; j < per_out; ++j)
+      f.w[(size_t)n * per_out + j] = (float)((double)w[(size_t)n * per_out + j] * sc);
+    f.b[n] = (float)((beta ? (double)beta[n] : 0.0) - (double)mean[n] * sc);
+  }
+  return f;
+}
+
+struct Prof {
+  bool on = false;
+  struct Pend {
+    int stage;
+    hipEvent_t a, b;
+  };
+  std::vector<hipEvent_t> pool;
+  std::vector<Pend> pend;
+  std::vector<std::string> names;
+  std::vector<double> ms;
+  std::vector<int64_t> cnt;
+  hipEvent_t get() {
+    if (!pool.empty()) {
+      hipEvent_t e = pool.back();
+      pool.pop_back();
+      return e;
+    }
+    hipEvent_t e = nullptr;
+    (void)hipEventCreate(&e);
+    return e;
+  }
+  int stage_id(const char* name) {
+    for (size_t i = 0; i < names.size(); ++i)
+      if (names[i] == name) return (int)i;
+    names.emplace_back(name);
+    ms.push_back(0.0);
+    cnt.push_back(0);
+    return (int)names.size() - 1;
+  }
+  ~Prof() {
+    for (auto& p : pend) {
+      (void)hipEventDestroy(p.a);
+      (void)hipEventDestroy(p.b);
+    }
+    for (auto e : pool) (void)hipEventDestroy(e);
+  }
+};
+
+}  // namespace
+
+struct hn_model {
+  Prof prof;
+  hn_arch_desc desc{};
+  int device = 0;
+  std::vector<void*> allocs;
+  HardnetDev hd;
+  float *stem_w = nullptr, *stem_b = nullptr;  // NAS stem
+  std::vector<NasLayer> layers;
+  float *head_w = nullptr, *head_b = nullptr;  // NAS head
+  int head_k = 0;
+  int chunk = 32768;
+  size_t ws_floats_per_patch = 0;  // per buffer
+  int n_bufs = 0;
+
+  template <class T>
+  int upload(const std::vector<T>& v, T** out) {
+    void* d = nullptr;
+    if (hipMalloc(&d, v.size() * sizeof(T)) != hipSuccess)
+      return fail(HN_ERR_NOMEM, "hipMalloc of parameters failed");
+    allocs.push_back(d);
+    HIPCHK(hipMemcpy(d, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    *out = static_cast<T*>(d);
+    return HN_OK;
+  }
+  ~hn_model() {
+    for (void* p : allocs) (void)hipFree(p);
+  }
+};
+
+// ---------------------------------------------------------------------------------------
+// parameter accounting
+// ---------------------------------------------------------------------------------------
+static int check_desc(const hn_arch_desc* d) {
+  if (!d) return fail(HN_ERR_ARG, "desc is NULL");
+  if (d->kind == HN_KIND_HARDNET) return HN_OK;
+  if (d->kind != HN_KIND_NAS) return fail(HN_ERR_ARG, "unknown desc->kind");
+  if (d->n_layers < 1 || d->n_layers > HN_MAX_LAYERS)
+    return fail(HN_ERR_ARG, "n_layers out of range");
+  int hw = 32, c = 32;
+  for (int i = 0; i < d->n_layers; ++i) {
+    if (d->op[i] < 0 || d->op[i] >= 17) return fail(HN_ERR_ARG, "op index out of range");
+    if (d->c_in[i] != c) return fail(HN_ERR_ARG, "c_in does not chain");
+    if (d->stride[i] != 1 && d->stride[i] != 2) return fail(HN_ERR_ARG, "stride must be 1/2");
+    if (d->c_out[i] % 4 || d->c_in[i] % 4 || d->c_out[i] > 256)
+      return fail(HN_ERR_ARG, "channel counts must be multiples of 4 and <= 256");
+    hw /= d->stride[i];
+    c = d->c_out[i];
+  }
+  if (hw != 4) return fail(HN_ERR_ARG, "NAS head expects a 4x4 final map (SEARCH_SPACE2)");
+  return HN_OK;
+}
+
+static size_t nas_layer_params(const hn_arch_desc* d, int i) {
+  const OpSpec& s = kOps[d->op[i]];
+  const size_t ci = d->c_in[i], co = d->c_out[i];
+  if (s.skip) return ci == co ? 0 : ci * co + 4 * co;
+  const size_t mid = ci * s.e;
+  size_t n = mid * (ci / s.g) + 4 * mid;  // pw
+  n += mid * s.k * s.k + 4 * mid;         // dw
+  n += co * (mid / s.g) + 4 * co;         // pwl
+  if (s.se) {
+    const size_t m = co / 4 > 8 ? co / 4 : 8;
+    n += m * co + m + co * m + co;
+  }
+  return n;
+}
+
+extern "C" int hn_param_count(const hn_arch_desc* desc, size_t* n_out) {
+  int rc = check_desc(desc);
+  if (rc) return rc;
+  if (!n_out) return fail(HN_ERR_ARG, "n_out is NULL");
+  if (desc->kind == HN_KIND_HARDNET) {
+    // 7 convs: weights + running_mean + running_var (BN affine=False), HardNet.py:280-302
+    *n_out = 1334560 + 2 * (32 + 32 + 64 + 64 + 128 + 128 + 128);
+    return HN_OK;
+  }
+  size_t n = 32 * 9 + 4 * 32;  // first: ConvBNRelu(1, 32, 3)
+  for (int i = 0; i < desc->n_layers; ++i) n += nas_layer_params(desc, i);
+  n += (size_t)128 * desc->c_out[desc->n_layers - 1] * 16 + 2 * 128;  // head conv + BN stats
+  *n_out = n;
+  return HN_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+// packing
+// ---------------------------------------------------------------------------------------
+// conv1..5 of HardNet as bf16x3 MFMA fragments: [cc][tap][ks][nt][plane][lane][8]
+static std::vector<uint16_t> pack_conv3x3(const std::vector<float>& w, int cin, int cout) {
+  const int ncc = cin / 32, ntot = cout / 32;
+  std::vector<uint16_t> out((size_t)ncc * 9 * 2 * ntot * 2 * 64 * 8);
+  size_t o = 0;
+  for (int cc = 0; cc < ncc; ++cc)
+    for (int tap = 0; tap < 9; ++tap)
+      for (int ks = 0; ks < 2; ++ks)
+        for (int nt = 0; nt < ntot; ++nt) {
+          uint16_t* hi = &out[o];
+          uint16_t* lo = &out[o + 64 * 8];
+          for (int lane = 0; lane < 64; ++lane)
+            for (int j = 0; j < 8; ++j) {
+              const int n = nt * 32 + (lane & 31);
+              const int c = cc * 32 + ks * 16 + (lane >> 5) * 8 + j;
+              const float v = w[((size_t)n * cin + c) * 9 + tap];
+              const uint16_t h = f2bf(v);
+              hi[lane * 8 + j] = h;
+              lo[lane * 8 + j] = f2bf(v - bf2f(h));
+            }
+          o += 2 * 64 * 8;
+        }
+  return out;
+}
+
+// head conv (kernel kk x kk over an NHWC map): GEMM k = (y*kk + x)*cin + c,
+// fragments [ks][nt][plane][lane][8]
+static std::vector<uint16_t> pack_head(const std::vector<float>& w, int cin, int kk) {
+  const int K = cin * kk * kk;
+  std::vector<uint16_t> out((size_t)(K / 16) * 4 * 2 * 64 * 8);
+  size_t o = 0;
+  for (int ks = 0; ks < K / 16; ++ks)
+    for (int nt = 0; nt < 4; ++nt) {
+      uint16_t* hi = &out[o];
+      uint16_t* lo = &out[o + 64 * 8];
+      for (int lane = 0; lane < 64; ++lane)
+        for (int j = 0; j < 8; ++j) {
+          const int n = nt * 32 + (lane & 31);
+          const int k = ks * 16 + (lane >> 5) * 8 + j;
+          const int c = k % cin, yx = k / cin;
+          const float v = w[((size_t)n * cin + c) * kk * kk + yx];
+          const uint16_t h = f2bf(v);
+          hi[lane * 8 + j] = h;
+          lo[lane * 8 + j] = f2bf(v - bf2f(h));
+        }
+      o += 2 * 64 * 8;
+    }
+  return out;
+}
+
+// [cout][kg] -> [kg][cout]
+static std::vector<float> transpose_pw(const std::vector<float>& w, int cout, int kg) {
+  std::vector<float> t((size_t)kg * cout);
+  for (int n = 0; n < cout; ++n)
+    for (int k = 0; k < kg; ++k) t[(size_t)k * cout + n] = w[(size_t)n * kg + k];
+  return t;
+}
+
+static int build_hardnet(hn_model* m, Cursor& cur) {
+  static const int cin[7] = {1, 32, 32, 64, 64, 128, 128};
+  static const int cout[7] = {32, 32, 64, 64, 128, 128, 128};
+  static const int ks[7] = {3, 3, 3, 3, 3, 3, 8};
+  const float eps = m->desc.bn_eps;
+  for (int l = 0; l < 7; ++l) {
+    const size_t per = (size_t)cin[l] * ks[l] * ks[l];
+    const float* w = cur.take(per * cout[l]);
+    const float* mean = cur.take(cout[l]);
+    const float* var = cur.take(cout[l]);
+    if (!cur.ok) return fail(HN_ERR_ARG, "host_params too short");
+    Folded f = fold(w, per, cout[l], nullptr, nullptr, mean, var, eps);
+    int rc;
+    if (l == 0) {
+      std::vector<float> sw(9 * 32);
+      for (int n = 0; n < 32; ++n)
+        for (int t = 0; t < 9; ++t) sw[t * 32 + n] = f.w[n * 9 + t];
+      if ((rc = m->upload(sw, &m->hd.stem_w))) return rc;
+      if ((rc = m->upload(f.b, &m->hd.stem_b))) return rc;
+      continue;
+    }
+    std::vector<uint16_t> pk = (l < 6) ? pack_conv3x3(f.w, cin[l], cout[l]) : pack_head(f.w, 128, 8);
+    uint16_t* d = nullptr;
+    if ((rc = m->upload(pk, &d))) return rc;
+    m->hd.wpack[l] = d;
+    if ((rc = m->upload(f.b, &m->hd.bias[l]))) return rc;
+  }
+  m->ws_floats_per_patch = 32 * 32 * 32;
+  m->n_bufs = 3;
+  return HN_OK;
+}
+
+static int take_cbr(hn_model* m, Cursor& cur, int cout, size_t per_out, Folded* f) {
+  const float* w = cur.take((size_t)cout * per_out);
+  const float* g = cur.take(cout);
+  const float* b = cur.take(cout);
+  const float* mu = cur.take(cout);
+  const float* var = cur.take(cout);
+  if (!cur.ok) return fail(HN_ERR_ARG, "host_params too short");
+  *f = fold(w, per_out, cout, g, b, mu, var, m->desc.bn_eps);
+  return HN_OK;
+}
+
+static int build_nas(hn_model* m, Cursor& cur) {
+  const hn_arch_desc& d = m->desc;
+  int rc;
+  Folded f;
+  if ((rc = take_cbr(m, cur, 32, 9, &f))) return rc;
+  {
+    std::vector<float> sw(9 * 32);
+    for (int n = 0; n < 32; ++n)
+      for (int t = 0; t < 9; ++t) sw[t * 32 + n] = f.w[n * 9 + t];
+    if ((rc = m->upload(sw, &m->stem_w))) return rc;
+    if ((rc = m->upload(f.b, &m->stem_b))) return rc;
+  }
+  size_t maxf = 32 * 32 * 32;
+  int hw = 32;
+  for (int i = 0; i < d.n_layers; ++i) {
+    NasLayer L;
+    const OpSpec& s = kOps[d.op[i]];
+    L.op = d.op[i];
+    L.cin = d.c_in[i];
+    L.cout = d.c_out[i];
+    L.stride = d.stride[i];
+    L.hin = hw;
+    L.hout = hw / L.stride;
+    L.skip = s.skip;
+    if (s.skip) {
+      L.skip_conv = L.cin != L.cout;
+      if (L.skip_conv) {
+        if ((rc = take_cbr(m, cur, L.cout, L.cin, &f))) return rc;
+        if ((rc = m->upload(transpose_pw(f.w, L.cout, L.cin), &L.pw_w))) return rc;
+        if ((rc = m->upload(f.b, &L.pw_b))) return rc;
+      }
+      maxf = std::max(maxf, (size_t)L.cin * L.hout * L.hout);
+      maxf = std::max(maxf, (size_t)L.cout * L.hout * L.hout);
+    } else {
+      L.e = s.e;
+      L.k = s.k;
+      L.g = s.g;
+      L.se = s.se;
+      L.mid = L.cin * L.e;
+      if ((rc = take_cbr(m, cur, L.mid, L.cin / L.g, &f))) return rc;
+      if ((rc = m->upload(transpose_pw(f.w, L.mid, L.cin / L.g), &L.pw_w))) return rc;
+      if ((rc = m->upload(f.b, &L.pw_b))) return rc;
+      if ((rc = take_cbr(m, cur, L.mid, (size_t)L.k * L.k, &f))) return rc;
+      {
+        std::vector<float> wd((size_t)L.k * L.k * L.mid);
+        for (int c = 0; c < L.mid; ++c)
+          for (int t = 0; t < L.k * L.k; ++t) wd[(size_t)t * L.mid + c] = f.w[(size_t)c * L.k * L.k + t];
+        if ((rc = m->upload(wd, &L.dw_w))) return rc;
+        if ((rc = m->upload(f.b, &L.dw_b))) return rc;
+      }
+      if ((rc = take_cbr(m, cur, L.cout, L.mid / L.g, &f))) return rc;
+      if ((rc = m->upload(transpose_pw(f.w, L.cout, L.mid / L.g), &L.pwl_w))) return rc;
+      if ((rc = m->upload(f.b, &L.pwl_b))) return rc;
+      if (L.se) {
+        L.semid = L.cout / 4 > 8 ? L.cout / 4 : 8;
+        const size_t n1 = (size_t)L.semid * L.cout;
+        const float* w1 = cur.take(n1);
+        const float* b1 = cur.take(L.semid);
+        const float* w2 = cur.take(n1);
+        const float* b2 = cur.take(L.cout);
+        if (!cur.ok) return fail(HN_ERR_ARG, "host_params too short");
+        if ((rc = m->upload(std::vector<float>(w1, w1 + n1), &L.se_w1))) return rc;
+        if ((rc = m->upload(std::vector<float>(b1, b1 + L.semid), &L.se_b1))) return rc;
+        if ((rc = m->upload(std::vector<float>(w2, w2 + n1), &L.se_w2))) return rc;
+        if ((rc = m->upload(std::vector<float>(b2, b2 + L.cout), &L.se_b2))) return rc;
+      }
+      maxf = std::max(maxf, (size_t)L.mid * L.hin * L.hin);
+      maxf = std::max(maxf, (size_t)L.mid * L.hout * L.hout);
+      maxf = std::max(maxf, (size_t)L.cout * L.hout * L.hout);
+    }
+    m->layers.push_back(L);
+    hw = L.hout;
+  }
+  const int cl = d.c_out[d.n_layers - 1];
+  const float* w = cur.take((size_t)128 * cl * 16);
+  const float* mu = cur.take(128);
+  const float* var = cur.take(128);
+  if (!cur.ok) return fail(HN_ERR_ARG, "host_params too short");
+  f = fold(w, (size_t)cl * 16, 128, nullptr, nullptr, mu, var, d.bn_eps);
+  {
+    const int K = cl * 16;
+    std::vector<float> wt((size_t)K * 128);
+    for (int n = 0; n < 128; ++n)
+      for (int c = 0; c < cl; ++c)
+        for (int yx = 0; yx < 16; ++yx)
+          wt[((size_t)yx * cl + c) * 128 + n] = f.w[((size_t)n * cl + c) * 16 + yx];
+    if ((rc = m->upload(wt, &m->head_w))) return rc;
+    if ((rc = m->upload(f.b, &m->head_b))) return rc;
+    m->head_k = K;
+  }
+  m->ws_floats_per_patch = maxf;
+  m->n_bufs = 4;
+  return HN_OK;
+}
+
+extern "C" int hn_create(const hn_arch_desc* desc, const float* host_params, size_t n_params,
+                         hn_model** out) {
+  int rc = check_desc(desc);
+  if (rc) return rc;
+  if (!out || !host_params) return fail(HN_ERR_ARG, "NULL argument");
+  size_t want = 0;
+  if ((rc = hn_param_count(desc, &want))) return rc;
+  if (want != n_params)
+    return fail(HN_ERR_ARG, "host_params has " + std::to_string(n_params) + " floats, expected " +
+                                std::to_string(want));
+  hn_model* m = new hn_model();
+  m->desc = *desc;
+  if (const char* e = std::getenv("HN_CHUNK")) m->chunk = std::max(64, std::atoi(e));
+  (void)hipGetDevice(&m->device);
+  Cursor cur{host_params, n_params};
+  rc = desc->kind == HN_KIND_HARDNET ? build_hardnet(m, cur) : build_nas(m, cur);
+  if (!rc && cur.i != n_params) rc = fail(HN_ERR_ARG, "host_params not fully consumed");
+  if (rc) {
+    delete m;
+    return rc;
+  }
+  *out = m;
+  return HN_OK;
+}
+
+extern "C" int hn_workspace_bytes(const hn_model* m, int64_t batch, size_t* bytes_out) {
+  if (!m || !bytes_out || batch < 0) return fail(HN_ERR_ARG, "bad argument");
+  const int64_t p = batch < m->chunk ? batch : m->chunk;
+  *bytes_out = (size_t)p * m->ws_floats_per_patch * m->n_bufs * sizeof(float);
+  return HN_OK;
+}
+
+// Launch one stage; with profiling on, bracket it by a hipEvent pair on the same stream.
+#define STAGE(NAME, CALL)                                                                  \
+  do {                                                                                     \
+    hipEvent_t a_ = nullptr;                                                               \
+    if (m->prof.on) {                                                                      \
+      a_ = m->prof.get();                                                                  \
+      HIPCHK(hipEventRecord(a_, st));                                                      \
+    }                                                                                      \
+    HIPCHK(CALL);                                                                          \
+    if (m->prof.on) {                                                                      \
+      hipEvent_t b_ = m->prof.get();                                                       \
+      HIPCHK(hipEventRecord(b_, st));                                                      \
+      m->prof.pend.push_back({m->prof.stage_id(NAME), a_, b_});                            \
+    }                                                                                      \
+  } while (0)
+
+static int forward_hardnet(hn_model* m, const float* in, int P, float* out, float* ws,
+                           hipStream_t st) {
+  const size_t per = m->ws_floats_per_patch * (size_t)P;
+  float* a0 = ws;
+  float* a1 = ws + per;
+  float* a2 = ws + 2 * per;
+  const float ineps = m->desc.input_norm_eps;
+  STAGE("stem", hn_launch_stem(in, a0, m->hd.stem_w, m->hd.stem_b, P, ineps >= 0.f, ineps, st));
+  STAGE("conv1", hn_launch_hardnet_conv(1, m->hd, a0, a1, P, st));
+  STAGE("conv2", hn_launch_hardnet_conv(2, m->hd, a1, a2, P, st));
+  STAGE("conv3", hn_launch_hardnet_conv(3, m->hd, a2, a1, P, st));
+  STAGE("conv4", hn_launch_hardnet_conv(4, m->hd, a1, a2, P, st));
+  STAGE("conv5", hn_launch_hardnet_conv(5, m->hd, a2, a1, P, st));
+  STAGE("head", hn_launch_head(a1, out, m->hd.wpack[6], m->hd.bias[6], P, 8192, m->desc.l2_eps, st));
+  return HN_OK;
+}
+
+static int forward_nas(hn_model* m, const float* in, int P, float* out, float* ws,
+                       hipStream_t st) {
+  const size_t per = m->ws_floats_per_patch * (size_t)P;
+  float* x = ws;
+  float* t1 = ws + per;
+  float* t2 = ws + 2 * per;
+  float* y = ws + 3 * per;
+  const float ineps = m->desc.input_norm_eps;
+  STAGE("stem", hn_launch_stem(in, x, m->stem_w, m->stem_b, P, ineps >= 0.f, ineps, st));
+  for (const NasLayer& L : m->layers) {
+    const long npix_out = (long)P * L.hout * L.hout;
+    if (L.skip) {
+      const float* src = x;
+      if (L.stride == 2) {
+        STAGE("maxpool", hn_launch_maxpool(x, t1, P, L.hin, L.cin, st));
+        src = t1;
+      }
+      if (L.skip_conv) {
+        STAGE("pw", hn_launch_pw(src, y, L.pw_w, L.pw_b, nullptr, npix_out, L.cin, L.cout, 1, true, 0, st));
+        std::swap(x, y);
+      } else if (L.stride == 2) {
+        std::swap(x, t1);
+      }
+      continue;
+    }
+    const long npix_in = (long)P * L.hin * L.hin;
+    STAGE("pw", hn_launch_pw(x, t1, L.pw_w, L.pw_b, nullptr, npix_in, L.cin, L.mid, L.g, true,
+                             L.g > 1 ? L.g : 0, st));
+    STAGE("dw", hn_launch_dw(t1, t2, L.dw_w, L.dw_b, P, L.hin, L.mid, L.k, L.stride, st));
+    const bool res = L.stride == 1 && L.cin == L.cout;
+    STAGE("pwl", hn_launch_pw(t2, y, L.pwl_w, L.pwl_b, res ? x : nullptr, npix_out, L.mid, L.cout,
+                              L.g, false, 0, st));
+    if (L.se)
+      STAGE("se", hn_launch_se(y, L.se_w1, L.se_b1, L.se_w2, L.se_b2, P, L.hout * L.hout, L.cout,
+                               L.semid, st));
+    std::swap(x, y);
+  }
+  STAGE("head", hn_launch_nas_head(x, out, m->head_w, m->head_b, P, m->head_k, m->desc.l2_eps, st));
+  return HN_OK;
+}
+
+extern "C" int hn_forward(hn_model* m, const float* d_in, int64_t batch, float* d_out,
+                          void* d_workspace, size_t workspace_bytes, void* hip_stream) {
+  if (!m) return fail(HN_ERR_ARG, "model is NULL");
+  if (batch < 0) return fail(HN_ERR_ARG, "negative batch");
+  if (batch == 0) return HN_OK;
+  if (!d_in || !d_out || !d_workspace) return fail(HN_ERR_ARG, "NULL device pointer");
+  if ((reinterpret_cast<uintptr_t>(d_in) | reinterpret_cast<uintptr_t>(d_out) |
+       reinterpret_cast<uintptr_t>(d_workspace)) & 15)
+    return fail(HN_ERR_ARG, "device pointers must be 16-byte aligned");
+  size_t need = 0;
+  hn_workspace_bytes(m, batch, &need);
+  if (workspace_bytes < need)
+    return fail(HN_ERR_WORKSPACE, "workspace too small: need " + std::to_string(need) + " bytes");
+  hipStream_t st = static_cast<hipStream_t>(hip_stream);
+  for (int64_t off = 0; off < batch; off += m->chunk) {
+    const int P = (int)std::min<int64_t>(m->chunk, batch - off);
+    const float* in = d_in + off * 1024;
+    float* out = d_out + off * 128;
+    float* ws = static_cast<float*>(d_workspace);
+    const int rc = m->desc.kind == HN_KIND_HARDNET ? forward_hardnet(m, in, P, out, ws, st)
+                                                   : forward_nas(m, in, P, out, ws, st);
+    if (rc) return rc;
+  }
+  return HN_OK;
+}
+
+extern "C" int hn_pairdist_workspace_bytes(int64_t batch, size_t* bytes_out) {
+  if (!bytes_out || batch < 0) return fail(HN_ERR_ARG, "bad argument");
+  *bytes_out = (size_t)(batch > 0 ? batch : 1) * sizeof(float);
+  return HN_OK;
+}
+
+extern "C" int hn_pairdist_hardneg(const float* d_anchor, const float* d_positive, int64_t batch,
+                                   int32_t dim, int32_t anchor_swap, float* d_pos,
+                                   float* d_min_neg, void* d_workspace, size_t workspace_bytes,
+                                   void* hip_stream) {
+  if (!d_anchor || !d_positive || !d_pos || !d_min_neg || !d_workspace)
+    return fail(HN_ERR_ARG, "NULL device pointer");
+  if (batch < 2 || batch > (1 << 30)) return fail(HN_ERR_ARG, "batch out of range");
+  if (dim != 128) return fail(HN_ERR_ARG, "dim must be 128");
+  size_t need = 0;
+  hn_pairdist_workspace_bytes(batch, &need);
+  if (workspace_bytes < need) return fail(HN_ERR_WORKSPACE, "workspace too small");
+  HIPCHK(hn_launch_pairdist(d_anchor, d_positive, (int)batch, dim, anchor_swap, d_pos, d_min_neg,
+                            d_workspace, static_cast<hipStream_t>(hip_stream)));
+  return HN_OK;
+}
+
+extern "C" int hn_set_profiling(hn_model* m, int enable) {
+  if (!m) return fail(HN_ERR_ARG, "model is NULL");
+  m->prof.on = enable != 0;
+  return HN_OK;
+}
+
+extern "C" int hn_stage_times(hn_model* m, int max_stages, const char** names_out,
+                              double* total_ms_out, int64_t* launches_out) {
+  if (!m) return -fail(HN_ERR_ARG, "model is NULL");
+  Prof& p = m->prof;
+  for (auto& e : p.pend) {
+    HIPCHK(hipEventSynchronize(e.b));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, e.a, e.b));
+    p.ms[e.stage] += ms;
+    p.cnt[e.stage] += 1;
+    p.pool.push_back(e.a);
+    p.pool.push_back(e.b);
+  }
+  p.pend.clear();
+  const int n = (int)std::min<size_t>(p.names.size(), (size_t)std::max(0, max_stages));
+  for (int i = 0; i < n; ++i) {
+    if (names_out) names_out[i] = p.names[i].c_str();
+    if (total_ms_out) total_ms_out[i] = p.ms[i];
+    if (launches_out) launches_out[i] = p.cnt[i];
+    p.ms[i] = 0.0;
+    p.cnt[i] = 0;
+  }
+  return n;
+}
+
+extern "C" void hn_destroy(hn_model* m) { delete m; }
+
+extern "C" const char* hn_last_error(void) { return g_err.c_str(); }
+
+extern "C" int hn_abi_version(void) { return HN_ABI_VERSION; }

@@ -1,0 +1,33 @@
+// Internal host-side interface between the C ABI (hn_api.hip) and the kernel files.
+#pragma once
+#include <hip/hip_runtime.h>
+
+// Device-resident, BN-folded, packed HardNet parameters.
+struct HardnetDev {
+  float* stem_w = nullptr;   // [9][32]   conv0 folded
+  float* stem_b = nullptr;   // [32]
+  void* wpack[7] = {};       // conv1..5: bf16 hi/lo MFMA fragments; [6] = head
+  float* bias[7] = {};       // folded BN bias per conv
+};
+
+hipError_t hn_launch_stem(const float* in, float* out, const float* w, const float* b, int P,
+                          bool norm, float eps, hipStream_t st);
+hipError_t hn_launch_hardnet_conv(int layer, const HardnetDev& d, const float* in, float* out,
+                                  int P, hipStream_t st);
+hipError_t hn_launch_head(const float* a, float* out, const void* wp, const float* bias, int P,
+                          int K, float l2eps, hipStream_t st);
+int hn_conv_lds_bytes(int layer);
+
+hipError_t hn_launch_pw(const float* in, float* out, const float* wt, const float* bias,
+                        const float* res, long npix, int cin, int cout, int groups, bool relu,
+                        int shuffle_g, hipStream_t st);
+hipError_t hn_launch_dw(const float* in, float* out, const float* wd, const float* bias, int P,
+                        int hin, int c, int k, int s, hipStream_t st);
+hipError_t hn_launch_maxpool(const float* in, float* out, int P, int hin, int c, hipStream_t st);
+hipError_t hn_launch_se(float* y, const float* w1, const float* b1, const float* w2,
+                        const float* b2, int P, int hw, int c, int mid, hipStream_t st);
+hipError_t hn_launch_nas_head(const float* a, float* out, const float* wt, const float* bias,
+                              int P, int K, float l2eps, hipStream_t st);
+
+hipError_t hn_launch_pairdist(const float* a, const float* p, int B, int D, int swap,
+                              float* pos, float* minneg, void* ws, hipStream_t st);

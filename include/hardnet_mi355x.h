@@ -1,0 +1,125 @@
+/*
+ * hardnet_mi355x.h -- C ABI of the MI355X-native HardNet / hardnetNAS descriptor forward.
+ *
+ * This is the drop-in boundary for the reference hot path
+ *   hardnet/HardNet.py:312-315          HardNet.forward(input [B,1,32,32]) -> [B,128]
+ *   hardnet/HardNet.py:306-310          HardNet.input_norm (fused into hn_forward)
+ *   hardnet/Utils.py:15-22              L2Norm (fused into hn_forward)
+ *   hardnetNAS/supernet_functions/model_supernet.py:70-85
+ *                                       sampled-supernet forward (argmax op per layer)
+ *   hardnet/Losses.py:5-13,87-154       distance_matrix_vector + loss_HardNet 'min' reduce
+ *                                       (hn_pairdist_hardneg)
+ * The reference is pure PyTorch and has no FFI of its own; the Python host package
+ * (hardnetnas_amd/_native.py) binds these entry points with ctypes -- see
+ * INTEGRATION.md for the binding a maintainer adds to the reference.
+ *
+ * Conventions
+ *  - Plain pointers and sizes only.  Device pointers are HIP device memory owned by the
+ *    caller; nothing is copied host<->device inside hn_forward.
+ *  - Every call is ordered on the caller's HIP stream (hipStream_t passed as void*;
+ *    NULL = the legacy default stream).  No allocation or synchronisation happens inside
+ *    hn_forward / hn_pairdist_hardneg, so they can be captured in a hipGraph.
+ *  - Return value 0 = success; nonzero = error, message in hn_last_error() (thread-local).
+ *    The library never exits the process.
+ */
+#ifndef HARDNET_MI355X_H
+#define HARDNET_MI355X_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HN_ABI_VERSION 1
+
+enum hn_status {
+  HN_OK = 0,
+  HN_ERR_ARG = 1,      /* invalid argument / shape / size mismatch */
+  HN_ERR_HIP = 2,      /* HIP runtime error (message has the HIP error string) */
+  HN_ERR_NOMEM = 3,    /* device allocation failed */
+  HN_ERR_WORKSPACE = 4 /* workspace too small for the requested batch */
+};
+
+enum hn_kind {
+  HN_KIND_HARDNET = 0, /* stock HardNet, hardnet/HardNet.py:275-304 */
+  HN_KIND_NAS = 1      /* sampled hardnetNAS net, model_supernet.py:53-85 */
+};
+
+#define HN_MAX_LAYERS 8
+
+/* Architecture description.
+ *  HardNet: only kind, input_norm_eps, l2_eps, bn_eps are read.
+ *  NAS:     op[i] = index into CANDIDATE_BLOCKS (lookup_table_builder.py:18-20);
+ *           c_in/c_out/stride from SEARCH_SPACE2 (lookup_table_builder.py:22-45).
+ *  input_norm_eps < 0 disables input_norm (the NAS nets have none);
+ *  l2_eps: HardNet 1e-10 inside the sqrt (Utils.py:18); NAS 0 (torch.norm, model_supernet.py:84). */
+typedef struct hn_arch_desc {
+  int32_t kind;
+  int32_t n_layers;
+  int32_t op[HN_MAX_LAYERS];
+  int32_t c_in[HN_MAX_LAYERS];
+  int32_t c_out[HN_MAX_LAYERS];
+  int32_t stride[HN_MAX_LAYERS];
+  float input_norm_eps;
+  float l2_eps;
+  float bn_eps;
+} hn_arch_desc;
+
+typedef struct hn_model hn_model;
+
+/* Number of floats hn_create expects in host_params for this architecture. */
+int hn_param_count(const hn_arch_desc* desc, size_t* n_out);
+
+/* Build a device model on the current HIP device from host fp32 parameters.
+ * host_params is the concatenation, in state_dict order, of every conv weight and
+ * BatchNorm tensor of the module (HardNet: for each of the 7 convs
+ *   features.{c}.weight, features.{b}.running_mean, features.{b}.running_var;
+ * NAS: see hardnetnas_amd/_native.py::state_dict_blob, which documents the order).
+ * BatchNorm (eval) is folded into the conv weights/bias here, once. */
+int hn_create(const hn_arch_desc* desc, const float* host_params, size_t n_params,
+              hn_model** out);
+
+/* Bytes of device workspace hn_forward needs for a batch of B patches. */
+int hn_workspace_bytes(const hn_model* m, int64_t batch, size_t* bytes_out);
+
+/* d_in: [B,1,32,32] fp32 contiguous (device); d_out: [B,128] fp32 (device).
+ * Eval-mode forward of the whole descriptor network (HardNet: input_norm, 7 conv+BN
+ * stages, ReLU, L2Norm; NAS: stem, 6 searched blocks, 4x4 head, BN, L2). */
+int hn_forward(hn_model* m, const float* d_in, int64_t batch, float* d_out,
+               void* d_workspace, size_t workspace_bytes, void* hip_stream);
+
+/* Fused distance_matrix_vector + hardest-in-batch negative (loss_HardNet 'min' reduce,
+ * hardnet/Losses.py:87-154) without materialising the B x B matrix.
+ * d_anchor, d_positive: [B,D] fp32.  Outputs (device, [B] fp32 each):
+ *   d_pos[i]     = dist(a_i, p_i) + 1e-8              (pos1)
+ *   d_min_neg[i] = min_j masked dist(a_i, p_j)        (row min, or min(row,col) if anchor_swap)
+ * d_workspace needs hn_pairdist_workspace_bytes(B). */
+int hn_pairdist_workspace_bytes(int64_t batch, size_t* bytes_out);
+int hn_pairdist_hardneg(const float* d_anchor, const float* d_positive, int64_t batch, int32_t dim,
+                        int32_t anchor_swap, float* d_pos, float* d_min_neg,
+                        void* d_workspace, size_t workspace_bytes, void* hip_stream);
+
+/* Per-stage timing (profiling aid used by bench.py): when enabled, hn_forward records a
+ * hipEvent pair around every kernel launch on the caller's stream.  hn_stage_times
+ * waits for the recorded events, accumulates their durations per stage name and returns
+ * the number of stages (<= max_stages); it then clears the accumulators.
+ * names_out[i] points to storage owned by the model. */
+int hn_set_profiling(hn_model* m, int enable);
+int hn_stage_times(hn_model* m, int max_stages, const char** names_out, double* total_ms_out,
+                   int64_t* launches_out);
+
+void hn_destroy(hn_model* m);
+
+/* Message of the last failing call on this thread ("" if none). */
+const char* hn_last_error(void);
+
+/* HN_ABI_VERSION of the loaded library. */
+int hn_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* HARDNET_MI355X_H */

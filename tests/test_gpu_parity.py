@@ -1,0 +1,157 @@
+"""Parity of the HIP path (through the C ABI) with the reference vectors and the oracle.
+
+Tolerances (BASELINE.json north_star: <= 1e-4 max abs on the 128-D descriptor):
+  HardNet  -- bf16x3 split-precision MFMA: 1e-4 max abs vs the reference fp32 forward.
+  NAS      -- exact fp32 VALU kernels:     2e-5 max abs.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from fixtures import NAS_NAMES, build_module, load, golden_inputs
+from oracle import hardnet_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+TOL = {"hardnet": 1e-4}
+NAS_TOL = 2e-5
+
+
+def _tol(name):
+    return TOL.get(name, NAS_TOL)
+
+
+def _native_lib_loaded():
+    maps = open("/proc/self/maps").read()
+    return "libhardnet_mi355x.so" in maps
+
+
+@pytest.mark.parametrize("name", ["hardnet"] + NAS_NAMES)
+def test_forward_matches_reference_vectors(name, cuda_device):
+    m, fx, _ = build_module(name)
+    m = m.to(cuda_device)
+    x = torch.from_numpy(golden_inputs(fx)).to(cuda_device)
+    with torch.no_grad():
+        y = m(x).cpu().numpy()
+    assert _native_lib_loaded()
+    err = np.abs(y - fx["y"]).max()
+    err64 = np.abs(y - fx["y64"]).max()
+    print(f"{name}: max|hip - ref32| = {err:.3e}, max|hip - ref64| = {err64:.3e}")
+    assert err <= _tol(name)
+    xe = torch.from_numpy(fx["x_edge"]).to(cuda_device)
+    with torch.no_grad():
+        ye = m(xe).cpu().numpy()
+    assert np.abs(ye - fx["y_edge"]).max() <= _tol(name)
+
+
+@pytest.mark.parametrize("name", ["hardnet", "wang2"])
+@pytest.mark.parametrize("b", [1, 3, 63, 65, 130, 257])
+def test_ragged_batches(name, b, cuda_device):
+    m, fx, _ = build_module(name)
+    m = m.to(cuda_device)
+    x = torch.from_numpy(golden_inputs(fx)[:b]).to(cuda_device)
+    with torch.no_grad():
+        y = m(x).cpu().numpy()
+    assert y.shape == (b, 128)
+    assert np.abs(y - fx["y"][:b]).max() <= _tol(name)
+
+
+def test_empty_batch(cuda_device):
+    m, _, _ = build_module("hardnet")
+    m = m.to(cuda_device)
+    with torch.no_grad():
+        y = m(torch.empty(0, 1, 32, 32, device=cuda_device))
+    assert tuple(y.shape) == (0, 128)
+
+
+@pytest.mark.parametrize("name", ["hardnet", "cov_a"])
+def test_chunked_forward_equals_unchunked(name, cuda_device, monkeypatch):
+    """HN_CHUNK splits the batch inside hn_forward; results must be identical."""
+    from hardnetnas_amd._native import NativeModel
+    m, fx, _ = build_module(name)
+    x = torch.from_numpy(golden_inputs(fx)).to(cuda_device)
+    full = NativeModel.from_module(m, cuda_device)(x)
+    monkeypatch.setenv("HN_CHUNK", "100")
+    chunked = NativeModel.from_module(m, cuda_device)(x)
+    assert torch.equal(full, chunked)
+
+
+def test_deterministic_and_batch_independent(cuda_device):
+    m, fx, _ = build_module("hardnet")
+    m = m.to(cuda_device)
+    x = torch.from_numpy(golden_inputs(fx)).to(cuda_device)
+    with torch.no_grad():
+        y1 = m(x)
+        y2 = m(x)
+        perm = torch.randperm(x.shape[0], device=cuda_device)
+        y3 = m(x[perm])
+        y4 = torch.cat([m(x[:100]), m(x[100:])])
+    assert torch.equal(y1, y2)
+    assert torch.equal(y3, y1[perm])
+    assert torch.equal(y4, y1)
+
+
+@pytest.mark.parametrize("name", ["hardnet", "wang2"])
+def test_large_batch_properties(name, cuda_device):
+    """Full-size path (65,536 patches): unit norm, finite, and a 512-row sample equals the
+    oracle on the same rows."""
+    from hardnetnas_amd import synth
+    m, fx, p = build_module(name)
+    m = m.to(cuda_device)
+    b = 65536
+    x = torch.from_numpy(synth.synth_patches(b, seed=3)).to(cuda_device)
+    with torch.no_grad():
+        y = m(x)
+    assert torch.isfinite(y).all()
+    nrm = y.norm(dim=1)
+    assert (nrm - 1).abs().max().item() < 1e-5
+    idx = torch.randint(0, b, (512,), generator=torch.Generator().manual_seed(0))
+    t = {k: torch.from_numpy(v) for k, v in p.items()}
+    xs = x[idx.to(cuda_device)].cpu()
+    if name == "hardnet":
+        ref = O.hardnet_forward(t, xs)
+    else:
+        ref = O.nas_forward(t, load("nas_" + name)["meta"]["ops"], xs)
+    assert (y[idx.to(cuda_device)].cpu() - ref).abs().max().item() <= _tol(name)
+
+
+def test_weights_update_triggers_repack(cuda_device):
+    m, fx, _ = build_module("hardnet")
+    m = m.to(cuda_device)
+    x = torch.from_numpy(golden_inputs(fx)[:16]).to(cuda_device)
+    with torch.no_grad():
+        y1 = m(x)
+        m.features[3].weight.mul_(1.5)
+        y2 = m(x)
+        m.features[3].weight.div_(1.5)
+        y3 = m(x)
+    assert not torch.allclose(y1, y2)
+    assert torch.equal(y1, y3)
+
+
+def test_train_mode_uses_autograd_path(cuda_device):
+    m, fx, _ = build_module("hardnet")
+    m = m.to(cuda_device).train()
+    x = torch.from_numpy(golden_inputs(fx)[:32]).to(cuda_device)
+    y = m(x)
+    y.sum().backward()
+    assert m.features[0].weight.grad is not None
+
+
+@pytest.mark.parametrize("b", [2, 64, 300, 4097])
+@pytest.mark.parametrize("swap", [False, True])
+def test_pairdist_hardneg_matches_oracle(b, swap, cuda_device):
+    from hardnetnas_amd._native import pairdist_hardneg
+    fx = load("losses")
+    if b in (64, 300):
+        a, p = torch.from_numpy(fx[f"a{b}"]), torch.from_numpy(fx[f"p{b}"])
+    else:
+        g = torch.Generator().manual_seed(b)
+        a = torch.nn.functional.normalize(torch.randn(b, 128, generator=g), dim=1)
+        p = torch.nn.functional.normalize(a + 0.3 * torch.randn(b, 128, generator=g), dim=1)
+    pos, mn = pairdist_hardneg(a.to(cuda_device), p.to(cuda_device), swap)
+    rpos, rmn = O.hardest_negative(a.double(), p.double(), swap)
+    assert (pos.cpu().double() - rpos).abs().max().item() < 1e-4
+    assert (mn.cpu().double() - rmn).abs().max().item() < 1e-4

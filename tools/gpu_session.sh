@@ -1,0 +1,23 @@
+#!/bin/bash
+# One GPU session on the gpurun box: tests, smoke, bench, rocprof kernel stats.
+# Each GPU step has its own time limit; a crash/abort/timeout (exit not 0 or 1) stops the
+# session, test failures (exit 1) do not.
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+run() {  # name, seconds, command...
+  local name=$1 secs=$2; shift 2
+  echo "== $name: $*" | tee -a gpurun_out/session.log
+  timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "== $name exit $rc" | tee -a gpurun_out/session.log
+  tail -5 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+STEPS=${STEPS:-pytest,smoke,bench,prof}
+[[ $STEPS == *pytest* ]] && run pytest_gpu 900 python -m pytest tests -m gpu -q -rf
+[[ $STEPS == *smoke* ]] && run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+[[ $STEPS == *bench* ]] && run bench 600 python bench.py ${BENCH_ARGS:-}
+[[ $STEPS == *prof* ]] && run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 3 --warmup 1 ${BENCH_ARGS:-}
+exit 0
