@@ -152,6 +152,8 @@ struct hn_model {
   float *head_w = nullptr, *head_b = nullptr;  // NAS head
   int head_k = 0;
   int chunk = 32768;
+  bool unfused_stem = false;  // HN_UNFUSED_STEM=1: separate stem kernel (A/B, debugging)
+  int variant[6] = {0, 0, 0, 0, 0, 0};  // HN_VARIANT="v0,v1,..,v5": conv tiling per layer
   size_t ws_floats_per_patch = 0;  // per buffer
   int n_bufs = 0;
 
@@ -436,6 +438,12 @@ extern "C" int hn_create(const hn_arch_desc* desc, const float* host_params, siz
   hn_model* m = new hn_model();
   m->desc = *desc;
   if (const char* e = std::getenv("HN_CHUNK")) m->chunk = std::max(64, std::atoi(e));
+  if (const char* e = std::getenv("HN_UNFUSED_STEM")) m->unfused_stem = std::atoi(e) != 0;
+  if (const char* e = std::getenv("HN_VARIANT")) {
+    int i = 0;
+    for (const char* c = e; *c && i < 6; ++c)
+      if (*c >= '0' && *c <= '9') m->variant[i++] = *c - '0';
+  }
   (void)hipGetDevice(&m->device);
   Cursor cur{host_params, n_params};
   rc = desc->kind == HN_KIND_HARDNET ? build_hardnet(m, cur) : build_nas(m, cur);
@@ -478,12 +486,16 @@ static int forward_hardnet(hn_model* m, const float* in, int P, float* out, floa
   float* a1 = ws + per;
   float* a2 = ws + 2 * per;
   const float ineps = m->desc.input_norm_eps;
-  STAGE("stem", hn_launch_stem(in, a0, m->hd.stem_w, m->hd.stem_b, P, ineps >= 0.f, ineps, st));
-  STAGE("conv1", hn_launch_hardnet_conv(1, m->hd, a0, a1, P, st));
-  STAGE("conv2", hn_launch_hardnet_conv(2, m->hd, a1, a2, P, st));
-  STAGE("conv3", hn_launch_hardnet_conv(3, m->hd, a2, a1, P, st));
-  STAGE("conv4", hn_launch_hardnet_conv(4, m->hd, a1, a2, P, st));
-  STAGE("conv5", hn_launch_hardnet_conv(5, m->hd, a2, a1, P, st));
+  if (m->unfused_stem) {
+    STAGE("stem", hn_launch_stem(in, a0, m->hd.stem_w, m->hd.stem_b, P, ineps >= 0.f, ineps, st));
+    STAGE("conv1", hn_launch_hardnet_conv(1, 0, m->hd, a0, a1, P, 0.f, st));
+  } else {
+    STAGE("stem+conv1", hn_launch_hardnet_conv(0, m->variant[0], m->hd, in, a1, P, ineps, st));
+  }
+  STAGE("conv2", hn_launch_hardnet_conv(2, m->variant[2], m->hd, a1, a2, P, 0.f, st));
+  STAGE("conv3", hn_launch_hardnet_conv(3, m->variant[3], m->hd, a2, a1, P, 0.f, st));
+  STAGE("conv4", hn_launch_hardnet_conv(4, m->variant[4], m->hd, a1, a2, P, 0.f, st));
+  STAGE("conv5", hn_launch_hardnet_conv(5, m->variant[5], m->hd, a2, a1, P, 0.f, st));
   STAGE("head", hn_launch_head(a1, out, m->hd.wpack[6], m->hd.bias[6], P, 8192, m->desc.l2_eps, st));
   return HN_OK;
 }

@@ -113,15 +113,32 @@ struct ConvCfg {
   }
 };
 
-template <int CIN, int COUT, int HIN, int S, int NP, int TR, int WM, int WN>
+// Blocks b, b+8, b+16, ... are dispatched to the same XCD (MI355X_MICROARCH.md, XCD
+// placement; a speed property only).  Give each XCD a contiguous range of tiles so the
+// row tiles of one patch -- which share halo rows -- hit the same L2.  Bijective for any
+// grid size (cdna_hip_programming.md T1).
+HN_DEV int xcd_remap(int bid, int nblocks) {
+  const int xcd = bid & 7, idx = bid >> 3;
+  const int q = nblocks >> 3, r = nblocks & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
+// STEM = true (conv1 only): `in` is the raw [P,1,32,32] patch batch; the kernel computes
+// input_norm (HardNet.py:306-310) and conv0+BN+ReLU (HardNet.py:281-283) for the window
+// rows it needs (VALU fp32, weights uniform -> scalar loads) straight into the LDS window,
+// so the 128 KB/patch a0 activation never touches HBM.
+template <int CIN, int COUT, int HIN, int S, int NP, int TR, int WM, int WN, bool STEM>
 __global__ __launch_bounds__(256) void k_conv3x3(const float* __restrict__ in, float* __restrict__ out,
                                                  const uint4* __restrict__ wp,
-                                                 const float* __restrict__ bias, int P) {
+                                                 const float* __restrict__ bias, int P,
+                                                 const float* __restrict__ stem_w,
+                                                 const float* __restrict__ stem_b, float eps) {
   using C = ConvCfg<CIN, COUT, HIN, S, NP, TR, WM, WN>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
-  const int pg = blockIdx.x / C::RT, rt = blockIdx.x % C::RT;
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int pg = tile / C::RT, rt = tile % C::RT;
   const int p0 = pg * NP, y0 = rt * TR;
   const int r = lane & 31, h = lane >> 5;
 
@@ -142,25 +159,89 @@ __global__ __launch_bounds__(256) void k_conv3x3(const float* __restrict__ in, f
 #pragma unroll 1
   for (int cc = 0; cc < C::NCC; ++cc) {
     if (cc) __syncthreads();
-    constexpr int UNITS = NP * C::RIN * C::NCOLS * 4;
-    for (int u = tid; u < UNITS; u += 256) {
-      const int g = u & 3, pix = u >> 2;
-      const int wc = pix % C::NCOLS, t2 = pix / C::NCOLS;
-      const int wr = t2 % C::RIN, np = t2 / C::RIN;
-      const int p = p0 + np, y = y0 * S - 1 + wr, x = wc - 1;
-      float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
-      if (p < P && y >= 0 && y < HIN && x >= 0 && x < HIN) {
-        const float4* src = reinterpret_cast<const float4*>(
-            in + (((size_t)p * HIN + y) * HIN + x) * CIN + cc * 32 + g * 8);
-        a = src[0];
-        b = src[1];
+    if constexpr (STEM) {
+      static_assert(CIN == 32 && HIN == 32 && S == 1 && NP == 1, "stem fusion is conv1-only");
+      float* pt = reinterpret_cast<float*>(smem + C::LDS);  // [34][34] normalised, zero ring
+      float* red = pt + 34 * 34;
+      const float4 v = reinterpret_cast<const float4*>(in + (size_t)p0 * 1024)[tid];
+      for (int i = tid; i < 34 * 34; i += 256) pt[i] = 0.f;
+      float mean = 0.f, sd = 1.f;
+      if (eps >= 0.f) {
+        const float s0 = wave_sum(v.x + v.y + v.z + v.w);
+        if (lane == 0) red[wave] = s0;
+        __syncthreads();
+        mean = (red[0] + red[1] + red[2] + red[3]) * (1.f / 1024.f);
+        const float d0 = v.x - mean, d1 = v.y - mean, d2 = v.z - mean, d3 = v.w - mean;
+        const float q = wave_sum(d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3);
+        if (lane == 0) red[4 + wave] = q;
+        __syncthreads();
+        sd = sqrtf((red[4] + red[5] + red[6] + red[7]) * (1.f / 1023.f)) + eps;
       }
-      uint4 hi, lo;
-      split8(a, b, hi, lo);
-      const int pc = (S == 1) ? wc : ((wc & 1) ? C::HALF + (wc >> 1) : (wc >> 1));
-      const int off = np * C::PS + wr * C::RS + pc * 80 + g * 16;
-      *reinterpret_cast<uint4*>(smem + off) = hi;
-      *reinterpret_cast<uint4*>(smem + C::PLANE + off) = lo;
+      __syncthreads();
+      {
+        const int q = 4 * tid, y = q >> 5, x = q & 31;
+        float* d = pt + (y + 1) * 34 + x + 1;
+        d[0] = (v.x - mean) / sd; d[1] = (v.y - mean) / sd;
+        d[2] = (v.z - mean) / sd; d[3] = (v.w - mean) / sd;
+      }
+      __syncthreads();
+      constexpr int NPIX = C::RIN * C::NCOLS;
+      for (int u = tid; u < NPIX; u += 256) {
+        const int wr = u / C::NCOLS, wc = u % C::NCOLS;
+        const int y = y0 - 1 + wr, x = wc - 1;
+        char* dst = smem + wr * C::RS + wc * 80;
+        if (y >= 0 && y < 32 && x >= 0 && x < 32) {
+          float xin[9];
+#pragma unroll
+          for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+            for (int kx = 0; kx < 3; ++kx) xin[ky * 3 + kx] = pt[(y + ky) * 34 + x + kx];
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            float a[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              const int c = g * 8 + j;
+              float s0 = 0.f;
+#pragma unroll
+              for (int tp = 0; tp < 9; ++tp) s0 = fmaf(xin[tp], stem_w[tp * 32 + c], s0);
+              a[j] = fmaxf(s0 + stem_b[c], 0.f);
+            }
+            uint4 hi, lo;
+            split8(make_float4(a[0], a[1], a[2], a[3]), make_float4(a[4], a[5], a[6], a[7]), hi, lo);
+            *reinterpret_cast<uint4*>(dst + g * 16) = hi;
+            *reinterpret_cast<uint4*>(dst + C::PLANE + g * 16) = lo;
+          }
+        } else {
+          const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            *reinterpret_cast<uint4*>(dst + g * 16) = z;
+            *reinterpret_cast<uint4*>(dst + C::PLANE + g * 16) = z;
+          }
+        }
+      }
+    } else {
+      constexpr int UNITS = NP * C::RIN * C::NCOLS * 4;
+      for (int u = tid; u < UNITS; u += 256) {
+        const int g = u & 3, pix = u >> 2;
+        const int wc = pix % C::NCOLS, t2 = pix / C::NCOLS;
+        const int wr = t2 % C::RIN, np = t2 / C::RIN;
+        const int p = p0 + np, y = y0 * S - 1 + wr, x = wc - 1;
+        float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+        if (p < P && y >= 0 && y < HIN && x >= 0 && x < HIN) {
+          const float4* src = reinterpret_cast<const float4*>(
+              in + (((size_t)p * HIN + y) * HIN + x) * CIN + cc * 32 + g * 8);
+          a = src[0];
+          b = src[1];
+        }
+        uint4 hi, lo;
+        split8(a, b, hi, lo);
+        const int pc = (S == 1) ? wc : ((wc & 1) ? C::HALF + (wc >> 1) : (wc >> 1));
+        const int off = np * C::PS + wr * C::RS + pc * 80 + g * 16;
+        *reinterpret_cast<uint4*>(smem + off) = hi;
+        *reinterpret_cast<uint4*>(smem + C::PLANE + off) = lo;
+      }
     }
     __syncthreads();
     const uint4* wcc = wp + (size_t)cc * 9 * 2 * C::NTOT * 2 * 64;
@@ -268,40 +349,43 @@ __global__ __launch_bounds__(256) void k_head(const float* __restrict__ a, float
 // ------------------------------------------------------------------------------------
 // host launchers
 // ------------------------------------------------------------------------------------
-#define HN_CONV(NAME, CIN, COUT, HIN, S, NP, TR, WM, WN)                                   \
+// stem-fused kernels carry the normalised patch (34x34 fp32) + 8 reduction floats
+template <class CFG, bool STEM>
+constexpr int conv_lds() { return CFG::LDS + (STEM ? (34 * 34 + 8) * 4 : 0); }
+
+#define HN_CONV(NAME, STEM, CIN, COUT, HIN, S, NP, TR, WM, WN)                             \
   using NAME##_cfg = ConvCfg<CIN, COUT, HIN, S, NP, TR, WM, WN>;                           \
   static hipError_t NAME(const float* in, float* out, const void* wp, const float* bias,   \
-                         int P, hipStream_t st) {                                          \
+                         int P, const float* sw, const float* sb, float eps,               \
+                         hipStream_t st) {                                                 \
+    constexpr int lds = conv_lds<NAME##_cfg, STEM>();                                      \
+    static bool attr = false;                                                              \
+    if (!attr) {                                                                           \
+      hipError_t e = hipFuncSetAttribute(                                                  \
+          reinterpret_cast<const void*>(&k_conv3x3<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM>), \
+          hipFuncAttributeMaxDynamicSharedMemorySize, lds);                                \
+      if (e != hipSuccess) return e;                                                       \
+      attr = true;                                                                         \
+    }                                                                                      \
     const int grid = (P + NP - 1) / NP * NAME##_cfg::RT;                                   \
-    hipLaunchKernelGGL((k_conv3x3<CIN, COUT, HIN, S, NP, TR, WM, WN>), dim3(grid),         \
-                       dim3(256), NAME##_cfg::LDS, st, in, out,                            \
-                       static_cast<const uint4*>(wp), bias, P);                            \
+    hipLaunchKernelGGL((k_conv3x3<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM>), dim3(grid),   \
+                       dim3(256), lds, st, in, out, static_cast<const uint4*>(wp), bias, P, \
+                       sw, sb, eps);                                                       \
     return hipGetLastError();                                                              \
   }
 
-HN_CONV(conv1_launch, 32, 32, 32, 1, 1, 8, 4, 1)
-HN_CONV(conv2_launch, 32, 64, 32, 2, 1, 8, 2, 2)
-HN_CONV(conv3_launch, 64, 64, 16, 1, 1, 16, 2, 2)
-HN_CONV(conv4_launch, 64, 128, 16, 2, 1, 8, 1, 4)
-HN_CONV(conv5_launch, 128, 128, 8, 1, 2, 8, 1, 4)
-
-static bool g_attr_done = false;
-static hipError_t set_attrs() {
-  if (g_attr_done) return hipSuccess;
-  hipError_t e;
-#define HN_ATTR(CFG, ...)                                                                   \
-  e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_conv3x3<__VA_ARGS__>),           \
-                          hipFuncAttributeMaxDynamicSharedMemorySize, CFG::LDS);            \
-  if (e != hipSuccess) return e;
-  HN_ATTR(conv1_launch_cfg, 32, 32, 32, 1, 1, 8, 4, 1)
-  HN_ATTR(conv2_launch_cfg, 32, 64, 32, 2, 1, 8, 2, 2)
-  HN_ATTR(conv3_launch_cfg, 64, 64, 16, 1, 1, 16, 2, 2)
-  HN_ATTR(conv4_launch_cfg, 64, 128, 16, 2, 1, 8, 1, 4)
-  HN_ATTR(conv5_launch_cfg, 128, 128, 8, 1, 2, 8, 1, 4)
-#undef HN_ATTR
-  g_attr_done = true;
-  return hipSuccess;
-}
+// variant 0 = default tiling; variant 1 = smaller LDS footprint / more workgroups per CU
+HN_CONV(conv1s_launch, true, 32, 32, 32, 1, 1, 8, 4, 1)
+HN_CONV(conv1s_v1, true, 32, 32, 32, 1, 1, 4, 4, 1)
+HN_CONV(conv1_launch, false, 32, 32, 32, 1, 1, 8, 4, 1)
+HN_CONV(conv2_launch, false, 32, 64, 32, 2, 1, 8, 2, 2)
+HN_CONV(conv2_v1, false, 32, 64, 32, 2, 1, 4, 2, 2)
+HN_CONV(conv3_launch, false, 64, 64, 16, 1, 1, 16, 2, 2)
+HN_CONV(conv3_v1, false, 64, 64, 16, 1, 1, 8, 2, 2)
+HN_CONV(conv4_launch, false, 64, 128, 16, 2, 1, 8, 1, 4)
+HN_CONV(conv4_v1, false, 64, 128, 16, 2, 1, 4, 1, 4)
+HN_CONV(conv5_launch, false, 128, 128, 8, 1, 2, 8, 1, 4)
+HN_CONV(conv5_v1, false, 128, 128, 8, 1, 1, 8, 1, 4)
 
 hipError_t hn_launch_stem(const float* in, float* out, const float* w, const float* b, int P,
                           bool norm, float eps, hipStream_t st) {
@@ -312,16 +396,23 @@ hipError_t hn_launch_stem(const float* in, float* out, const float* w, const flo
   return hipGetLastError();
 }
 
-hipError_t hn_launch_hardnet_conv(int layer, const HardnetDev& d, const float* in, float* out,
-                                  int P, hipStream_t st) {
-  hipError_t e = set_attrs();
-  if (e != hipSuccess) return e;
+// layer 0 = fused stem (input_norm + conv0) + conv1 from the raw patches
+hipError_t hn_launch_hardnet_conv(int layer, int variant, const HardnetDev& d, const float* in,
+                                  float* out, int P, float eps, hipStream_t st) {
+  const bool v1 = variant == 1;
   switch (layer) {
-    case 1: return conv1_launch(in, out, d.wpack[1], d.bias[1], P, st);
-    case 2: return conv2_launch(in, out, d.wpack[2], d.bias[2], P, st);
-    case 3: return conv3_launch(in, out, d.wpack[3], d.bias[3], P, st);
-    case 4: return conv4_launch(in, out, d.wpack[4], d.bias[4], P, st);
-    case 5: return conv5_launch(in, out, d.wpack[5], d.bias[5], P, st);
+    case 0:
+      return (v1 ? conv1s_v1 : conv1s_launch)(in, out, d.wpack[1], d.bias[1], P, d.stem_w,
+                                               d.stem_b, eps, st);
+    case 1: return conv1_launch(in, out, d.wpack[1], d.bias[1], P, nullptr, nullptr, 0.f, st);
+    case 2:
+      return (v1 ? conv2_v1 : conv2_launch)(in, out, d.wpack[2], d.bias[2], P, nullptr, nullptr, 0.f, st);
+    case 3:
+      return (v1 ? conv3_v1 : conv3_launch)(in, out, d.wpack[3], d.bias[3], P, nullptr, nullptr, 0.f, st);
+    case 4:
+      return (v1 ? conv4_v1 : conv4_launch)(in, out, d.wpack[4], d.bias[4], P, nullptr, nullptr, 0.f, st);
+    case 5:
+      return (v1 ? conv5_v1 : conv5_launch)(in, out, d.wpack[5], d.bias[5], P, nullptr, nullptr, 0.f, st);
   }
   return hipErrorInvalidValue;
 }

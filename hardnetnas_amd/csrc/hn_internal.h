@@ -12,8 +12,8 @@ struct HardnetDev {
 
 hipError_t hn_launch_stem(const float* in, float* out, const float* w, const float* b, int P,
                           bool norm, float eps, hipStream_t st);
-hipError_t hn_launch_hardnet_conv(int layer, const HardnetDev& d, const float* in, float* out,
-                                  int P, hipStream_t st);
+hipError_t hn_launch_hardnet_conv(int layer, int variant, const HardnetDev& d, const float* in,
+                                  float* out, int P, float eps, hipStream_t st);
 hipError_t hn_launch_head(const float* a, float* out, const void* wp, const float* bias, int P,
                           int K, float l2eps, hipStream_t st);
 int hn_conv_lds_bytes(int layer);

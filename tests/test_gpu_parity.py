@@ -78,6 +78,25 @@ def test_chunked_forward_equals_unchunked(name, cuda_device, monkeypatch):
     assert torch.equal(full, chunked)
 
 
+@pytest.mark.parametrize("variant", ["111111", "010101", "101010"])
+def test_tiling_variants_match_reference(variant, cuda_device, monkeypatch):
+    from hardnetnas_amd._native import NativeModel
+    m, fx, _ = build_module("hardnet")
+    monkeypatch.setenv("HN_VARIANT", variant)
+    x = torch.from_numpy(golden_inputs(fx)).to(cuda_device)
+    y = NativeModel.from_module(m, cuda_device)(x).cpu().numpy()
+    assert np.abs(y - fx["y"]).max() <= TOL["hardnet"]
+
+
+def test_unfused_stem_matches(cuda_device, monkeypatch):
+    from hardnetnas_amd._native import NativeModel
+    m, fx, _ = build_module("hardnet")
+    monkeypatch.setenv("HN_UNFUSED_STEM", "1")
+    x = torch.from_numpy(golden_inputs(fx)).to(cuda_device)
+    y = NativeModel.from_module(m, cuda_device)(x).cpu().numpy()
+    assert np.abs(y - fx["y"]).max() <= TOL["hardnet"]
+
+
 def test_deterministic_and_batch_independent(cuda_device):
     m, fx, _ = build_module("hardnet")
     m = m.to(cuda_device)

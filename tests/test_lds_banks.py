@@ -13,11 +13,16 @@ GROUPS += [[l + 32 for l in g] for g in GROUPS]
 
 # (CIN, COUT, HIN, S, NP, TR, WM, WN) -- the HN_CONV instantiations
 CONFIGS = {
-    1: (32, 32, 32, 1, 1, 8, 4, 1),
-    2: (32, 64, 32, 2, 1, 8, 2, 2),
-    3: (64, 64, 16, 1, 1, 16, 2, 2),
-    4: (64, 128, 16, 2, 1, 8, 1, 4),
-    5: (128, 128, 8, 1, 2, 8, 1, 4),
+    "1": (32, 32, 32, 1, 1, 8, 4, 1),
+    "1v1": (32, 32, 32, 1, 1, 4, 4, 1),
+    "2": (32, 64, 32, 2, 1, 8, 2, 2),
+    "2v1": (32, 64, 32, 2, 1, 4, 2, 2),
+    "3": (64, 64, 16, 1, 1, 16, 2, 2),
+    "3v1": (64, 64, 16, 1, 1, 8, 2, 2),
+    "4": (64, 128, 16, 2, 1, 8, 1, 4),
+    "4v1": (64, 128, 16, 2, 1, 4, 1, 4),
+    "5": (128, 128, 8, 1, 2, 8, 1, 4),
+    "5v1": (128, 128, 8, 1, 1, 8, 1, 4),
 }
 
 
