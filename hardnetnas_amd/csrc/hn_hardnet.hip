@@ -13,6 +13,8 @@
 #include "hn_common.h"
 #include "hn_internal.h"
 
+#include <cstdlib>
+
 // ------------------------------------------------------------------------------------
 // stem
 // ------------------------------------------------------------------------------------
@@ -132,7 +134,8 @@ __global__ __launch_bounds__(256) void k_conv3x3(const float* __restrict__ in, f
                                                  const uint4* __restrict__ wp,
                                                  const float* __restrict__ bias, int P,
                                                  const float* __restrict__ stem_w,
-                                                 const float* __restrict__ stem_b, float eps) {
+                                                 const float* __restrict__ stem_b, float eps,
+                                                 int dbg) {
   using C = ConvCfg<CIN, COUT, HIN, S, NP, TR, WM, WN>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -185,53 +188,73 @@ __global__ __launch_bounds__(256) void k_conv3x3(const float* __restrict__ in, f
         d[2] = (v.z - mean) / sd; d[3] = (v.w - mean) / sd;
       }
       __syncthreads();
+      // conv0 on the MFMA: C[32 ch][32 px] = W0^T[32 ch][16 taps] x X[16 taps][32 px]
+      // (taps 9..15 zero), bf16x3.  Lane (r, h) then owns 16 channels of window pixel r.
       constexpr int NPIX = C::RIN * C::NCOLS;
-      for (int u = tid; u < NPIX; u += 256) {
-        const int wr = u / C::NCOLS, wc = u % C::NCOLS;
+      constexpr int NT0 = (NPIX + 31) / 32;
+      bf16x8 w0h, w0l;
+      float b16[16];
+      {
+        __bf16 hh[8], ll[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int tap = 8 * h + j;
+          split_bf16(tap < 9 ? stem_w[tap * 32 + r] : 0.f, hh[j], ll[j]);
+        }
+        w0h = *reinterpret_cast<const bf16x8*>(hh);
+        w0l = *reinterpret_cast<const bf16x8*>(ll);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) b16[i] = stem_b[(i & 3) + 8 * (i >> 2) + 4 * h];
+      }
+#pragma unroll 1
+      for (int t = wave; t < NT0; t += 4) {
+        const int pix = t * 32 + r;
+        const int wr = pix / C::NCOLS, wc = pix % C::NCOLS;
         const int y = y0 - 1 + wr, x = wc - 1;
-        char* dst = smem + wr * C::RS + wc * 80;
-        if (y >= 0 && y < 32 && x >= 0 && x < 32) {
-          float xin[9];
+        const bool inside = pix < NPIX && (unsigned)y < 32u && (unsigned)x < 32u;
+        const int yc = inside ? y : 0, xc = inside ? x : 0;
+        __bf16 xh[8], xl[8];
 #pragma unroll
-          for (int ky = 0; ky < 3; ++ky)
+        for (int j = 0; j < 8; ++j) {
+          const int tap = 8 * h + j;
+          const float v = tap < 9 ? pt[(yc + tap / 3) * 34 + xc + tap % 3] : 0.f;
+          split_bf16(v, xh[j], xl[j]);
+        }
+        const f32x16 c0 = mfma3(w0h, w0l, *reinterpret_cast<const bf16x8*>(xh),
+                                *reinterpret_cast<const bf16x8*>(xl), f32x16{});
+        if (pix < NPIX) {
+          char* dst = smem + wr * C::RS + wc * 80 + 8 * h;
 #pragma unroll
-            for (int kx = 0; kx < 3; ++kx) xin[ky * 3 + kx] = pt[(y + ky) * 34 + x + kx];
+          for (int q = 0; q < 4; ++q) {  // channels 8q + 4h + {0..3}
+            __bf16 oh[4], ol[4];
 #pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            float a[8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-              const int c = g * 8 + j;
-              float s0 = 0.f;
-#pragma unroll
-              for (int tp = 0; tp < 9; ++tp) s0 = fmaf(xin[tp], stem_w[tp * 32 + c], s0);
-              a[j] = fmaxf(s0 + stem_b[c], 0.f);
+            for (int j = 0; j < 4; ++j) {
+              const float v = inside ? fmaxf(c0[4 * q + j] + b16[4 * q + j], 0.f) : 0.f;
+              split_bf16(v, oh[j], ol[j]);
             }
-            uint4 hi, lo;
-            split8(make_float4(a[0], a[1], a[2], a[3]), make_float4(a[4], a[5], a[6], a[7]), hi, lo);
-            *reinterpret_cast<uint4*>(dst + g * 16) = hi;
-            *reinterpret_cast<uint4*>(dst + C::PLANE + g * 16) = lo;
-          }
-        } else {
-          const uint4 z = make_uint4(0u, 0u, 0u, 0u);
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            *reinterpret_cast<uint4*>(dst + g * 16) = z;
-            *reinterpret_cast<uint4*>(dst + C::PLANE + g * 16) = z;
+            *reinterpret_cast<uint2*>(dst + 16 * q) = *reinterpret_cast<const uint2*>(oh);
+            *reinterpret_cast<uint2*>(dst + C::PLANE + 16 * q) = *reinterpret_cast<const uint2*>(ol);
           }
         }
       }
     } else {
+      // unit = (window pixel, 8-channel group); thread's units are tid + 256*k.  The
+      // window coordinates advance incrementally (no per-unit division); offsets are
+      // 32-bit relative to the tile's first patch.
       constexpr int UNITS = NP * C::RIN * C::NCOLS * 4;
+      constexpr int DPIX = 256 / 4;                        // pixels advanced per iteration
+      constexpr int DWC = DPIX % C::NCOLS, DWR = DPIX / C::NCOLS;
+      const float* pin = in + (size_t)p0 * HIN * HIN * CIN + cc * 32;
+      const int g = tid & 3;
+      int wc = (tid >> 2) % C::NCOLS, wr = (tid >> 2) / C::NCOLS, np = 0;
+      while (wr >= C::RIN) { wr -= C::RIN; ++np; }
+#pragma unroll 2
       for (int u = tid; u < UNITS; u += 256) {
-        const int g = u & 3, pix = u >> 2;
-        const int wc = pix % C::NCOLS, t2 = pix / C::NCOLS;
-        const int wr = t2 % C::RIN, np = t2 / C::RIN;
-        const int p = p0 + np, y = y0 * S - 1 + wr, x = wc - 1;
+        const int y = y0 * S - 1 + wr, x = wc - 1;
         float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
-        if (p < P && y >= 0 && y < HIN && x >= 0 && x < HIN) {
-          const float4* src = reinterpret_cast<const float4*>(
-              in + (((size_t)p * HIN + y) * HIN + x) * CIN + cc * 32 + g * 8);
+        if ((NP == 1 || p0 + np < P) && (unsigned)y < (unsigned)HIN && (unsigned)x < (unsigned)HIN) {
+          const float4* src =
+              reinterpret_cast<const float4*>(pin + ((np * HIN + y) * HIN + x) * CIN + g * 8);
           a = src[0];
           b = src[1];
         }
@@ -241,52 +264,84 @@ __global__ __launch_bounds__(256) void k_conv3x3(const float* __restrict__ in, f
         const int off = np * C::PS + wr * C::RS + pc * 80 + g * 16;
         *reinterpret_cast<uint4*>(smem + off) = hi;
         *reinterpret_cast<uint4*>(smem + C::PLANE + off) = lo;
+        wc += DWC;
+        wr += DWR;
+        if (wc >= C::NCOLS) { wc -= C::NCOLS; ++wr; }
+        while (wr >= C::RIN) { wr -= C::RIN; ++np; }
       }
     }
     __syncthreads();
+    // 18 k-steps (9 taps x 2 halves of the 32-channel chunk), software-pipelined:
+    // B fragments (global/L2) are loaded 2 steps ahead, A fragments (LDS) 1 step ahead.
     const uint4* wcc = wp + (size_t)cc * 9 * 2 * C::NTOT * 2 * 64;
+    constexpr int NKS = 18;
+    uint4 bq[3][C::NT][2];
+    uint4 aq[2][C::MT][2];
+    auto load_b = [&](int ksx, uint4 (&dst)[C::NT][2]) {
 #pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const int ky = tap / 3, kx = tap % 3;
-        const int toff = ky * C::RS + C::colofs(kx) * 80 + ks * 32;
-        bf16x8 bh[C::NT], bl[C::NT];
-#pragma unroll
-        for (int nt = 0; nt < C::NT; ++nt) {
-          const int idx = (((tap * 2 + ks) * C::NTOT + wn * C::NT + nt) * 2) * 64 + lane;
-          bh[nt] = as_bf16x8(wcc[idx]);
-          bl[nt] = as_bf16x8(wcc[idx + 64]);
-        }
-#pragma unroll
-        for (int mt = 0; mt < C::MT; ++mt) {
-          const bf16x8 ah = as_bf16x8(*reinterpret_cast<const uint4*>(smem + abase[mt] + toff));
-          const bf16x8 al =
-              as_bf16x8(*reinterpret_cast<const uint4*>(smem + C::PLANE + abase[mt] + toff));
-#pragma unroll
-          for (int nt = 0; nt < C::NT; ++nt) acc[mt][nt] = mfma3(ah, al, bh[nt], bl[nt], acc[mt][nt]);
-        }
+      for (int nt = 0; nt < C::NT; ++nt) {
+        const int idx = ((ksx * C::NTOT + wn * C::NT + nt) * 2) * 64 + lane;
+        dst[nt][0] = wcc[idx];
+        dst[nt][1] = wcc[idx + 64];
       }
+    };
+    auto load_a = [&](int ksx, uint4 (&dst)[C::MT][2]) {
+      const int tap = ksx >> 1, ks = ksx & 1;
+      const int toff = (tap / 3) * C::RS + C::colofs(tap % 3) * 80 + ks * 32;
+#pragma unroll
+      for (int mt = 0; mt < C::MT; ++mt) {
+        dst[mt][0] = *reinterpret_cast<const uint4*>(smem + abase[mt] + toff);
+        dst[mt][1] = *reinterpret_cast<const uint4*>(smem + C::PLANE + abase[mt] + toff);
+      }
+    };
+    load_b(0, bq[0]);
+    load_b(1, bq[1]);
+    load_a(0, aq[0]);
+#pragma unroll
+    for (int ksx = 0; ksx < NKS; ++ksx) {
+      if (ksx + 2 < NKS) load_b(ksx + 2, bq[(ksx + 2) % 3]);
+      if (ksx + 1 < NKS) load_a(ksx + 1, aq[(ksx + 1) & 1]);
+      // pin the issue order: hipcc otherwise sinks the prefetches next to their use
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int mt = 0; mt < C::MT; ++mt) {
+        const bf16x8 ah = as_bf16x8(aq[ksx & 1][mt][0]), al = as_bf16x8(aq[ksx & 1][mt][1]);
+#pragma unroll
+        for (int nt = 0; nt < C::NT; ++nt)
+          acc[mt][nt] = mfma3(ah, al, as_bf16x8(bq[ksx % 3][nt][0]), as_bf16x8(bq[ksx % 3][nt][1]),
+                              acc[mt][nt]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
 
-  // epilogue: + folded-BN bias, ReLU, NHWC fp32 store
+  // epilogue: + folded-BN bias, ReLU, NHWC fp32 store.  Tiles cover whole output rows
+  // (and whole patches when NP > 1), so tile row m is output pixel (p0*HOUT + y0)*WOUT + m
+  // and every (mt, nt, i) offset from the lane's base pointer is a compile-time constant.
+  float* obase = out + ((size_t)(p0 * C::HOUT + y0) * C::WOUT + wm * C::MT * 32 + 4 * h) * COUT +
+                 wn * C::NT * 32 + r;
+  if (dbg & 1) {  // ablation: keep the accumulators live, one store per lane instead of 16*MT*NT
+    float sum = 0.f;
 #pragma unroll
-  for (int nt = 0; nt < C::NT; ++nt) {
-    const int n = (wn * C::NT + nt) * 32 + r;
-    const float bv = bias[n];
+    for (int mt = 0; mt < C::MT; ++mt)
 #pragma unroll
-    for (int mt = 0; mt < C::MT; ++mt) {
+      for (int nt = 0; nt < C::NT; ++nt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sum += acc[mt][nt][i];
+    obase[0] = sum;
+    return;
+  }
+#pragma unroll
+  for (int mt = 0; mt < C::MT; ++mt) {
+    const bool ok = NP == 1 || p0 + ((wm * C::MT + mt) * 32) / (TR * C::WOUT) < P;
+    if (!ok) continue;
+#pragma unroll
+    for (int nt = 0; nt < C::NT; ++nt) {
+      const float bv = bias[(wn * C::NT + nt) * 32 + r];
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const int row = (i & 3) + 8 * (i >> 2) + 4 * h;
-        const int m = (wm * C::MT + mt) * 32 + row;
-        const int np = m / (TR * C::WOUT), rem = m % (TR * C::WOUT);
-        const int yl = rem / C::WOUT, xo = rem % C::WOUT;
-        const int p = p0 + np;
-        if (p < P)
-          out[(((size_t)p * C::HOUT + y0 + yl) * C::WOUT + xo) * COUT + n] =
-              fmaxf(acc[mt][nt][i] + bv, 0.f);
+        const int row = (i & 3) + 8 * (i >> 2);
+        obase[(mt * 32 + row) * COUT + nt * 32] = fmaxf(acc[mt][nt][i] + bv, 0.f);
       }
     }
   }
@@ -349,6 +404,15 @@ __global__ __launch_bounds__(256) void k_head(const float* __restrict__ a, float
 // ------------------------------------------------------------------------------------
 // host launchers
 // ------------------------------------------------------------------------------------
+static int g_dbg = -1;  // HN_DEBUG bits: 1 = skip conv epilogue stores (ablation only)
+static int dbg_flags() {
+  if (g_dbg < 0) {
+    const char* e = std::getenv("HN_DEBUG");
+    g_dbg = e ? std::atoi(e) : 0;
+  }
+  return g_dbg;
+}
+
 // stem-fused kernels carry the normalised patch (34x34 fp32) + 8 reduction floats
 template <class CFG, bool STEM>
 constexpr int conv_lds() { return CFG::LDS + (STEM ? (34 * 34 + 8) * 4 : 0); }
@@ -368,9 +432,10 @@ constexpr int conv_lds() { return CFG::LDS + (STEM ? (34 * 34 + 8) * 4 : 0); }
       attr = true;                                                                         \
     }                                                                                      \
     const int grid = (P + NP - 1) / NP * NAME##_cfg::RT;                                   \
+    (void)dbg_flags();                                                                     \
     hipLaunchKernelGGL((k_conv3x3<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM>), dim3(grid),   \
                        dim3(256), lds, st, in, out, static_cast<const uint4*>(wp), bias, P, \
-                       sw, sb, eps);                                                       \
+                       sw, sb, eps, g_dbg);                                                \
     return hipGetLastError();                                                              \
   }
 
