@@ -47,11 +47,39 @@ PEAK_FP32 = 157.3                 # TFLOP/s f32 (vector == f32 MFMA)
 PEAK_HBM = 8000.0                 # GB/s
 
 # algorithmic work per patch of each HardNet stage
-HARDNET_STAGE_MAC = {"stem": 294912, "conv1": 9437184, "conv2": 4718592, "conv3": 9437184,
-                     "conv4": 4718592, "conv5": 9437184, "head": 1048576}
-HARDNET_STAGE_BYTES = {"stem": 4096 + 131072, "conv1": 2 * 131072, "conv2": 131072 + 65536,
-                       "conv3": 2 * 65536, "conv4": 65536 + 32768, "conv5": 2 * 32768,
-                       "head": 32768 + 512}
+HARDNET_STAGE_MAC = {"stem": 294912, "conv1": 9437184, "stem+conv1": 294912 + 9437184,
+                     "conv2": 4718592, "conv3": 9437184, "conv4": 4718592, "conv5": 9437184,
+                     "head": 1048576}
+HARDNET_STAGE_BYTES = {"stem": 4096 + 131072, "conv1": 2 * 131072, "stem+conv1": 4096 + 131072,
+                       "conv2": 131072 + 65536, "conv3": 2 * 65536, "conv4": 65536 + 32768,
+                       "conv5": 2 * 32768, "head": 32768 + 512}
+
+
+def nas_stage_bytes(ops) -> dict:
+    """Algorithmic HBM bytes per patch of each NAS stage class, summed over its launches in
+    one forward (fp32 NHWC in + out (+ residual read)), mirroring hn_api.hip::forward_nas."""
+    out = {"stem": 4096 + 32 * 32 * 32 * 4, "pw": 0, "dw": 0, "pwl": 0, "maxpool": 0, "se": 0,
+           "head": 0}
+    hw = 32
+    for op, (ci, co, s) in zip(A.arch_ops(ops), A.SEARCH_SPACE2):
+        spec = A.OP_SPECS[op]
+        ho = hw // s
+        if spec.kind == "skip":
+            if s == 2:
+                out["maxpool"] += 4 * (ci * hw * hw + ci * ho * ho)
+            if ci != co:
+                out["pw"] += 4 * (ci * ho * ho + co * ho * ho)
+        else:
+            mid = A.ir_mid(ci, spec.expansion)
+            out["pw"] += 4 * (ci * hw * hw + mid * hw * hw)
+            out["dw"] += 4 * (mid * hw * hw + mid * ho * ho)
+            res = (s == 1 and ci == co)
+            out["pwl"] += 4 * (mid * ho * ho + co * ho * ho + (co * ho * ho if res else 0))
+            if spec.se:
+                out["se"] += 4 * 2 * co * ho * ho
+        hw = ho
+    out["head"] = 4 * (A.SEARCH_SPACE2[-1][1] * 16 + 2 * 128)
+    return out
 
 
 def build_model(name: str):
@@ -195,9 +223,12 @@ def main():
             unit = "TFLOP/s"
             alg = HARDNET_STAGE_BYTES[dom] * patches_per_launch
         else:
-            alg = None
+            # NAS: HBM-bound fp32 kernels; a stage class aggregates its launches (e.g. every
+            # pw of the 6 blocks), so use its summed algorithmic bytes / summed device time
+            per_patch = nas_stage_bytes(args.model).get(dom, 0)
+            alg = per_patch * b / launches_per_step
             bound, peak, unit = "hbm", PEAK_HBM, "GB/s"
-            achieved = None
+            achieved = per_patch * b * args.steps / (dom_ms * 1e-3) / 1e9
         traffic = read_traffic(args.model, dom)
         roof = {"bound": bound, "kernel": dom,
                 "achieved": round(achieved, 2) if achieved is not None else None,

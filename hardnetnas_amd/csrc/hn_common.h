@@ -18,18 +18,36 @@ HN_DEV void split_bf16(float x, __bf16& hi, __bf16& lo) {
   lo = (__bf16)(x - (float)hi);
 }
 
-// 8 fp32 -> 8 bf16 hi + 8 bf16 lo packed as two 16-byte vectors.
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+// 8 fp32 -> 8 bf16 hi + 8 bf16 lo packed as two 16-byte vectors.  Built as vector
+// elements (no local arrays + pointer casts, which hipcc can leave in scratch).
 HN_DEV void split8(const float4& a, const float4& b, uint4& hi, uint4& lo) {
-  __bf16 h[8], l[8];
-  split_bf16(a.x, h[0], l[0]); split_bf16(a.y, h[1], l[1]);
-  split_bf16(a.z, h[2], l[2]); split_bf16(a.w, h[3], l[3]);
-  split_bf16(b.x, h[4], l[4]); split_bf16(b.y, h[5], l[5]);
-  split_bf16(b.z, h[6], l[6]); split_bf16(b.w, h[7], l[7]);
-  hi = *reinterpret_cast<const uint4*>(h);
-  lo = *reinterpret_cast<const uint4*>(l);
+  const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  bf16x8 h, l;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    h[j] = (__bf16)v[j];
+    l[j] = (__bf16)(v[j] - (float)h[j]);
+  }
+  hi = __builtin_bit_cast(uint4, h);
+  lo = __builtin_bit_cast(uint4, l);
 }
 
 HN_DEV bf16x8 as_bf16x8(const uint4& v) { return __builtin_bit_cast(bf16x8, v); }
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// Buffer resource over [base, base + bytes): the descriptor lives in SGPRs, loads take a
+// per-lane byte offset (one VGPR) plus a wave-uniform soffset/immediate, so unrolled
+// K-loops do not keep one 64-bit address per load live (cdna_hip_programming.md T8/T20).
+HN_DEV __amdgpu_buffer_rsrc_t make_rsrc(const void* base, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+HN_DEV uint4 buf_load16(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff) {
+  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
 
 HN_DEV f32x16 mfma3(const bf16x8& ah, const bf16x8& al, const bf16x8& bh, const bf16x8& bl,
                     f32x16 acc) {

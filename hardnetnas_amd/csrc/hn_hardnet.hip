@@ -13,6 +13,7 @@
 #include "hn_common.h"
 #include "hn_internal.h"
 
+#include <algorithm>
 #include <cstdlib>
 
 // ------------------------------------------------------------------------------------
@@ -106,7 +107,7 @@ struct ConvCfg {
   static constexpr int PS = RIN * RS;
   static constexpr int PLANE = NP * PS;
   static constexpr int LDS = 2 * PLANE;
-  static_assert(WM * WN == 4, "4 waves");
+  static_assert(WM * WN == 2 || WM * WN == 4 || WM * WN == 8, "2/4/8 waves");
   static_assert(MT >= 1 && NT >= 1 && MT * WM * 32 == BM && NT * WN * 32 == COUT, "tiling");
   static_assert(NP == 1 || TR == HOUT, "multi-patch tiles cover whole patches");
   static_assert((TR * WOUT) % 32 == 0, "M tiles stay inside one patch");
@@ -195,14 +196,13 @@ __global__ __launch_bounds__(256) void k_conv3x3(const float* __restrict__ in, f
       bf16x8 w0h, w0l;
       float b16[16];
       {
-        __bf16 hh[8], ll[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int tap = 8 * h + j;
-          split_bf16(tap < 9 ? stem_w[tap * 32 + r] : 0.f, hh[j], ll[j]);
+          const float v = tap < 9 ? stem_w[tap * 32 + r] : 0.f;
+          w0h[j] = (__bf16)v;
+          w0l[j] = (__bf16)(v - (float)w0h[j]);
         }
-        w0h = *reinterpret_cast<const bf16x8*>(hh);
-        w0l = *reinterpret_cast<const bf16x8*>(ll);
 #pragma unroll
         for (int i = 0; i < 16; ++i) b16[i] = stem_b[(i & 3) + 8 * (i >> 2) + 4 * h];
       }
@@ -213,27 +213,28 @@ __global__ __launch_bounds__(256) void k_conv3x3(const float* __restrict__ in, f
         const int y = y0 - 1 + wr, x = wc - 1;
         const bool inside = pix < NPIX && (unsigned)y < 32u && (unsigned)x < 32u;
         const int yc = inside ? y : 0, xc = inside ? x : 0;
-        __bf16 xh[8], xl[8];
+        bf16x8 xh, xl;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int tap = 8 * h + j;
           const float v = tap < 9 ? pt[(yc + tap / 3) * 34 + xc + tap % 3] : 0.f;
-          split_bf16(v, xh[j], xl[j]);
+          xh[j] = (__bf16)v;
+          xl[j] = (__bf16)(v - (float)xh[j]);
         }
-        const f32x16 c0 = mfma3(w0h, w0l, *reinterpret_cast<const bf16x8*>(xh),
-                                *reinterpret_cast<const bf16x8*>(xl), f32x16{});
+        const f32x16 c0 = mfma3(w0h, w0l, xh, xl, f32x16{});
         if (pix < NPIX) {
           char* dst = smem + wr * C::RS + wc * 80 + 8 * h;
 #pragma unroll
           for (int q = 0; q < 4; ++q) {  // channels 8q + 4h + {0..3}
-            __bf16 oh[4], ol[4];
+            bf16x4 oh, ol;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
               const float v = inside ? fmaxf(c0[4 * q + j] + b16[4 * q + j], 0.f) : 0.f;
-              split_bf16(v, oh[j], ol[j]);
+              oh[j] = (__bf16)v;
+              ol[j] = (__bf16)(v - (float)oh[j]);
             }
-            *reinterpret_cast<uint2*>(dst + 16 * q) = *reinterpret_cast<const uint2*>(oh);
-            *reinterpret_cast<uint2*>(dst + C::PLANE + 16 * q) = *reinterpret_cast<const uint2*>(ol);
+            *reinterpret_cast<uint2*>(dst + 16 * q) = __builtin_bit_cast(uint2, oh);
+            *reinterpret_cast<uint2*>(dst + C::PLANE + 16 * q) = __builtin_bit_cast(uint2, ol);
           }
         }
       }
@@ -303,24 +304,28 @@ __global__ __launch_bounds__(256) void k_conv3x3(const float* __restrict__ in, f
       if (ksx + 1 < NKS) load_a(ksx + 1, aq[(ksx + 1) & 1]);
       // pin the issue order: hipcc otherwise sinks the prefetches next to their use
       __builtin_amdgcn_sched_barrier(0);
+      // weights are the MFMA A operand (rows = output channels), the activation window
+      // the B operand (columns = output pixels): C[channel][pixel], so each lane ends up
+      // with 4 consecutive channels of one pixel per register group (16-byte stores).
 #pragma unroll
       for (int mt = 0; mt < C::MT; ++mt) {
-        const bf16x8 ah = as_bf16x8(aq[ksx & 1][mt][0]), al = as_bf16x8(aq[ksx & 1][mt][1]);
+        const bf16x8 xh = as_bf16x8(aq[ksx & 1][mt][0]), xl = as_bf16x8(aq[ksx & 1][mt][1]);
 #pragma unroll
         for (int nt = 0; nt < C::NT; ++nt)
-          acc[mt][nt] = mfma3(ah, al, as_bf16x8(bq[ksx % 3][nt][0]), as_bf16x8(bq[ksx % 3][nt][1]),
+          acc[mt][nt] = mfma3(as_bf16x8(bq[ksx % 3][nt][0]), as_bf16x8(bq[ksx % 3][nt][1]), xh, xl,
                               acc[mt][nt]);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
   }
 
-  // epilogue: + folded-BN bias, ReLU, NHWC fp32 store.  Tiles cover whole output rows
-  // (and whole patches when NP > 1), so tile row m is output pixel (p0*HOUT + y0)*WOUT + m
-  // and every (mt, nt, i) offset from the lane's base pointer is a compile-time constant.
-  float* obase = out + ((size_t)(p0 * C::HOUT + y0) * C::WOUT + wm * C::MT * 32 + 4 * h) * COUT +
-                 wn * C::NT * 32 + r;
-  if (dbg & 1) {  // ablation: keep the accumulators live, one store per lane instead of 16*MT*NT
+  // epilogue: + folded-BN bias, ReLU, NHWC fp32 16-byte stores.  acc[mt][nt] is
+  // C[channel][pixel]: lane (r, h) holds pixel r of the M tile and channels
+  // 8q + 4h + {0..3} (q = 0..3) of the N tile.  Tiles cover whole output rows (and whole
+  // patches when NP > 1), so tile pixel m is output pixel (p0*HOUT + y0)*WOUT + m.
+  float* obase = out + ((size_t)(p0 * C::HOUT + y0) * C::WOUT + wm * C::MT * 32 + r) * COUT +
+                 wn * C::NT * 32 + 4 * h;
+  if (dbg & 1) {  // ablation: keep the accumulators live, one store per lane
     float sum = 0.f;
 #pragma unroll
     for (int mt = 0; mt < C::MT; ++mt)
@@ -332,18 +337,356 @@ __global__ __launch_bounds__(256) void k_conv3x3(const float* __restrict__ in, f
     return;
   }
 #pragma unroll
-  for (int mt = 0; mt < C::MT; ++mt) {
-    const bool ok = NP == 1 || p0 + ((wm * C::MT + mt) * 32) / (TR * C::WOUT) < P;
-    if (!ok) continue;
+  for (int nt = 0; nt < C::NT; ++nt) {
+    float4 bv[4];
 #pragma unroll
-    for (int nt = 0; nt < C::NT; ++nt) {
-      const float bv = bias[(wn * C::NT + nt) * 32 + r];
+    for (int q = 0; q < 4; ++q)
+      bv[q] = *reinterpret_cast<const float4*>(bias + (wn * C::NT + nt) * 32 + 8 * q + 4 * h);
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int row = (i & 3) + 8 * (i >> 2);
-        obase[(mt * 32 + row) * COUT + nt * 32] = fmaxf(acc[mt][nt][i] + bv, 0.f);
+    for (int mt = 0; mt < C::MT; ++mt) {
+      const bool ok = NP == 1 || p0 + ((wm * C::MT + mt) * 32) / (TR * C::WOUT) < P;
+      if (!ok) continue;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float4 v;
+        v.x = fmaxf(acc[mt][nt][4 * q + 0] + bv[q].x, 0.f);
+        v.y = fmaxf(acc[mt][nt][4 * q + 1] + bv[q].y, 0.f);
+        v.z = fmaxf(acc[mt][nt][4 * q + 2] + bv[q].z, 0.f);
+        v.w = fmaxf(acc[mt][nt][4 * q + 3] + bv[q].w, 0.f);
+        *reinterpret_cast<float4*>(obase + (size_t)mt * 32 * COUT + nt * 32 + 8 * q) = v;
       }
     }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// k_conv_pipe: persistent, double-buffered version of k_conv3x3.
+//
+// Each workgroup loops over its tiles (tile = rb + k*gridDim, rb XCD-remapped) and over
+// the 32-channel chunks of each tile ("stages").  While the MFMA K-loop of stage s reads
+// LDS buffer s&1, the global loads of stage s+1's window are issued *inside* that loop,
+// one unit per K-step after the weight loads of the step (vmcnt retires in issue order,
+// so a weight-fragment wait never waits on a younger window load); after the K-loop the
+// prefetched registers are split to bf16 hi/lo and written into buffer (s+1)&1, and one
+// barrier ends the stage.  STEM (conv1): the next tile's raw patch is prefetched the same
+// way and input_norm + conv0 (MFMA) fill the next window.
+// ------------------------------------------------------------------------------------
+template <int CIN, int COUT, int HIN, int S, int NP, int TR, int WM, int WN, bool STEM>
+struct PipeCfg : ConvCfg<CIN, COUT, HIN, S, NP, TR, WM, WN> {
+  using B = ConvCfg<CIN, COUT, HIN, S, NP, TR, WM, WN>;
+  static constexpr int NW = WM * WN, NTHR = NW * 64;
+  static constexpr int UNITS = NP * B::RIN * B::NCOLS * 4;
+  static constexpr int UPT = (UNITS + NTHR - 1) / NTHR;
+  static constexpr int BUF = B::LDS;
+  static constexpr int PBUF = 2 * BUF;
+  static constexpr int SMEM = 2 * BUF + (STEM ? 34 * 34 * 4 : 0);
+  static_assert(UPT <= 18, "prefetch fits in the K-loop");
+};
+
+// ABL (ablation builds only, never shipped): bit0 no weight loads in the K-loop, bit1 no
+// LDS fragment reads, bit2 no next-stage staging.
+template <int CIN, int COUT, int HIN, int S, int NP, int TR, int WM, int WN, bool STEM, int ABL = 0>
+__global__ __launch_bounds__(WM * WN * 64, 2) void k_conv_pipe(
+    const float* __restrict__ in, float* __restrict__ out, const uint4* __restrict__ wp,
+    const float* __restrict__ bias, int P, const float* __restrict__ stem_w,
+    const float* __restrict__ stem_b, float eps) {
+  using C = PipeCfg<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int r = lane & 31, h = lane >> 5;
+  const int nwg = gridDim.x, rb = xcd_remap(blockIdx.x, nwg);
+  const int ntiles = (P + NP - 1) / NP * C::RT;
+  const int my_tiles = rb < ntiles ? (ntiles - 1 - rb) / nwg + 1 : 0;
+  const int NS = my_tiles * C::NCC;
+  if (NS == 0) return;
+
+  int abase[C::MT];
+#pragma unroll
+  for (int mt = 0; mt < C::MT; ++mt) {
+    const int m = (wm * C::MT + mt) * 32 + r;
+    const int np = m / (TR * C::WOUT), rem = m % (TR * C::WOUT);
+    const int yl = rem / C::WOUT, xo = rem % C::WOUT;
+    abase[mt] = np * C::PS + yl * S * C::RS + xo * 80 + h * 16;
+  }
+
+  auto tile_of = [&](int s, int& p0, int& y0) {
+    const int t = rb + (s / C::NCC) * nwg;
+    p0 = (t / C::RT) * NP;
+    y0 = (t % C::RT) * TR;
+  };
+
+  // ---------------- window staging (non-stem): prefetch registers -------------------
+  float4 pf[C::UPT][2];
+  auto prefetch_unit = [&](int s, int k) {
+    const int u = tid + k * C::NTHR;
+    int p0, y0;
+    tile_of(s, p0, y0);
+    const int cc = s % C::NCC;
+    const int g = u & 3, pix = u >> 2;
+    const int wc = pix % C::NCOLS, t2 = pix / C::NCOLS;
+    const int wr = t2 % C::RIN, np = t2 / C::RIN;
+    const int y = y0 * S - 1 + wr, x = wc - 1;
+    pf[k][0] = pf[k][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (u < C::UNITS && (NP == 1 || p0 + np < P) && (unsigned)y < (unsigned)HIN &&
+        (unsigned)x < (unsigned)HIN) {
+      const float4* src = reinterpret_cast<const float4*>(
+          in + ((((size_t)p0 + np) * HIN + y) * HIN + x) * CIN + cc * 32 + g * 8);
+      pf[k][0] = src[0];
+      pf[k][1] = src[1];
+    }
+  };
+  auto write_unit = [&](char* dst, int k) {
+    const int u = tid + k * C::NTHR;
+    if (u < C::UNITS) {
+      const int g = u & 3, pix = u >> 2;
+      const int wc = pix % C::NCOLS, t2 = pix / C::NCOLS;
+      const int wr = t2 % C::RIN, np = t2 / C::RIN;
+      uint4 hi, lo;
+      split8(pf[k][0], pf[k][1], hi, lo);
+      const int pc = (S == 1) ? wc : ((wc & 1) ? C::HALF + (wc >> 1) : (wc >> 1));
+      const int off = np * C::PS + wr * C::RS + pc * 80 + g * 16;
+      *reinterpret_cast<uint4*>(dst + off) = hi;
+      *reinterpret_cast<uint4*>(dst + C::PLANE + off) = lo;
+    }
+  };
+  auto write_window = [&](char* dst) {
+#pragma unroll
+    for (int k = 0; k < C::UPT; ++k) write_unit(dst, k);
+  };
+
+  // ---------------- stem staging: raw patch -> input_norm -> conv0 (MFMA) -----------
+  float4 pv[4];  // the whole 1024-float patch, per wave (lane l holds float4s l + 64k)
+  float* pt = reinterpret_cast<float*>(smem + C::PBUF);
+  auto patch_ptr = [&](int s) {
+    int p0, y0;
+    tile_of(s, p0, y0);
+    return reinterpret_cast<const float4*>(in + (size_t)p0 * 1024) + lane;
+  };
+  if constexpr (STEM) {
+    static_assert(CIN == 32 && HIN == 32 && S == 1 && NP == 1, "stem fusion is conv1-only");
+    for (int i = tid; i < 34 * 34; i += C::NTHR) pt[i] = 0.f;  // zero ring, interior rewritten
+    __syncthreads();
+  }
+  auto stem_stage = [&](int s, char* dst) {
+    int p0, y0;
+    tile_of(s, p0, y0);
+    float mean = 0.f, sd = 1.f;
+    if (eps >= 0.f) {  // HardNet.py:307-310, every wave reduces the full patch itself
+      float a = 0.f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) a += (pv[k].x + pv[k].y) + (pv[k].z + pv[k].w);
+      mean = wave_sum(a) * (1.f / 1024.f);
+      float q = 0.f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float d0 = pv[k].x - mean, d1 = pv[k].y - mean, d2 = pv[k].z - mean,
+                    d3 = pv[k].w - mean;
+        q += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
+      }
+      sd = sqrtf(wave_sum(q) * (1.f / 1023.f)) + eps;
+    }
+    // each wave writes its share of the normalised patch; explicit constant-index cases
+    // (a pv[wave] form would be a runtime-indexed array -> scratch)
+    const int wu = __builtin_amdgcn_readfirstlane(wave);
+#define HN_PUT(K)                                                                          \
+  {                                                                                        \
+    const int q4 = 4 * (lane + 64 * K), y = q4 >> 5, x = q4 & 31;                          \
+    float* d = pt + (y + 1) * 34 + x + 1;                                                  \
+    d[0] = (pv[K].x - mean) / sd; d[1] = (pv[K].y - mean) / sd;                             \
+    d[2] = (pv[K].z - mean) / sd; d[3] = (pv[K].w - mean) / sd;                             \
+  }
+    if (wu % 4 == 0 || C::NW == 1) HN_PUT(0)
+    if (wu % 4 == 1 || C::NW <= 1) HN_PUT(1)
+    if (wu % 4 == 2 || (C::NW <= 2 && wu % 2 == 0)) HN_PUT(2)
+    if (wu % 4 == 3 || (C::NW <= 2 && wu % 2 == 1)) HN_PUT(3)
+#undef HN_PUT
+    __syncthreads();
+    constexpr int NPIX = C::RIN * C::NCOLS;
+    constexpr int NT0 = (NPIX + 31) / 32;
+    bf16x8 w0h, w0l;  // conv0 weights as the A operand (rows = channels), taps 9..15 zero
+    {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int tap = 8 * h + j;
+        const float v = tap < 9 ? stem_w[tap * 32 + r] : 0.f;
+        w0h[j] = (__bf16)v;
+        w0l[j] = (__bf16)(v - (float)w0h[j]);
+      }
+    }
+#pragma unroll 1
+    for (int t = wave; t < NT0; t += C::NW) {
+      const int pix = t * 32 + r;
+      const int wr = pix / C::NCOLS, wc = pix % C::NCOLS;
+      const int y = y0 - 1 + wr, x = wc - 1;
+      const bool inside = pix < NPIX && (unsigned)y < 32u && (unsigned)x < 32u;
+      const int yc = inside ? y : 0, xc = inside ? x : 0;
+      bf16x8 xh, xl;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int tap = 8 * h + j;
+        const float v = tap < 9 ? pt[(yc + tap / 3) * 34 + xc + tap % 3] : 0.f;
+        xh[j] = (__bf16)v;
+        xl[j] = (__bf16)(v - (float)xh[j]);
+      }
+      const f32x16 c0 = mfma3(w0h, w0l, xh, xl, f32x16{});
+      if (pix < NPIX) {
+        char* o = dst + wr * C::RS + wc * 80 + 8 * h;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          bf16x4 oh, ol;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float v =
+                inside ? fmaxf(c0[4 * q + j] + stem_b[8 * q + 4 * h + j], 0.f) : 0.f;
+            oh[j] = (__bf16)v;
+            ol[j] = (__bf16)(v - (float)oh[j]);
+          }
+          *reinterpret_cast<uint2*>(o + 16 * q) = __builtin_bit_cast(uint2, oh);
+          *reinterpret_cast<uint2*>(o + C::PLANE + 16 * q) = __builtin_bit_cast(uint2, ol);
+        }
+      }
+    }
+  };
+
+  // ---------------- prologue ---------------------------------------------------------
+  char* const buf0 = smem;
+  char* const buf1 = smem + C::BUF;
+  if constexpr (STEM) {
+    {
+      const float4* pp = patch_ptr(0);
+      pv[0] = pp[0]; pv[1] = pp[64]; pv[2] = pp[128]; pv[3] = pp[192];
+    }
+    stem_stage(0, buf0);
+  } else {
+#pragma unroll
+    for (int k = 0; k < C::UPT; ++k) prefetch_unit(0, k);
+    write_window(buf0);
+  }
+  __syncthreads();
+
+  f32x16 acc[C::MT][C::NT];
+#pragma unroll
+  for (int mt = 0; mt < C::MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < C::NT; ++nt) acc[mt][nt] = f32x16{};
+
+#pragma unroll 1
+  for (int s = 0; s < NS; ++s) {
+    const char* cur = (s & 1) ? buf1 : buf0;
+    char* nxt = (s & 1) ? buf0 : buf1;
+    const int cc = s % C::NCC;
+    const bool more = s + 1 < NS;
+    constexpr int NKS = 18;
+    constexpr unsigned CHUNK_BYTES = 9 * 2 * C::NTOT * 2 * 64 * 16;
+    const __amdgpu_buffer_rsrc_t wr_ = make_rsrc(wp, C::NCC * CHUNK_BYTES);
+    const unsigned wvoff = (wn * C::NT * 2 * 64 + lane) * 16;
+    const unsigned wsoff = cc * CHUNK_BYTES;
+    uint4 bq[3][C::NT][2];
+    uint4 aq[2][C::MT][2];
+    auto load_b = [&](int ksx, uint4 (&dst)[C::NT][2]) {
+#pragma unroll
+      for (int nt = 0; nt < C::NT; ++nt) {
+        const unsigned k = ((ksx * C::NTOT + nt) * 2) * 64 * 16;
+        dst[nt][0] = buf_load16(wr_, wvoff, wsoff + k);
+        dst[nt][1] = buf_load16(wr_, wvoff, wsoff + k + 64 * 16);
+      }
+    };
+    auto load_a = [&](int ksx, uint4 (&dst)[C::MT][2]) {
+      const int tap = ksx >> 1, ks = ksx & 1;
+      const int toff = (tap / 3) * C::RS + C::colofs(tap % 3) * 80 + ks * 32;
+#pragma unroll
+      for (int mt = 0; mt < C::MT; ++mt) {
+        dst[mt][0] = *reinterpret_cast<const uint4*>(cur + abase[mt] + toff);
+        dst[mt][1] = *reinterpret_cast<const uint4*>(cur + C::PLANE + abase[mt] + toff);
+      }
+    };
+    load_b(0, bq[0]);
+    load_b(1, bq[1]);
+    load_a(0, aq[0]);
+#pragma unroll
+    for (int ksx = 0; ksx < NKS; ++ksx) {
+      if (!(ABL & 1) && ksx + 2 < NKS) load_b(ksx + 2, bq[(ksx + 2) % 3]);
+      if ((ABL & 1) && ksx + 2 < NKS) {
+#pragma unroll
+        for (int nt = 0; nt < C::NT; ++nt) {
+          bq[(ksx + 2) % 3][nt][0] = bq[ksx % 3][nt][0];
+          bq[(ksx + 2) % 3][nt][1] = bq[ksx % 3][nt][1];
+        }
+      }
+      // next stage's window: the loads of unit ksx are issued at K-step ksx and the unit
+      // is split + written into the other LDS buffer two K-steps later (the double buffer
+      // makes `nxt` writable for the whole stage), so the staging VALU co-issues with the
+      // MFMAs of this wave
+      if (!STEM && !(ABL & 4) && more && ksx >= 2 && ksx - 2 < C::UPT) write_unit(nxt, ksx - 2);
+      if (!(ABL & 4) && more) {  // next stage's window loads, one unit per K-step
+        if constexpr (STEM) {
+          if (ksx == 0) pv[0] = patch_ptr(s + 1)[0];
+          if (ksx == 1) pv[1] = patch_ptr(s + 1)[64];
+          if (ksx == 2) pv[2] = patch_ptr(s + 1)[128];
+          if (ksx == 3) pv[3] = patch_ptr(s + 1)[192];
+        } else {
+          if (ksx < C::UPT) prefetch_unit(s + 1, ksx);
+        }
+      }
+      if (!(ABL & 2) && ksx + 1 < NKS) load_a(ksx + 1, aq[(ksx + 1) & 1]);
+      if ((ABL & 2) && ksx + 1 < NKS) {
+#pragma unroll
+        for (int mt = 0; mt < C::MT; ++mt) {
+          aq[(ksx + 1) & 1][mt][0] = aq[ksx & 1][mt][0];
+          aq[(ksx + 1) & 1][mt][1] = aq[ksx & 1][mt][1];
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int mt = 0; mt < C::MT; ++mt) {
+        const bf16x8 xh = as_bf16x8(aq[ksx & 1][mt][0]), xl = as_bf16x8(aq[ksx & 1][mt][1]);
+#pragma unroll
+        for (int nt = 0; nt < C::NT; ++nt)
+          acc[mt][nt] = mfma3(as_bf16x8(bq[ksx % 3][nt][0]), as_bf16x8(bq[ksx % 3][nt][1]), xh, xl,
+                              acc[mt][nt]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+
+    if (cc == C::NCC - 1) {  // epilogue of this tile (see k_conv3x3)
+      int p0, y0;
+      tile_of(s, p0, y0);
+      float* obase = out + ((size_t)(p0 * C::HOUT + y0) * C::WOUT + wm * C::MT * 32 + r) * COUT +
+                     wn * C::NT * 32 + 4 * h;
+#pragma unroll
+      for (int nt = 0; nt < C::NT; ++nt) {
+        float4 bv[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          bv[q] = *reinterpret_cast<const float4*>(bias + (wn * C::NT + nt) * 32 + 8 * q + 4 * h);
+#pragma unroll
+        for (int mt = 0; mt < C::MT; ++mt) {
+          const bool ok = NP == 1 || p0 + ((wm * C::MT + mt) * 32) / (TR * C::WOUT) < P;
+          if (ok) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              float4 v;
+              v.x = fmaxf(acc[mt][nt][4 * q + 0] + bv[q].x, 0.f);
+              v.y = fmaxf(acc[mt][nt][4 * q + 1] + bv[q].y, 0.f);
+              v.z = fmaxf(acc[mt][nt][4 * q + 2] + bv[q].z, 0.f);
+              v.w = fmaxf(acc[mt][nt][4 * q + 3] + bv[q].w, 0.f);
+              *reinterpret_cast<float4*>(obase + (size_t)mt * 32 * COUT + nt * 32 + 8 * q) = v;
+            }
+          }
+          acc[mt][nt] = f32x16{};
+        }
+      }
+    }
+    if (!(ABL & 4) && more) {
+      if constexpr (STEM) {
+        stem_stage(s + 1, nxt);
+      } else {
+#pragma unroll
+        for (int k = NKS - 2; k < C::UPT; ++k) write_unit(nxt, k);  // units beyond the K-loop
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -452,6 +795,51 @@ HN_CONV(conv4_v1, false, 64, 128, 16, 2, 1, 4, 1, 4)
 HN_CONV(conv5_launch, false, 128, 128, 8, 1, 2, 8, 1, 4)
 HN_CONV(conv5_v1, false, 128, 128, 8, 1, 1, 8, 1, 4)
 
+// persistent launch: grid = min(tiles, resident workgroups) (occupancy query, cached)
+#define HN_PIPE(NAME, STEM, CIN, COUT, HIN, S, NP, TR, WM, WN) HN_PIPE_A(NAME, STEM, CIN, COUT, HIN, S, NP, TR, WM, WN, 0)
+#define HN_PIPE_A(NAME, STEM, CIN, COUT, HIN, S, NP, TR, WM, WN, ABL)                      \
+  using NAME##_cfg = PipeCfg<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM>;                     \
+  static hipError_t NAME(const float* in, float* out, const void* wp, const float* bias,   \
+                         int P, const float* sw, const float* sb, float eps,               \
+                         hipStream_t st) {                                                 \
+    constexpr int lds = NAME##_cfg::SMEM;                                                  \
+    const void* fn = reinterpret_cast<const void*>(                                        \
+        &k_conv_pipe<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM, ABL>);                       \
+    static int resident = 0;                                                               \
+    if (!resident) {                                                                       \
+      hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds); \
+      if (e != hipSuccess) return e;                                                       \
+      int per_cu = 0, dev = 0, cus = 0;                                                    \
+      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, NAME##_cfg::NTHR, lds); \
+      if (e != hipSuccess) return e;                                                       \
+      (void)hipGetDevice(&dev);                                                            \
+      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);       \
+      resident = std::max(1, per_cu) * std::max(1, cus);                                   \
+    }                                                                                      \
+    const int tiles = (P + NP - 1) / NP * NAME##_cfg::RT;                                  \
+    const int grid = std::min(tiles, resident);                                            \
+    hipLaunchKernelGGL((k_conv_pipe<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM, ABL>), dim3(grid), \
+                       dim3(NAME##_cfg::NTHR), lds, st, in, out,                           \
+                       static_cast<const uint4*>(wp), bias, P, sw, sb, eps);               \
+    return hipGetLastError();                                                              \
+  }
+
+HN_PIPE(pipe1s, true, 32, 32, 32, 1, 1, 4, 4, 1)
+HN_PIPE(pipe1s_t8, true, 32, 32, 32, 1, 1, 8, 4, 1)
+HN_PIPE(pipe2, false, 32, 64, 32, 2, 1, 4, 2, 2)
+HN_PIPE(pipe2_t2, false, 32, 64, 32, 2, 1, 2, 1, 2)
+HN_PIPE(pipe3, false, 64, 64, 16, 1, 1, 8, 2, 2)
+HN_PIPE(pipe3_t16, false, 64, 64, 16, 1, 1, 16, 2, 2)
+HN_PIPE(pipe4, false, 64, 128, 16, 2, 1, 4, 1, 4)
+HN_PIPE(pipe4_t8, false, 64, 128, 16, 2, 1, 8, 1, 4)
+HN_PIPE(pipe5, false, 128, 128, 8, 1, 1, 8, 1, 4)
+HN_PIPE(pipe5_np2, false, 128, 128, 8, 1, 2, 8, 1, 4)
+// conv3 ablation builds (HN_VARIANT digit 4..7 for layer 3 -> ABL 1, 2, 4, 7)
+HN_PIPE_A(pipe3_a1, false, 64, 64, 16, 1, 1, 8, 2, 2, 1)
+HN_PIPE_A(pipe3_a2, false, 64, 64, 16, 1, 1, 8, 2, 2, 2)
+HN_PIPE_A(pipe3_a4, false, 64, 64, 16, 1, 1, 8, 2, 2, 4)
+HN_PIPE_A(pipe3_a7, false, 64, 64, 16, 1, 1, 8, 2, 2, 7)
+
 hipError_t hn_launch_stem(const float* in, float* out, const float* w, const float* b, int P,
                           bool norm, float eps, hipStream_t st) {
   if (norm)
@@ -465,6 +853,22 @@ hipError_t hn_launch_stem(const float* in, float* out, const float* w, const flo
 hipError_t hn_launch_hardnet_conv(int layer, int variant, const HardnetDev& d, const float* in,
                                   float* out, int P, float eps, hipStream_t st) {
   const bool v1 = variant == 1;
+  if (layer == 3 && variant >= 4) {
+    auto f = variant == 4 ? pipe3_a1 : variant == 5 ? pipe3_a2 : variant == 6 ? pipe3_a4 : pipe3_a7;
+    return f(in, out, d.wpack[3], d.bias[3], P, nullptr, nullptr, 0.f, st);
+  }
+  if (variant >= 2) {  // persistent pipelined kernels: 2 = smaller tile, 3 = larger tile
+    const bool big = variant == 3;
+    switch (layer) {
+      case 0:
+        return (big ? pipe1s_t8 : pipe1s)(in, out, d.wpack[1], d.bias[1], P, d.stem_w, d.stem_b, eps, st);
+      case 2: return (big ? pipe2 : pipe2_t2)(in, out, d.wpack[2], d.bias[2], P, nullptr, nullptr, 0.f, st);
+      case 3: return (big ? pipe3_t16 : pipe3)(in, out, d.wpack[3], d.bias[3], P, nullptr, nullptr, 0.f, st);
+      case 4: return (big ? pipe4_t8 : pipe4)(in, out, d.wpack[4], d.bias[4], P, nullptr, nullptr, 0.f, st);
+      case 5: return (big ? pipe5_np2 : pipe5)(in, out, d.wpack[5], d.bias[5], P, nullptr, nullptr, 0.f, st);
+    }
+    return hipErrorInvalidValue;
+  }
   switch (layer) {
     case 0:
       return (v1 ? conv1s_v1 : conv1s_launch)(in, out, d.wpack[1], d.bias[1], P, d.stem_w,

@@ -11,6 +11,9 @@
 #include "hn_common.h"
 #include "hn_internal.h"
 
+#include <cstdlib>
+#include <type_traits>
+
 __global__ __launch_bounds__(256) void k_pw(const float* __restrict__ in, float* __restrict__ out,
                                             const float* __restrict__ wt,   // [KG][COUT]
                                             const float* __restrict__ bias, // [COUT]
@@ -58,6 +61,105 @@ __global__ __launch_bounds__(256) void k_pw(const float* __restrict__ in, float*
   } else {
     *reinterpret_cast<float4*>(o + n) = acc;
   }
+}
+
+// LDS-tiled pointwise GEMM: one workgroup computes TM pixels x TN output channels of one
+// group (K = cin/groups, chunked by 32); each thread a 4 px x 4 ch register tile, so
+// TM = 4096 / TN (TN = 16/32/64 follows the group width -- no idle threads on the narrow
+// grouped convs).  fp32 FMA chains, exact like the reference's fp32 conv up to summation
+// order.  Also the NAS head GEMM (K = 16*C, N = 128).
+constexpr int PW_TK = 32;
+template <int TN>
+__global__ __launch_bounds__(256) void k_pw_tiled(const float* __restrict__ in, float* __restrict__ out,
+                                                  const float* __restrict__ wt,   // [KG][COUT]
+                                                  const float* __restrict__ bias,
+                                                  const float* __restrict__ res, long npix, int cin,
+                                                  int cout, int groups, int relu, int shuffle_g) {
+  constexpr int TXN = TN / 4, TM = 4096 / TN;
+  __shared__ float xs[PW_TK][TM + 4];  // k-major: xs[k][pixel]
+  __shared__ float ws[PW_TK][TN];
+  const int t = threadIdx.x, tx = t % TXN, ty = t / TXN;
+  const int kg = cin / groups, ng = cout / groups;
+  const int ntn = (ng + TN - 1) / TN;
+  const int g = blockIdx.y / ntn, n0 = (blockIdx.y % ntn) * TN;
+  const long p0 = (long)blockIdx.x * TM;
+  float acc[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = n0 + tx * 4 + j;
+    const float bv = n < ng ? bias[g * ng + n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i][j] = bv;
+  }
+  for (int k0 = 0; k0 < kg; k0 += PW_TK) {
+    const int kc = min(PW_TK, kg - k0);
+    __syncthreads();
+    for (int e = t; e < TM * (PW_TK / 4); e += 256) {
+      const int px = e / (PW_TK / 4), k4 = (e % (PW_TK / 4)) * 4;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (p0 + px < npix && k4 < kc)
+        v = *reinterpret_cast<const float4*>(in + (p0 + px) * cin + g * kg + k0 + k4);
+      xs[k4 + 0][px] = v.x; xs[k4 + 1][px] = v.y; xs[k4 + 2][px] = v.z; xs[k4 + 3][px] = v.w;
+    }
+    for (int e = t; e < PW_TK * TXN; e += 256) {
+      const int k = e / TXN, n4 = (e % TXN) * 4;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (k < kc && n0 + n4 < ng)
+        v = *reinterpret_cast<const float4*>(wt + (long)(k0 + k) * cout + g * ng + n0 + n4);
+      *reinterpret_cast<float4*>(&ws[k][n4]) = v;
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int k = 0; k < kc; ++k) {
+      const float4 a = *reinterpret_cast<const float4*>(&xs[k][ty * 4]);
+      const float4 b = *reinterpret_cast<const float4*>(&ws[k][tx * 4]);
+      const float av[4] = {a.x, a.y, a.z, a.w}, bv[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(av[i], bv[j], acc[i][j]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const long px = p0 + ty * 4 + i;
+    const int nl = n0 + tx * 4;
+    if (px >= npix || nl >= ng) continue;
+    const int n = g * ng + nl;
+    float4 v = make_float4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]);
+    if (relu) {
+      v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+    }
+    if (res) {
+      const float4 rv = *reinterpret_cast<const float4*>(res + px * cout + n);
+      v.x += rv.x; v.y += rv.y; v.z += rv.z; v.w += rv.w;
+    }
+    float* o = out + px * cout;
+    if (shuffle_g > 1) {  // channel c = j*(C/g)+i  ->  position i*g + j
+      const int cg = cout / shuffle_g;
+      const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = n + j;
+        o[(c % cg) * shuffle_g + c / cg] = vv[j];
+      }
+    } else {
+      *reinterpret_cast<float4*>(o + n) = v;
+    }
+  }
+}
+
+// y / sqrt(sum y^2 + eps) over rows of 128 (model_supernet.py:84 has eps = 0), in place.
+__global__ __launch_bounds__(256) void k_l2rows(float* __restrict__ y, int P, float l2eps) {
+  const int t = threadIdx.x;
+  const int p = blockIdx.x * 8 + (t >> 5);
+  const int n = (t & 31) * 4;
+  if (p >= P) return;
+  float4 v = *reinterpret_cast<const float4*>(y + (long)p * 128 + n);
+  const float ss = half_sum(v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w);
+  const float norm = sqrtf(ss + l2eps);
+  v.x /= norm; v.y /= norm; v.z /= norm; v.w /= norm;
+  *reinterpret_cast<float4*>(y + (long)p * 128 + n) = v;
 }
 
 template <int K>
@@ -191,8 +293,26 @@ static inline unsigned blocks(long n, int per) { return (unsigned)((n + per - 1)
 hipError_t hn_launch_pw(const float* in, float* out, const float* wt, const float* bias,
                         const float* res, long npix, int cin, int cout, int groups, bool relu,
                         int shuffle_g, hipStream_t st) {
-  hipLaunchKernelGGL(k_pw, dim3(blocks(npix * (cout / 4), 256)), dim3(256), 0, st, in, out, wt,
-                     bias, res, npix, cin, cout, groups, relu ? 1 : 0, shuffle_g);
+  static int naive = -1;
+  if (naive < 0) naive = std::getenv("HN_NAIVE_PW") ? 1 : 0;
+  if (naive) {
+    hipLaunchKernelGGL(k_pw, dim3(blocks(npix * (cout / 4), 256)), dim3(256), 0, st, in, out, wt,
+                       bias, res, npix, cin, cout, groups, relu ? 1 : 0, shuffle_g);
+  } else {
+    const int ng = cout / groups;
+    auto launch = [&](auto tn) {
+      constexpr int TN = decltype(tn)::value, TM = 4096 / TN;
+      const dim3 grid((unsigned)((npix + TM - 1) / TM), groups * ((ng + TN - 1) / TN));
+      hipLaunchKernelGGL(k_pw_tiled<TN>, grid, dim3(256), 0, st, in, out, wt, bias, res, npix,
+                         cin, cout, groups, relu ? 1 : 0, shuffle_g);
+    };
+    if (ng <= 16)
+      launch(std::integral_constant<int, 16>{});
+    else if (ng <= 32)
+      launch(std::integral_constant<int, 32>{});
+    else
+      launch(std::integral_constant<int, 64>{});
+  }
   return hipGetLastError();
 }
 
@@ -225,7 +345,9 @@ hipError_t hn_launch_se(float* y, const float* w1, const float* b1, const float*
 
 hipError_t hn_launch_nas_head(const float* a, float* out, const float* wt, const float* bias,
                               int P, int K, float l2eps, hipStream_t st) {
-  hipLaunchKernelGGL(k_nas_head, dim3((P + 3) / 4), dim3(128), 0, st, a, out, wt, bias, P, K,
-                     l2eps);
+  // [P, K] x [K, 128] on the tiled GEMM, then the row L2 normalisation
+  hipError_t e = hn_launch_pw(a, out, wt, bias, nullptr, P, K, 128, 1, false, 0, st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_l2rows, dim3((P + 7) / 8), dim3(256), 0, st, out, P, l2eps);
   return hipGetLastError();
 }

@@ -92,3 +92,12 @@ def test_eval_cuda_path_has_no_silent_fallback(monkeypatch):
     monkeypatch.setenv("HN_LIB", "/nonexistent/libhardnet_mi355x.so")
     with pytest.raises(RuntimeError, match="not found"):
         N.load_library()
+
+
+def test_bench_knows_every_hardnet_stage():
+    """bench.py's per-stage FLOP/byte tables cover every stage name hn_forward records."""
+    import bench
+    src = open(os.path.join(ROOT, "hardnetnas_amd", "csrc", "hn_api.hip")).read()
+    fwd = src[src.index("static int forward_hardnet("):src.index("static int forward_nas(")]
+    names = set(re.findall(r'STAGE\("([^"]+)"', fwd))
+    assert names and names <= set(bench.HARDNET_STAGE_MAC) and names <= set(bench.HARDNET_STAGE_BYTES)
