@@ -155,7 +155,7 @@ struct hn_model {
   bool unfused_stem = false;  // HN_UNFUSED_STEM=1: separate stem kernel (A/B, debugging)
   // conv tiling per layer (index 0 = stem+conv1, 2..5 = conv2..5); defaults are the best
   // measured on MI355X (tools/tune_variants.py); HN_VARIANT="003303" style override
-  int variant[6] = {0, 0, 3, 3, 0, 3};
+  int variant[6] = {6, 0, 5, 6, 6, 3};
   size_t ws_floats_per_patch = 0;  // per buffer
   int n_bufs = 0;
 

@@ -380,6 +380,7 @@ struct PipeCfg : ConvCfg<CIN, COUT, HIN, S, NP, TR, WM, WN> {
   static constexpr int BUF = B::LDS;
   static constexpr int PBUF = 2 * BUF;
   static constexpr int SMEM = 2 * BUF + (STEM ? 34 * 34 * 4 : 0);
+  static_assert(SMEM <= 160 * 1024, "LDS");
   static_assert(UPT <= 18, "prefetch fits in the K-loop");
 };
 
@@ -691,6 +692,319 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void k_conv_pipe(
 }
 
 // ------------------------------------------------------------------------------------
+// k_conv_ws: warp-specialised persistent conv.  NWC = WM*WN compute waves run the MFMA
+// K-loop on LDS buffer s&1 (weight fragments streamed 2 K-steps ahead); 4 producer waves
+// own the next stage's window: they issue ALL its global loads at once (their vmcnt is
+// their own, so the compute waves' weight waits never queue behind them -- the in-order
+// vmcnt problem of k_conv_pipe), then split to bf16 hi/lo into buffer (s+1)&1.  One
+// barrier per stage.  For the HBM-heavy stride-2 layers this keeps ~UNITS*32 B per
+// workgroup in flight instead of one unit per K-step.
+// ------------------------------------------------------------------------------------
+template <int CIN, int COUT, int HIN, int S, int NP, int TR, int WM, int WN, bool STEM = false>
+struct WsCfg : ConvCfg<CIN, COUT, HIN, S, NP, TR, WM, WN> {
+  using B = ConvCfg<CIN, COUT, HIN, S, NP, TR, WM, WN>;
+  static constexpr int NWC = WM * WN, NWP = 4, NTHR = (NWC + NWP) * 64, PTHR = NWP * 64;
+  static constexpr int UNITS = NP * B::RIN * B::NCOLS * 4;
+  static constexpr int UPT = STEM ? 1 : (UNITS + PTHR - 1) / PTHR;
+  static constexpr int BUF = B::LDS;
+  static constexpr int PBUF = 34 * 34 * 4;  // one private normalised patch per producer wave
+  static constexpr int SMEM = 2 * BUF + (STEM ? NWP * PBUF : 0);
+  static_assert(SMEM <= 160 * 1024, "LDS");
+};
+
+// STEM (conv1 only): the producers load the raw patch, reduce mean/std per wave, write the
+// normalised patch into their own LDS copy (no cross-wave hand-off) and run conv0 on the
+// MFMA straight into the next window (input_norm + conv0 + BN + ReLU, HardNet.py:281-283,
+// 306-310).
+template <int CIN, int COUT, int HIN, int S, int NP, int TR, int WM, int WN, bool STEM>
+__global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_ws(
+    const float* __restrict__ in, float* __restrict__ out, const uint4* __restrict__ wp,
+    const float* __restrict__ bias, int P, const float* __restrict__ stem_w,
+    const float* __restrict__ stem_b, float eps) {
+  using C = WsCfg<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool producer = wave >= C::NWC;
+  const int r = lane & 31, h = lane >> 5;
+  const int nwg = gridDim.x, rb = xcd_remap(blockIdx.x, nwg);
+  const int ntiles = (P + NP - 1) / NP * C::RT;
+  // STEM: each workgroup takes a contiguous range of tiles, so consecutive stages mostly
+  // share a patch and the producers normalise each patch once; otherwise strided tiles.
+  const int per = (ntiles + nwg - 1) / nwg;
+  const int t_begin = STEM ? rb * per : rb;
+  const int my_tiles = STEM ? max(0, min(per, ntiles - t_begin))
+                            : (rb < ntiles ? (ntiles - 1 - rb) / nwg + 1 : 0);
+  const int NS = my_tiles * C::NCC;
+  if (NS == 0) return;
+  char* const buf0 = smem;
+  char* const buf1 = smem + C::BUF;
+
+  auto tile_of = [&](int s, int& p0, int& y0) {
+    const int t = STEM ? t_begin + s / C::NCC : rb + (s / C::NCC) * nwg;
+    p0 = (t / C::RT) * NP;
+    y0 = (t % C::RT) * TR;
+  };
+  // ---- producer side ----
+  const int ptid = tid - C::NWC * 64;
+  float4 pf[C::UPT][2];
+  auto produce_loads = [&](int s) {
+    int p0, y0;
+    tile_of(s, p0, y0);
+    const int cc = s % C::NCC;
+#pragma unroll
+    for (int k = 0; k < C::UPT; ++k) {
+      const int u = ptid + k * C::PTHR;
+      const int g = u & 3, pix = u >> 2;
+      const int wc = pix % C::NCOLS, t2 = pix / C::NCOLS;
+      const int wr = t2 % C::RIN, np = t2 / C::RIN;
+      const int y = y0 * S - 1 + wr, x = wc - 1;
+      pf[k][0] = pf[k][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (u < C::UNITS && (NP == 1 || p0 + np < P) && (unsigned)y < (unsigned)HIN &&
+          (unsigned)x < (unsigned)HIN) {
+        const float4* src = reinterpret_cast<const float4*>(
+            in + ((((size_t)p0 + np) * HIN + y) * HIN + x) * CIN + cc * 32 + g * 8);
+        pf[k][0] = src[0];
+        pf[k][1] = src[1];
+      }
+    }
+  };
+  auto produce_write = [&](char* dst) {
+#pragma unroll
+    for (int k = 0; k < C::UPT; ++k) {
+      const int u = ptid + k * C::PTHR;
+      if (u < C::UNITS) {
+        const int g = u & 3, pix = u >> 2;
+        const int wc = pix % C::NCOLS, t2 = pix / C::NCOLS;
+        const int wr = t2 % C::RIN, np = t2 / C::RIN;
+        uint4 hi, lo;
+        split8(pf[k][0], pf[k][1], hi, lo);
+        const int pc = (S == 1) ? wc : ((wc & 1) ? C::HALF + (wc >> 1) : (wc >> 1));
+        const int off = np * C::PS + wr * C::RS + pc * 80 + g * 16;
+        *reinterpret_cast<uint4*>(dst + off) = hi;
+        *reinterpret_cast<uint4*>(dst + C::PLANE + off) = lo;
+      }
+    }
+  };
+
+  // ---- stem producer (STEM only) ----
+  const int pw_ = wave - C::NWC;
+  float* pt = reinterpret_cast<float*>(smem + 2 * C::BUF + (producer ? pw_ : 0) * C::PBUF);
+  float4 pv[4];
+  int cur_patch = -1;
+  bf16x8 w0h{}, w0l{};
+  float b16[16];
+  if (STEM && producer) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int tap = 8 * h + j;
+      const float v = tap < 9 ? stem_w[tap * 32 + r] : 0.f;
+      w0h[j] = (__bf16)v;
+      w0l[j] = (__bf16)(v - (float)w0h[j]);
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) b16[i] = stem_b[8 * (i >> 2) + 4 * h + (i & 3)];
+  }
+  auto stem_loads = [&](int s) {
+    int p0, y0;
+    tile_of(s, p0, y0);
+    if (p0 == cur_patch) return;
+    const float4* pp = reinterpret_cast<const float4*>(in + (size_t)p0 * 1024) + lane;
+    pv[0] = pp[0]; pv[1] = pp[64]; pv[2] = pp[128]; pv[3] = pp[192];
+  };
+  auto stem_write = [&](int s, char* dst) {
+    int p0, y0;
+    tile_of(s, p0, y0);
+    if (p0 != cur_patch) {
+    cur_patch = p0;
+    float mean = 0.f, sd = 1.f;
+    if (eps >= 0.f) {
+      float a = 0.f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) a += (pv[k].x + pv[k].y) + (pv[k].z + pv[k].w);
+      mean = wave_sum(a) * (1.f / 1024.f);
+      float q = 0.f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float d0 = pv[k].x - mean, d1 = pv[k].y - mean, d2 = pv[k].z - mean,
+                    d3 = pv[k].w - mean;
+        q += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
+      }
+      sd = sqrtf(wave_sum(q) * (1.f / 1023.f)) + eps;
+    }
+    const float inv = 1.f / sd;  // one division; (x-mean)*inv is within 1 ulp of the reference's /
+#define HN_PUT(K)                                                                          \
+  {                                                                                        \
+    const int q4 = 4 * (lane + 64 * K), y = q4 >> 5, x = q4 & 31;                          \
+    float* d = pt + (y + 1) * 34 + x + 1;                                                  \
+    d[0] = (pv[K].x - mean) * inv; d[1] = (pv[K].y - mean) * inv;                           \
+    d[2] = (pv[K].z - mean) * inv; d[3] = (pv[K].w - mean) * inv;                           \
+  }
+    HN_PUT(0) HN_PUT(1) HN_PUT(2) HN_PUT(3)
+#undef HN_PUT
+    }
+    constexpr int NPIX = C::RIN * C::NCOLS;
+    constexpr int NT0 = (NPIX + 31) / 32;
+#pragma unroll 1
+    for (int t = pw_; t < NT0; t += C::NWP) {
+      const int pix = t * 32 + r;
+      const int wr = pix / C::NCOLS, wc = pix % C::NCOLS;
+      const int y = y0 - 1 + wr, x = wc - 1;
+      const bool inside = pix < NPIX && (unsigned)y < 32u && (unsigned)x < 32u;
+      const int yc = inside ? y : 0, xc = inside ? x : 0;
+      bf16x8 xh, xl;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int tap = 8 * h + j;
+        const float v = tap < 9 ? pt[(yc + tap / 3) * 34 + xc + tap % 3] : 0.f;
+        xh[j] = (__bf16)v;
+        xl[j] = (__bf16)(v - (float)xh[j]);
+      }
+      const f32x16 c0 = mfma3(w0h, w0l, xh, xl, f32x16{});
+      if (pix < NPIX) {
+        char* o = dst + wr * C::RS + wc * 80 + 8 * h;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          bf16x4 oh, ol;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float v = inside ? fmaxf(c0[4 * q + j] + b16[4 * q + j], 0.f) : 0.f;
+            oh[j] = (__bf16)v;
+            ol[j] = (__bf16)(v - (float)oh[j]);
+          }
+          *reinterpret_cast<uint2*>(o + 16 * q) = __builtin_bit_cast(uint2, oh);
+          *reinterpret_cast<uint2*>(o + C::PLANE + 16 * q) = __builtin_bit_cast(uint2, ol);
+        }
+      }
+    }
+  };
+
+  if (producer) {
+    if constexpr (STEM) {
+      static_assert(CIN == 32 && HIN == 32 && S == 1 && NP == 1, "stem fusion is conv1-only");
+      for (int i = lane; i < 34 * 34; i += 64) pt[i] = 0.f;  // own zero ring
+      stem_loads(0);
+      stem_write(0, buf0);
+    } else {
+      produce_loads(0);
+      produce_write(buf0);
+    }
+  }
+  __syncthreads();
+
+  if (producer) {
+#pragma unroll 1
+    for (int s = 0; s < NS; ++s) {
+      if (s + 1 < NS) {
+        if constexpr (STEM) {
+          stem_loads(s + 1);
+          stem_write(s + 1, (s & 1) ? buf0 : buf1);
+        } else {
+          produce_loads(s + 1);
+          produce_write((s & 1) ? buf0 : buf1);
+        }
+      }
+      __syncthreads();
+    }
+    return;
+  }
+
+  // ---- compute side ----
+  const int wm = wave / WN, wn = wave % WN;
+  int abase[C::MT];
+#pragma unroll
+  for (int mt = 0; mt < C::MT; ++mt) {
+    const int m = (wm * C::MT + mt) * 32 + r;
+    const int np = m / (TR * C::WOUT), rem = m % (TR * C::WOUT);
+    const int yl = rem / C::WOUT, xo = rem % C::WOUT;
+    abase[mt] = np * C::PS + yl * S * C::RS + xo * 80 + h * 16;
+  }
+  constexpr unsigned CHUNK_BYTES = 9 * 2 * C::NTOT * 2 * 64 * 16;
+  const __amdgpu_buffer_rsrc_t wr_ = make_rsrc(wp, C::NCC * CHUNK_BYTES);
+  const unsigned wvoff = (wn * C::NT * 2 * 64 + lane) * 16;
+  f32x16 acc[C::MT][C::NT];
+#pragma unroll
+  for (int mt = 0; mt < C::MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < C::NT; ++nt) acc[mt][nt] = f32x16{};
+
+#pragma unroll 1
+  for (int s = 0; s < NS; ++s) {
+    const char* cur = (s & 1) ? buf1 : buf0;
+    const int cc = s % C::NCC;
+    const unsigned wsoff = cc * CHUNK_BYTES;
+    constexpr int NKS = 18;
+    uint4 bq[3][C::NT][2];
+    uint4 aq[2][C::MT][2];
+    auto load_b = [&](int ksx, uint4 (&dst)[C::NT][2]) {
+#pragma unroll
+      for (int nt = 0; nt < C::NT; ++nt) {
+        const unsigned k = ((ksx * C::NTOT + nt) * 2) * 64 * 16;
+        dst[nt][0] = buf_load16(wr_, wvoff, wsoff + k);
+        dst[nt][1] = buf_load16(wr_, wvoff, wsoff + k + 64 * 16);
+      }
+    };
+    auto load_a = [&](int ksx, uint4 (&dst)[C::MT][2]) {
+      const int tap = ksx >> 1, ks = ksx & 1;
+      const int toff = (tap / 3) * C::RS + C::colofs(tap % 3) * 80 + ks * 32;
+#pragma unroll
+      for (int mt = 0; mt < C::MT; ++mt) {
+        dst[mt][0] = *reinterpret_cast<const uint4*>(cur + abase[mt] + toff);
+        dst[mt][1] = *reinterpret_cast<const uint4*>(cur + C::PLANE + abase[mt] + toff);
+      }
+    };
+    load_b(0, bq[0]);
+    load_b(1, bq[1]);
+    load_a(0, aq[0]);
+#pragma unroll
+    for (int ksx = 0; ksx < NKS; ++ksx) {
+      if (ksx + 2 < NKS) load_b(ksx + 2, bq[(ksx + 2) % 3]);
+      if (ksx + 1 < NKS) load_a(ksx + 1, aq[(ksx + 1) & 1]);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int mt = 0; mt < C::MT; ++mt) {
+        const bf16x8 xh = as_bf16x8(aq[ksx & 1][mt][0]), xl = as_bf16x8(aq[ksx & 1][mt][1]);
+#pragma unroll
+        for (int nt = 0; nt < C::NT; ++nt)
+          acc[mt][nt] = mfma3(as_bf16x8(bq[ksx % 3][nt][0]), as_bf16x8(bq[ksx % 3][nt][1]), xh, xl,
+                              acc[mt][nt]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (cc == C::NCC - 1) {
+      int p0, y0;
+      tile_of(s, p0, y0);
+      float* obase = out + ((size_t)(p0 * C::HOUT + y0) * C::WOUT + wm * C::MT * 32 + r) * COUT +
+                     wn * C::NT * 32 + 4 * h;
+#pragma unroll
+      for (int nt = 0; nt < C::NT; ++nt) {
+        float4 bv[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          bv[q] = *reinterpret_cast<const float4*>(bias + (wn * C::NT + nt) * 32 + 8 * q + 4 * h);
+#pragma unroll
+        for (int mt = 0; mt < C::MT; ++mt) {
+          const bool ok = NP == 1 || p0 + ((wm * C::MT + mt) * 32) / (TR * C::WOUT) < P;
+          if (ok) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              float4 v;
+              v.x = fmaxf(acc[mt][nt][4 * q + 0] + bv[q].x, 0.f);
+              v.y = fmaxf(acc[mt][nt][4 * q + 1] + bv[q].y, 0.f);
+              v.z = fmaxf(acc[mt][nt][4 * q + 2] + bv[q].z, 0.f);
+              v.w = fmaxf(acc[mt][nt][4 * q + 3] + bv[q].w, 0.f);
+              *reinterpret_cast<float4*>(obase + (size_t)mt * 32 * COUT + nt * 32 + 8 * q) = v;
+            }
+          }
+          acc[mt][nt] = f32x16{};
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------------------------
 // head: [P, K] x [K, 128] + bias, L2 normalise rows.  4 waves = 2 (M) x 2 (N);
 // each wave 32 patches x 64 columns.
 // ------------------------------------------------------------------------------------
@@ -840,6 +1154,44 @@ HN_PIPE_A(pipe3_a2, false, 64, 64, 16, 1, 1, 8, 2, 2, 2)
 HN_PIPE_A(pipe3_a4, false, 64, 64, 16, 1, 1, 8, 2, 2, 4)
 HN_PIPE_A(pipe3_a7, false, 64, 64, 16, 1, 1, 8, 2, 2, 7)
 
+#define HN_WS(NAME, CIN, COUT, HIN, S, NP, TR, WM, WN) HN_WS_S(NAME, false, CIN, COUT, HIN, S, NP, TR, WM, WN)
+#define HN_WS_S(NAME, STEM, CIN, COUT, HIN, S, NP, TR, WM, WN)                             \
+  using NAME##_cfg = WsCfg<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM>;                       \
+  static hipError_t NAME(const float* in, float* out, const void* wp, const float* bias,   \
+                         int P, const float* sw, const float* sb, float eps, hipStream_t st) { \
+    constexpr int lds = NAME##_cfg::SMEM;                                                  \
+    const void* fn =                                                                       \
+        reinterpret_cast<const void*>(&k_conv_ws<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM>); \
+    static int resident = 0;                                                               \
+    if (!resident) {                                                                       \
+      hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds); \
+      if (e != hipSuccess) return e;                                                       \
+      int per_cu = 0, dev = 0, cus = 0;                                                    \
+      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, NAME##_cfg::NTHR, lds); \
+      if (e != hipSuccess) return e;                                                       \
+      (void)hipGetDevice(&dev);                                                            \
+      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);       \
+      resident = std::max(1, per_cu) * std::max(1, cus);                                   \
+    }                                                                                      \
+    const int tiles = (P + NP - 1) / NP * NAME##_cfg::RT;                                  \
+    const int grid = std::min(tiles, resident);                                            \
+    hipLaunchKernelGGL((k_conv_ws<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM>), dim3(grid),   \
+                       dim3(NAME##_cfg::NTHR), lds, st, in, out,                           \
+                       static_cast<const uint4*>(wp), bias, P, sw, sb, eps);               \
+    return hipGetLastError();                                                              \
+  }
+
+HN_WS_S(ws1s, true, 32, 32, 32, 1, 1, 4, 4, 1)
+HN_WS_S(ws1s_t8, true, 32, 32, 32, 1, 1, 8, 4, 1)
+HN_WS(ws2, 32, 64, 32, 2, 1, 4, 2, 2)
+HN_WS(ws2_t2, 32, 64, 32, 2, 1, 2, 1, 2)
+HN_WS(ws3, 64, 64, 16, 1, 1, 8, 2, 2)
+HN_WS(ws3_t16, 64, 64, 16, 1, 1, 16, 2, 2)
+HN_WS(ws4, 64, 128, 16, 2, 1, 4, 1, 4)
+HN_WS(ws4_t8, 64, 128, 16, 2, 1, 8, 1, 4)
+HN_WS(ws5, 128, 128, 8, 1, 1, 8, 1, 4)
+HN_WS(ws5_np2, 128, 128, 8, 1, 2, 8, 1, 4)
+
 hipError_t hn_launch_stem(const float* in, float* out, const float* w, const float* b, int P,
                           bool norm, float eps, hipStream_t st) {
   if (norm)
@@ -853,6 +1205,18 @@ hipError_t hn_launch_stem(const float* in, float* out, const float* w, const flo
 hipError_t hn_launch_hardnet_conv(int layer, int variant, const HardnetDev& d, const float* in,
                                   float* out, int P, float eps, hipStream_t st) {
   const bool v1 = variant == 1;
+  if (variant == 5 || variant == 6) {  // warp-specialised: 5 = smaller tile, 6 = larger
+    const bool big = variant == 6;
+    switch (layer) {
+      case 0:
+        return (big ? ws1s_t8 : ws1s)(in, out, d.wpack[1], d.bias[1], P, d.stem_w, d.stem_b, eps, st);
+      case 2: return (big ? ws2_t2 : ws2)(in, out, d.wpack[2], d.bias[2], P, nullptr, nullptr, 0.f, st);
+      case 3: return (big ? ws3_t16 : ws3)(in, out, d.wpack[3], d.bias[3], P, nullptr, nullptr, 0.f, st);
+      case 4: return (big ? ws4_t8 : ws4)(in, out, d.wpack[4], d.bias[4], P, nullptr, nullptr, 0.f, st);
+      case 5: return (big ? ws5_np2 : ws5)(in, out, d.wpack[5], d.bias[5], P, nullptr, nullptr, 0.f, st);
+    }
+    return hipErrorInvalidValue;
+  }
   if (layer == 3 && variant >= 4) {
     auto f = variant == 4 ? pipe3_a1 : variant == 5 ? pipe3_a2 : variant == 6 ? pipe3_a4 : pipe3_a7;
     return f(in, out, d.wpack[3], d.bias[3], P, nullptr, nullptr, 0.f, st);

@@ -23,6 +23,7 @@ CONFIGS = {
     "4v1": (64, 128, 16, 2, 1, 4, 1, 4),
     "5": (128, 128, 8, 1, 2, 8, 1, 4),
     "5v1": (128, 128, 8, 1, 1, 8, 1, 4),
+    "2t2": (32, 64, 32, 2, 1, 2, 1, 2),
 }
 
 
@@ -82,3 +83,5 @@ def test_conv_window_reads_conflict_free(layer):
 def test_conv_lds_fits(layer):
     g = geometry(*CONFIGS[layer])
     assert g["lds"] <= 160 * 1024
+    cin, cout = CONFIGS[layer][0], CONFIGS[layer][1]
+    assert cin % 32 == 0 and cout % (32 * CONFIGS[layer][7]) == 0
