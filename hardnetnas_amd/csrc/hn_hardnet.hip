@@ -1059,6 +1059,108 @@ __global__ __launch_bounds__(256) void k_head(const float* __restrict__ a, float
 }
 
 // ------------------------------------------------------------------------------------
+// k_head2: the same GEMM + bias + L2 with both operands staged through double-buffered LDS
+// in K-chunks of 32: all global loads of chunk c+1 are issued before the MFMAs of chunk c
+// (A rows fp32 -> bf16 hi/lo, 80-byte rows = conflict-free ds_read_b128; B fragments
+// copied linearly), so the K-loop reads only LDS.  4 waves = 2 (M: 32 patches) x 2 (N: 64).
+// ------------------------------------------------------------------------------------
+template <int K>
+__global__ __launch_bounds__(256) void k_head2(const float* __restrict__ a, float* __restrict__ out,
+                                               const uint4* __restrict__ wp,
+                                               const float* __restrict__ bias, int P, float l2eps) {
+  constexpr int KC = 32, NCH = K / KC;
+  constexpr int AROW = 80;                    // bytes per patch row per plane (64 data + 16 pad)
+  constexpr int APLANE = 64 * AROW;           // 64 patches
+  constexpr int ABYTES = 2 * APLANE;          // hi + lo
+  constexpr int BBYTES = 2 * 4 * 2 * 64 * 16;  // 2 k-steps x 4 ntiles x 2 planes x 1 KB
+  constexpr int BUF = ABYTES + BBYTES;
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+  __shared__ float ssq[2][64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int r = lane & 31, h = lane >> 5;
+  const int pbase = blockIdx.x * 64;
+  // staging assignment: A = 64 rows x 32 fp32 = 512 float4 (2 per thread);
+  // B = 2 ks x 4 nt x 2 planes x 64 lanes = 1024 uint4 (4 per thread)
+  const int arow0 = tid >> 3, acol = (tid & 7) * 4;  // rows arow0 and arow0 + 32
+  const int pa0 = min(pbase + arow0, P - 1), pa1 = min(pbase + arow0 + 32, P - 1);
+  float4 ra0, ra1;
+  uint4 rb0, rb1, rb2, rb3;  // named registers: an indexed array here ends up in scratch
+#define HN_LOAD_CHUNK(c)                                                                   \
+  {                                                                                        \
+    ra0 = *reinterpret_cast<const float4*>(a + (size_t)pa0 * K + (c) * KC + acol);         \
+    ra1 = *reinterpret_cast<const float4*>(a + (size_t)pa1 * K + (c) * KC + acol);         \
+    const uint4* wc_ = wp + (size_t)(c) * 1024 + tid;                                      \
+    rb0 = wc_[0]; rb1 = wc_[256]; rb2 = wc_[512]; rb3 = wc_[768];                          \
+  }
+  auto put_row = [&](char* buf, int row, const float4 v) {
+    bf16x4 hi, lo;
+    hi[0] = (__bf16)v.x; lo[0] = (__bf16)(v.x - (float)hi[0]);
+    hi[1] = (__bf16)v.y; lo[1] = (__bf16)(v.y - (float)hi[1]);
+    hi[2] = (__bf16)v.z; lo[2] = (__bf16)(v.z - (float)hi[2]);
+    hi[3] = (__bf16)v.w; lo[3] = (__bf16)(v.w - (float)hi[3]);
+    *reinterpret_cast<uint2*>(buf + row * AROW + acol * 2) = __builtin_bit_cast(uint2, hi);
+    *reinterpret_cast<uint2*>(buf + APLANE + row * AROW + acol * 2) = __builtin_bit_cast(uint2, lo);
+  };
+#define HN_STORE_CHUNK(buf)                                                                \
+  {                                                                                        \
+    put_row(buf, arow0, ra0);                                                              \
+    put_row(buf, arow0 + 32, ra1);                                                         \
+    uint4* bd_ = reinterpret_cast<uint4*>(buf + ABYTES) + tid;                             \
+    bd_[0] = rb0; bd_[256] = rb1; bd_[512] = rb2; bd_[768] = rb3;                          \
+  }
+  f32x16 acc[2] = {f32x16{}, f32x16{}};
+  HN_LOAD_CHUNK(0)
+  HN_STORE_CHUNK(smem)
+  __syncthreads();
+#pragma unroll 1
+  for (int c = 0; c < NCH; ++c) {
+    const char* cur = smem + (c & 1) * BUF;
+    if (c + 1 < NCH) HN_LOAD_CHUNK(c + 1)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int aoff = (wm * 32 + r) * AROW + ks * 32 + h * 16;
+      const bf16x8 ah = as_bf16x8(*reinterpret_cast<const uint4*>(cur + aoff));
+      const bf16x8 al = as_bf16x8(*reinterpret_cast<const uint4*>(cur + APLANE + aoff));
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        const int boff = ABYTES + (((ks * 4 + wn * 2 + nt) * 2) * 64 + lane) * 16;
+        const bf16x8 bh = as_bf16x8(*reinterpret_cast<const uint4*>(cur + boff));
+        const bf16x8 bl = as_bf16x8(*reinterpret_cast<const uint4*>(cur + boff + 64 * 16));
+        acc[nt] = mfma3(ah, al, bh, bl, acc[nt]);
+      }
+    }
+    if (c + 1 < NCH) HN_STORE_CHUNK(smem + ((c + 1) & 1) * BUF)
+    __syncthreads();
+  }
+#undef HN_LOAD_CHUNK
+#undef HN_STORE_CHUNK
+  const float b0 = bias[wn * 64 + r], b1 = bias[wn * 64 + 32 + r];
+  float part[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    acc[0][i] += b0;
+    acc[1][i] += b1;
+    part[i] = half_sum(acc[0][i] * acc[0][i] + acc[1][i] * acc[1][i]);
+  }
+  if (r == 0) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) ssq[wn][wm * 32 + (i & 3) + 8 * (i >> 2) + 4 * h] = part[i];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int row = (i & 3) + 8 * (i >> 2) + 4 * h;
+    const int p = pbase + wm * 32 + row;
+    const float norm = sqrtf(ssq[0][wm * 32 + row] + ssq[1][wm * 32 + row] + l2eps);
+    if (p < P) {
+      out[(size_t)p * 128 + wn * 64 + r] = acc[0][i] / norm;
+      out[(size_t)p * 128 + wn * 64 + 32 + r] = acc[1][i] / norm;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
 // host launchers
 // ------------------------------------------------------------------------------------
 static int g_dbg = -1;  // HN_DEBUG bits: 1 = skip conv epilogue stores (ablation only)
@@ -1253,11 +1355,15 @@ hipError_t hn_launch_hardnet_conv(int layer, int variant, const HardnetDev& d, c
 hipError_t hn_launch_head(const float* a, float* out, const void* wp, const float* bias, int P,
                           int K, float l2eps, hipStream_t st) {
   const int grid = (P + 63) / 64;
-  if (K == 8192)
+  static int old = -1;
+  if (old < 0) old = std::getenv("HN_HEAD_V1") ? 1 : 0;
+  if (K != 8192) return hipErrorInvalidValue;
+  if (old)
     hipLaunchKernelGGL(k_head<8192>, dim3(grid), dim3(256), 0, st, a, out,
                        static_cast<const uint4*>(wp), bias, P, l2eps);
   else
-    return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_head2<8192>, dim3(grid), dim3(256), 0, st, a, out,
+                       static_cast<const uint4*>(wp), bias, P, l2eps);
   return hipGetLastError();
 }
 
