@@ -200,6 +200,66 @@ __global__ __launch_bounds__(256) void k_dw(const float* __restrict__ in, float*
   *reinterpret_cast<float4*>(out + (((p * hout) + yo) * (long)hout + xo) * c + c4) = acc;
 }
 
+// LDS-staged depthwise conv: one workgroup = (patch, strip of T output rows, 32-channel
+// group).  The zero-padded input strip [(T-1)*S+K rows][W+K-1 cols][32 ch] fp32 and the
+// tap weights are staged once; each thread then computes 4 channels of output pixels from
+// LDS (ds_read_b128: for S = 1 the 16-lane groups hit 16 distinct slots).
+template <int K, int S, int HIN, int T>
+__global__ __launch_bounds__(256) void k_dw_lds(const float* __restrict__ in, float* __restrict__ out,
+                                                const float* __restrict__ wd,  // [K*K][C]
+                                                const float* __restrict__ bias, int P, int c) {
+  constexpr int HOUT = HIN / S, PAD = K / 2;
+  constexpr int RIN = (T - 1) * S + K, WIN = HIN + K - 1;
+  constexpr int ROWB = WIN * 32;  // floats per LDS row
+  __shared__ __attribute__((aligned(16))) float xs[RIN * ROWB];
+  __shared__ __attribute__((aligned(16))) float ws[K * K * 32];
+  const int t = threadIdx.x;
+  const int ngrp = c / 32;
+  const int strips = HOUT / T;
+  const int bid = blockIdx.x;
+  const int cg = bid % ngrp, st = (bid / ngrp) % strips;
+  const long p = bid / ngrp / strips;
+  const int y0 = st * T;                 // first output row
+  const int iy0 = y0 * S - PAD;          // first input row of the strip
+  const float* src = in + p * HIN * HIN * c + cg * 32;
+  for (int e = t; e < RIN * WIN * 8; e += 256) {
+    const int q = e & 7, pix = e >> 3;
+    const int col = pix % WIN, row = pix / WIN;
+    const int y = iy0 + row, x = col - PAD;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if ((unsigned)y < (unsigned)HIN && (unsigned)x < (unsigned)HIN)
+      v = *reinterpret_cast<const float4*>(src + ((long)y * HIN + x) * c + q * 4);
+    *reinterpret_cast<float4*>(&xs[row * ROWB + col * 32 + q * 4]) = v;
+  }
+  for (int e = t; e < K * K * 8; e += 256) {
+    const int q = e & 7, tap = e >> 3;
+    *reinterpret_cast<float4*>(&ws[tap * 32 + q * 4]) =
+        *reinterpret_cast<const float4*>(wd + (long)tap * c + cg * 32 + q * 4);
+  }
+  __syncthreads();
+  const int q = t & 7;
+  const float4 b = *reinterpret_cast<const float4*>(bias + cg * 32 + q * 4);
+  for (int o = t >> 3; o < T * HOUT; o += 32) {
+    const int yo = o / HOUT, xo = o % HOUT;
+    float4 acc = b;
+#pragma unroll
+    for (int ky = 0; ky < K; ++ky)
+#pragma unroll
+      for (int kx = 0; kx < K; ++kx) {
+        const float4 v =
+            *reinterpret_cast<const float4*>(&xs[(yo * S + ky) * ROWB + (xo * S + kx) * 32 + q * 4]);
+        const float4 w = *reinterpret_cast<const float4*>(&ws[(ky * K + kx) * 32 + q * 4]);
+        acc.x = fmaf(v.x, w.x, acc.x);
+        acc.y = fmaf(v.y, w.y, acc.y);
+        acc.z = fmaf(v.z, w.z, acc.z);
+        acc.w = fmaf(v.w, w.w, acc.w);
+      }
+    acc.x = fmaxf(acc.x, 0.f); acc.y = fmaxf(acc.y, 0.f);
+    acc.z = fmaxf(acc.z, 0.f); acc.w = fmaxf(acc.w, 0.f);
+    *reinterpret_cast<float4*>(out + ((p * HOUT + y0 + yo) * (long)HOUT + xo) * c + cg * 32 + q * 4) = acc;
+  }
+}
+
 __global__ __launch_bounds__(256) void k_maxpool(const float* __restrict__ in, float* __restrict__ out,
                                                  int P, int hin, int c) {
   const int hout = hin / 2, cq = c >> 2;
@@ -316,9 +376,29 @@ hipError_t hn_launch_pw(const float* in, float* out, const float* wt, const floa
   return hipGetLastError();
 }
 
+template <int K, int S, int HIN, int T>
+static hipError_t dw_lds(const float* in, float* out, const float* wd, const float* bias, int P,
+                         int c, hipStream_t st) {
+  const unsigned grid = (unsigned)P * (HIN / S / T) * (c / 32);
+  hipLaunchKernelGGL((k_dw_lds<K, S, HIN, T>), dim3(grid), dim3(256), 0, st, in, out, wd, bias, P, c);
+  return hipGetLastError();
+}
+
 hipError_t hn_launch_dw(const float* in, float* out, const float* wd, const float* bias, int P,
                         int hin, int c, int k, int s, hipStream_t st) {
   const int hout = hin / s;
+  static int naive = -1;
+  if (naive < 0) naive = std::getenv("HN_NAIVE_DW") ? 1 : 0;
+  if (!naive && c % 32 == 0) {
+    // strips of T output rows: LDS <= ~60 KB for every SEARCH_SPACE2 shape
+#define HN_DWCASE(KK, SS, HH, TT) \
+  if (k == KK && s == SS && hin == HH) return dw_lds<KK, SS, HH, TT>(in, out, wd, bias, P, c, st);
+    HN_DWCASE(3, 1, 32, 8) HN_DWCASE(3, 2, 32, 4) HN_DWCASE(5, 1, 32, 8) HN_DWCASE(5, 2, 32, 4)
+    HN_DWCASE(3, 1, 16, 8) HN_DWCASE(3, 2, 16, 8) HN_DWCASE(5, 1, 16, 8) HN_DWCASE(5, 2, 16, 8)
+    HN_DWCASE(3, 1, 8, 8) HN_DWCASE(3, 2, 8, 4) HN_DWCASE(5, 1, 8, 8) HN_DWCASE(5, 2, 8, 4)
+    HN_DWCASE(3, 1, 4, 4) HN_DWCASE(5, 1, 4, 4)
+#undef HN_DWCASE
+  }
   const unsigned g = blocks((long)P * hout * hout * (c / 4), 256);
   if (k == 3)
     hipLaunchKernelGGL(k_dw<3>, dim3(g), dim3(256), 0, st, in, out, wd, bias, P, hin, c, s);
