@@ -43,7 +43,8 @@ class HnArchDesc(ctypes.Structure):
 
 
 EXPORTED = ["hn_param_count", "hn_create", "hn_workspace_bytes", "hn_forward",
-            "hn_pairdist_workspace_bytes", "hn_pairdist_hardneg", "hn_set_profiling",
+            "hn_pairdist_workspace_bytes", "hn_pairdist_hardneg", "hn_fpr95_workspace_bytes",
+            "hn_fpr95", "hn_set_profiling",
             "hn_stage_times", "hn_destroy", "hn_last_error", "hn_abi_version"]
 
 
@@ -73,6 +74,8 @@ def load_library():
         lib.hn_forward.argtypes = [P, P, I64, P, P, S, P]
         lib.hn_pairdist_workspace_bytes.argtypes = [I64, ctypes.POINTER(S)]
         lib.hn_pairdist_hardneg.argtypes = [P, P, I64, I32, I32, P, P, P, S, P]
+        lib.hn_fpr95_workspace_bytes.argtypes = [I64, ctypes.POINTER(S)]
+        lib.hn_fpr95.argtypes = [P, P, P, I64, I32, P, P, P, S, P]
         lib.hn_set_profiling.argtypes = [P, ctypes.c_int]
         lib.hn_stage_times.argtypes = [P, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),
                                        ctypes.POINTER(ctypes.c_double), ctypes.POINTER(I64)]
@@ -81,7 +84,8 @@ def load_library():
         lib.hn_last_error.restype = ctypes.c_char_p
         for name in ("hn_param_count", "hn_create", "hn_workspace_bytes", "hn_forward",
                      "hn_pairdist_workspace_bytes", "hn_pairdist_hardneg", "hn_abi_version",
-                     "hn_set_profiling", "hn_stage_times"):
+                     "hn_set_profiling", "hn_stage_times", "hn_fpr95_workspace_bytes",
+                     "hn_fpr95"):
             getattr(lib, name).restype = ctypes.c_int
         _lib = lib
         return lib
@@ -236,3 +240,25 @@ def pairdist_hardneg(anchor: torch.Tensor, positive: torch.Tensor, anchor_swap: 
                                        pos.data_ptr(), mn.data_ptr(), ws.data_ptr(), ws.numel(),
                                        stream), "hn_pairdist_hardneg")
     return pos, mn
+
+
+def fpr95(out_a: torch.Tensor, out_p: torch.Tensor, labels: torch.Tensor):
+    """(fpr95, pair distances) on device: the eval loop of hardnet/HardNet.py:450-472
+    (``sqrt(sum((a-p)^2))`` per pair) + ``ErrorRateAt95Recall`` (EvalMetrics.py:6-19)."""
+    lib = load_library()
+    if out_a.shape != out_p.shape or out_a.dim() != 2 or labels.numel() != out_a.shape[0]:
+        raise ValueError("expected [n,D] descriptors and [n] labels")
+    a = out_a.contiguous().float()
+    p = out_p.contiguous().float()
+    lab = labels.to(device=a.device, dtype=torch.int32).contiguous()
+    n, d = a.shape
+    sz = ctypes.c_size_t()
+    _check(lib.hn_fpr95_workspace_bytes(n, ctypes.byref(sz)), "hn_fpr95_workspace_bytes")
+    ws = torch.empty(max(sz.value, 16), device=a.device, dtype=torch.uint8)
+    dists = torch.empty(n, device=a.device, dtype=torch.float32)
+    res = torch.empty(1, device=a.device, dtype=torch.float64)
+    stream = torch.cuda.current_stream(a.device).cuda_stream
+    with torch.cuda.device(a.device):
+        _check(lib.hn_fpr95(a.data_ptr(), p.data_ptr(), lab.data_ptr(), n, d, dists.data_ptr(),
+                            res.data_ptr(), ws.data_ptr(), ws.numel(), stream), "hn_fpr95")
+    return float(res.item()), dists

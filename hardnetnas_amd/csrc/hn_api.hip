@@ -591,6 +591,26 @@ extern "C" int hn_pairdist_hardneg(const float* d_anchor, const float* d_positiv
   return HN_OK;
 }
 
+extern "C" int hn_fpr95_workspace_bytes(int64_t n, size_t* bytes_out) {
+  if (!bytes_out || n < 1 || n > (int64_t)1 << 30) return fail(HN_ERR_ARG, "n out of range");
+  HIPCHK(hn_fpr95_ws_bytes(n, bytes_out));
+  return HN_OK;
+}
+
+extern "C" int hn_fpr95(const float* d_anchor, const float* d_positive, const int32_t* d_labels,
+                        int64_t n, int32_t dim, float* d_dists, double* d_fpr, void* d_workspace,
+                        size_t workspace_bytes, void* hip_stream) {
+  if (!d_anchor || !d_positive || !d_labels || !d_fpr || !d_workspace)
+    return fail(HN_ERR_ARG, "NULL device pointer");
+  if (n < 1 || n > (int64_t)1 << 30 || dim < 1) return fail(HN_ERR_ARG, "bad n / dim");
+  size_t need = 0;
+  HIPCHK(hn_fpr95_ws_bytes(n, &need));
+  if (workspace_bytes < need) return fail(HN_ERR_WORKSPACE, "workspace too small");
+  HIPCHK(hn_launch_fpr95(d_anchor, d_positive, d_labels, n, dim, d_dists, d_fpr, d_workspace,
+                         workspace_bytes, static_cast<hipStream_t>(hip_stream)));
+  return HN_OK;
+}
+
 extern "C" int hn_set_profiling(hn_model* m, int enable) {
   if (!m) return fail(HN_ERR_ARG, "model is NULL");
   m->prof.on = enable != 0;

@@ -101,6 +101,17 @@ int hn_pairdist_hardneg(const float* d_anchor, const float* d_positive, int64_t 
                         int32_t anchor_swap, float* d_pos, float* d_min_neg,
                         void* d_workspace, size_t workspace_bytes, void* hip_stream);
 
+/* FPR at 95 % recall of an evaluation batch of descriptor pairs (hardnet/HardNet.py:450-472
+ * + hardnet/EvalMetrics.py:6-19): per-pair L2 distance, scores -> distances transform, sort,
+ * first index reaching 95 % recall, FP / (FP + TN).
+ * d_anchor, d_positive: [n,dim] fp32; d_labels: [n] int32 (1 = match).  Outputs: d_dists
+ * ([n] fp32 pair distances, may be NULL) and d_fpr (one double; NaN if there are no
+ * negatives).  Ties are ordered stably (numpy's quicksort order is unspecified). */
+int hn_fpr95_workspace_bytes(int64_t n, size_t* bytes_out);
+int hn_fpr95(const float* d_anchor, const float* d_positive, const int32_t* d_labels, int64_t n,
+             int32_t dim, float* d_dists, double* d_fpr, void* d_workspace, size_t workspace_bytes,
+             void* hip_stream);
+
 /* Per-stage timing (profiling aid used by bench.py): when enabled, hn_forward records a
  * hipEvent pair around every kernel launch on the caller's stream.  hn_stage_times
  * waits for the recorded events, accumulates their durations per stage name and returns

@@ -174,3 +174,36 @@ def test_pairdist_hardneg_matches_oracle(b, swap, cuda_device):
     rpos, rmn = O.hardest_negative(a.double(), p.double(), swap)
     assert (pos.cpu().double() - rpos).abs().max().item() < 1e-4
     assert (mn.cpu().double() - rmn).abs().max().item() < 1e-4
+
+
+def test_fpr95_matches_reference_vectors(cuda_device):
+    """Device FPR95 vs ErrorRateAt95Recall (reference-generated values, tests/golden/losses.npz)
+    using descriptors whose pair distances equal the fixture distances."""
+    from hardnetnas_amd._native import fpr95
+    fx = load("losses")
+    for lab_k, dist_k, want_k in (("fpr_kat_labels", "fpr_kat_dists", "fpr_kat"),
+                                  ("fpr_labels", "fpr_dists", "fpr")):
+        labels = torch.from_numpy(fx[lab_k].astype(np.int32))
+        d = torch.from_numpy(fx[dist_k].astype(np.float32))
+        a = torch.zeros(len(d), 128)
+        p = torch.zeros(len(d), 128)
+        p[:, 0] = d                       # |a - p| = d exactly
+        got, dd = fpr95(a.to(cuda_device), p.to(cuda_device), labels.to(cuda_device))
+        assert torch.allclose(dd.cpu(), d, rtol=1e-6, atol=0)
+        # fp32 keys vs the reference's float64: an adjacent swap could move one sample
+        assert got == pytest.approx(float(fx[want_k]), abs=2.0 / len(d))
+
+
+def test_fpr95_on_descriptors_matches_oracle(cuda_device):
+    from hardnetnas_amd._native import fpr95
+    g = torch.Generator().manual_seed(7)
+    n = 20000
+    a = torch.nn.functional.normalize(torch.randn(n, 128, generator=g), dim=1)
+    lab = (torch.rand(n, generator=g) > 0.5).int()
+    noise = torch.where(lab[:, None] == 1, 0.4, 1.5) * torch.randn(n, 128, generator=g)
+    p = torch.nn.functional.normalize(a + noise, dim=1)
+    got, dd = fpr95(a.to(cuda_device), p.to(cuda_device), lab.to(cuda_device))
+    d_ref = torch.sqrt(torch.sum((a - p) ** 2, 1)).numpy()
+    ref = O.error_rate_at_95_recall(lab.numpy(), 1.0 / (d_ref + 1e-8))
+    assert np.abs(dd.cpu().numpy() - d_ref).max() < 1e-6
+    assert got == pytest.approx(ref, abs=2.0 / n)   # tie order may move one sample
