@@ -571,7 +571,9 @@ extern "C" int hn_forward(hn_model* m, const float* d_in, int64_t batch, float* 
 
 extern "C" int hn_pairdist_workspace_bytes(int64_t batch, size_t* bytes_out) {
   if (!bytes_out || batch < 0) return fail(HN_ERR_ARG, "bad argument");
-  *bytes_out = (size_t)(batch > 0 ? batch : 1) * sizeof(float);
+  // column minima + |a|^2 + |p|^2 (each padded to 64 entries)
+  const size_t n = (size_t)((batch > 0 ? batch : 1) + 63) / 64 * 64;
+  *bytes_out = 3 * n * sizeof(float);
   return HN_OK;
 }
 

@@ -11,6 +11,8 @@
 #include "hn_common.h"
 #include "hn_internal.h"
 
+#include <cstdlib>
+
 namespace {
 constexpr int TM = 64, TN = 64, D = 128, LDP = D + 4;
 
@@ -120,6 +122,147 @@ __global__ __launch_bounds__(256) void k_combine(float* rowmin, const unsigned* 
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i < B) rowmin[i] = fminf(rowmin[i], __uint_as_float(colmin[i]));
 }
+// ---------------------------------------------------------------------------------------
+// MFMA version.  x(i,j) = (|a_i|^2 + |p_j|^2) - 2 a_i.p_j with the dot on the bf16 MFMA in
+// bf16x3 split precision; dm = sqrt(x + 1e-6) + 1e-8 is monotone in x, so minima are
+// tracked on x: per anchor row the min over unmasked off-diagonal entries (xu) and over the
+// +10 entries (diagonal and dm < 0.008, xm); min_neg = xu exists ? dm(xu) : dm(xm) + 10 --
+// exactly the reference's min over (dm + 10*eye + 10*[dm + 10*eye < 0.008]).  pos (the
+// diagonal) is recomputed in exact fp32 by k_pos.  One workgroup = 128 anchors (4 waves x
+// 32, A fragments resident in registers) sweeping positives in double-buffered LDS tiles
+// of 64 (rows padded to 272 B: conflict-free ds_read_b128).
+// ---------------------------------------------------------------------------------------
+constexpr float kDm8Thr = (0.008f - 1e-8f);  // dm < 0.008  <=>  sqrt(x+1e-6) < 0.008 - 1e-8
+
+__device__ __forceinline__ float dm_of(float x) { return sqrtf(x + 1e-6f) + 1e-8f; }
+
+__global__ __launch_bounds__(256) void k_sq(const float* __restrict__ v, int B, float* __restrict__ sq) {
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (i >= B) return;
+  const float a0 = v[(size_t)i * 128 + lane], a1 = v[(size_t)i * 128 + 64 + lane];
+  const float s = wave_sum(a0 * a0 + a1 * a1);
+  if (lane == 0) sq[i] = s;
+}
+
+__global__ __launch_bounds__(256) void k_pos(const float* __restrict__ a, const float* __restrict__ p,
+                                             const float* __restrict__ asq, const float* __restrict__ psq,
+                                             int B, float* __restrict__ pos) {
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (i >= B) return;
+  const float d = wave_sum(a[(size_t)i * 128 + lane] * p[(size_t)i * 128 + lane] +
+                           a[(size_t)i * 128 + 64 + lane] * p[(size_t)i * 128 + 64 + lane]);
+  if (lane == 0) pos[i] = dm_of((asq[i] + psq[i]) - 2.0f * d);
+}
+
+__global__ __launch_bounds__(256) void k_pairdist_mfma(const float* __restrict__ a, const float* __restrict__ p,
+                                                       const float* __restrict__ asq,
+                                                       const float* __restrict__ psq, int B, int swap,
+                                                       float* __restrict__ rowmin,
+                                                       unsigned* __restrict__ colmin) {
+  constexpr int TN = 64, ROWB = 272, PLANE = TN * ROWB, BUF = 2 * PLANE + TN * 4;
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int i0 = blockIdx.x * 128 + wave * 32;  // this wave's anchors
+  // A fragments: lane (r, h) holds anchor i0+r, k = 16 ks + 8 h + j
+  bf16x8 ah[8], al[8];
+  {
+    const int ia = min(i0 + r, B - 1);
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      const float4 x0 = *reinterpret_cast<const float4*>(a + (size_t)ia * 128 + ks * 16 + h * 8);
+      const float4 x1 = *reinterpret_cast<const float4*>(a + (size_t)ia * 128 + ks * 16 + h * 8 + 4);
+      uint4 hi, lo;
+      split8(x0, x1, hi, lo);
+      ah[ks] = as_bf16x8(hi);
+      al[ks] = as_bf16x8(lo);
+    }
+  }
+  float arow[16];  // |a|^2 of the rows this lane's accumulator registers hold
+#pragma unroll
+  for (int i = 0; i < 16; ++i) arow[i] = asq[min(i0 + (i & 3) + 8 * (i >> 2) + 4 * h, B - 1)];
+  float xu[16], xm[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) { xu[i] = INFINITY; xm[i] = INFINITY; }
+
+  // P tile staging: 64 rows x 128 fp32 = 2048 float4 -> 8 per thread
+  const int srow = tid >> 2, scol = (tid & 3) * 32;  // each thread: 32 consecutive floats of one row
+  float4 pr[8];
+  auto load_tile = [&](int j0) {
+    const int jr = min(j0 + srow, B - 1);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) pr[q] = *reinterpret_cast<const float4*>(p + (size_t)jr * 128 + scol + q * 4);
+  };
+  auto store_tile = [&](char* buf, int j0) {
+#pragma unroll
+    for (int q = 0; q < 8; q += 2) {
+      uint4 hi, lo;
+      split8(pr[q], pr[q + 1], hi, lo);
+      *reinterpret_cast<uint4*>(buf + srow * ROWB + (scol + q * 4) * 2) = hi;
+      *reinterpret_cast<uint4*>(buf + PLANE + srow * ROWB + (scol + q * 4) * 2) = lo;
+    }
+    if (tid < TN) reinterpret_cast<float*>(buf + 2 * PLANE)[tid] = psq[min(j0 + tid, B - 1)];
+  };
+  const int ntile = (B + TN - 1) / TN;
+  load_tile(0);
+  store_tile(smem, 0);
+  __syncthreads();
+#pragma unroll 1
+  for (int t = 0; t < ntile; ++t) {
+    const char* cur = smem + (t & 1) * BUF;
+    const int j0 = t * TN;
+    if (t + 1 < ntile) load_tile(j0 + TN);
+    const float* ps = reinterpret_cast<const float*>(cur + 2 * PLANE);
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      f32x16 acc{};
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) {
+        const int off = (nt * 32 + r) * ROWB + (ks * 16 + h * 8) * 2;
+        const bf16x8 bh = as_bf16x8(*reinterpret_cast<const uint4*>(cur + off));
+        const bf16x8 bl = as_bf16x8(*reinterpret_cast<const uint4*>(cur + PLANE + off));
+        acc = mfma3(ah[ks], al[ks], bh, bl, acc);
+      }
+      const int j = j0 + nt * 32 + r;  // this lane's column
+      const float pj = ps[nt * 32 + r];
+      float cu = INFINITY, cm = INFINITY;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int row = i0 + (i & 3) + 8 * (i >> 2) + 4 * h;
+        const float x = (arow[i] + pj) - 2.0f * acc[i];
+        const bool valid = j < B && row < B;
+        const bool plus10 = row == j || sqrtf(fmaxf(x + 1e-6f, 0.f)) < kDm8Thr;
+        const float xv = valid ? x : INFINITY;
+        if (plus10) { xm[i] = fminf(xm[i], xv); cm = fminf(cm, xv); }
+        else { xu[i] = fminf(xu[i], xv); cu = fminf(cu, xv); }
+      }
+      if (swap) {
+        cu = fminf(cu, __shfl_xor(cu, 32, 64));
+        cm = fminf(cm, __shfl_xor(cm, 32, 64));
+        if (h == 0 && j < B) {
+          const float ce = fminf(cu < INFINITY ? dm_of(cu) : INFINITY,
+                                 cm < INFINITY ? dm_of(cm) + 10.f : INFINITY);
+          if (ce < INFINITY) atomicMin(colmin + j, __float_as_uint(ce));
+        }
+      }
+    }
+    if (t + 1 < ntile) store_tile(smem + ((t + 1) & 1) * BUF, j0 + TN);
+    __syncthreads();
+  }
+  // row minima: reduce over the 32 lanes of each half-wave (the columns)
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    float u = xu[i], m = xm[i];
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) {
+      u = fminf(u, __shfl_xor(u, o, 64));
+      m = fminf(m, __shfl_xor(m, o, 64));
+    }
+    const int row = i0 + (i & 3) + 8 * (i >> 2) + 4 * h;
+    if (r == 0 && row < B) rowmin[row] = u < INFINITY ? dm_of(u) : dm_of(m) + 10.f;
+  }
+}
+
 }  // namespace
 
 hipError_t hn_launch_pairdist(const float* a, const float* p, int B, int D_, int swap,
@@ -127,6 +270,20 @@ hipError_t hn_launch_pairdist(const float* a, const float* p, int B, int D_, int
   if (D_ != D) return hipErrorInvalidValue;
   unsigned* cm = static_cast<unsigned*>(ws);
   const unsigned g = (B + 255) / 256;
+  static int valu = -1;
+  if (valu < 0) valu = std::getenv("HN_PAIRDIST_VALU") ? 1 : 0;
+  if (!valu) {
+    float* asq = reinterpret_cast<float*>(cm + ((B + 63) / 64) * 64);
+    float* psq = asq + ((B + 63) / 64) * 64;
+    if (swap) hipLaunchKernelGGL(k_colmin_init, dim3(g), dim3(256), 0, st, cm, B);
+    hipLaunchKernelGGL(k_sq, dim3((B + 3) / 4), dim3(256), 0, st, a, B, asq);
+    hipLaunchKernelGGL(k_sq, dim3((B + 3) / 4), dim3(256), 0, st, p, B, psq);
+    hipLaunchKernelGGL(k_pos, dim3((B + 3) / 4), dim3(256), 0, st, a, p, asq, psq, B, pos);
+    hipLaunchKernelGGL(k_pairdist_mfma, dim3((B + 127) / 128), dim3(256), 0, st, a, p, asq, psq,
+                       B, swap, minneg, cm);
+    if (swap) hipLaunchKernelGGL(k_combine, dim3(g), dim3(256), 0, st, minneg, cm, B);
+    return hipGetLastError();
+  }
   if (swap) hipLaunchKernelGGL(k_colmin_init, dim3(g), dim3(256), 0, st, cm, B);
   hipLaunchKernelGGL(k_pairdist, dim3((B + TM - 1) / TM), dim3(256), 0, st, a, p, B, swap, pos,
                      minneg, cm);
