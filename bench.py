@@ -97,6 +97,10 @@ def build_model(name: str):
     return m.eval()
 
 
+# BASELINE config 4: 16,777,216 patches sharded over 8 ranks (weak scaling: fixed per rank)
+CONFIG4_PER_RANK = 16_777_216 // 8
+
+
 def synth_input_on_device(b: int, device, seed: int) -> torch.Tensor:
     g = torch.Generator(device=device).manual_seed(seed)
     q = torch.randint(0, 256, (b, 1, 32, 32), device=device, generator=g, dtype=torch.int32)
@@ -155,7 +159,9 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--model", default="hardnet")
-    ap.add_argument("--batch", type=int, default=262144, help="patches per GPU per step")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="patches per GPU per step (default: 262,144 = BASELINE config 2 at N=1; "
+                         "2,097,152 per rank = config 4's 16.7M patches over 8 GPUs when N > 1)")
     ap.add_argument("--no-allgather", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -174,6 +180,8 @@ def main():
     model = build_model(args.model)
     nm = NativeModel.from_module(model, dev)
     b = args.batch
+    if b is None:
+        b = CONFIG4_PER_RANK if (world > 1 and args.model == "hardnet") else 262144
     x = synth_input_on_device(b, dev, seed=1000 + rank)
     out = torch.empty((b, 128), device=dev)
     ws = torch.empty(nm.workspace_bytes(b), device=dev, dtype=torch.uint8)
@@ -250,6 +258,7 @@ def main():
             "config": {"workload": ("Stock HardNet forward" if args.model == "hardnet"
                                     else f"hardnetNAS {args.model} forward")
                        + f", {b} synthetic 32x32 patches per GPU"
+                       + (" (BASELINE config 4 per-rank shard)" if world > 1 and b == CONFIG4_PER_RANK else "")
                        + (", RCCL all-gather of descriptors" if world > 1 and not args.no_allgather else ""),
                        "model": args.model, "global_batch": b * world, "per_gpu_batch": b,
                        "parallelism": f"dp{world}",

@@ -44,7 +44,7 @@ class HnArchDesc(ctypes.Structure):
 
 EXPORTED = ["hn_param_count", "hn_create", "hn_workspace_bytes", "hn_forward",
             "hn_pairdist_workspace_bytes", "hn_pairdist_hardneg", "hn_fpr95_workspace_bytes",
-            "hn_fpr95", "hn_set_profiling",
+            "hn_fpr95", "hn_preprocess", "hn_set_profiling",
             "hn_stage_times", "hn_destroy", "hn_last_error", "hn_abi_version"]
 
 
@@ -76,6 +76,7 @@ def load_library():
         lib.hn_pairdist_hardneg.argtypes = [P, P, I64, I32, I32, P, P, P, S, P]
         lib.hn_fpr95_workspace_bytes.argtypes = [I64, ctypes.POINTER(S)]
         lib.hn_fpr95.argtypes = [P, P, P, I64, I32, P, P, P, S, P]
+        lib.hn_preprocess.argtypes = [P, I64, I32, I32, I32, ctypes.c_float, ctypes.c_float, P, P]
         lib.hn_set_profiling.argtypes = [P, ctypes.c_int]
         lib.hn_stage_times.argtypes = [P, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),
                                        ctypes.POINTER(ctypes.c_double), ctypes.POINTER(I64)]
@@ -262,3 +263,35 @@ def fpr95(out_a: torch.Tensor, out_p: torch.Tensor, labels: torch.Tensor):
         _check(lib.hn_fpr95(a.data_ptr(), p.data_ptr(), lab.data_ptr(), n, d, dists.data_ptr(),
                             res.data_ptr(), ws.data_ptr(), ws.numel(), stream), "hn_fpr95")
     return float(res.item()), dists
+
+
+RESIZE_MODES = {"none": 0, "cv2": 1, "pil": 2}  # enum hn_resize
+
+
+def preprocess(u8: torch.Tensor, resize: str = "cv2", normalize: bool = True,
+               mean: float = 0.443728476019, std: float = 0.20197947209,
+               out: torch.Tensor = None) -> torch.Tensor:
+    """uint8 patches [n,64,64] (or [n,1,64,64] / [n,64,64,1]; [n,32,32] for resize='none')
+    -> fp32 [n,1,32,32] on device, bit-exact with the reference loaders:
+    resize='cv2' + normalize = ``transform`` (hardnet/HardNet.py:345-349, cv2_scale Utils.py:10-11);
+    resize='pil', normalize=False = augmented ``transform_test`` (HardNet.py:333-337).
+    Defaults for mean/std are the reference's --mean-image/--std-image (HardNet.py:86-89)."""
+    lib = load_library()
+    if resize not in RESIZE_MODES:
+        raise ValueError(f"resize must be one of {sorted(RESIZE_MODES)}")
+    if u8.dtype != torch.uint8 or not u8.is_cuda:
+        raise ValueError("expected a uint8 HIP tensor")
+    hw = 32 if resize == "none" else 64
+    n = u8.shape[0]
+    if u8.numel() != n * hw * hw:
+        raise ValueError(f"expected {hw}x{hw} patches, got shape {tuple(u8.shape)}")
+    x = u8.contiguous()
+    if out is None:
+        out = torch.empty((n, 1, 32, 32), device=x.device, dtype=torch.float32)
+    elif out.shape != (n, 1, 32, 32) or out.dtype != torch.float32 or not out.is_contiguous():
+        raise ValueError("out must be a contiguous fp32 [n,1,32,32] tensor")
+    stream = torch.cuda.current_stream(x.device).cuda_stream
+    with torch.cuda.device(x.device):
+        _check(lib.hn_preprocess(x.data_ptr(), n, hw, RESIZE_MODES[resize], int(normalize),
+                                 mean, std, out.data_ptr(), stream), "hn_preprocess")
+    return out

@@ -613,6 +613,26 @@ extern "C" int hn_fpr95(const float* d_anchor, const float* d_positive, const in
   return HN_OK;
 }
 
+extern "C" int hn_preprocess(const uint8_t* d_in, int64_t n, int32_t in_hw, int32_t resize,
+                             int32_t normalize, float mean, float stdv, float* d_out,
+                             void* hip_stream) {
+  if (n < 0) return fail(HN_ERR_ARG, "n < 0");
+  if (resize != HN_RESIZE_NONE && resize != HN_RESIZE_CV2_LINEAR && resize != HN_RESIZE_PIL_BILINEAR)
+    return fail(HN_ERR_ARG, "unknown resize mode " + std::to_string(resize));
+  const int want = resize == HN_RESIZE_NONE ? 32 : 64;
+  if (in_hw != want)
+    return fail(HN_ERR_ARG, "in_hw must be " + std::to_string(want) + " for this resize mode, got " +
+                                std::to_string(in_hw));
+  if (n == 0) return HN_OK;
+  if (!d_in || !d_out) return fail(HN_ERR_ARG, "NULL device pointer");
+  if ((reinterpret_cast<uintptr_t>(d_in) | reinterpret_cast<uintptr_t>(d_out)) & 15)
+    return fail(HN_ERR_ARG, "d_in / d_out must be 16-byte aligned");
+  if (normalize && !(stdv != 0.0f)) return fail(HN_ERR_ARG, "std must be nonzero");
+  HIPCHK(hn_launch_preprocess(d_in, n, resize, normalize, mean, stdv, d_out,
+                              static_cast<hipStream_t>(hip_stream)));
+  return HN_OK;
+}
+
 extern "C" int hn_set_profiling(hn_model* m, int enable) {
   if (!m) return fail(HN_ERR_ARG, "model is NULL");
   m->prof.on = enable != 0;

@@ -33,5 +33,7 @@ hipError_t hn_launch_pairdist(const float* a, const float* p, int B, int D, int 
                               float* pos, float* minneg, void* ws, hipStream_t st);
 
 hipError_t hn_fpr95_ws_bytes(int64_t n, size_t* bytes);
+hipError_t hn_launch_preprocess(const uint8_t* in, int64_t n, int resize, int norm, float mean,
+                                float stdv, float* out, hipStream_t st);
 hipError_t hn_launch_fpr95(const float* a, const float* p, const int* labels, int64_t n, int dim,
                            float* dists, double* fpr, void* ws, size_t ws_bytes, hipStream_t st);

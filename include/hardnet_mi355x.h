@@ -112,6 +112,18 @@ int hn_fpr95(const float* d_anchor, const float* d_positive, const int32_t* d_la
              int32_t dim, float* d_dists, double* d_fpr, void* d_workspace, size_t workspace_bytes,
              void* hip_stream);
 
+/* Patch preprocessing: uint8 patches -> fp32 [n,1,32,32] network input,
+ * bit-exact with the reference loaders.
+ *   HN_RESIZE_CV2_LINEAR   hardnet/HardNet.py:345-349 'transform' + Utils.py:10-11 cv2_scale:
+ *                          64x64 -> 32x32 cv2 INTER_LINEAR (= OpenCV's 2x area-fast path)
+ *   HN_RESIZE_PIL_BILINEAR hardnet/HardNet.py:333-337 'transform_test': PIL Resize(32), bilinear
+ *   HN_RESIZE_NONE         input already 32x32 (cv2.resize to the same size is a copy)
+ * then ToTensor (/255) and, if normalize != 0, Normalize((mean,), (std,)) in fp32.
+ * d_in: [n, in_hw, in_hw] uint8 (in_hw 64 for the resizing modes, 32 for NONE). */
+enum hn_resize { HN_RESIZE_NONE = 0, HN_RESIZE_CV2_LINEAR = 1, HN_RESIZE_PIL_BILINEAR = 2 };
+int hn_preprocess(const uint8_t* d_in, int64_t n, int32_t in_hw, int32_t resize, int32_t normalize,
+                  float mean, float std, float* d_out, void* hip_stream);
+
 /* Per-stage timing (profiling aid used by bench.py): when enabled, hn_forward records a
  * hipEvent pair around every kernel launch on the caller's stream.  hn_stage_times
  * waits for the recorded events, accumulates their durations per stage name and returns

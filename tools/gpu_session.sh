@@ -16,8 +16,10 @@ run() {  # name, seconds, command...
   return 0
 }
 STEPS=${STEPS:-pytest,smoke,bench,prof}
-[[ $STEPS == *pytest* ]] && run pytest_gpu 500 python -m pytest tests -m gpu -q -rf
+[[ $STEPS == *pytest* ]] && run pytest_gpu 500 python -m pytest ${PYTEST_FILES:-tests} -m gpu -q -rf
 [[ $STEPS == *smoke* ]] && run smoke 200 python -c "import __graft_entry__ as g; g.smoke()"
 [[ $STEPS == *bench* ]] && run bench 300 python bench.py ${BENCH_ARGS:-}
 [[ $STEPS == *prof* ]] && run rocprof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 3 --warmup 1 ${BENCH_ARGS:-}
+[[ $STEPS == *pre* ]] && run bench_pre 200 python tools/bench_preprocess.py
+[[ $STEPS == *pairs* ]] && run bench_pairs 200 python tools/bench_pairs.py
 exit 0
