@@ -57,22 +57,30 @@ HARDNET_STAGE_BYTES = {"stem": 4096 + 131072, "conv1": 2 * 131072, "stem+conv1":
 
 def nas_stage_bytes(ops) -> dict:
     """Algorithmic HBM bytes per patch of each NAS stage class, summed over its launches in
-    one forward (fp32 NHWC in + out (+ residual read)), mirroring hn_api.hip::forward_nas."""
-    out = {"stem": 4096 + 32 * 32 * 32 * 4, "pw": 0, "dw": 0, "pwl": 0, "maxpool": 0, "se": 0,
-           "head": 0}
+    one forward (fp32 NHWC in + out (+ residual read)), mirroring hn_api.hip::forward_nas
+    (stem + layer 0 run as one fused "front" kernel unless HN_NO_FRONT=1)."""
+    front = os.environ.get("HN_NO_FRONT", "0") in ("", "0")
+    out = {"stem": 0 if front else 4096 + 32 * 32 * 32 * 4, "front": 0, "pw": 0, "dw": 0,
+           "pwl": 0, "maxpool": 0, "se": 0, "head": 0}
     hw = 32
-    for op, (ci, co, s) in zip(A.arch_ops(ops), A.SEARCH_SPACE2):
+    for i, (op, (ci, co, s)) in enumerate(zip(A.arch_ops(ops), A.SEARCH_SPACE2)):
         spec = A.OP_SPECS[op]
         ho = hw // s
+        fused = front and i == 0
         if spec.kind == "skip":
-            if s == 2:
+            if fused:
+                out["front"] += 4096 + 4 * ci * ho * ho
+            elif s == 2:
                 out["maxpool"] += 4 * (ci * hw * hw + ci * ho * ho)
             if ci != co:
                 out["pw"] += 4 * (ci * ho * ho + co * ho * ho)
         else:
             mid = A.ir_mid(ci, spec.expansion)
-            out["pw"] += 4 * (ci * hw * hw + mid * hw * hw)
-            out["dw"] += 4 * (mid * hw * hw + mid * ho * ho)
+            if fused:
+                out["front"] += 4096 + 4 * mid * ho * ho
+            else:
+                out["pw"] += 4 * (ci * hw * hw + mid * hw * hw)
+                out["dw"] += 4 * (mid * hw * hw + mid * ho * ho)
             res = (s == 1 and ci == co)
             out["pwl"] += 4 * (mid * ho * ho + co * ho * ho + (co * ho * ho if res else 0))
             if spec.se:

@@ -52,6 +52,8 @@ struct NasLayer {
   float *pw_w = nullptr, *pw_b = nullptr, *dw_w = nullptr, *dw_b = nullptr;
   float *pwl_w = nullptr, *pwl_b = nullptr;
   float *se_w1 = nullptr, *se_b1 = nullptr, *se_w2 = nullptr, *se_b2 = nullptr;
+  uint16_t* front_a = nullptr;  // fused front (layer 0): pw as MFMA A operand, dw channel order
+  float* front_b = nullptr;
 };
 
 struct Cursor {
@@ -153,6 +155,8 @@ struct hn_model {
   int head_k = 0;
   int chunk = 32768;
   bool unfused_stem = false;  // HN_UNFUSED_STEM=1: separate stem kernel (A/B, debugging)
+  int front = 0;  // NAS: 1 = stem + layer-0 IRF pw/dw fused, 2 = stem + layer-0 maxpool fused
+  bool no_front = false;  // HN_NO_FRONT=1: unfused NAS stem/layer 0 (A/B, debugging)
   // conv tiling per layer (index 0 = stem+conv1, 2..5 = conv2..5); defaults are the best
   // measured on MI355X (tools/tune_variants.py); HN_VARIANT="003303" style override
   int variant[6] = {6, 0, 5, 6, 6, 3};
@@ -289,6 +293,32 @@ static std::vector<float> transpose_pw(const std::vector<float>& w, int cout, in
   return t;
 }
 
+// Fused-front pw weights (fp16 hi/lo) as the MFMA A operand (rows = output channels in dw order, i.e.
+// after ChannelShuffle(g); grouped conv densified with zeros; K = 32 stem channels):
+// [MID/32][kstep][plane hi/lo][lane][8] bf16, lane (r = l & 31, h = l >> 5) holding
+// W'[32m + r][16*kstep + 8h + j].
+static void pack_front(const Folded& f, int mid, int g, std::vector<uint16_t>* a,
+                       std::vector<float>* bias) {
+  const int cin = 32, kg = cin / g, cg = mid / g;
+  auto src = [&](int d) { return g > 1 ? (d % g) * cg + d / g : d; };  // fbnet_builder.py:332-349
+  a->assign((size_t)mid / 32 * 2 * 2 * 64 * 8, 0);
+  bias->resize(mid);
+  for (int d = 0; d < mid; ++d) (*bias)[d] = f.b[src(d)];
+  for (int mc = 0; mc < mid / 32; ++mc)
+    for (int ks = 0; ks < 2; ++ks)
+      for (int lane = 0; lane < 64; ++lane)
+        for (int j = 0; j < 8; ++j) {
+          const int d = 32 * mc + (lane & 31), k = 16 * ks + 8 * (lane >> 5) + j;
+          const int c = src(d), grp = c / (mid / g);
+          const float v = (k >= grp * kg && k < (grp + 1) * kg) ? f.w[(size_t)c * kg + (k - grp * kg)] : 0.f;
+          const _Float16 hv = (_Float16)v;  // fp16x3 split (hn_common.h split8_f16)
+          const _Float16 lv = (_Float16)(v - (float)hv);
+          const size_t o = ((((size_t)mc * 2 + ks) * 2) * 64 + lane) * 8 + j;
+          std::memcpy(&(*a)[o], &hv, 2);
+          std::memcpy(&(*a)[o + 64 * 8], &lv, 2);
+        }
+}
+
 static int build_hardnet(hn_model* m, Cursor& cur) {
   static const int cin[7] = {1, 32, 32, 64, 64, 128, 128};
   static const int cout[7] = {32, 32, 64, 64, 128, 128, 128};
@@ -358,6 +388,8 @@ static int build_nas(hn_model* m, Cursor& cur) {
     L.skip = s.skip;
     if (s.skip) {
       L.skip_conv = L.cin != L.cout;
+      if (i == 0 && !m->no_front && L.cin == 32 && L.cout == 32 && L.hin == 32 && L.stride == 2)
+        m->front = 2;
       if (L.skip_conv) {
         if ((rc = take_cbr(m, cur, L.cout, L.cin, &f))) return rc;
         if ((rc = m->upload(transpose_pw(f.w, L.cout, L.cin), &L.pw_w))) return rc;
@@ -374,6 +406,15 @@ static int build_nas(hn_model* m, Cursor& cur) {
       if ((rc = take_cbr(m, cur, L.mid, L.cin / L.g, &f))) return rc;
       if ((rc = m->upload(transpose_pw(f.w, L.mid, L.cin / L.g), &L.pw_w))) return rc;
       if ((rc = m->upload(f.b, &L.pw_b))) return rc;
+      if (i == 0 && !m->no_front && L.cin == 32 && L.hin == 32 && L.stride == 2 &&
+          hn_front_supported(L.k, L.mid)) {
+        std::vector<uint16_t> a;
+        std::vector<float> b;
+        pack_front(f, L.mid, L.g, &a, &b);
+        if ((rc = m->upload(a, &L.front_a))) return rc;
+        if ((rc = m->upload(b, &L.front_b))) return rc;
+        m->front = 1;
+      }
       if ((rc = take_cbr(m, cur, L.mid, (size_t)L.k * L.k, &f))) return rc;
       {
         std::vector<float> wd((size_t)L.k * L.k * L.mid);
@@ -441,6 +482,7 @@ extern "C" int hn_create(const hn_arch_desc* desc, const float* host_params, siz
   m->desc = *desc;
   if (const char* e = std::getenv("HN_CHUNK")) m->chunk = std::max(64, std::atoi(e));
   if (const char* e = std::getenv("HN_UNFUSED_STEM")) m->unfused_stem = std::atoi(e) != 0;
+  if (const char* e = std::getenv("HN_NO_FRONT")) m->no_front = std::atoi(e) != 0;
   if (const char* e = std::getenv("HN_VARIANT")) {
     int i = 0;
     for (const char* c = e; *c && i < 6; ++c)
@@ -510,8 +552,27 @@ static int forward_nas(hn_model* m, const float* in, int P, float* out, float* w
   float* t2 = ws + 2 * per;
   float* y = ws + 3 * per;
   const float ineps = m->desc.input_norm_eps;
-  STAGE("stem", hn_launch_stem(in, x, m->stem_w, m->stem_b, P, ineps >= 0.f, ineps, st));
-  for (const NasLayer& L : m->layers) {
+  size_t first = 0;
+  if (m->front) {
+    const NasLayer& L = m->layers[0];
+    const bool mp = m->front == 2;
+    const HnFrontArgs fa{in, mp ? x : t2, m->stem_w, m->stem_b,
+                         reinterpret_cast<const uint4*>(L.front_a), L.front_b, L.dw_w, L.dw_b};
+    STAGE("front", hn_launch_front(fa, P, L.k, L.mid, mp, ineps >= 0.f, ineps, st));
+    if (!mp) {  // layer 0 is stride 2: no residual
+      STAGE("pwl", hn_launch_pw(t2, y, L.pwl_w, L.pwl_b, nullptr, (long)P * L.hout * L.hout, L.mid,
+                                L.cout, L.g, false, 0, st));
+      if (L.se)
+        STAGE("se", hn_launch_se(y, L.se_w1, L.se_b1, L.se_w2, L.se_b2, P, L.hout * L.hout, L.cout,
+                                 L.semid, st));
+      std::swap(x, y);
+    }
+    first = 1;
+  } else {
+    STAGE("stem", hn_launch_stem(in, x, m->stem_w, m->stem_b, P, ineps >= 0.f, ineps, st));
+  }
+  for (size_t li = first; li < m->layers.size(); ++li) {
+    const NasLayer& L = m->layers[li];
     const long npix_out = (long)P * L.hout * L.hout;
     if (L.skip) {
       const float* src = x;

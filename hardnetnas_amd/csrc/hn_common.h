@@ -36,6 +36,23 @@ HN_DEV void split8(const float4& a, const float4& b, uint4& hi, uint4& lo) {
 
 HN_DEV bf16x8 as_bf16x8(const uint4& v) { return __builtin_bit_cast(bf16x8, v); }
 
+// fp16 variant of the split ("fp16x3"): 11-bit halves, so hi + lo carries ~22 bits and the
+// dropped lo*lo term is ~2^-22 relative -- used where activations are range-bounded (the
+// NAS front: no input_norm, ReLU outputs of O(1)); same MFMA rate as bf16.
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+HN_DEV void split8_f16(const float4& a, const float4& b, uint4& hi, uint4& lo) {
+  const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  f16x8 h, l;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    h[j] = (_Float16)v[j];
+    l[j] = (_Float16)(v[j] - (float)h[j]);
+  }
+  hi = __builtin_bit_cast(uint4, h);
+  lo = __builtin_bit_cast(uint4, l);
+}
+HN_DEV f16x8 as_f16x8(const uint4& v) { return __builtin_bit_cast(f16x8, v); }
+
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 // Buffer resource over [base, base + bytes): the descriptor lives in SGPRs, loads take a
@@ -54,6 +71,14 @@ HN_DEV f32x16 mfma3(const bf16x8& ah, const bf16x8& al, const bf16x8& bh, const 
   acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
   acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
   acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
+  return acc;
+}
+
+HN_DEV f32x16 mfma3_f16(const f16x8& ah, const f16x8& al, const f16x8& bh, const f16x8& bl,
+                        f32x16 acc) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc, 0, 0, 0);
   return acc;
 }
 

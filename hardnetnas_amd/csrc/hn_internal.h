@@ -33,6 +33,20 @@ hipError_t hn_launch_pairdist(const float* a, const float* p, int B, int D, int 
                               float* pos, float* minneg, void* ws, hipStream_t st);
 
 hipError_t hn_fpr95_ws_bytes(int64_t n, size_t* bytes);
+// fused NAS front (stem + layer 0), hn_front.hip
+struct HnFrontArgs {
+  const float* in;
+  float* out;
+  const float* stem_w;  // [9][32]
+  const float* stem_b;
+  const uint4* apack;   // pw A operand, [MID/32][kstep 2][plane 2][lane 64] x 8 bf16
+  const float* pw_b;    // [MID], dw channel order
+  const float* dw_w;    // [K*K][MID]
+  const float* dw_b;
+};
+bool hn_front_supported(int k, int mid);
+hipError_t hn_launch_front(const HnFrontArgs& a, int P, int k, int mid, bool maxpool, bool norm,
+                           float eps, hipStream_t st);
 hipError_t hn_launch_preprocess(const uint8_t* in, int64_t n, int resize, int norm, float mean,
                                 float stdv, float* out, hipStream_t st);
 hipError_t hn_launch_fpr95(const float* a, const float* p, const int* labels, int64_t n, int dim,

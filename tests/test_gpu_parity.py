@@ -207,3 +207,49 @@ def test_fpr95_on_descriptors_matches_oracle(cuda_device):
     ref = O.error_rate_at_95_recall(lab.numpy(), 1.0 / (d_ref + 1e-8))
     assert np.abs(dd.cpu().numpy() - d_ref).max() < 1e-6
     assert got == pytest.approx(ref, abs=2.0 / n)   # tie order may move one sample
+
+
+@pytest.mark.parametrize("name", ["wang2", "wang3", "wang4", "cov_a"])
+def test_nas_unfused_front_matches(name, cuda_device, monkeypatch):
+    """HN_NO_FRONT=1 keeps the layer-by-layer stem + layer-0 kernels reachable and exact."""
+    from hardnetnas_amd._native import NativeModel
+    m, fx, _ = build_module(name)
+    monkeypatch.setenv("HN_NO_FRONT", "1")
+    x = torch.from_numpy(golden_inputs(fx)).to(cuda_device)
+    nm = NativeModel.from_module(m, cuda_device)
+    nm.set_profiling(True)
+    y = nm(x).cpu().numpy()
+    assert "front" not in nm.stage_times()
+    assert np.abs(y - fx["y"]).max() <= NAS_TOL
+
+
+def _synth_nas(ops, seed=99):
+    from hardnetnas_amd import synth
+    from hardnetnas_amd.model import HardNetNAS
+    m = HardNetNAS(list(ops))
+    sd = m.state_dict()
+    w = synth.synth_state_dict({k: tuple(v.shape) for k, v in sd.items()}, seed)
+    for k in w:
+        sd[k] = torch.from_numpy(w[k])
+    m.load_state_dict(sd)
+    return m.eval(), {k: torch.from_numpy(v) for k, v in w.items()}
+
+
+@pytest.mark.parametrize("op", ["skip", "ir_k3_e1", "ir_k3_e3", "ir_k3_s4", "ir_k5_e1", "ir_k5_e3",
+                                "ir_k5_s4", "ir_k3_e1_se", "ir_k3_e3_se", "ir_k3_s4_se",
+                                "ir_k5_e1_se", "ir_k5_e3_se", "ir_k5_s4_se", "ir_k3_s2",
+                                "ir_k5_s2", "ir_k3_s2_se", "ir_k5_s2_se"])
+def test_every_candidate_op_at_layer0_fused_front(op, cuda_device):
+    """Each of the 17 CANDIDATE_BLOCKS as layer 0 (the fused stem+layer-0 kernel) against the
+    fp32 oracle on synthetic weights; ragged batch exercises the last workgroup."""
+    from hardnetnas_amd import synth
+    from hardnetnas_amd._native import NativeModel
+    ops = [op, "ir_k3_e1", "skip", "ir_k5_s2", "skip", "ir_k3_e1"]
+    m, p = _synth_nas(ops)
+    x = torch.from_numpy(synth.synth_patches(77, seed=5))
+    ref = O.nas_forward(p, ops, x).numpy()
+    nm = NativeModel.from_module(m, cuda_device)
+    nm.set_profiling(True)
+    y = nm(x.to(cuda_device)).cpu().numpy()
+    assert "front" in nm.stage_times()
+    assert np.abs(y - ref).max() <= NAS_TOL
