@@ -155,6 +155,7 @@ struct hn_model {
   int head_k = 0;
   int chunk = 32768;
   bool unfused_stem = false;  // HN_UNFUSED_STEM=1: separate stem kernel (A/B, debugging)
+  uint16_t* front_spack = nullptr;  // fused front: stem as MFMA A operand
   int front = 0;  // NAS: 1 = stem + layer-0 IRF pw/dw fused, 2 = stem + layer-0 maxpool fused
   bool no_front = false;  // HN_NO_FRONT=1: unfused NAS stem/layer 0 (A/B, debugging)
   // conv tiling per layer (index 0 = stem+conv1, 2..5 = conv2..5); defaults are the best
@@ -293,10 +294,30 @@ static std::vector<float> transpose_pw(const std::vector<float>& w, int cout, in
   return t;
 }
 
-// Fused-front pw weights (fp16 hi/lo) as the MFMA A operand (rows = output channels in dw order, i.e.
-// after ChannelShuffle(g); grouped conv densified with zeros; K = 32 stem channels):
-// [MID/32][kstep][plane hi/lo][lane][8] bf16, lane (r = l & 31, h = l >> 5) holding
-// W'[32m + r][16*kstep + 8h + j].
+static void put_f16_split(float v, uint16_t* hi, uint16_t* lo) {  // hn_common.h split8_f16
+  const _Float16 hv = (_Float16)v;
+  const _Float16 lv = (_Float16)(v - (float)hv);
+  std::memcpy(hi, &hv, 2);
+  std::memcpy(lo, &lv, 2);
+}
+
+// Fused-front stem weights as the MFMA A operand: [plane hi/lo][lane][8] fp16, lane
+// (r = l & 31 = output channel, h = l >> 5) holding taps 8h..8h+7 (taps >= 9 are zero).
+static std::vector<uint16_t> pack_front_stem(const Folded& f) {
+  std::vector<uint16_t> a(2 * 64 * 8, 0);
+  for (int lane = 0; lane < 64; ++lane)
+    for (int j = 0; j < 8; ++j) {
+      const int r = lane & 31, tap = 8 * (lane >> 5) + j;
+      put_f16_split(tap < 9 ? f.w[(size_t)r * 9 + tap] : 0.f, &a[lane * 8 + j], &a[64 * 8 + lane * 8 + j]);
+    }
+  return a;
+}
+
+// Fused-front pw weights (fp16 hi/lo) as the MFMA A operand (rows = output channels in dw
+// order, i.e. after ChannelShuffle(g); grouped conv densified with zeros):
+// [MID/32][kstep][plane hi/lo][lane][8] fp16, lane (r = l & 31, h = l >> 5), element j
+// multiplying stem channel kappa(16*kstep + 8h + j) -- the order in which the stem MFMA
+// leaves its outputs in the lanes (C row (i & 3) + 8 (i >> 2) + 4h for i = 8*kstep + j).
 static void pack_front(const Folded& f, int mid, int g, std::vector<uint16_t>* a,
                        std::vector<float>* bias) {
   const int cin = 32, kg = cin / g, cg = mid / g;
@@ -308,14 +329,12 @@ static void pack_front(const Folded& f, int mid, int g, std::vector<uint16_t>* a
     for (int ks = 0; ks < 2; ++ks)
       for (int lane = 0; lane < 64; ++lane)
         for (int j = 0; j < 8; ++j) {
-          const int d = 32 * mc + (lane & 31), k = 16 * ks + 8 * (lane >> 5) + j;
+          const int d = 32 * mc + (lane & 31), h = lane >> 5;
+          const int k = (j & 3) + 8 * (2 * ks + (j >> 2)) + 4 * h;  // stem channel
           const int c = src(d), grp = c / (mid / g);
           const float v = (k >= grp * kg && k < (grp + 1) * kg) ? f.w[(size_t)c * kg + (k - grp * kg)] : 0.f;
-          const _Float16 hv = (_Float16)v;  // fp16x3 split (hn_common.h split8_f16)
-          const _Float16 lv = (_Float16)(v - (float)hv);
           const size_t o = ((((size_t)mc * 2 + ks) * 2) * 64 + lane) * 8 + j;
-          std::memcpy(&(*a)[o], &hv, 2);
-          std::memcpy(&(*a)[o + 64 * 8], &lv, 2);
+          put_f16_split(v, &(*a)[o], &(*a)[o + 64 * 8]);
         }
 }
 
@@ -373,6 +392,7 @@ static int build_nas(hn_model* m, Cursor& cur) {
       for (int t = 0; t < 9; ++t) sw[t * 32 + n] = f.w[n * 9 + t];
     if ((rc = m->upload(sw, &m->stem_w))) return rc;
     if ((rc = m->upload(f.b, &m->stem_b))) return rc;
+    if (!m->no_front && (rc = m->upload(pack_front_stem(f), &m->front_spack))) return rc;
   }
   size_t maxf = 32 * 32 * 32;
   int hw = 32;
@@ -556,7 +576,7 @@ static int forward_nas(hn_model* m, const float* in, int P, float* out, float* w
   if (m->front) {
     const NasLayer& L = m->layers[0];
     const bool mp = m->front == 2;
-    const HnFrontArgs fa{in, mp ? x : t2, m->stem_w, m->stem_b,
+    const HnFrontArgs fa{in, mp ? x : t2, reinterpret_cast<const uint4*>(m->front_spack), m->stem_b,
                          reinterpret_cast<const uint4*>(L.front_a), L.front_b, L.dw_w, L.dw_b};
     STAGE("front", hn_launch_front(fa, P, L.k, L.mid, mp, ineps >= 0.f, ineps, st));
     if (!mp) {  // layer 0 is stride 2: no residual

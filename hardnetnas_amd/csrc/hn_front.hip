@@ -11,8 +11,9 @@
 //
 // One workgroup (4 waves) owns a band of 4 output rows of one patch.  The band's
 // 2*3+k pw rows (halo recomputed by the neighbouring band) are produced row by row: a wave
-// computes the stem for one image row (32 pixels) on the VALU straight into the MFMA
-// B-operand layout (lane = pixel, 16 channels per lane), keeps it in registers, and runs
+// computes the stem for one image row (32 pixels) as one fp16x3 MFMA tile whose output
+// layout (lane = pixel, 16 channels per lane) is directly the pw B operand, keeps it in
+// registers, and runs
 // the 1x1 conv for each 32-channel chunk of MID as a 32x32x32 fp16x3 MFMA tile (weights =
 // A operand, BN scale folded, shuffle folded into the row order, groups densified).  The
 // chunk's pw rows go to LDS; the depthwise conv reads them from LDS (fp32 VALU) and
@@ -26,10 +27,19 @@ constexpr int FRONT_IRF = 0, FRONT_MAXPOOL = 1;
 constexpr int RB = 4;   // output rows per band
 constexpr int PS = 36;  // floats per pixel in the LDS pw band (32 channels + 4 pad)
 
+// dw/maxpool read mapping: lane -> (pixel ox in 0..7, channel quad q) chosen so that every
+// 16-lane ds_read_b128 group (MI355X_MICROARCH.md LDS) hits 16 distinct 16-byte slots of a
+// bank row for the s2 window reads (slot = 2*ox + q + 9*dx mod 16 at PS = 36 floats);
+// derived in tests/test_lds_banks.py::test_front_dw_lane_map.  Encoded ox*8 + q.
+__constant__ unsigned char kDwLane[64] = {
+    0,  1,  2,  3,  46, 47, 8,  9,  10, 11, 12, 13, 4,  5,  6,  7,  20, 21, 28, 29, 14, 15,
+    22, 23, 30, 31, 38, 39, 36, 37, 44, 45, 52, 53, 54, 55, 58, 59, 60, 61, 62, 63, 24, 25,
+    16, 17, 18, 19, 32, 33, 40, 41, 26, 27, 34, 35, 42, 43, 50, 51, 48, 49, 56, 57};
+
 template <int K, int MID, int MODE, bool NORM>
 __global__ __launch_bounds__(256) void k_front(const float* __restrict__ in,
                                                float* __restrict__ out,
-                                               const float* __restrict__ stem_w,  // [9][32]
+                                               const uint4* __restrict__ spack,  // stem A operand
                                                const float* __restrict__ stem_b,  // [32]
                                                const uint4* __restrict__ apack,
                                                const float* __restrict__ pw_b,  // [MID] (dw order)
@@ -42,8 +52,8 @@ __global__ __launch_bounds__(256) void k_front(const float* __restrict__ in,
   constexpr int PC = 32 + 2 * PAD;       // columns incl. zero padding
   constexpr int NT = (IR + 3) / 4;       // row tiles per wave
   constexpr int OC = MODE == FRONT_MAXPOOL ? 32 : MID;
+  constexpr int DYU = KK == 3 ? 3 : 1;  // k5: rolled dy loop keeps VGPRs (and occupancy) in check
   __shared__ float s_in[34 * 34];
-  __shared__ __attribute__((aligned(16))) float s_sw[9 * 32 + 32];
   __shared__ __attribute__((aligned(16))) float s_pw[IR * PC * PS];
   __shared__ __attribute__((aligned(16))) float s_dw[KK * KK * 32 + 32];
   __shared__ float red[8];
@@ -54,12 +64,20 @@ __global__ __launch_bounds__(256) void k_front(const float* __restrict__ in,
   const int r0 = (blockIdx.x & 3) * RB;
   const int row0 = 2 * r0 - PAD;
 
-  // ---- phase 0: patch (+ input_norm) and stem weights to LDS, zero the pw band --------
+  // ---- phase 0: patch (+ input_norm) to LDS; zero the pw band's padding -----------------
   const float4 v = reinterpret_cast<const float4*>(in + patch * 1024)[t];
   for (int i = t; i < 34 * 34; i += 256) s_in[i] = 0.f;
-  for (int i = t; i < IR * PC * PS / 4; i += 256)
-    reinterpret_cast<float4*>(s_pw)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int i = t; i < 9 * 32 + 32; i += 256) s_sw[i] = i < 288 ? stem_w[i] : stem_b[i - 288];
+  for (int i = t; i < IR * 2 * PAD * (PS / 4); i += 256) {  // left/right pad columns
+    const int ri = i / (2 * PAD * (PS / 4)), rem = i % (2 * PAD * (PS / 4)), c = rem / (PS / 4);
+    reinterpret_cast<float4*>(s_pw)[(ri * PC + (c < PAD ? c : 32 + c)) * (PS / 4) + rem % (PS / 4)] =
+        make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+#pragma unroll
+  for (int ri = 0; ri < IR; ++ri) {  // rows outside the image (first / last band only)
+    if (row0 + ri >= 0 && row0 + ri < 32) continue;
+    for (int i = t; i < 32 * (PS / 4); i += 256)
+      reinterpret_cast<float4*>(s_pw)[(ri * PC + PAD) * (PS / 4) + i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
   float mean = 0.f, sd = 1.f;
   if (NORM) {  // (x - mean) / (std_unbiased + eps), as k_stem
     const float s = wave_sum(v.x + v.y + v.z + v.w);
@@ -85,59 +103,61 @@ __global__ __launch_bounds__(256) void k_front(const float* __restrict__ in,
   }
   __syncthreads();
 
-  // ---- phase A: stem rows of the band (lane: pixel px, channels 8h..8h+7, 16+8h..+7) ----
+  // ---- phase A: stem rows on the MFMA ---------------------------------------------------
+  // A = stem weights [32 ch][16 = 9 taps + 0], B = im2col of one image row (lane: pixel px,
+  // taps 8h..8h+7).  C leaves channel 4h + 8q + r (i = 4q + r) of pixel px in acc[i]; that
+  // order is used as-is as the pw contraction index (pw weights are packed to match).
+  const f16x8 sah = as_f16x8(spack[lane]), sal = as_f16x8(spack[64 + lane]);
+  float4 sb[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) sb[q] = *reinterpret_cast<const float4*>(stem_b + 8 * q + 4 * h);
   uint4 bh[NT][2], bl[NT][2];
 #pragma unroll
   for (int i = 0; i < NT; ++i) {
     const int ri = w + 4 * i, y = row0 + ri;
     bh[i][0] = bh[i][1] = bl[i][0] = bl[i][1] = make_uint4(0, 0, 0, 0);
     if (ri >= IR || y < 0 || y >= 32) continue;  // wave-uniform
-    float a[16];
-    {
-      const float4* b4 = reinterpret_cast<const float4*>(s_sw + 288);
-      const float4 b0 = b4[2 * h], b1 = b4[2 * h + 1], b2 = b4[4 + 2 * h], b3 = b4[5 + 2 * h];
-      a[0] = b0.x; a[1] = b0.y; a[2] = b0.z; a[3] = b0.w; a[4] = b1.x; a[5] = b1.y; a[6] = b1.z; a[7] = b1.w;
-      a[8] = b2.x; a[9] = b2.y; a[10] = b2.z; a[11] = b2.w; a[12] = b3.x; a[13] = b3.y; a[14] = b3.z; a[15] = b3.w;
-    }
+    float tp[8];
 #pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
-      const float xv = s_in[(y + tap / 3) * 34 + px + tap % 3];
-      const float4* w4 = reinterpret_cast<const float4*>(s_sw + tap * 32);
-      const float4 w0 = w4[2 * h], w1 = w4[2 * h + 1], w2 = w4[4 + 2 * h], w3 = w4[5 + 2 * h];
-      a[0] = fmaf(w0.x, xv, a[0]); a[1] = fmaf(w0.y, xv, a[1]); a[2] = fmaf(w0.z, xv, a[2]); a[3] = fmaf(w0.w, xv, a[3]);
-      a[4] = fmaf(w1.x, xv, a[4]); a[5] = fmaf(w1.y, xv, a[5]); a[6] = fmaf(w1.z, xv, a[6]); a[7] = fmaf(w1.w, xv, a[7]);
-      a[8] = fmaf(w2.x, xv, a[8]); a[9] = fmaf(w2.y, xv, a[9]); a[10] = fmaf(w2.z, xv, a[10]); a[11] = fmaf(w2.w, xv, a[11]);
-      a[12] = fmaf(w3.x, xv, a[12]); a[13] = fmaf(w3.y, xv, a[13]); a[14] = fmaf(w3.z, xv, a[14]); a[15] = fmaf(w3.w, xv, a[15]);
+    for (int j = 0; j < 8; ++j) {
+      const int tap = 8 * h + j;  // h = 1 holds tap 8 and zeros
+      tp[j] = tap < 9 ? s_in[(y + tap / 3) * 34 + px + tap % 3] : 0.f;
     }
+    uint4 xh, xl;
+    split8_f16(make_float4(tp[0], tp[1], tp[2], tp[3]), make_float4(tp[4], tp[5], tp[6], tp[7]), xh, xl);
+    f32x16 c = {};
+    c = mfma3_f16(sah, sal, as_f16x8(xh), as_f16x8(xl), c);
+    float4 o[4];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) a[j] = fmaxf(a[j], 0.f);
+    for (int q = 0; q < 4; ++q)
+      o[q] = make_float4(fmaxf(c[4 * q] + sb[q].x, 0.f), fmaxf(c[4 * q + 1] + sb[q].y, 0.f),
+                         fmaxf(c[4 * q + 2] + sb[q].z, 0.f), fmaxf(c[4 * q + 3] + sb[q].w, 0.f));
     if (MODE == FRONT_MAXPOOL) {
       float4* d = reinterpret_cast<float4*>(s_pw + (ri * PC + PAD + px) * PS);
-      d[2 * h] = make_float4(a[0], a[1], a[2], a[3]);
-      d[2 * h + 1] = make_float4(a[4], a[5], a[6], a[7]);
-      d[4 + 2 * h] = make_float4(a[8], a[9], a[10], a[11]);
-      d[5 + 2 * h] = make_float4(a[12], a[13], a[14], a[15]);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) d[2 * q + h] = o[q];
     } else {
-      split8_f16(make_float4(a[0], a[1], a[2], a[3]), make_float4(a[4], a[5], a[6], a[7]), bh[i][0], bl[i][0]);
-      split8_f16(make_float4(a[8], a[9], a[10], a[11]), make_float4(a[12], a[13], a[14], a[15]), bh[i][1], bl[i][1]);
+      split8_f16(o[0], o[1], bh[i][0], bl[i][0]);
+      split8_f16(o[2], o[3], bh[i][1], bl[i][1]);
     }
   }
 
+  const int lm = kDwLane[lane], dq = lm & 7, dox = lm >> 3;
   if (MODE == FRONT_MAXPOOL) {
     __syncthreads();
     // MaxPool2d(3, 2, 1): padding never wins since every window holds a ReLU output >= 0
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int item = t + 256 * j, q = item & 7, p = item >> 3, orr = p >> 4, ox = p & 15;
+      const int p = 8 * (w + 4 * j) + dox, orr = p >> 4, ox = p & 15;
       float4 m = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
       for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
         for (int dx = 0; dx < 3; ++dx) {
-          const float4 a = *reinterpret_cast<const float4*>(s_pw + ((2 * orr + dy) * PC + 2 * ox + dx) * PS + 4 * q);
+          const float4 a = *reinterpret_cast<const float4*>(s_pw + ((2 * orr + dy) * PC + 2 * ox + dx) * PS + 4 * dq);
           m.x = fmaxf(m.x, a.x); m.y = fmaxf(m.y, a.y); m.z = fmaxf(m.z, a.z); m.w = fmaxf(m.w, a.w);
         }
-      *reinterpret_cast<float4*>(out + ((patch * 16 + r0 + orr) * 16 + ox) * 32 + 4 * q) = m;
+      *reinterpret_cast<float4*>(out + ((patch * 16 + r0 + orr) * 16 + ox) * 32 + 4 * dq) = m;
     }
     return;
   }
@@ -174,21 +194,21 @@ __global__ __launch_bounds__(256) void k_front(const float* __restrict__ in,
                                    fmaxf(acc[4 * q + 2] + bias[q].z, 0.f), fmaxf(acc[4 * q + 3] + bias[q].w, 0.f));
     }
     __syncthreads();
-#pragma unroll
+#pragma unroll 1
     for (int j = 0; j < 2; ++j) {
-      const int item = t + 256 * j, q = item & 7, p = item >> 3, orr = p >> 4, ox = p & 15;
-      float4 acc = reinterpret_cast<const float4*>(s_dw + KK * KK * 32)[q];
-#pragma unroll
+      const int p = 8 * (w + 4 * j) + dox, orr = p >> 4, ox = p & 15;
+      float4 acc = reinterpret_cast<const float4*>(s_dw + KK * KK * 32)[dq];
+#pragma unroll DYU
       for (int dy = 0; dy < KK; ++dy)
 #pragma unroll
         for (int dx = 0; dx < KK; ++dx) {
-          const float4 wv = reinterpret_cast<const float4*>(s_dw + (dy * KK + dx) * 32)[q];
-          const float4 a = *reinterpret_cast<const float4*>(s_pw + ((2 * orr + dy) * PC + 2 * ox + dx) * PS + 4 * q);
+          const float4 wv = reinterpret_cast<const float4*>(s_dw + (dy * KK + dx) * 32)[dq];
+          const float4 a = *reinterpret_cast<const float4*>(s_pw + ((2 * orr + dy) * PC + 2 * ox + dx) * PS + 4 * dq);
           acc.x = fmaf(wv.x, a.x, acc.x); acc.y = fmaf(wv.y, a.y, acc.y);
           acc.z = fmaf(wv.z, a.z, acc.z); acc.w = fmaf(wv.w, a.w, acc.w);
         }
       acc.x = fmaxf(acc.x, 0.f); acc.y = fmaxf(acc.y, 0.f); acc.z = fmaxf(acc.z, 0.f); acc.w = fmaxf(acc.w, 0.f);
-      *reinterpret_cast<float4*>(out + ((patch * 16 + r0 + orr) * 16 + ox) * OC + 32 * m + 4 * q) = acc;
+      *reinterpret_cast<float4*>(out + ((patch * 16 + r0 + orr) * 16 + ox) * OC + 32 * m + 4 * dq) = acc;
     }
     __syncthreads();
   }
@@ -198,10 +218,10 @@ template <int K, int MID, int MODE>
 hipError_t front_launch(const HnFrontArgs& a, int P, bool norm, float eps, hipStream_t st) {
   const dim3 grid((unsigned)P * 4), block(256);
   if (norm)
-    hipLaunchKernelGGL((k_front<K, MID, MODE, true>), grid, block, 0, st, a.in, a.out, a.stem_w, a.stem_b,
+    hipLaunchKernelGGL((k_front<K, MID, MODE, true>), grid, block, 0, st, a.in, a.out, a.spack, a.stem_b,
                        a.apack, a.pw_b, a.dw_w, a.dw_b, eps);
   else
-    hipLaunchKernelGGL((k_front<K, MID, MODE, false>), grid, block, 0, st, a.in, a.out, a.stem_w, a.stem_b,
+    hipLaunchKernelGGL((k_front<K, MID, MODE, false>), grid, block, 0, st, a.in, a.out, a.spack, a.stem_b,
                        a.apack, a.pw_b, a.dw_w, a.dw_b, eps);
   return hipGetLastError();
 }

@@ -37,9 +37,9 @@ hipError_t hn_fpr95_ws_bytes(int64_t n, size_t* bytes);
 struct HnFrontArgs {
   const float* in;
   float* out;
-  const float* stem_w;  // [9][32]
+  const uint4* spack;   // stem A operand, [plane 2][lane 64] x 8 fp16 (taps 8h..8h+7)
   const float* stem_b;
-  const uint4* apack;   // pw A operand, [MID/32][kstep 2][plane 2][lane 64] x 8 bf16
+  const uint4* apack;   // pw A operand, [MID/32][kstep 2][plane 2][lane 64] x 8 fp16
   const float* pw_b;    // [MID], dw channel order
   const float* dw_w;    // [K*K][MID]
   const float* dw_b;

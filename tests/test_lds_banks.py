@@ -85,3 +85,35 @@ def test_conv_lds_fits(layer):
     assert g["lds"] <= 160 * 1024
     cin, cout = CONFIGS[layer][0], CONFIGS[layer][1]
     assert cin % 32 == 0 and cout % (32 * CONFIGS[layer][7]) == 0
+
+
+def _front_dw_lane_map():
+    src = open(__file__.replace("tests/test_lds_banks.py", "hardnetnas_amd/csrc/hn_front.hip")).read()
+    body = src[src.index("kDwLane[64] = {") + len("kDwLane[64] = {"):]
+    return [int(v) for v in body[:body.index("}")].replace("\n", " ").split(",") if v.strip()]
+
+
+def test_front_dw_lane_map():
+    """hn_front.hip dw / maxpool window reads: lane -> (ox, q) table is a bijection onto the
+    8x8 (pixel, channel-quad) block and every ds_read_b128 16-lane group hits 16 distinct
+    16-byte slots for all kx taps (pixel stride PS = 36 floats, stride-2 columns)."""
+    tab = _front_dw_lane_map()
+    assert sorted(tab) == list(range(64))
+    for g in GROUPS:
+        for base_ox in (0, 8):
+            for dx in range(5):
+                slots = set()
+                for lane in g:
+                    ox, q = base_ox + (tab[lane] >> 3), tab[lane] & 7
+                    byte = ((2 * ox + dx) * 36 + 4 * q) * 4
+                    slots.add((byte // 16) % 16)
+                assert len(slots) == 16, (g, dx)
+
+
+def test_front_pw_epilogue_writes_conflict_free():
+    """MFMA epilogue (pw and the maxpool stem path): lane (px = l & 31, h) writes float4
+    2q + h of pixel px at PS = 36 floats -- conflict-free for every q."""
+    for g in GROUPS:
+        for q in range(4):
+            slots = {(((lane & 31) * 36 + 4 * (2 * q + (lane >> 5))) * 4 // 16) % 16 for lane in g}
+            assert len(slots) == 16
