@@ -60,8 +60,9 @@ def nas_stage_bytes(ops) -> dict:
     one forward (fp32 NHWC in + out (+ residual read)), mirroring hn_api.hip::forward_nas
     (stem + layer 0 run as one fused "front" kernel unless HN_NO_FRONT=1)."""
     front = os.environ.get("HN_NO_FRONT", "0") in ("", "0")
-    out = {"stem": 0 if front else 4096 + 32 * 32 * 32 * 4, "front": 0, "pw": 0, "dw": 0,
-           "pwl": 0, "maxpool": 0, "se": 0, "head": 0}
+    irf = os.environ.get("HN_NO_IRF", "0") in ("", "0")
+    out = {"stem": 0 if front else 4096 + 32 * 32 * 32 * 4, "front": 0, "irf": 0, "pw": 0,
+           "dw": 0, "pwl": 0, "maxpool": 0, "se": 0, "head": 0}
     hw = 32
     for i, (op, (ci, co, s)) in enumerate(zip(A.arch_ops(ops), A.SEARCH_SPACE2)):
         spec = A.OP_SPECS[op]
@@ -78,6 +79,13 @@ def nas_stage_bytes(ops) -> dict:
             mid = A.ir_mid(ci, spec.expansion)
             if fused:
                 out["front"] += 4096 + 4 * mid * ho * ho
+            elif irf and i > 0:
+                # fused block: x in + y out (the residual re-read of x is not counted)
+                out["irf"] += 4 * (ci * hw * hw + co * ho * ho)
+                if spec.se:
+                    out["se"] += 4 * 2 * co * ho * ho
+                hw = ho
+                continue
             else:
                 out["pw"] += 4 * (ci * hw * hw + mid * hw * hw)
                 out["dw"] += 4 * (mid * hw * hw + mid * ho * ho)

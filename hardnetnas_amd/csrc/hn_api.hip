@@ -54,6 +54,8 @@ struct NasLayer {
   float *se_w1 = nullptr, *se_b1 = nullptr, *se_w2 = nullptr, *se_b2 = nullptr;
   uint16_t* front_a = nullptr;  // fused front (layer 0): pw as MFMA A operand, dw channel order
   float* front_b = nullptr;
+  uint16_t *irf_pw_a = nullptr, *irf_pwl_a = nullptr;  // fused IRF block (layers >= 1)
+  float* irf_pw_b = nullptr;
 };
 
 struct Cursor {
@@ -158,6 +160,7 @@ struct hn_model {
   uint16_t* front_spack = nullptr;  // fused front: stem as MFMA A operand
   int front = 0;  // NAS: 1 = stem + layer-0 IRF pw/dw fused, 2 = stem + layer-0 maxpool fused
   bool no_front = false;  // HN_NO_FRONT=1: unfused NAS stem/layer 0 (A/B, debugging)
+  bool no_irf = false;    // HN_NO_IRF=1: layer-by-layer pw/dw/pwl kernels (A/B, debugging)
   // conv tiling per layer (index 0 = stem+conv1, 2..5 = conv2..5); defaults are the best
   // measured on MI355X (tools/tune_variants.py); HN_VARIANT="003303" style override
   int variant[6] = {6, 0, 5, 6, 6, 3};
@@ -338,6 +341,27 @@ static void pack_front(const Folded& f, int mid, int g, std::vector<uint16_t>* a
         }
 }
 
+// 1x1 conv [cout][cin/g] (groups densified with zeros, output rows permuted by row_src) as
+// the fp16x3 MFMA A operand: [cout/32][cin/16][plane][lane][8], lane (r = l & 31, h = l >> 5)
+// holding W[row_src(32t + r)][16s + 8h + j].
+template <class RowSrc>
+static std::vector<uint16_t> pack_1x1_a(const std::vector<float>& w, int cout, int cin, int g,
+                                        RowSrc row_src) {
+  const int kg = cin / g;
+  std::vector<uint16_t> a((size_t)cout / 32 * (cin / 16) * 2 * 64 * 8, 0);
+  for (int tt = 0; tt < cout / 32; ++tt)
+    for (int ks = 0; ks < cin / 16; ++ks)
+      for (int lane = 0; lane < 64; ++lane)
+        for (int j = 0; j < 8; ++j) {
+          const int c = row_src(32 * tt + (lane & 31)), k = 16 * ks + 8 * (lane >> 5) + j;
+          const int grp = c / (cout / g);
+          const float v = (k >= grp * kg && k < (grp + 1) * kg) ? w[(size_t)c * kg + (k - grp * kg)] : 0.f;
+          const size_t o = ((((size_t)tt * (cin / 16) + ks) * 2) * 64 + lane) * 8 + j;
+          put_f16_split(v, &a[o], &a[o + 64 * 8]);
+        }
+  return a;
+}
+
 static int build_hardnet(hn_model* m, Cursor& cur) {
   static const int cin[7] = {1, 32, 32, 64, 64, 128, 128};
   static const int cout[7] = {32, 32, 64, 64, 128, 128, 128};
@@ -435,6 +459,15 @@ static int build_nas(hn_model* m, Cursor& cur) {
         if ((rc = m->upload(b, &L.front_b))) return rc;
         m->front = 1;
       }
+      const bool irf = i > 0 && !m->no_irf && hn_irf_supported(L.cin, L.cout, L.hin, L.stride, L.k, L.mid);
+      if (irf) {
+        const int g = L.g, cg = L.mid / g;
+        auto src = [&](int d) { return g > 1 ? (d % g) * cg + d / g : d; };  // ChannelShuffle
+        if ((rc = m->upload(pack_1x1_a(f.w, L.mid, L.cin, g, src), &L.irf_pw_a))) return rc;
+        std::vector<float> b(L.mid);
+        for (int d = 0; d < L.mid; ++d) b[d] = f.b[src(d)];
+        if ((rc = m->upload(b, &L.irf_pw_b))) return rc;
+      }
       if ((rc = take_cbr(m, cur, L.mid, (size_t)L.k * L.k, &f))) return rc;
       {
         std::vector<float> wd((size_t)L.k * L.k * L.mid);
@@ -446,6 +479,9 @@ static int build_nas(hn_model* m, Cursor& cur) {
       if ((rc = take_cbr(m, cur, L.cout, L.mid / L.g, &f))) return rc;
       if ((rc = m->upload(transpose_pw(f.w, L.cout, L.mid / L.g), &L.pwl_w))) return rc;
       if ((rc = m->upload(f.b, &L.pwl_b))) return rc;
+      if (L.irf_pw_a &&
+          (rc = m->upload(pack_1x1_a(f.w, L.cout, L.mid, L.g, [](int c) { return c; }), &L.irf_pwl_a)))
+        return rc;
       if (L.se) {
         L.semid = L.cout / 4 > 8 ? L.cout / 4 : 8;
         const size_t n1 = (size_t)L.semid * L.cout;
@@ -503,6 +539,7 @@ extern "C" int hn_create(const hn_arch_desc* desc, const float* host_params, siz
   if (const char* e = std::getenv("HN_CHUNK")) m->chunk = std::max(64, std::atoi(e));
   if (const char* e = std::getenv("HN_UNFUSED_STEM")) m->unfused_stem = std::atoi(e) != 0;
   if (const char* e = std::getenv("HN_NO_FRONT")) m->no_front = std::atoi(e) != 0;
+  if (const char* e = std::getenv("HN_NO_IRF")) m->no_irf = std::atoi(e) != 0;
   if (const char* e = std::getenv("HN_VARIANT")) {
     int i = 0;
     for (const char* c = e; *c && i < 6; ++c)
@@ -606,6 +643,16 @@ static int forward_nas(hn_model* m, const float* in, int P, float* out, float* w
       } else if (L.stride == 2) {
         std::swap(x, t1);
       }
+      continue;
+    }
+    if (L.irf_pwl_a) {
+      const HnIrfArgs ia{x, y, reinterpret_cast<const uint4*>(L.irf_pw_a), L.irf_pw_b, L.dw_w, L.dw_b,
+                         reinterpret_cast<const uint4*>(L.irf_pwl_a), L.pwl_b};
+      STAGE("irf", hn_launch_irf(ia, P, L.cin, L.cout, L.hin, L.stride, L.k, L.mid, st));
+      if (L.se)
+        STAGE("se", hn_launch_se(y, L.se_w1, L.se_b1, L.se_w2, L.se_b2, P, L.hout * L.hout, L.cout,
+                                 L.semid, st));
+      std::swap(x, y);
       continue;
     }
     const long npix_in = (long)P * L.hin * L.hin;

@@ -47,6 +47,20 @@ struct HnFrontArgs {
 bool hn_front_supported(int k, int mid);
 hipError_t hn_launch_front(const HnFrontArgs& a, int P, int k, int mid, bool maxpool, bool norm,
                            float eps, hipStream_t st);
+// fused IRF block (pw -> dw -> pwl [+ residual]) for layers 1..5, hn_irf.hip
+struct HnIrfArgs {
+  const float* x;
+  float* y;
+  const uint4* pw_a;   // [MID/32][CIN/16][plane 2][lane 64] x 8 fp16, rows in dw order
+  const float* pw_b;   // [MID] dw order
+  const float* dw_w;   // [K*K][MID]
+  const float* dw_b;
+  const uint4* pwl_a;  // [COUT/32][MID/16][plane 2][lane 64] x 8 fp16
+  const float* pwl_b;  // [COUT]
+};
+bool hn_irf_supported(int cin, int cout, int hin, int s, int k, int mid);
+hipError_t hn_launch_irf(const HnIrfArgs& a, int P, int cin, int cout, int hin, int s, int k, int mid,
+                         hipStream_t st);
 hipError_t hn_launch_preprocess(const uint8_t* in, int64_t n, int resize, int norm, float mean,
                                 float stdv, float* out, hipStream_t st);
 hipError_t hn_launch_fpr95(const float* a, const float* p, const int* labels, int64_t n, int dim,

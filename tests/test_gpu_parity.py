@@ -253,3 +253,40 @@ def test_every_candidate_op_at_layer0_fused_front(op, cuda_device):
     y = nm(x.to(cuda_device)).cpu().numpy()
     assert "front" in nm.stage_times()
     assert np.abs(y - ref).max() <= NAS_TOL
+
+
+ALL_OPS = ["skip", "ir_k3_e1", "ir_k3_e3", "ir_k3_s4", "ir_k5_e1", "ir_k5_e3", "ir_k5_s4",
+           "ir_k3_e1_se", "ir_k3_e3_se", "ir_k3_s4_se", "ir_k5_e1_se", "ir_k5_e3_se",
+           "ir_k5_s4_se", "ir_k3_s2", "ir_k5_s2", "ir_k3_s2_se", "ir_k5_s2_se"]
+
+
+@pytest.mark.parametrize("op", ALL_OPS[1:])
+def test_every_candidate_op_at_every_layer_fused_irf(op, cuda_device):
+    """The op at all six slots: layer 0 through the fused front, layers 1..5 through the
+    fused IRF block kernel (every SEARCH_SPACE2 shape incl. 16/8/4 px and e3/e4 MID); ragged
+    batch 37 exercises partial tiles (NPB = 1/4/8 patches per workgroup)."""
+    from hardnetnas_amd import synth
+    from hardnetnas_amd._native import NativeModel
+    ops = [op] * 6
+    m, p = _synth_nas(ops, seed=7)
+    x = torch.from_numpy(synth.synth_patches(37, seed=9))
+    ref = O.nas_forward(p, ops, x).numpy()
+    nm = NativeModel.from_module(m, cuda_device)
+    nm.set_profiling(True)
+    y = nm(x.to(cuda_device)).cpu().numpy()
+    st = nm.stage_times()
+    assert st["irf"][1] == 5 and "pw" not in st
+    assert np.abs(y - ref).max() <= NAS_TOL
+
+
+@pytest.mark.parametrize("name", ["wang2", "wang4"])
+def test_nas_unfused_irf_matches(name, cuda_device, monkeypatch):
+    from hardnetnas_amd._native import NativeModel
+    m, fx, _ = build_module(name)
+    monkeypatch.setenv("HN_NO_IRF", "1")
+    x = torch.from_numpy(golden_inputs(fx)).to(cuda_device)
+    nm = NativeModel.from_module(m, cuda_device)
+    nm.set_profiling(True)
+    y = nm(x).cpu().numpy()
+    assert "irf" not in nm.stage_times()
+    assert np.abs(y - fx["y"]).max() <= NAS_TOL
