@@ -58,7 +58,8 @@ HARDNET_STAGE_BYTES = {"stem": 4096 + 131072, "conv1": 2 * 131072, "stem+conv1":
 def nas_stage_bytes(ops) -> dict:
     """Algorithmic HBM bytes per patch of each NAS stage class, summed over its launches in
     one forward (fp32 NHWC in + out (+ residual read)), mirroring hn_api.hip::forward_nas
-    (stem + layer 0 run as one fused "front" kernel unless HN_NO_FRONT=1)."""
+    (stem + layer 0 run as one fused "front" kernel unless HN_NO_FRONT=1; IRF layers 1..5 as
+    fused "irf" blocks unless HN_NO_IRF=1)."""
     front = os.environ.get("HN_NO_FRONT", "0") in ("", "0")
     irf = os.environ.get("HN_NO_IRF", "0") in ("", "0")
     out = {"stem": 0 if front else 4096 + 32 * 32 * 32 * 4, "front": 0, "irf": 0, "pw": 0,
@@ -77,18 +78,16 @@ def nas_stage_bytes(ops) -> dict:
                 out["pw"] += 4 * (ci * ho * ho + co * ho * ho)
         else:
             mid = A.ir_mid(ci, spec.expansion)
-            if fused:
-                out["front"] += 4096 + 4 * mid * ho * ho
-            elif irf and i > 0:
-                # fused block: x in + y out (the residual re-read of x is not counted)
-                out["irf"] += 4 * (ci * hw * hw + co * ho * ho)
+            if fused or (irf and i > 0):
+                # fused front (stem + layer 0) / fused block: x in + y out only (the residual
+                # re-read of x is not counted)
+                out["front" if fused else "irf"] += (4096 if fused else 4 * ci * hw * hw) + 4 * co * ho * ho
                 if spec.se:
                     out["se"] += 4 * 2 * co * ho * ho
                 hw = ho
                 continue
-            else:
-                out["pw"] += 4 * (ci * hw * hw + mid * hw * hw)
-                out["dw"] += 4 * (mid * hw * hw + mid * ho * ho)
+            out["pw"] += 4 * (ci * hw * hw + mid * hw * hw)
+            out["dw"] += 4 * (mid * hw * hw + mid * ho * ho)
             res = (s == 1 and ci == co)
             out["pwl"] += 4 * (mid * ho * ho + co * ho * ho + (co * ho * ho if res else 0))
             if spec.se:

@@ -479,7 +479,7 @@ static int build_nas(hn_model* m, Cursor& cur) {
       if ((rc = take_cbr(m, cur, L.cout, L.mid / L.g, &f))) return rc;
       if ((rc = m->upload(transpose_pw(f.w, L.cout, L.mid / L.g), &L.pwl_w))) return rc;
       if ((rc = m->upload(f.b, &L.pwl_b))) return rc;
-      if (L.irf_pw_a &&
+      if ((L.irf_pw_a || (i == 0 && L.front_a)) &&
           (rc = m->upload(pack_1x1_a(f.w, L.cout, L.mid, L.g, [](int c) { return c; }), &L.irf_pwl_a)))
         return rc;
       if (L.se) {
@@ -613,17 +613,13 @@ static int forward_nas(hn_model* m, const float* in, int P, float* out, float* w
   if (m->front) {
     const NasLayer& L = m->layers[0];
     const bool mp = m->front == 2;
-    const HnFrontArgs fa{in, mp ? x : t2, reinterpret_cast<const uint4*>(m->front_spack), m->stem_b,
-                         reinterpret_cast<const uint4*>(L.front_a), L.front_b, L.dw_w, L.dw_b};
+    const HnFrontArgs fa{in, x, reinterpret_cast<const uint4*>(m->front_spack), m->stem_b,
+                         reinterpret_cast<const uint4*>(L.front_a), L.front_b, L.dw_w, L.dw_b,
+                         reinterpret_cast<const uint4*>(L.irf_pwl_a), L.pwl_b};
     STAGE("front", hn_launch_front(fa, P, L.k, L.mid, mp, ineps >= 0.f, ineps, st));
-    if (!mp) {  // layer 0 is stride 2: no residual
-      STAGE("pwl", hn_launch_pw(t2, y, L.pwl_w, L.pwl_b, nullptr, (long)P * L.hout * L.hout, L.mid,
-                                L.cout, L.g, false, 0, st));
-      if (L.se)
-        STAGE("se", hn_launch_se(y, L.se_w1, L.se_b1, L.se_w2, L.se_b2, P, L.hout * L.hout, L.cout,
-                                 L.semid, st));
-      std::swap(x, y);
-    }
+    if (!mp && L.se)
+      STAGE("se", hn_launch_se(x, L.se_w1, L.se_b1, L.se_w2, L.se_b2, P, L.hout * L.hout, L.cout,
+                               L.semid, st));
     first = 1;
   } else {
     STAGE("stem", hn_launch_stem(in, x, m->stem_w, m->stem_b, P, ineps >= 0.f, ineps, st));

@@ -4,8 +4,8 @@
 // 32x32 stage (stem output, pw output) never reach HBM.
 //
 //   MODE FRONT_IRF:     IRFBlock pw 1x1 (groups, BN, ReLU) [+ ChannelShuffle] -> dw kxk s2
-//                       (BN, ReLU)  (fbnet_builder.py:455-570); writes the dw output
-//                       [P,16,16,MID]; pwl/residual/SE follow as separate kernels.
+//                       (BN, ReLU) -> pwl 1x1 (groups, BN)  (fbnet_builder.py:455-570);
+//                       writes the layer-0 output [P,16,16,32] (SE, if any, follows as k_se).
 //   MODE FRONT_MAXPOOL: the "skip" op at stride 2 = MaxPool2d(3, 2, 1)
 //                       (fbnet_builder.py:202-228); writes [P,16,16,32].
 //
@@ -16,8 +16,9 @@
 // registers, and runs
 // the 1x1 conv for each 32-channel chunk of MID as a 32x32x32 fp16x3 MFMA tile (weights =
 // A operand, BN scale folded, shuffle folded into the row order, groups densified).  The
-// chunk's pw rows go to LDS; the depthwise conv reads them from LDS (fp32 VALU) and
-// writes float4s of 4 channels to HBM.
+// chunk's pw rows go to LDS; the depthwise conv reads them from LDS (fp32 VALU), each lane
+// producing exactly the 8 channels it holds as a pwl B operand, so the pwl fp16x3 MFMA
+// accumulates over the MID chunks in registers; only the 32-channel block output reaches HBM.
 #include "hn_common.h"
 #include "hn_internal.h"
 
@@ -45,13 +46,15 @@ __global__ __launch_bounds__(256) void k_front(const float* __restrict__ in,
                                                const float* __restrict__ pw_b,  // [MID] (dw order)
                                                const float* __restrict__ dw_w,  // [K*K][MID]
                                                const float* __restrict__ dw_b,  // [MID]
+                                               const uint4* __restrict__ pwl_a,  // [1][MID/16][2][64]
+                                               const float* __restrict__ pwl_b,  // [32]
                                                float eps) {
   constexpr int KK = MODE == FRONT_MAXPOOL ? 3 : K;
   constexpr int PAD = KK / 2;
   constexpr int IR = 2 * (RB - 1) + KK;  // pw rows of the band
   constexpr int PC = 32 + 2 * PAD;       // columns incl. zero padding
   constexpr int NT = (IR + 3) / 4;       // row tiles per wave
-  constexpr int OC = MODE == FRONT_MAXPOOL ? 32 : MID;
+  constexpr int OC = 32;  // layer-0 output channels (SEARCH_SPACE2[0] = (32, 32, 2))
   constexpr int DYU = KK == 3 ? 3 : 1;  // k5: rolled dy loop keeps VGPRs (and occupancy) in check
   __shared__ float s_in[34 * 34];
   __shared__ __attribute__((aligned(16))) float s_pw[IR * PC * PS];
@@ -162,7 +165,8 @@ __global__ __launch_bounds__(256) void k_front(const float* __restrict__ in,
     return;
   }
 
-  // ---- phases B/C per 32-channel chunk of MID ------------------------------------------
+  // ---- phases B/C/D per 32-channel chunk of MID -----------------------------------------
+  f32x16 oacc = {};
 #pragma unroll 1
   for (int m = 0; m < MID / 32; ++m) {
     // dw weights + bias of the chunk
@@ -194,35 +198,73 @@ __global__ __launch_bounds__(256) void k_front(const float* __restrict__ in,
                                    fmaxf(acc[4 * q + 2] + bias[q].z, 0.f), fmaxf(acc[4 * q + 3] + bias[q].w, 0.f));
     }
     __syncthreads();
-#pragma unroll 1
-    for (int j = 0; j < 2; ++j) {
-      const int p = 8 * (w + 4 * j) + dox, orr = p >> 4, ox = p & 15;
-      float4 acc = reinterpret_cast<const float4*>(s_dw + KK * KK * 32)[dq];
+    // dw straight into the pwl B-operand layout: wave w owns band pixel tile (w & 1) and
+    // K-step (w >> 1) of this chunk; lane (px, h) computes channels 16*(w>>1) + 8h .. +7 of
+    // band pixel 32*(w&1) + px, splits them and multiplies with the pwl weights of that
+    // K-step.  Waves 2/3 hold partial sums over the odd K-steps, folded in at the end.
+    {
+      const int p = 32 * (w & 1) + px, orr = p >> 4, ox = p & 15, c0 = 16 * (w >> 1) + 8 * h;
+      float4 a0 = *reinterpret_cast<const float4*>(s_dw + KK * KK * 32 + c0);
+      float4 a1 = *reinterpret_cast<const float4*>(s_dw + KK * KK * 32 + c0 + 4);
 #pragma unroll DYU
       for (int dy = 0; dy < KK; ++dy)
 #pragma unroll
         for (int dx = 0; dx < KK; ++dx) {
-          const float4 wv = reinterpret_cast<const float4*>(s_dw + (dy * KK + dx) * 32)[dq];
-          const float4 a = *reinterpret_cast<const float4*>(s_pw + ((2 * orr + dy) * PC + 2 * ox + dx) * PS + 4 * dq);
-          acc.x = fmaf(wv.x, a.x, acc.x); acc.y = fmaf(wv.y, a.y, acc.y);
-          acc.z = fmaf(wv.z, a.z, acc.z); acc.w = fmaf(wv.w, a.w, acc.w);
+          const float* wp = s_dw + (dy * KK + dx) * 32 + c0;
+          const float4 w0 = *reinterpret_cast<const float4*>(wp), w1 = *reinterpret_cast<const float4*>(wp + 4);
+          const float* ip = s_pw + ((2 * orr + dy) * PC + 2 * ox + dx) * PS + c0;
+          const float4 x0 = *reinterpret_cast<const float4*>(ip), x1 = *reinterpret_cast<const float4*>(ip + 4);
+          a0.x = fmaf(w0.x, x0.x, a0.x); a0.y = fmaf(w0.y, x0.y, a0.y);
+          a0.z = fmaf(w0.z, x0.z, a0.z); a0.w = fmaf(w0.w, x0.w, a0.w);
+          a1.x = fmaf(w1.x, x1.x, a1.x); a1.y = fmaf(w1.y, x1.y, a1.y);
+          a1.z = fmaf(w1.z, x1.z, a1.z); a1.w = fmaf(w1.w, x1.w, a1.w);
         }
-      acc.x = fmaxf(acc.x, 0.f); acc.y = fmaxf(acc.y, 0.f); acc.z = fmaxf(acc.z, 0.f); acc.w = fmaxf(acc.w, 0.f);
-      *reinterpret_cast<float4*>(out + ((patch * 16 + r0 + orr) * 16 + ox) * OC + 32 * m + 4 * dq) = acc;
+      a0.x = fmaxf(a0.x, 0.f); a0.y = fmaxf(a0.y, 0.f); a0.z = fmaxf(a0.z, 0.f); a0.w = fmaxf(a0.w, 0.f);
+      a1.x = fmaxf(a1.x, 0.f); a1.y = fmaxf(a1.y, 0.f); a1.z = fmaxf(a1.z, 0.f); a1.w = fmaxf(a1.w, 0.f);
+      uint4 xh, xl;
+      split8_f16(a0, a1, xh, xl);
+      const uint4* lp = pwl_a + ((size_t)(2 * m + (w >> 1)) * 2) * 64 + lane;
+      oacc = mfma3_f16(as_f16x8(lp[0]), as_f16x8(lp[64]), as_f16x8(xh), as_f16x8(xl), oacc);
     }
-    __syncthreads();
+    __syncthreads();  // s_pw / s_dw are rewritten by the next chunk
+  }
+  // fold the odd-K-step partial sums of waves 2/3 into waves 0/1 (s_pw is free now)
+  if (w >= 2) {
+    float4* d = reinterpret_cast<float4*>(s_pw) + ((w - 2) * 64 + lane) * 4;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) d[q] = make_float4(oacc[4 * q], oacc[4 * q + 1], oacc[4 * q + 2], oacc[4 * q + 3]);
+  }
+  __syncthreads();
+  if (w < 2) {
+    const float4* d = reinterpret_cast<const float4*>(s_pw) + (w * 64 + lane) * 4;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 v = d[q];
+      oacc[4 * q] += v.x; oacc[4 * q + 1] += v.y; oacc[4 * q + 2] += v.z; oacc[4 * q + 3] += v.w;
+    }
+  }
+  if (w < 2) {  // output pixel 32w + px of the band = row r0 + (32w + px) / 16
+    const int p = 32 * w + px;
+    float* dst = out + ((patch * 16 + r0 + (p >> 4)) * 16 + (p & 15)) * OC;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 b = *reinterpret_cast<const float4*>(pwl_b + 8 * q + 4 * h);
+      *reinterpret_cast<float4*>(dst + 8 * q + 4 * h) =
+          make_float4(oacc[4 * q] + b.x, oacc[4 * q + 1] + b.y, oacc[4 * q + 2] + b.z, oacc[4 * q + 3] + b.w);
+    }
   }
 }
+
 
 template <int K, int MID, int MODE>
 hipError_t front_launch(const HnFrontArgs& a, int P, bool norm, float eps, hipStream_t st) {
   const dim3 grid((unsigned)P * 4), block(256);
   if (norm)
     hipLaunchKernelGGL((k_front<K, MID, MODE, true>), grid, block, 0, st, a.in, a.out, a.spack, a.stem_b,
-                       a.apack, a.pw_b, a.dw_w, a.dw_b, eps);
+                       a.apack, a.pw_b, a.dw_w, a.dw_b, a.pwl_a, a.pwl_b, eps);
   else
     hipLaunchKernelGGL((k_front<K, MID, MODE, false>), grid, block, 0, st, a.in, a.out, a.spack, a.stem_b,
-                       a.apack, a.pw_b, a.dw_w, a.dw_b, eps);
+                       a.apack, a.pw_b, a.dw_w, a.dw_b, a.pwl_a, a.pwl_b, eps);
   return hipGetLastError();
 }
 

@@ -43,6 +43,8 @@ struct HnFrontArgs {
   const float* pw_b;    // [MID], dw channel order
   const float* dw_w;    // [K*K][MID]
   const float* dw_b;
+  const uint4* pwl_a;   // pwl A operand, [1][MID/16][plane 2][lane 64] x 8 fp16
+  const float* pwl_b;   // [32]
 };
 bool hn_front_supported(int k, int mid);
 hipError_t hn_launch_front(const HnFrontArgs& a, int P, int k, int mid, bool maxpool, bool norm,
