@@ -154,6 +154,7 @@ struct hn_model {
   float *stem_w = nullptr, *stem_b = nullptr;  // NAS stem
   std::vector<NasLayer> layers;
   float *head_w = nullptr, *head_b = nullptr;  // NAS head
+  uint16_t* head_pack = nullptr;               // NAS head as fp16x3 MFMA B operand (K = 2048)
   int head_k = 0;
   int chunk = 32768;
   bool unfused_stem = false;  // HN_UNFUSED_STEM=1: separate stem kernel (A/B, debugging)
@@ -266,7 +267,14 @@ static std::vector<uint16_t> pack_conv3x3(const std::vector<float>& w, int cin, 
 
 // head conv (kernel kk x kk over an NHWC map): GEMM k = (y*kk + x)*cin + c,
 // fragments [ks][nt][plane][lane][8]
-static std::vector<uint16_t> pack_head(const std::vector<float>& w, int cin, int kk) {
+static void put_f16_split(float v, uint16_t* hi, uint16_t* lo) {  // hn_common.h split8_f16
+  const _Float16 hv = (_Float16)v;
+  const _Float16 lv = (_Float16)(v - (float)hv);
+  std::memcpy(hi, &hv, 2);
+  std::memcpy(lo, &lv, 2);
+}
+
+static std::vector<uint16_t> pack_head(const std::vector<float>& w, int cin, int kk, bool f16 = false) {
   const int K = cin * kk * kk;
   std::vector<uint16_t> out((size_t)(K / 16) * 4 * 2 * 64 * 8);
   size_t o = 0;
@@ -280,9 +288,13 @@ static std::vector<uint16_t> pack_head(const std::vector<float>& w, int cin, int
           const int k = ks * 16 + (lane >> 5) * 8 + j;
           const int c = k % cin, yx = k / cin;
           const float v = w[((size_t)n * cin + c) * kk * kk + yx];
-          const uint16_t h = f2bf(v);
-          hi[lane * 8 + j] = h;
-          lo[lane * 8 + j] = f2bf(v - bf2f(h));
+          if (f16) {
+            put_f16_split(v, &hi[lane * 8 + j], &lo[lane * 8 + j]);
+          } else {
+            const uint16_t h = f2bf(v);
+            hi[lane * 8 + j] = h;
+            lo[lane * 8 + j] = f2bf(v - bf2f(h));
+          }
         }
       o += 2 * 64 * 8;
     }
@@ -297,12 +309,6 @@ static std::vector<float> transpose_pw(const std::vector<float>& w, int cout, in
   return t;
 }
 
-static void put_f16_split(float v, uint16_t* hi, uint16_t* lo) {  // hn_common.h split8_f16
-  const _Float16 hv = (_Float16)v;
-  const _Float16 lv = (_Float16)(v - (float)hv);
-  std::memcpy(hi, &hv, 2);
-  std::memcpy(lo, &lv, 2);
-}
 
 // Fused-front stem weights as the MFMA A operand: [plane hi/lo][lane][8] fp16, lane
 // (r = l & 31 = output channel, h = l >> 5) holding taps 8h..8h+7 (taps >= 9 are zero).
@@ -518,6 +524,7 @@ static int build_nas(hn_model* m, Cursor& cur) {
     if ((rc = m->upload(wt, &m->head_w))) return rc;
     if ((rc = m->upload(f.b, &m->head_b))) return rc;
     m->head_k = K;
+    if (K == 2048 && (rc = m->upload(pack_head(f.w, cl, 4, true), &m->head_pack))) return rc;
   }
   m->ws_floats_per_patch = maxf;
   m->n_bufs = 4;
@@ -663,7 +670,10 @@ static int forward_nas(hn_model* m, const float* in, int P, float* out, float* w
                                L.semid, st));
     std::swap(x, y);
   }
-  STAGE("head", hn_launch_nas_head(x, out, m->head_w, m->head_b, P, m->head_k, m->desc.l2_eps, st));
+  if (m->head_pack)
+    STAGE("head", hn_launch_head(x, out, m->head_pack, m->head_b, P, m->head_k, m->desc.l2_eps, st, true));
+  else
+    STAGE("head", hn_launch_nas_head(x, out, m->head_w, m->head_b, P, m->head_k, m->desc.l2_eps, st));
   return HN_OK;
 }
 

@@ -1064,7 +1064,7 @@ __global__ __launch_bounds__(256) void k_head(const float* __restrict__ a, float
 // (A rows fp32 -> bf16 hi/lo, 80-byte rows = conflict-free ds_read_b128; B fragments
 // copied linearly), so the K-loop reads only LDS.  4 waves = 2 (M: 32 patches) x 2 (N: 64).
 // ------------------------------------------------------------------------------------
-template <int K>
+template <int K, bool F16>
 __global__ __launch_bounds__(256) void k_head2(const float* __restrict__ a, float* __restrict__ out,
                                                const uint4* __restrict__ wp,
                                                const float* __restrict__ bias, int P, float l2eps) {
@@ -1094,13 +1094,27 @@ __global__ __launch_bounds__(256) void k_head2(const float* __restrict__ a, floa
     rb0 = wc_[0]; rb1 = wc_[256]; rb2 = wc_[512]; rb3 = wc_[768];                          \
   }
   auto put_row = [&](char* buf, int row, const float4 v) {
-    bf16x4 hi, lo;
-    hi[0] = (__bf16)v.x; lo[0] = (__bf16)(v.x - (float)hi[0]);
-    hi[1] = (__bf16)v.y; lo[1] = (__bf16)(v.y - (float)hi[1]);
-    hi[2] = (__bf16)v.z; lo[2] = (__bf16)(v.z - (float)hi[2]);
-    hi[3] = (__bf16)v.w; lo[3] = (__bf16)(v.w - (float)hi[3]);
-    *reinterpret_cast<uint2*>(buf + row * AROW + acol * 2) = __builtin_bit_cast(uint2, hi);
-    *reinterpret_cast<uint2*>(buf + APLANE + row * AROW + acol * 2) = __builtin_bit_cast(uint2, lo);
+    uint2 hv, lv;
+    if (F16) {  // fp16x3 split (hn_common.h split8_f16)
+      typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+      f16x4 hi, lo;
+      hi[0] = (_Float16)v.x; lo[0] = (_Float16)(v.x - (float)hi[0]);
+      hi[1] = (_Float16)v.y; lo[1] = (_Float16)(v.y - (float)hi[1]);
+      hi[2] = (_Float16)v.z; lo[2] = (_Float16)(v.z - (float)hi[2]);
+      hi[3] = (_Float16)v.w; lo[3] = (_Float16)(v.w - (float)hi[3]);
+      hv = __builtin_bit_cast(uint2, hi);
+      lv = __builtin_bit_cast(uint2, lo);
+    } else {
+      bf16x4 hi, lo;
+      hi[0] = (__bf16)v.x; lo[0] = (__bf16)(v.x - (float)hi[0]);
+      hi[1] = (__bf16)v.y; lo[1] = (__bf16)(v.y - (float)hi[1]);
+      hi[2] = (__bf16)v.z; lo[2] = (__bf16)(v.z - (float)hi[2]);
+      hi[3] = (__bf16)v.w; lo[3] = (__bf16)(v.w - (float)hi[3]);
+      hv = __builtin_bit_cast(uint2, hi);
+      lv = __builtin_bit_cast(uint2, lo);
+    }
+    *reinterpret_cast<uint2*>(buf + row * AROW + acol * 2) = hv;
+    *reinterpret_cast<uint2*>(buf + APLANE + row * AROW + acol * 2) = lv;
   };
 #define HN_STORE_CHUNK(buf)                                                                \
   {                                                                                        \
@@ -1120,14 +1134,17 @@ __global__ __launch_bounds__(256) void k_head2(const float* __restrict__ a, floa
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int aoff = (wm * 32 + r) * AROW + ks * 32 + h * 16;
-      const bf16x8 ah = as_bf16x8(*reinterpret_cast<const uint4*>(cur + aoff));
-      const bf16x8 al = as_bf16x8(*reinterpret_cast<const uint4*>(cur + APLANE + aoff));
+      const uint4 ah = *reinterpret_cast<const uint4*>(cur + aoff);
+      const uint4 al = *reinterpret_cast<const uint4*>(cur + APLANE + aoff);
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt) {
         const int boff = ABYTES + (((ks * 4 + wn * 2 + nt) * 2) * 64 + lane) * 16;
-        const bf16x8 bh = as_bf16x8(*reinterpret_cast<const uint4*>(cur + boff));
-        const bf16x8 bl = as_bf16x8(*reinterpret_cast<const uint4*>(cur + boff + 64 * 16));
-        acc[nt] = mfma3(ah, al, bh, bl, acc[nt]);
+        const uint4 bh = *reinterpret_cast<const uint4*>(cur + boff);
+        const uint4 bl = *reinterpret_cast<const uint4*>(cur + boff + 64 * 16);
+        if (F16)
+          acc[nt] = mfma3_f16(as_f16x8(ah), as_f16x8(al), as_f16x8(bh), as_f16x8(bl), acc[nt]);
+        else
+          acc[nt] = mfma3(as_bf16x8(ah), as_bf16x8(al), as_bf16x8(bh), as_bf16x8(bl), acc[nt]);
       }
     }
     if (c + 1 < NCH) HN_STORE_CHUNK(smem + ((c + 1) & 1) * BUF)
@@ -1353,17 +1370,19 @@ hipError_t hn_launch_hardnet_conv(int layer, int variant, const HardnetDev& d, c
 }
 
 hipError_t hn_launch_head(const float* a, float* out, const void* wp, const float* bias, int P,
-                          int K, float l2eps, hipStream_t st) {
+                          int K, float l2eps, hipStream_t st, bool f16) {
   const int grid = (P + 63) / 64;
   static int old = -1;
   if (old < 0) old = std::getenv("HN_HEAD_V1") ? 1 : 0;
-  if (K != 8192) return hipErrorInvalidValue;
-  if (old)
-    hipLaunchKernelGGL(k_head<8192>, dim3(grid), dim3(256), 0, st, a, out,
-                       static_cast<const uint4*>(wp), bias, P, l2eps);
+  const uint4* w = static_cast<const uint4*>(wp);
+  if (K == 8192 && !f16 && old)
+    hipLaunchKernelGGL(k_head<8192>, dim3(grid), dim3(256), 0, st, a, out, w, bias, P, l2eps);
+  else if (K == 8192 && !f16)
+    hipLaunchKernelGGL((k_head2<8192, false>), dim3(grid), dim3(256), 0, st, a, out, w, bias, P, l2eps);
+  else if (K == 2048 && f16)  // NAS head: 4x4 conv 128 -> 128 (model_supernet.py:64-68)
+    hipLaunchKernelGGL((k_head2<2048, true>), dim3(grid), dim3(256), 0, st, a, out, w, bias, P, l2eps);
   else
-    hipLaunchKernelGGL(k_head2<8192>, dim3(grid), dim3(256), 0, st, a, out,
-                       static_cast<const uint4*>(wp), bias, P, l2eps);
+    return hipErrorInvalidValue;
   return hipGetLastError();
 }
 

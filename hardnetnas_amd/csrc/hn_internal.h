@@ -15,7 +15,7 @@ hipError_t hn_launch_stem(const float* in, float* out, const float* w, const flo
 hipError_t hn_launch_hardnet_conv(int layer, int variant, const HardnetDev& d, const float* in,
                                   float* out, int P, float eps, hipStream_t st);
 hipError_t hn_launch_head(const float* a, float* out, const void* wp, const float* bias, int P,
-                          int K, float l2eps, hipStream_t st);
+                          int K, float l2eps, hipStream_t st, bool f16 = false);
 int hn_conv_lds_bytes(int layer);
 
 hipError_t hn_launch_pw(const float* in, float* out, const float* wt, const float* bias,

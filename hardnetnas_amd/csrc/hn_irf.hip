@@ -6,8 +6,9 @@
 // in one kernel, so the MID-channel intermediates (pw output, dw output) never reach HBM:
 // the block reads x once and writes y once (the residual re-reads x, usually from L2).
 //
-// A workgroup (4 waves) owns a tile of NI = 256 input pixels (NPB whole patches: 1 at 16x16,
-// 4 at 8x8, 16 -- or 8 when CIN = 128 -- at 4x4).  Per 32-channel chunk of MID:
+// Persistent workgroups (4 waves) walk a contiguous range of tiles of NI = 256 input pixels
+// (NPB whole patches: 1 at 16x16, 4 at 8x8, 16 -- or 8 when CIN = 128 -- at 4x4), prefetching
+// the next tile's input into registers.  Per 32-channel chunk of MID:
 //   pw  : 1x1 conv as 32x32 fp16x3 MFMA tiles (weights = A, BN folded, ChannelShuffle folded
 //         into the row order, groups densified).  B operands (x, split into fp16 hi/lo) are
 //         loaded once per tile and stay in registers across chunks.  bias+ReLU -> LDS (fp32).
@@ -18,6 +19,8 @@
 //         registers; epilogue adds bias (+ residual) and stores float4s.
 #include "hn_common.h"
 #include "hn_internal.h"
+
+#include <algorithm>
 
 namespace {
 
@@ -57,27 +60,49 @@ __global__ __launch_bounds__(256) void k_irf(const float* __restrict__ x, float*
 
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int px = lane & 31, h = lane >> 5;
-  const long p0 = (long)blockIdx.x * NPB;  // first patch of the tile
+  // persistent: a contiguous range of tiles per workgroup; the next tile's input is
+  // prefetched into registers while the current one is computed
+  // register prefetch + persistence only where the VGPR budget allows it without losing
+  // occupancy (CIN = 32); otherwise one tile per workgroup
+  constexpr bool PREF = CIN == 32;
+  const int ntiles = (P + NPB - 1) / NPB;
+  const int per = PREF ? (ntiles + (int)gridDim.x - 1) / (int)gridDim.x : 1;
+  const int tbeg = (int)blockIdx.x * per, tend = PREF ? min(ntiles, tbeg + per) : tbeg + 1;
+  if (tbeg >= ntiles) return;  // workgroup-uniform
+
+  float4 pa[TI][KS], pb[TI][KS];
+#define HN_IRF_LOAD(TILE)                                                                   \
+  {                                                                                         \
+    const long q0 = (long)(TILE) * NPB;                                                     \
+    const int nv = (int)min<long>(NPB, P - q0);                                             \
+    _Pragma("unroll") for (int i = 0; i < TI; ++i) {                                        \
+      const int p = (4 * i + w) * 32 + px;                                                  \
+      const bool ok = p < nv * HIN * HIN;                                                   \
+      _Pragma("unroll") for (int s = 0; s < KS; ++s) {                                      \
+        pa[i][s] = pb[i][s] = make_float4(0.f, 0.f, 0.f, 0.f);                              \
+        if (ok) {                                                                           \
+          const float4* src = reinterpret_cast<const float4*>(                              \
+              x + (q0 * (HIN * HIN) + p) * CIN + 16 * s + 8 * h);                           \
+          pa[i][s] = src[0];                                                                \
+          pb[i][s] = src[1];                                                                \
+        }                                                                                   \
+      }                                                                                     \
+    }                                                                                       \
+  }
+  if (PREF) HN_IRF_LOAD(tbeg)
+#pragma unroll 1
+  for (int tile = tbeg; tile < tend; ++tile) {
+  if (!PREF) HN_IRF_LOAD(tile)
+  const long p0 = (long)tile * NPB;  // first patch of the tile
   const int npv = (int)min<long>(NPB, P - p0);
-  const float* xt = x + p0 * (HIN * HIN * CIN);
 
   // ---- pw B operands: pixel tiles 4i + w of the workgroup tile (lane: pixel, 8 channels) --
   uint4 bh[TI][KS], bl[TI][KS];
 #pragma unroll
-  for (int i = 0; i < TI; ++i) {
-    const int p = (4 * i + w) * 32 + px;
-    const bool ok = p < npv * HIN * HIN;
+  for (int i = 0; i < TI; ++i)
 #pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
-      if (ok) {
-        const float4* src = reinterpret_cast<const float4*>(xt + (size_t)p * CIN + 16 * s + 8 * h);
-        a = src[0];
-        b = src[1];
-      }
-      split8_f16(a, b, bh[i][s], bl[i][s]);
-    }
-  }
+    for (int s = 0; s < KS; ++s) split8_f16(pa[i][s], pb[i][s], bh[i][s], bl[i][s]);
+  if (PREF && tile + 1 < tend) HN_IRF_LOAD(tile + 1)
 
   f32x16 acc[TW];
 #pragma unroll
@@ -196,13 +221,26 @@ __global__ __launch_bounds__(256) void k_irf(const float* __restrict__ x, float*
       *reinterpret_cast<float4*>(dst + c0) = v;
     }
   }
+  }  // tile loop
+#undef HN_IRF_LOAD
 }
 
 template <int CIN, int COUT, int HIN, int S, int K, int MID>
 hipError_t irf_launch(const HnIrfArgs& a, int P, hipStream_t st) {
   constexpr int NPB = IrfTile<CIN, HIN>::NPB;
-  hipLaunchKernelGGL((k_irf<CIN, COUT, HIN, S, K, MID>), dim3((unsigned)((P + NPB - 1) / NPB)), dim3(256), 0,
-                     st, a.x, a.y, a.pw_a, a.pw_b, a.dw_w, a.dw_b, a.pwl_a, a.pwl_b, P);
+  const void* fn = reinterpret_cast<const void*>(&k_irf<CIN, COUT, HIN, S, K, MID>);
+  static int resident = 0;  // persistent grid: every workgroup resident at once
+  if (!resident) {
+    int per_cu = 0, dev = 0, cus = 0;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, 0);
+    if (e != hipSuccess) return e;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    resident = std::max(1, per_cu) * std::max(1, cus);
+  }
+  const int grid = CIN == 32 ? std::min((P + NPB - 1) / NPB, resident) : (P + NPB - 1) / NPB;
+  hipLaunchKernelGGL((k_irf<CIN, COUT, HIN, S, K, MID>), dim3(grid), dim3(256), 0, st, a.x, a.y, a.pw_a,
+                     a.pw_b, a.dw_w, a.dw_b, a.pwl_a, a.pwl_b, P);
   return hipGetLastError();
 }
 

@@ -15,7 +15,7 @@ for f in sorted(glob.glob(os.path.join(root, "p*", "run_counter_collection.csv")
         k = r["Kernel_Name"]
         if pats and not any(p in k for p in pats):
             continue
-        k = k.split("(")[0][:70]
+        k = k.replace("(anonymous namespace)::", "").split("(")[0][:70]
         tot[k][r["Counter_Name"]] += float(r["Counter_Value"])
         disp[k][r["Counter_Name"]].add(r["Dispatch_Id"])
 for k in sorted(tot):
