@@ -5,7 +5,7 @@
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));  // arithmetic on it emits v_pk_fma_f32
 
 #define HN_DEV __device__ __forceinline__
 

@@ -48,7 +48,7 @@ __global__ __launch_bounds__(256) void k_front(const float* __restrict__ in,
                                                const float* __restrict__ dw_b,  // [MID]
                                                const uint4* __restrict__ pwl_a,  // [1][MID/16][2][64]
                                                const float* __restrict__ pwl_b,  // [32]
-                                               float eps) {
+                                               int P, float eps) {
   constexpr int KK = MODE == FRONT_MAXPOOL ? 3 : K;
   constexpr int PAD = KK / 2;
   constexpr int IR = 2 * (RB - 1) + KK;  // pw rows of the band
@@ -63,8 +63,11 @@ __global__ __launch_bounds__(256) void k_front(const float* __restrict__ in,
 
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int px = lane & 31, h = lane >> 5;
-  const long patch = blockIdx.x >> 2;
-  const int r0 = (blockIdx.x & 3) * RB;
+  // XCD-aware: workgroups b, b+8, b+16, b+24 (dispatched round-robin to the same XCD) are
+  // the 4 bands of one patch, so the patch is read from HBM once and then hits that L2
+  const long patch = (long)(blockIdx.x >> 5) * 8 + (blockIdx.x & 7);
+  const int r0 = ((blockIdx.x >> 3) & 3) * RB;
+  if (patch >= P) return;  // grid is padded to a multiple of 32 workgroups
   const int row0 = 2 * r0 - PAD;
 
   // ---- phase 0: patch (+ input_norm) to LDS; zero the pw band's padding -----------------
@@ -118,8 +121,7 @@ __global__ __launch_bounds__(256) void k_front(const float* __restrict__ in,
 #pragma unroll
   for (int i = 0; i < NT; ++i) {
     const int ri = w + 4 * i, y = row0 + ri;
-    bh[i][0] = bh[i][1] = bl[i][0] = bl[i][1] = make_uint4(0, 0, 0, 0);
-    if (ri >= IR || y < 0 || y >= 32) continue;  // wave-uniform
+    if (ri >= IR || y < 0 || y >= 32) continue;  // wave-uniform; such tiles are never read
     float tp[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -204,25 +206,21 @@ __global__ __launch_bounds__(256) void k_front(const float* __restrict__ in,
     // K-step.  Waves 2/3 hold partial sums over the odd K-steps, folded in at the end.
     {
       const int p = 32 * (w & 1) + px, orr = p >> 4, ox = p & 15, c0 = 16 * (w >> 1) + 8 * h;
-      float4 a0 = *reinterpret_cast<const float4*>(s_dw + KK * KK * 32 + c0);
-      float4 a1 = *reinterpret_cast<const float4*>(s_dw + KK * KK * 32 + c0 + 4);
+      f32x4 a0 = *reinterpret_cast<const f32x4*>(s_dw + KK * KK * 32 + c0);
+      f32x4 a1 = *reinterpret_cast<const f32x4*>(s_dw + KK * KK * 32 + c0 + 4);
 #pragma unroll DYU
       for (int dy = 0; dy < KK; ++dy)
 #pragma unroll
         for (int dx = 0; dx < KK; ++dx) {
           const float* wp = s_dw + (dy * KK + dx) * 32 + c0;
-          const float4 w0 = *reinterpret_cast<const float4*>(wp), w1 = *reinterpret_cast<const float4*>(wp + 4);
           const float* ip = s_pw + ((2 * orr + dy) * PC + 2 * ox + dx) * PS + c0;
-          const float4 x0 = *reinterpret_cast<const float4*>(ip), x1 = *reinterpret_cast<const float4*>(ip + 4);
-          a0.x = fmaf(w0.x, x0.x, a0.x); a0.y = fmaf(w0.y, x0.y, a0.y);
-          a0.z = fmaf(w0.z, x0.z, a0.z); a0.w = fmaf(w0.w, x0.w, a0.w);
-          a1.x = fmaf(w1.x, x1.x, a1.x); a1.y = fmaf(w1.y, x1.y, a1.y);
-          a1.z = fmaf(w1.z, x1.z, a1.z); a1.w = fmaf(w1.w, x1.w, a1.w);
+          a0 = __builtin_elementwise_fma(*reinterpret_cast<const f32x4*>(wp), *reinterpret_cast<const f32x4*>(ip), a0);
+          a1 = __builtin_elementwise_fma(*reinterpret_cast<const f32x4*>(wp + 4), *reinterpret_cast<const f32x4*>(ip + 4), a1);
         }
-      a0.x = fmaxf(a0.x, 0.f); a0.y = fmaxf(a0.y, 0.f); a0.z = fmaxf(a0.z, 0.f); a0.w = fmaxf(a0.w, 0.f);
-      a1.x = fmaxf(a1.x, 0.f); a1.y = fmaxf(a1.y, 0.f); a1.z = fmaxf(a1.z, 0.f); a1.w = fmaxf(a1.w, 0.f);
+      a0 = __builtin_elementwise_max(a0, f32x4{});
+      a1 = __builtin_elementwise_max(a1, f32x4{});
       uint4 xh, xl;
-      split8_f16(a0, a1, xh, xl);
+      split8_f16(make_float4(a0.x, a0.y, a0.z, a0.w), make_float4(a1.x, a1.y, a1.z, a1.w), xh, xl);
       const uint4* lp = pwl_a + ((size_t)(2 * m + (w >> 1)) * 2) * 64 + lane;
       oacc = mfma3_f16(as_f16x8(lp[0]), as_f16x8(lp[64]), as_f16x8(xh), as_f16x8(xl), oacc);
     }
@@ -258,13 +256,13 @@ __global__ __launch_bounds__(256) void k_front(const float* __restrict__ in,
 
 template <int K, int MID, int MODE>
 hipError_t front_launch(const HnFrontArgs& a, int P, bool norm, float eps, hipStream_t st) {
-  const dim3 grid((unsigned)P * 4), block(256);
+  const dim3 grid((unsigned)((P + 7) / 8) * 32), block(256);
   if (norm)
     hipLaunchKernelGGL((k_front<K, MID, MODE, true>), grid, block, 0, st, a.in, a.out, a.spack, a.stem_b,
-                       a.apack, a.pw_b, a.dw_w, a.dw_b, a.pwl_a, a.pwl_b, eps);
+                       a.apack, a.pw_b, a.dw_w, a.dw_b, a.pwl_a, a.pwl_b, P, eps);
   else
     hipLaunchKernelGGL((k_front<K, MID, MODE, false>), grid, block, 0, st, a.in, a.out, a.spack, a.stem_b,
-                       a.apack, a.pw_b, a.dw_w, a.dw_b, a.pwl_a, a.pwl_b, eps);
+                       a.apack, a.pw_b, a.dw_w, a.dw_b, a.pwl_a, a.pwl_b, P, eps);
   return hipGetLastError();
 }
 

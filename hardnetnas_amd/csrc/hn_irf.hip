@@ -4,7 +4,8 @@
 //   y = pwl(dw(shuffle(pw(x)))) [+ x]        (SE, when present, runs after as k_se)
 //
 // in one kernel, so the MID-channel intermediates (pw output, dw output) never reach HBM:
-// the block reads x once and writes y once (the residual re-reads x, usually from L2).
+// the block reads x once and writes y once (the residual comes from the x operands already
+// in registers).
 //
 // Persistent workgroups (4 waves) walk a contiguous range of tiles of NI = 256 input pixels
 // (NPB whole patches: 1 at 16x16, 4 at 8x8, 16 -- or 8 when CIN = 128 -- at 4x4), prefetching
@@ -16,7 +17,7 @@
 //         thread sliding a register window along a run of R output pixels of one row for 4
 //         channels; result -> LDS (fp32).
 //   pwl : 1x1 conv (BN, no ReLU) as fp16x3 MFMA tiles accumulating over the chunks in
-//         registers; epilogue adds bias (+ residual) and stores float4s.
+//         registers (+ the residual as identity-weight K-steps); bias, float4 stores.
 #include "hn_common.h"
 #include "hn_internal.h"
 
@@ -150,8 +151,8 @@ __global__ __launch_bounds__(256) void k_irf(const float* __restrict__ x, float*
       const int q = it & 7, run = it >> 3;
       const int o0 = run * R;  // first output pixel (tile-local)
       const int pl = o0 / (HOUT * HOUT), oy = (o0 / HOUT) % HOUT, ox0 = o0 % HOUT;
-      const float4 b4 = reinterpret_cast<const float4*>(s_w + K * K * 32)[q];
-      float4 o[R];
+      const f32x4 b4 = reinterpret_cast<const f32x4*>(s_w + K * K * 32)[q];
+      f32x4 o[R];
 #pragma unroll
       for (int r = 0; r < R; ++r) o[r] = b4;
       const int ix0 = ox0 * S - PAD;
@@ -160,28 +161,22 @@ __global__ __launch_bounds__(256) void k_irf(const float* __restrict__ x, float*
         const int iy = oy * S + dy - PAD;
         if (iy < 0 || iy >= HIN) continue;
         const float* rowp = s_pw + ((pl * HIN + iy) * HIN) * PS + 4 * q;
-        float4 win[WIN];
+        f32x4 win[WIN];
 #pragma unroll
         for (int c = 0; c < WIN; ++c) {
           const int ix = ix0 + c;
-          win[c] = (ix >= 0 && ix < HIN) ? *reinterpret_cast<const float4*>(rowp + ix * PS)
-                                         : make_float4(0.f, 0.f, 0.f, 0.f);
+          win[c] = (ix >= 0 && ix < HIN) ? *reinterpret_cast<const f32x4*>(rowp + ix * PS) : f32x4{};
         }
 #pragma unroll
         for (int dx = 0; dx < K; ++dx) {
-          const float4 wv = reinterpret_cast<const float4*>(s_w + (dy * K + dx) * 32)[q];
+          const f32x4 wv = reinterpret_cast<const f32x4*>(s_w + (dy * K + dx) * 32)[q];
 #pragma unroll
-          for (int r = 0; r < R; ++r) {
-            const float4 a = win[r * S + dx];
-            o[r].x = fmaf(wv.x, a.x, o[r].x); o[r].y = fmaf(wv.y, a.y, o[r].y);
-            o[r].z = fmaf(wv.z, a.z, o[r].z); o[r].w = fmaf(wv.w, a.w, o[r].w);
-          }
+          for (int r = 0; r < R; ++r) o[r] = __builtin_elementwise_fma(wv, win[r * S + dx], o[r]);
         }
       }
 #pragma unroll
       for (int r = 0; r < R; ++r)
-        *reinterpret_cast<float4*>(s_dw + (o0 + r) * PS + 4 * q) =
-            make_float4(fmaxf(o[r].x, 0.f), fmaxf(o[r].y, 0.f), fmaxf(o[r].z, 0.f), fmaxf(o[r].w, 0.f));
+        *reinterpret_cast<f32x4*>(s_dw + (o0 + r) * PS + 4 * q) = __builtin_elementwise_max(o[r], f32x4{});
     }
     __syncthreads();
     // ---- pwl (accumulate this chunk's 32 mid channels = 2 K-steps) -----------------------
@@ -200,25 +195,38 @@ __global__ __launch_bounds__(256) void k_irf(const float* __restrict__ x, float*
     __syncthreads();  // s_pw / s_dw / s_w are rewritten by the next chunk
   }
 
-  // ---- epilogue: bias (+ residual), float4 stores ------------------------------------------
+  // ---- residual: y += x as two more MFMA K-steps per tile with an identity A operand
+  // against the x B operands already in registers (x = hi + lo to ~2^-22; no second read of
+  // x from HBM).  With S = 1, NI = NO, so the wave's pwl pixel tiles are its pw tiles.
+  if (RES) {
+#pragma unroll
+    for (int i = 0; i < TW; ++i) {
+      constexpr int TPW = NOT / 4;  // pixel tiles per wave (= TI)
+      const int ii = i % TPW, ct = i / TPW;
+#pragma unroll
+      for (int sl = 0; sl < 2; ++sl) {
+        f16x8 id;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) id[j] = (_Float16)((px == 16 * sl + 8 * h + j) ? 1.f : 0.f);
+        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(id, as_f16x8(bl[ii][2 * ct + sl]), acc[i], 0, 0, 0);
+        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(id, as_f16x8(bh[ii][2 * ct + sl]), acc[i], 0, 0, 0);
+      }
+    }
+  }
+
+  // ---- epilogue: bias, float4 stores -------------------------------------------------------
 #pragma unroll
   for (int i = 0; i < TW; ++i) {
     const int tile = 4 * i + w, pt = tile % NOT, ct = tile / NOT;
     const int o = pt * 32 + px;
     if (o >= npv * HOUT * HOUT) continue;
     float* dst = y + (p0 * (HOUT * HOUT) + o) * COUT + 32 * ct;
-    const float* rsrc = x + (p0 * (HIN * HIN) + o) * CIN + 32 * ct;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int c0 = 8 * q + 4 * h;
       const float4 b = *reinterpret_cast<const float4*>(pwl_b + 32 * ct + c0);
-      float4 v = make_float4(acc[i][4 * q] + b.x, acc[i][4 * q + 1] + b.y, acc[i][4 * q + 2] + b.z,
-                             acc[i][4 * q + 3] + b.w);
-      if (RES) {
-        const float4 rv = *reinterpret_cast<const float4*>(rsrc + c0);
-        v.x += rv.x; v.y += rv.y; v.z += rv.z; v.w += rv.w;
-      }
-      *reinterpret_cast<float4*>(dst + c0) = v;
+      *reinterpret_cast<float4*>(dst + c0) = make_float4(acc[i][4 * q] + b.x, acc[i][4 * q + 1] + b.y,
+                                                         acc[i][4 * q + 2] + b.z, acc[i][4 * q + 3] + b.w);
     }
   }
   }  // tile loop
