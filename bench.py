@@ -48,9 +48,11 @@ PEAK_HBM = 8000.0                 # GB/s
 
 # algorithmic work per patch of each HardNet stage
 HARDNET_STAGE_MAC = {"stem": 294912, "conv1": 9437184, "stem+conv1": 294912 + 9437184,
+                     "stem+conv1+conv2": 294912 + 9437184 + 4718592,
                      "conv2": 4718592, "conv3": 9437184, "conv4": 4718592, "conv5": 9437184,
                      "head": 1048576}
 HARDNET_STAGE_BYTES = {"stem": 4096 + 131072, "conv1": 2 * 131072, "stem+conv1": 4096 + 131072,
+                       "stem+conv1+conv2": 4096 + 65536,
                        "conv2": 131072 + 65536, "conv3": 2 * 65536, "conv4": 65536 + 32768,
                        "conv5": 2 * 32768, "head": 32768 + 512}
 

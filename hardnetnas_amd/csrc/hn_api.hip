@@ -158,6 +158,7 @@ struct hn_model {
   int head_k = 0;
   int chunk = 32768;
   bool unfused_stem = false;  // HN_UNFUSED_STEM=1: separate stem kernel (A/B, debugging)
+  bool c12 = true;            // fused stem+conv1+conv2 (k_c12); HN_NO_C12=1 -> separate kernels
   uint16_t* front_spack = nullptr;  // fused front: stem as MFMA A operand
   int front = 0;  // NAS: 1 = stem + layer-0 IRF pw/dw fused, 2 = stem + layer-0 maxpool fused
   bool no_front = false;  // HN_NO_FRONT=1: unfused NAS stem/layer 0 (A/B, debugging)
@@ -368,6 +369,26 @@ static std::vector<uint16_t> pack_1x1_a(const std::vector<float>& w, int cout, i
   return a;
 }
 
+// 3x3 conv (cin = 32, BN folded) as 16x16x32 bf16 hi/lo A operands for k_c12:
+// [tap 9][group of 16 output channels][plane][lane 64][8], lane (row = l & 15 -> output
+// channel 16 g + row, k-group l >> 4 -> input channels 8 (l >> 4) + j).
+static std::vector<uint16_t> pack_c12(const std::vector<float>& w, int cout) {
+  const int cin = 32, ng = cout / 16;
+  std::vector<uint16_t> a((size_t)9 * ng * 2 * 64 * 8);
+  for (int tap = 0; tap < 9; ++tap)
+    for (int g = 0; g < ng; ++g)
+      for (int lane = 0; lane < 64; ++lane)
+        for (int j = 0; j < 8; ++j) {
+          const int oc = 16 * g + (lane & 15), ic = 8 * (lane >> 4) + j;
+          const float v = w[((size_t)oc * cin + ic) * 9 + tap];
+          const uint16_t hv = f2bf(v);
+          const size_t o = (((size_t)tap * ng + g) * 2 * 64 + lane) * 8 + j;
+          a[o] = hv;
+          a[o + 64 * 8] = f2bf(v - bf2f(hv));
+        }
+  return a;
+}
+
 static int build_hardnet(hn_model* m, Cursor& cur) {
   static const int cin[7] = {1, 32, 32, 64, 64, 128, 128};
   static const int cout[7] = {32, 32, 64, 64, 128, 128, 128};
@@ -394,6 +415,11 @@ static int build_hardnet(hn_model* m, Cursor& cur) {
     if ((rc = m->upload(pk, &d))) return rc;
     m->hd.wpack[l] = d;
     if ((rc = m->upload(f.b, &m->hd.bias[l]))) return rc;
+    if (l == 1 || l == 2) {
+      uint16_t* c = nullptr;
+      if ((rc = m->upload(pack_c12(f.w, cout[l]), &c))) return rc;
+      (l == 1 ? m->hd.c12_w1 : m->hd.c12_w2) = c;
+    }
   }
   m->ws_floats_per_patch = 32 * 32 * 32;
   m->n_bufs = 3;
@@ -546,6 +572,7 @@ extern "C" int hn_create(const hn_arch_desc* desc, const float* host_params, siz
   if (const char* e = std::getenv("HN_CHUNK")) m->chunk = std::max(64, std::atoi(e));
   if (const char* e = std::getenv("HN_UNFUSED_STEM")) m->unfused_stem = std::atoi(e) != 0;
   if (const char* e = std::getenv("HN_NO_FRONT")) m->no_front = std::atoi(e) != 0;
+  if (const char* e = std::getenv("HN_NO_C12")) m->c12 = std::atoi(e) == 0;
   if (const char* e = std::getenv("HN_NO_IRF")) m->no_irf = std::atoi(e) != 0;
   if (const char* e = std::getenv("HN_VARIANT")) {
     int i = 0;
@@ -594,13 +621,17 @@ static int forward_hardnet(hn_model* m, const float* in, int P, float* out, floa
   float* a1 = ws + per;
   float* a2 = ws + 2 * per;
   const float ineps = m->desc.input_norm_eps;
-  if (m->unfused_stem) {
-    STAGE("stem", hn_launch_stem(in, a0, m->hd.stem_w, m->hd.stem_b, P, ineps >= 0.f, ineps, st));
-    STAGE("conv1", hn_launch_hardnet_conv(1, 0, m->hd, a0, a1, P, 0.f, st));
+  if (m->c12 && !m->unfused_stem) {
+    STAGE("stem+conv1+conv2", hn_launch_c12(in, a2, m->hd, P, ineps, st));
   } else {
-    STAGE("stem+conv1", hn_launch_hardnet_conv(0, m->variant[0], m->hd, in, a1, P, ineps, st));
+    if (m->unfused_stem) {
+      STAGE("stem", hn_launch_stem(in, a0, m->hd.stem_w, m->hd.stem_b, P, ineps >= 0.f, ineps, st));
+      STAGE("conv1", hn_launch_hardnet_conv(1, 0, m->hd, a0, a1, P, 0.f, st));
+    } else {
+      STAGE("stem+conv1", hn_launch_hardnet_conv(0, m->variant[0], m->hd, in, a1, P, ineps, st));
+    }
+    STAGE("conv2", hn_launch_hardnet_conv(2, m->variant[2], m->hd, a1, a2, P, 0.f, st));
   }
-  STAGE("conv2", hn_launch_hardnet_conv(2, m->variant[2], m->hd, a1, a2, P, 0.f, st));
   STAGE("conv3", hn_launch_hardnet_conv(3, m->variant[3], m->hd, a2, a1, P, 0.f, st));
   STAGE("conv4", hn_launch_hardnet_conv(4, m->variant[4], m->hd, a1, a2, P, 0.f, st));
   STAGE("conv5", hn_launch_hardnet_conv(5, m->variant[5], m->hd, a2, a1, P, 0.f, st));

@@ -1,0 +1,244 @@
+// k_c12: HardNet input_norm + conv0 + conv1 + conv2 (hardnet/HardNet.py:281-289, 306-310) in
+// one kernel, so the two 128 KB/patch activations a0 and a1 never reach HBM: the kernel reads
+// the 4 KB patch and writes a2 (64 KB/patch, [P,16,16,64] fp32 NHWC).
+//
+// Persistent workgroups of 8 waves walk a contiguous range of (patch, band) items; a band is
+// 4 rows of conv2 output.  Per band:
+//   P1 stem : the 11 a0 rows the band needs (halo recomputed by the neighbour band) on the
+//             MFMA (32x32x16 bf16x3, K = 9 taps), BN+ReLU, split to bf16 hi/lo -> LDS window W0.
+//   P2 conv1: the 9 a1 rows as 16x16x32 bf16x3 MFMA tiles (16 pixels x 16 channels, K = 32
+//             channels per tap), each wave owning one 16-channel half with its 9 taps of
+//             weights resident in VGPRs; BN+ReLU, split -> LDS window W1 (even/odd columns
+//             split for the stride-2 reads of conv2).
+//   P3 conv2: 4 rows x 16 pixels x 64 channels as 16x16x32 tiles, each wave owning one
+//             16-channel quarter (weights resident); BN+ReLU -> float4 stores of a2.
+// LDS pixel stride 160 B (bf16 hi 64 B | lo 64 B | pad 32 B): every ds_read_b128 of a
+// 16x16x32 operand (lane: pixel l & 15, channels 8 (l >> 4) ..) hits 16 distinct 16-byte
+// slots per 16-lane group (tests/test_lds_banks.py::test_c12_windows).
+// Two barriers per band: P3 of band b overlaps P1 of band b+1 across waves.
+#include "hn_common.h"
+#include "hn_internal.h"
+
+#include <algorithm>
+
+namespace {
+
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+
+constexpr int RB2 = 4;                  // conv2 output rows per band
+constexpr int NA0 = 2 * RB2 + 3;        // a0 rows per band (11)
+constexpr int NA1 = 2 * RB2 + 1;        // a1 rows per band (9)
+constexpr int PXB = 160;                // bytes per pixel in W0 / W1
+constexpr int W0C = 34, W1C = 33;       // columns (x = -1 .. 32 / -1 .. 31)
+constexpr int W0B = NA0 * W0C * PXB;    // 59,840
+constexpr int W1B = NA1 * W1C * PXB;    // 47,520
+constexpr int NWAVE = 8;
+
+HN_DEV f32x4v mfma16(const uint4& a, const uint4& b, f32x4v c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a), as_bf16x8(b), c, 0, 0, 0);
+}
+
+HN_DEV uint2 pack_bf16x4(float a, float b, float c, float d, uint2& lo) {
+  bf16x4 h, l;
+  h[0] = (__bf16)a; l[0] = (__bf16)(a - (float)h[0]);
+  h[1] = (__bf16)b; l[1] = (__bf16)(b - (float)h[1]);
+  h[2] = (__bf16)c; l[2] = (__bf16)(c - (float)h[2]);
+  h[3] = (__bf16)d; l[3] = (__bf16)(d - (float)h[3]);
+  lo = __builtin_bit_cast(uint2, l);
+  return __builtin_bit_cast(uint2, h);
+}
+
+// W1 column slot of a1 column x (x = -1 .. 31): even (x + 1) -> (x + 1) / 2, odd -> 17 + x / 2
+HN_DEV int w1_slot(int x) { return ((x + 1) & 1) ? 17 + (x >> 1) : (x + 1) >> 1; }
+
+__global__ __launch_bounds__(NWAVE * 64) void k_c12(
+    const float* __restrict__ in, float* __restrict__ out, const float* __restrict__ stem_w,
+    const float* __restrict__ stem_b, const uint4* __restrict__ w1p, const float* __restrict__ b1,
+    const uint4* __restrict__ w2p, const float* __restrict__ b2, int P, float eps) {
+  __shared__ __attribute__((aligned(16))) char s_w0[W0B];
+  __shared__ __attribute__((aligned(16))) char s_w1[W1B];
+  __shared__ float s_in[34 * 34];
+  __shared__ float red[2 * NWAVE];
+
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int r32 = lane & 31, h32 = lane >> 5;  // 32x32x16 lane roles (stem)
+  const int c16 = lane & 15, g16 = lane >> 4;  // 16x16x32 lane roles (conv1/conv2)
+
+  const long nitems = (long)P * 4;
+  const long per = (nitems + gridDim.x - 1) / gridDim.x;
+  const long ib = (long)xcd_remap(blockIdx.x, gridDim.x) * per;
+  const long ie = min(nitems, ib + per);
+  if (ib >= ie) return;  // workgroup-uniform
+
+  // ---- one-time init: zero both windows (borders and never-written slots stay zero) ----
+  for (int i = t; i < W0B / 16; i += NWAVE * 64) reinterpret_cast<uint4*>(s_w0)[i] = make_uint4(0, 0, 0, 0);
+  for (int i = t; i < W1B / 16; i += NWAVE * 64) reinterpret_cast<uint4*>(s_w1)[i] = make_uint4(0, 0, 0, 0);
+  for (int i = t; i < 34 * 34; i += NWAVE * 64) s_in[i] = 0.f;
+
+  // stem A operand (32x32x16): lane (channel r32, taps 8*h32 ..), bf16 hi/lo
+  bf16x8 sah, sal;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int tap = 8 * h32 + j;
+    const float v = tap < 9 ? stem_w[tap * 32 + r32] : 0.f;
+    sah[j] = (__bf16)v;
+    sal[j] = (__bf16)(v - (float)sah[j]);
+  }
+  // conv1 / conv2 A operands resident in VGPRs: [tap][plane]
+  const int chh = w & 1, chq = w & 3;
+  uint4 a1w[9][2], a2w[9][2];
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap) {
+#pragma unroll
+    for (int pl = 0; pl < 2; ++pl) {
+      a1w[tap][pl] = w1p[((tap * 2 + chh) * 2 + pl) * 64 + lane];
+      a2w[tap][pl] = w2p[((tap * 4 + chq) * 2 + pl) * 64 + lane];
+    }
+  }
+  const f32x4v bias1 = *reinterpret_cast<const f32x4v*>(b1 + 16 * chh + 4 * g16);
+  const f32x4v bias2 = *reinterpret_cast<const f32x4v*>(b2 + 16 * chq + 4 * g16);
+
+  long cur_patch = -1;
+#pragma unroll 1
+  for (long item = ib; item < ie; ++item) {
+    const long patch = item >> 2;
+    const int r0 = (int)(item & 3) * RB2;
+    if (patch != cur_patch) {  // workgroup-uniform
+      cur_patch = patch;
+      const float2 v = reinterpret_cast<const float2*>(in + patch * 1024)[t];
+      float mean = 0.f, sd = 1.f;
+      if (eps >= 0.f) {  // input_norm: (x - mean) / (std_unbiased + eps), HardNet.py:306-310
+        const float s = wave_sum(v.x + v.y);
+        if (lane == 0) red[w] = s;
+        __syncthreads();
+        float a = 0.f;
+#pragma unroll
+        for (int i = 0; i < NWAVE; ++i) a += red[i];
+        mean = a * (1.f / 1024.f);
+        const float d0 = v.x - mean, d1 = v.y - mean;
+        const float q = wave_sum(d0 * d0 + d1 * d1);
+        if (lane == 0) red[NWAVE + w] = q;
+        __syncthreads();
+        a = 0.f;
+#pragma unroll
+        for (int i = 0; i < NWAVE; ++i) a += red[NWAVE + i];
+        sd = sqrtf(a * (1.f / 1023.f)) + eps;
+      }
+      const float inv = 1.f / sd;  // as k_conv_ws's stem: (x - mean) * (1/sd)
+      const int q2 = 2 * t, y = q2 >> 5, x = q2 & 31;
+      s_in[(y + 1) * 34 + x + 1] = (v.x - mean) * inv;
+      s_in[(y + 1) * 34 + x + 2] = (v.y - mean) * inv;
+      __syncthreads();
+    }
+
+    // ---- P1: stem rows -> W0 ---------------------------------------------------------------
+    const int y0base = 2 * r0 - 2;
+#pragma unroll 1
+    for (int ri = w; ri < NA0; ri += NWAVE) {
+      const int y = y0base + ri;  // a0 row
+      char* rowp = s_w0 + ri * W0C * PXB;
+      if (y < 0 || y >= 32) {  // zero padding row (interior columns)
+        for (int i = lane; i < 32 * (PXB / 16); i += 64)
+          reinterpret_cast<uint4*>(rowp + PXB)[i] = make_uint4(0, 0, 0, 0);
+        continue;
+      }
+      bf16x8 xh, xl;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int tap = 8 * h32 + j;
+        const float v = tap < 9 ? s_in[(y + tap / 3) * 34 + r32 + tap % 3] : 0.f;
+        xh[j] = (__bf16)v;
+        xl[j] = (__bf16)(v - (float)xh[j]);
+      }
+      const f32x16 c0 = mfma3(sah, sal, xh, xl, f32x16{});
+      char* o = rowp + (r32 + 1) * PXB + 8 * h32;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 b = *reinterpret_cast<const float4*>(stem_b + 8 * q + 4 * h32);
+        uint2 lo;
+        const uint2 hi = pack_bf16x4(fmaxf(c0[4 * q] + b.x, 0.f), fmaxf(c0[4 * q + 1] + b.y, 0.f),
+                                     fmaxf(c0[4 * q + 2] + b.z, 0.f), fmaxf(c0[4 * q + 3] + b.w, 0.f), lo);
+        *reinterpret_cast<uint2*>(o + 16 * q) = hi;
+        *reinterpret_cast<uint2*>(o + 64 + 16 * q) = lo;
+      }
+    }
+    __syncthreads();
+
+    // ---- P2: conv1 -> W1 (units: a1 row x pixel half; this wave's channel half) -------------
+#pragma unroll 1
+    for (int u = w >> 1; u < NA1 * 2; u += NWAVE / 2) {
+      const int row1 = u >> 1, pxh = u & 1;
+      const int y1 = 2 * r0 - 1 + row1;
+      const int x = 16 * pxh + c16;
+      char* dst = s_w1 + (row1 * W1C + w1_slot(x)) * PXB + 32 * chh + 8 * g16;
+      if (y1 < 0 || y1 >= 32) {  // zero padding row of a1
+        *reinterpret_cast<uint2*>(dst) = make_uint2(0, 0);
+        *reinterpret_cast<uint2*>(dst + 64) = make_uint2(0, 0);
+        continue;
+      }
+      f32x4v acc = {};
+      const char* src = s_w0 + (row1 * W0C + x) * PXB + 16 * g16;
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const char* p = src + ((tap / 3) * W0C + tap % 3) * PXB;
+        const uint4 bh = *reinterpret_cast<const uint4*>(p);
+        const uint4 bl = *reinterpret_cast<const uint4*>(p + 64);
+        acc = mfma16(a1w[tap][1], bh, acc);
+        acc = mfma16(a1w[tap][0], bl, acc);
+        acc = mfma16(a1w[tap][0], bh, acc);
+      }
+      acc = __builtin_elementwise_max(acc + bias1, f32x4v{});
+      uint2 lo;
+      const uint2 hi = pack_bf16x4(acc[0], acc[1], acc[2], acc[3], lo);
+      *reinterpret_cast<uint2*>(dst) = hi;
+      *reinterpret_cast<uint2*>(dst + 64) = lo;
+    }
+    __syncthreads();
+
+    // ---- P3: conv2 (stride 2) -> a2 in HBM (units: output row; this wave's quarter) ---------
+#pragma unroll 1
+    for (int oy = w >> 2; oy < RB2; oy += NWAVE / 4) {
+      f32x4v acc = {};
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int dy = tap / 3, dx = tap % 3;
+        // output column c16 reads a1 column 2*c16 - 1 + dx
+        const int slot = dx == 1 ? 17 + c16 : c16 + (dx >> 1);
+        const char* p = s_w1 + ((2 * oy + dy) * W1C + slot) * PXB + 16 * g16;
+        const uint4 bh = *reinterpret_cast<const uint4*>(p);
+        const uint4 bl = *reinterpret_cast<const uint4*>(p + 64);
+        acc = mfma16(a2w[tap][1], bh, acc);
+        acc = mfma16(a2w[tap][0], bl, acc);
+        acc = mfma16(a2w[tap][0], bh, acc);
+      }
+      acc = __builtin_elementwise_max(acc + bias2, f32x4v{});
+      float* o = out + ((patch * 16 + r0 + oy) * 16 + c16) * 64 + 16 * chq + 4 * g16;
+      *reinterpret_cast<f32x4v*>(o) = acc;
+    }
+    // no barrier: the next band's P1 writes only W0, which P3 does not read; its first
+    // barrier orders this P3's W1 reads before the next P2's W1 writes
+  }
+}
+
+}  // namespace
+
+hipError_t hn_launch_c12(const float* in, float* out, const HardnetDev& d, int P, float eps,
+                         hipStream_t st) {
+  if (P <= 0) return hipSuccess;
+  static int resident = 0;
+  if (!resident) {
+    int per_cu = 0, dev = 0, cus = 0;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&k_c12),
+                                                                 NWAVE * 64, 0);
+    if (e != hipSuccess) return e;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    resident = std::max(1, per_cu) * std::max(1, cus);
+  }
+  const int grid = (int)std::min<long>((long)P * 4, resident);
+  hipLaunchKernelGGL(k_c12, dim3(grid), dim3(NWAVE * 64), 0, st, in, out, d.stem_w, d.stem_b,
+                     static_cast<const uint4*>(d.c12_w1), d.bias[1], static_cast<const uint4*>(d.c12_w2),
+                     d.bias[2], P, eps);
+  return hipGetLastError();
+}

@@ -82,6 +82,14 @@ HN_DEV f32x16 mfma3_f16(const f16x8& ah, const f16x8& al, const f16x8& bh, const
   return acc;
 }
 
+// Blocks are dispatched round-robin over the 8 XCDs (block b -> XCD b % 8); remap so that
+// consecutive logical tiles run on the same XCD and share its L2.
+HN_DEV int xcd_remap(int bid, int nblocks) {
+  const int xcd = bid & 7, idx = bid >> 3;
+  const int q = nblocks >> 3, r = nblocks & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
 HN_DEV float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -120,11 +120,6 @@ struct ConvCfg {
 // placement; a speed property only).  Give each XCD a contiguous range of tiles so the
 // row tiles of one patch -- which share halo rows -- hit the same L2.  Bijective for any
 // grid size (cdna_hip_programming.md T1).
-HN_DEV int xcd_remap(int bid, int nblocks) {
-  const int xcd = bid & 7, idx = bid >> 3;
-  const int q = nblocks >> 3, r = nblocks & 7;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
-}
 
 // STEM = true (conv1 only): `in` is the raw [P,1,32,32] patch batch; the kernel computes
 // input_norm (HardNet.py:306-310) and conv0+BN+ReLU (HardNet.py:281-283) for the window

@@ -8,7 +8,12 @@ struct HardnetDev {
   float* stem_b = nullptr;   // [32]
   void* wpack[7] = {};       // conv1..5: bf16 hi/lo MFMA fragments; [6] = head
   float* bias[7] = {};       // folded BN bias per conv
+  void* c12_w1 = nullptr;    // conv1 / conv2 as 16x16x32 A operands for the fused k_c12
+  void* c12_w2 = nullptr;
 };
+// fused input_norm + conv0 + conv1 + conv2 (hn_c12.hip): [P,1,32,32] -> a2 [P,16,16,64]
+hipError_t hn_launch_c12(const float* in, float* out, const HardnetDev& d, int P, float eps,
+                         hipStream_t st);
 
 hipError_t hn_launch_stem(const float* in, float* out, const float* w, const float* b, int P,
                           bool norm, float eps, hipStream_t st);

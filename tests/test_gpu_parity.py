@@ -83,9 +83,30 @@ def test_tiling_variants_match_reference(variant, cuda_device, monkeypatch):
     from hardnetnas_amd._native import NativeModel
     m, fx, _ = build_module("hardnet")
     monkeypatch.setenv("HN_VARIANT", variant)
+    monkeypatch.setenv("HN_NO_C12", "1")  # the per-layer conv1 / conv2 kernels
     x = torch.from_numpy(golden_inputs(fx)).to(cuda_device)
     y = NativeModel.from_module(m, cuda_device)(x).cpu().numpy()
     assert np.abs(y - fx["y"]).max() <= TOL["hardnet"]
+
+
+def test_fused_c12_is_default_and_matches_layerwise(cuda_device, monkeypatch):
+    """k_c12 (input_norm + conv0 + conv1 + conv2 in one kernel) runs by default; it matches the
+    reference vectors and the layer-by-layer kernels (HN_NO_C12=1) on ragged batches that end
+    mid-workgroup-range."""
+    from hardnetnas_amd._native import NativeModel
+    m, fx, _ = build_module("hardnet")
+    x = torch.from_numpy(golden_inputs(fx)).to(cuda_device)
+    nm = NativeModel.from_module(m, cuda_device)
+    nm.set_profiling(True)
+    y = nm(x).cpu().numpy()
+    assert "stem+conv1+conv2" in nm.stage_times()
+    assert np.abs(y - fx["y"]).max() <= TOL["hardnet"]
+    xe = torch.from_numpy(fx["x_edge"]).to(cuda_device)
+    assert np.abs(nm(xe).cpu().numpy() - fx["y_edge"]).max() <= TOL["hardnet"]
+    monkeypatch.setenv("HN_NO_C12", "1")
+    lw = NativeModel.from_module(m, cuda_device)
+    for b in (1, 5, 255):
+        assert np.abs(nm(x[:b]).cpu().numpy() - lw(x[:b]).cpu().numpy()).max() <= 2e-5
 
 
 def test_unfused_stem_matches(cuda_device, monkeypatch):
