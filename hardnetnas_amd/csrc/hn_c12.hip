@@ -179,14 +179,21 @@ __global__ __launch_bounds__(NWAVE * 64) void k_c12(
       }
       f32x4v acc = {};
       const char* src = s_w0 + (row1 * W0C + x) * PXB + 16 * g16;
+      // B fragments one tap ahead of the MFMAs (two register sets)
+      uint4 bh[2], bl[2];
+      bh[0] = *reinterpret_cast<const uint4*>(src);
+      bl[0] = *reinterpret_cast<const uint4*>(src + 64);
 #pragma unroll
       for (int tap = 0; tap < 9; ++tap) {
-        const char* p = src + ((tap / 3) * W0C + tap % 3) * PXB;
-        const uint4 bh = *reinterpret_cast<const uint4*>(p);
-        const uint4 bl = *reinterpret_cast<const uint4*>(p + 64);
-        acc = mfma16(a1w[tap][1], bh, acc);
-        acc = mfma16(a1w[tap][0], bl, acc);
-        acc = mfma16(a1w[tap][0], bh, acc);
+        if (tap + 1 < 9) {
+          const char* p = src + (((tap + 1) / 3) * W0C + (tap + 1) % 3) * PXB;
+          bh[(tap + 1) & 1] = *reinterpret_cast<const uint4*>(p);
+          bl[(tap + 1) & 1] = *reinterpret_cast<const uint4*>(p + 64);
+        }
+        __builtin_amdgcn_sched_barrier(0);  // keep the next tap's reads ahead of these MFMAs
+        acc = mfma16(a1w[tap][1], bh[tap & 1], acc);
+        acc = mfma16(a1w[tap][0], bl[tap & 1], acc);
+        acc = mfma16(a1w[tap][0], bh[tap & 1], acc);
       }
       acc = __builtin_elementwise_max(acc + bias1, f32x4v{});
       uint2 lo;
@@ -200,17 +207,24 @@ __global__ __launch_bounds__(NWAVE * 64) void k_c12(
 #pragma unroll 1
     for (int oy = w >> 2; oy < RB2; oy += NWAVE / 4) {
       f32x4v acc = {};
+      // output column c16 reads a1 column 2*c16 - 1 + dx: W1 slot c16 (dx 0), 17 + c16 (dx 1),
+      // c16 + 1 (dx 2); B fragments one tap ahead of the MFMAs
+      const char* src = s_w1 + (2 * oy * W1C + c16) * PXB + 16 * g16;
+      uint4 bh[2], bl[2];
+      bh[0] = *reinterpret_cast<const uint4*>(src);
+      bl[0] = *reinterpret_cast<const uint4*>(src + 64);
 #pragma unroll
       for (int tap = 0; tap < 9; ++tap) {
-        const int dy = tap / 3, dx = tap % 3;
-        // output column c16 reads a1 column 2*c16 - 1 + dx
-        const int slot = dx == 1 ? 17 + c16 : c16 + (dx >> 1);
-        const char* p = s_w1 + ((2 * oy + dy) * W1C + slot) * PXB + 16 * g16;
-        const uint4 bh = *reinterpret_cast<const uint4*>(p);
-        const uint4 bl = *reinterpret_cast<const uint4*>(p + 64);
-        acc = mfma16(a2w[tap][1], bh, acc);
-        acc = mfma16(a2w[tap][0], bl, acc);
-        acc = mfma16(a2w[tap][0], bh, acc);
+        if (tap + 1 < 9) {
+          const int dy = (tap + 1) / 3, dx = (tap + 1) % 3;
+          const char* p = src + (dy * W1C + (dx == 1 ? 17 : (dx >> 1))) * PXB;
+          bh[(tap + 1) & 1] = *reinterpret_cast<const uint4*>(p);
+          bl[(tap + 1) & 1] = *reinterpret_cast<const uint4*>(p + 64);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        acc = mfma16(a2w[tap][1], bh[tap & 1], acc);
+        acc = mfma16(a2w[tap][0], bl[tap & 1], acc);
+        acc = mfma16(a2w[tap][0], bh[tap & 1], acc);
       }
       acc = __builtin_elementwise_max(acc + bias2, f32x4v{});
       float* o = out + ((patch * 16 + r0 + oy) * 16 + c16) * 64 + 16 * chq + 4 * g16;
