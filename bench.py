@@ -280,7 +280,7 @@ def main():
                        "model": args.model, "global_batch": b * world, "per_gpu_batch": b,
                        "parallelism": f"dp{world}",
                        "precision": "bf16x3 split-precision MFMA, fp32 accumulate" if args.model == "hardnet"
-                       else "fp32 VALU",
+                       else "fp16x3 split-precision MFMA for 1x1 convs and head, fp32 VALU depthwise",
                        "flop_per_patch": flop_per_patch(args.model)},
             "roofline": roof,
             "cpu_baseline": None,
