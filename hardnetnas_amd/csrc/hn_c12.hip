@@ -20,6 +20,7 @@
 #include "hn_internal.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace {
 
@@ -51,6 +52,9 @@ HN_DEV uint2 pack_bf16x4(float a, float b, float c, float d, uint2& lo) {
 // W1 column slot of a1 column x (x = -1 .. 31): even (x + 1) -> (x + 1) / 2, odd -> 17 + x / 2
 HN_DEV int w1_slot(int x) { return ((x + 1) & 1) ? 17 + (x >> 1) : (x + 1) >> 1; }
 
+// ABL (ablation builds for profiling only; 0 in production): bit 0 skips P1's MFMA work,
+// bit 1 skips P2's, bit 2 skips P3's (the phases still run their LDS traffic and barriers).
+template <int ABL>
 __global__ __launch_bounds__(NWAVE * 64) void k_c12(
     const float* __restrict__ in, float* __restrict__ out, const float* __restrict__ stem_w,
     const float* __restrict__ stem_b, const uint4* __restrict__ w1p, const float* __restrict__ b1,
@@ -100,13 +104,16 @@ __global__ __launch_bounds__(NWAVE * 64) void k_c12(
   const f32x4v bias2 = *reinterpret_cast<const f32x4v*>(b2 + 16 * chq + 4 * g16);
 
   long cur_patch = -1;
+  // the next patch's pixels are fetched one patch ahead (2 floats per thread)
+  float2 vnext = reinterpret_cast<const float2*>(in + (ib >> 2) * 1024)[t];
 #pragma unroll 1
   for (long item = ib; item < ie; ++item) {
     const long patch = item >> 2;
     const int r0 = (int)(item & 3) * RB2;
     if (patch != cur_patch) {  // workgroup-uniform
       cur_patch = patch;
-      const float2 v = reinterpret_cast<const float2*>(in + patch * 1024)[t];
+      const float2 v = vnext;
+      if (((patch + 1) << 2) < ie) vnext = reinterpret_cast<const float2*>(in + (patch + 1) * 1024)[t];
       float mean = 0.f, sd = 1.f;
       if (eps >= 0.f) {  // input_norm: (x - mean) / (std_unbiased + eps), HardNet.py:306-310
         const float s = wave_sum(v.x + v.y);
@@ -151,16 +158,29 @@ __global__ __launch_bounds__(NWAVE * 64) void k_c12(
         xh[j] = (__bf16)v;
         xl[j] = (__bf16)(v - (float)xh[j]);
       }
-      const f32x16 c0 = mfma3(sah, sal, xh, xl, f32x16{});
-      char* o = rowp + (r32 + 1) * PXB + 8 * h32;
+      const f32x16 c0 = (ABL & 1) ? f32x16{} : mfma3(sah, sal, xh, xl, f32x16{});
+      // lane (px, h) holds channels 8q + 4h .. +3; permlane32_swap pairs (q, q+1) so that
+      // lanes 0-31 hold channels 8q .. 8q+7 and lanes 32-63 channels 8q+8 .. 8q+15 of the
+      // same pixel (T21): 4 ds_write_b128 instead of 8 ds_write_b64
+      uint2 hi[4], lo[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const float4 b = *reinterpret_cast<const float4*>(stem_b + 8 * q + 4 * h32);
-        uint2 lo;
-        const uint2 hi = pack_bf16x4(fmaxf(c0[4 * q] + b.x, 0.f), fmaxf(c0[4 * q + 1] + b.y, 0.f),
-                                     fmaxf(c0[4 * q + 2] + b.z, 0.f), fmaxf(c0[4 * q + 3] + b.w, 0.f), lo);
-        *reinterpret_cast<uint2*>(o + 16 * q) = hi;
-        *reinterpret_cast<uint2*>(o + 64 + 16 * q) = lo;
+        hi[q] = pack_bf16x4(fmaxf(c0[4 * q] + b.x, 0.f), fmaxf(c0[4 * q + 1] + b.y, 0.f),
+                            fmaxf(c0[4 * q + 2] + b.z, 0.f), fmaxf(c0[4 * q + 3] + b.w, 0.f), lo[q]);
+      }
+      char* o = rowp + (r32 + 1) * PXB + 16 * h32;
+#pragma unroll
+      for (int k = 0; k < 4; k += 2) {
+        auto sw = [](uint2& a, uint2& b) {
+          const auto rx = __builtin_amdgcn_permlane32_swap(a.x, b.x, false, false);
+          const auto ry = __builtin_amdgcn_permlane32_swap(a.y, b.y, false, false);
+          a.x = rx[0]; b.x = rx[1]; a.y = ry[0]; b.y = ry[1];
+        };
+        sw(hi[k], hi[k + 1]);
+        sw(lo[k], lo[k + 1]);
+        *reinterpret_cast<uint4*>(o + 16 * k) = make_uint4(hi[k].x, hi[k].y, hi[k + 1].x, hi[k + 1].y);
+        *reinterpret_cast<uint4*>(o + 64 + 16 * k) = make_uint4(lo[k].x, lo[k].y, lo[k + 1].x, lo[k + 1].y);
       }
     }
     __syncthreads();
@@ -191,15 +211,27 @@ __global__ __launch_bounds__(NWAVE * 64) void k_c12(
           bl[(tap + 1) & 1] = *reinterpret_cast<const uint4*>(p + 64);
         }
         __builtin_amdgcn_sched_barrier(0);  // keep the next tap's reads ahead of these MFMAs
-        acc = mfma16(a1w[tap][1], bh[tap & 1], acc);
-        acc = mfma16(a1w[tap][0], bl[tap & 1], acc);
-        acc = mfma16(a1w[tap][0], bh[tap & 1], acc);
+        if (ABL & 2) {
+          acc[0] += __builtin_bit_cast(float, bh[tap & 1].x ^ bl[tap & 1].y);
+        } else {
+          acc = mfma16(a1w[tap][1], bh[tap & 1], acc);
+          acc = mfma16(a1w[tap][0], bl[tap & 1], acc);
+          acc = mfma16(a1w[tap][0], bh[tap & 1], acc);
+        }
       }
       acc = __builtin_elementwise_max(acc + bias1, f32x4v{});
+      // lane (c, g) holds channels 4g .. 4g+3; permlane16_swap (odd rows of vdst <-> even rows
+      // of src) leaves the even row with hi channels 4g .. 4g+7 and the odd row with lo
+      // channels 4g-4 .. 4g+3: one ds_write_b128 per lane instead of two ds_write_b64
       uint2 lo;
-      const uint2 hi = pack_bf16x4(acc[0], acc[1], acc[2], acc[3], lo);
-      *reinterpret_cast<uint2*>(dst) = hi;
-      *reinterpret_cast<uint2*>(dst + 64) = lo;
+      uint2 hi = pack_bf16x4(acc[0], acc[1], acc[2], acc[3], lo);
+      {
+        const auto rx = __builtin_amdgcn_permlane16_swap(hi.x, lo.x, false, false);
+        const auto ry = __builtin_amdgcn_permlane16_swap(hi.y, lo.y, false, false);
+        hi.x = rx[0]; lo.x = rx[1]; hi.y = ry[0]; lo.y = ry[1];
+      }
+      char* d16 = s_w1 + (row1 * W1C + w1_slot(x)) * PXB + 32 * chh + 16 * (g16 >> 1) + 64 * (g16 & 1);
+      *reinterpret_cast<uint4*>(d16) = make_uint4(hi.x, hi.y, lo.x, lo.y);
     }
     __syncthreads();
 
@@ -222,9 +254,13 @@ __global__ __launch_bounds__(NWAVE * 64) void k_c12(
           bl[(tap + 1) & 1] = *reinterpret_cast<const uint4*>(p + 64);
         }
         __builtin_amdgcn_sched_barrier(0);
-        acc = mfma16(a2w[tap][1], bh[tap & 1], acc);
-        acc = mfma16(a2w[tap][0], bl[tap & 1], acc);
-        acc = mfma16(a2w[tap][0], bh[tap & 1], acc);
+        if (ABL & 4) {
+          acc[0] += __builtin_bit_cast(float, bh[tap & 1].x ^ bl[tap & 1].y);
+        } else {
+          acc = mfma16(a2w[tap][1], bh[tap & 1], acc);
+          acc = mfma16(a2w[tap][0], bl[tap & 1], acc);
+          acc = mfma16(a2w[tap][0], bh[tap & 1], acc);
+        }
       }
       acc = __builtin_elementwise_max(acc + bias2, f32x4v{});
       float* o = out + ((patch * 16 + r0 + oy) * 16 + c16) * 64 + 16 * chq + 4 * g16;
@@ -240,19 +276,33 @@ __global__ __launch_bounds__(NWAVE * 64) void k_c12(
 hipError_t hn_launch_c12(const float* in, float* out, const HardnetDev& d, int P, float eps,
                          hipStream_t st) {
   if (P <= 0) return hipSuccess;
+  static int abl = -1;
+  if (abl < 0) abl = std::getenv("HN_C12_ABL") ? std::atoi(std::getenv("HN_C12_ABL")) & 7 : 0;
   static int resident = 0;
   if (!resident) {
     int per_cu = 0, dev = 0, cus = 0;
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&k_c12),
-                                                                 NWAVE * 64, 0);
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &per_cu, reinterpret_cast<const void*>(&k_c12<0>), NWAVE * 64, 0);
     if (e != hipSuccess) return e;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     resident = std::max(1, per_cu) * std::max(1, cus);
   }
   const int grid = (int)std::min<long>((long)P * 4, resident);
-  hipLaunchKernelGGL(k_c12, dim3(grid), dim3(NWAVE * 64), 0, st, in, out, d.stem_w, d.stem_b,
-                     static_cast<const uint4*>(d.c12_w1), d.bias[1], static_cast<const uint4*>(d.c12_w2),
-                     d.bias[2], P, eps);
+#define HN_C12_GO(A)                                                                              \
+  hipLaunchKernelGGL(k_c12<A>, dim3(grid), dim3(NWAVE * 64), 0, st, in, out, d.stem_w, d.stem_b,  \
+                     static_cast<const uint4*>(d.c12_w1), d.bias[1],                              \
+                     static_cast<const uint4*>(d.c12_w2), d.bias[2], P, eps)
+  switch (abl) {
+    case 0: HN_C12_GO(0); break;
+    case 1: HN_C12_GO(1); break;
+    case 2: HN_C12_GO(2); break;
+    case 3: HN_C12_GO(3); break;
+    case 4: HN_C12_GO(4); break;
+    case 5: HN_C12_GO(5); break;
+    case 6: HN_C12_GO(6); break;
+    default: HN_C12_GO(7); break;
+  }
+#undef HN_C12_GO
   return hipGetLastError();
 }
