@@ -19,12 +19,14 @@ HARDNET = {(32, 32, 32, 1): "stem+conv1", (32, 32, 32, 0): "conv1", (32, 64, 32,
 
 
 def stage_of(name: str):
-    m = re.search(r"k_conv(?:3x3|_pipe)<(\d+), (\d+), (\d+), \d+, \d+, \d+, \d+, \d+, (true|false)", name)
+    m = re.search(r"k_conv(?:3x3|_pipe|_ws)<(\d+), (\d+), (\d+), \d+, \d+, \d+, \d+, \d+, (true|false)", name)
     if m:
         key = (int(m.group(1)), int(m.group(2)), int(m.group(3)), int(m.group(4) == "true"))
         return HARDNET.get(key)
-    if "k_head<" in name:
-        return "head"
+    for k, st in (("k_c12<", "stem+conv1+conv2"), ("k_front<", "front"), ("k_irf<", "irf"),
+                  ("k_head<", "head"), ("k_head2<", "head")):
+        if k in name:
+            return st
     if "k_stem<" in name:
         return "stem"
     for k, st in (("k_pw_tiled<", "pw"), ("k_pw(", "pw"), ("k_dw<", "dw"),
