@@ -159,6 +159,7 @@ struct hn_model {
   int chunk = 32768;
   bool unfused_stem = false;  // HN_UNFUSED_STEM=1: separate stem kernel (A/B, debugging)
   bool c12 = true;            // fused stem+conv1+conv2 (k_c12); HN_NO_C12=1 -> separate kernels
+  int subchunk = 8192;        // HardNet conv stages per sub-chunk (HN_SUBCHUNK)
   uint16_t* front_spack = nullptr;  // fused front: stem as MFMA A operand
   int front = 0;  // NAS: 1 = stem + layer-0 IRF pw/dw fused, 2 = stem + layer-0 maxpool fused
   bool no_front = false;  // HN_NO_FRONT=1: unfused NAS stem/layer 0 (A/B, debugging)
@@ -573,6 +574,7 @@ extern "C" int hn_create(const hn_arch_desc* desc, const float* host_params, siz
   if (const char* e = std::getenv("HN_UNFUSED_STEM")) m->unfused_stem = std::atoi(e) != 0;
   if (const char* e = std::getenv("HN_NO_FRONT")) m->no_front = std::atoi(e) != 0;
   if (const char* e = std::getenv("HN_NO_C12")) m->c12 = std::atoi(e) == 0;
+  if (const char* e = std::getenv("HN_SUBCHUNK")) m->subchunk = std::max(64, std::atoi(e));
   if (const char* e = std::getenv("HN_NO_IRF")) m->no_irf = std::atoi(e) != 0;
   if (const char* e = std::getenv("HN_VARIANT")) {
     int i = 0;
@@ -622,7 +624,21 @@ static int forward_hardnet(hn_model* m, const float* in, int P, float* out, floa
   float* a2 = ws + 2 * per;
   const float ineps = m->desc.input_norm_eps;
   if (m->c12 && !m->unfused_stem) {
-    STAGE("stem+conv1+conv2", hn_launch_c12(in, a2, m->hd, P, ineps, st));
+    // conv stages in sub-chunks (HN_SUBCHUNK, default 8192 patches): a sub-chunk's a2..a4
+    // (512 MiB for a2) partly stays in the 256 MiB Infinity Cache between its kernels; the
+    // head GEMM, which needs many patches per launch to fill the GPU, runs once per chunk
+    // over the a5 of all sub-chunks.
+    const int sub = std::max(1, std::min(P, m->subchunk));
+    for (int s0 = 0; s0 < P; s0 += sub) {
+      const int n = std::min(sub, P - s0);
+      float* a5 = a1 + (size_t)s0 * 8192;
+      STAGE("stem+conv1+conv2", hn_launch_c12(in + (size_t)s0 * 1024, a2, m->hd, n, ineps, st));
+      STAGE("conv3", hn_launch_hardnet_conv(3, m->variant[3], m->hd, a2, a0, n, 0.f, st));
+      STAGE("conv4", hn_launch_hardnet_conv(4, m->variant[4], m->hd, a0, a2, n, 0.f, st));
+      STAGE("conv5", hn_launch_hardnet_conv(5, m->variant[5], m->hd, a2, a5, n, 0.f, st));
+    }
+    STAGE("head", hn_launch_head(a1, out, m->hd.wpack[6], m->hd.bias[6], P, 8192, m->desc.l2_eps, st));
+    return HN_OK;
   } else {
     if (m->unfused_stem) {
       STAGE("stem", hn_launch_stem(in, a0, m->hd.stem_w, m->hd.stem_b, P, ineps >= 0.f, ineps, st));
