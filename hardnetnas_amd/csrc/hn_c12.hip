@@ -33,7 +33,6 @@ constexpr int PXB = 160;                // bytes per pixel in W0 / W1
 constexpr int W0C = 34, W1C = 33;       // columns (x = -1 .. 32 / -1 .. 31)
 constexpr int W0B = NA0 * W0C * PXB;    // 59,840
 constexpr int W1B = NA1 * W1C * PXB;    // 47,520
-constexpr int NWAVE = 8;
 
 HN_DEV f32x4v mfma16(const uint4& a, const uint4& b, f32x4v c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a), as_bf16x8(b), c, 0, 0, 0);
@@ -52,17 +51,26 @@ HN_DEV uint2 pack_bf16x4(float a, float b, float c, float d, uint2& lo) {
 // W1 column slot of a1 column x (x = -1 .. 31): even (x + 1) -> (x + 1) / 2, odd -> 17 + x / 2
 HN_DEV int w1_slot(int x) { return ((x + 1) & 1) ? 17 + (x >> 1) : (x + 1) >> 1; }
 
-// ABL (ablation builds for profiling only; 0 in production): bit 0 skips P1's MFMA work,
+// ABL (ablation builds for profiling only; 0 in production): bit 3 skips P1 entirely,
+// bit 4 skips the P2/P3 B-fragment LDS reads; bit 0 skips P1's MFMA work,
 // bit 1 skips P2's, bit 2 skips P3's (the phases still run their LDS traffic and barriers).
-template <int ABL>
-__global__ __launch_bounds__(NWAVE * 64) void k_c12(
+//
+// NW = 8: two waves per SIMD, each wave holds one conv1 16-channel group and one conv2
+//         group (144 VGPRs of weights).
+// NW = 4: one wave per SIMD with the 512-register file: each wave holds both conv1 groups and
+//         two conv2 groups (288 registers of weights), so every B fragment read from LDS feeds
+//         two output groups (half the LDS reads per MFMA).
+template <int ABL, int NW>
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1, NW / 4))) void k_c12(
     const float* __restrict__ in, float* __restrict__ out, const float* __restrict__ stem_w,
     const float* __restrict__ stem_b, const uint4* __restrict__ w1p, const float* __restrict__ b1,
     const uint4* __restrict__ w2p, const float* __restrict__ b2, int P, float eps) {
   __shared__ __attribute__((aligned(16))) char s_w0[W0B];
   __shared__ __attribute__((aligned(16))) char s_w1[W1B];
   __shared__ float s_in[34 * 34];
-  __shared__ float red[2 * NWAVE];
+  __shared__ float red[2 * NW];
+  constexpr int G1 = 8 / NW, G2 = 8 / NW;     // conv1 / conv2 output groups per wave
+  constexpr int NCH1 = 2 / G1, NCH2 = 4 / G2;  // waves sharing a P2 unit / a P3 row
 
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -76,9 +84,9 @@ __global__ __launch_bounds__(NWAVE * 64) void k_c12(
   if (ib >= ie) return;  // workgroup-uniform
 
   // ---- one-time init: zero both windows (borders and never-written slots stay zero) ----
-  for (int i = t; i < W0B / 16; i += NWAVE * 64) reinterpret_cast<uint4*>(s_w0)[i] = make_uint4(0, 0, 0, 0);
-  for (int i = t; i < W1B / 16; i += NWAVE * 64) reinterpret_cast<uint4*>(s_w1)[i] = make_uint4(0, 0, 0, 0);
-  for (int i = t; i < 34 * 34; i += NWAVE * 64) s_in[i] = 0.f;
+  for (int i = t; i < W0B / 16; i += NW * 64) reinterpret_cast<uint4*>(s_w0)[i] = make_uint4(0, 0, 0, 0);
+  for (int i = t; i < W1B / 16; i += NW * 64) reinterpret_cast<uint4*>(s_w1)[i] = make_uint4(0, 0, 0, 0);
+  for (int i = t; i < 34 * 34; i += NW * 64) s_in[i] = 0.f;
 
   // stem A operand (32x32x16): lane (channel r32, taps 8*h32 ..), bf16 hi/lo
   bf16x8 sah, sal;
@@ -89,60 +97,76 @@ __global__ __launch_bounds__(NWAVE * 64) void k_c12(
     sah[j] = (__bf16)v;
     sal[j] = (__bf16)(v - (float)sah[j]);
   }
-  // conv1 / conv2 A operands resident in VGPRs: [tap][plane]
-  const int chh = w & 1, chq = w & 3;
-  uint4 a1w[9][2], a2w[9][2];
+  // conv1 / conv2 A operands resident in registers: [tap][group][plane]
+  const int cs1 = w % NCH1, cs2 = w % NCH2;
+  uint4 a1w[9][G1][2], a2w[9][G2][2];
+  f32x4v bias1[G1], bias2[G2];
 #pragma unroll
-  for (int tap = 0; tap < 9; ++tap) {
+  for (int g = 0; g < G1; ++g) {
+    const int chh = cs1 * G1 + g;
 #pragma unroll
-    for (int pl = 0; pl < 2; ++pl) {
-      a1w[tap][pl] = w1p[((tap * 2 + chh) * 2 + pl) * 64 + lane];
-      a2w[tap][pl] = w2p[((tap * 4 + chq) * 2 + pl) * 64 + lane];
-    }
+    for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+      for (int pl = 0; pl < 2; ++pl) a1w[tap][g][pl] = w1p[((tap * 2 + chh) * 2 + pl) * 64 + lane];
+    bias1[g] = *reinterpret_cast<const f32x4v*>(b1 + 16 * chh + 4 * g16);
   }
-  const f32x4v bias1 = *reinterpret_cast<const f32x4v*>(b1 + 16 * chh + 4 * g16);
-  const f32x4v bias2 = *reinterpret_cast<const f32x4v*>(b2 + 16 * chq + 4 * g16);
+#pragma unroll
+  for (int g = 0; g < G2; ++g) {
+    const int chq = cs2 * G2 + g;
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+      for (int pl = 0; pl < 2; ++pl) a2w[tap][g][pl] = w2p[((tap * 4 + chq) * 2 + pl) * 64 + lane];
+    bias2[g] = *reinterpret_cast<const f32x4v*>(b2 + 16 * chq + 4 * g16);
+  }
 
   long cur_patch = -1;
   // the next patch's pixels are fetched one patch ahead (2 floats per thread)
-  float2 vnext = reinterpret_cast<const float2*>(in + (ib >> 2) * 1024)[t];
+  constexpr int PPT = 1024 / (NW * 64);  // patch pixels per thread (2 or 4)
+  typedef float pxv __attribute__((ext_vector_type(PPT)));
+  pxv vnext = reinterpret_cast<const pxv*>(in + (ib >> 2) * 1024)[t];
 #pragma unroll 1
   for (long item = ib; item < ie; ++item) {
     const long patch = item >> 2;
     const int r0 = (int)(item & 3) * RB2;
     if (patch != cur_patch) {  // workgroup-uniform
       cur_patch = patch;
-      const float2 v = vnext;
-      if (((patch + 1) << 2) < ie) vnext = reinterpret_cast<const float2*>(in + (patch + 1) * 1024)[t];
+      const pxv v = vnext;
+      if (((patch + 1) << 2) < ie) vnext = reinterpret_cast<const pxv*>(in + (patch + 1) * 1024)[t];
       float mean = 0.f, sd = 1.f;
       if (eps >= 0.f) {  // input_norm: (x - mean) / (std_unbiased + eps), HardNet.py:306-310
-        const float s = wave_sum(v.x + v.y);
-        if (lane == 0) red[w] = s;
-        __syncthreads();
         float a = 0.f;
 #pragma unroll
-        for (int i = 0; i < NWAVE; ++i) a += red[i];
-        mean = a * (1.f / 1024.f);
-        const float d0 = v.x - mean, d1 = v.y - mean;
-        const float q = wave_sum(d0 * d0 + d1 * d1);
-        if (lane == 0) red[NWAVE + w] = q;
+        for (int j = 0; j < PPT; ++j) a += v[j];
+        const float s = wave_sum(a);
+        if (lane == 0) red[w] = s;
         __syncthreads();
         a = 0.f;
 #pragma unroll
-        for (int i = 0; i < NWAVE; ++i) a += red[NWAVE + i];
+        for (int i = 0; i < NW; ++i) a += red[i];
+        mean = a * (1.f / 1024.f);
+        float q = 0.f;
+#pragma unroll
+        for (int j = 0; j < PPT; ++j) q += (v[j] - mean) * (v[j] - mean);
+        q = wave_sum(q);
+        if (lane == 0) red[NW + w] = q;
+        __syncthreads();
+        a = 0.f;
+#pragma unroll
+        for (int i = 0; i < NW; ++i) a += red[NW + i];
         sd = sqrtf(a * (1.f / 1023.f)) + eps;
       }
       const float inv = 1.f / sd;  // as k_conv_ws's stem: (x - mean) * (1/sd)
-      const int q2 = 2 * t, y = q2 >> 5, x = q2 & 31;
-      s_in[(y + 1) * 34 + x + 1] = (v.x - mean) * inv;
-      s_in[(y + 1) * 34 + x + 2] = (v.y - mean) * inv;
+      const int q0 = PPT * t, y = q0 >> 5, x = q0 & 31;
+#pragma unroll
+      for (int j = 0; j < PPT; ++j) s_in[(y + 1) * 34 + x + 1 + j] = (v[j] - mean) * inv;
       __syncthreads();
     }
 
     // ---- P1: stem rows -> W0 ---------------------------------------------------------------
     const int y0base = 2 * r0 - 2;
 #pragma unroll 1
-    for (int ri = w; ri < NA0; ri += NWAVE) {
+    for (int ri = w; ri < ((ABL & 8) ? 0 : NA0); ri += NW) {
       const int y = y0base + ri;  // a0 row
       char* rowp = s_w0 + ri * W0C * PXB;
       if (y < 0 || y >= 32) {  // zero padding row (interior columns)
@@ -185,86 +209,103 @@ __global__ __launch_bounds__(NWAVE * 64) void k_c12(
     }
     __syncthreads();
 
-    // ---- P2: conv1 -> W1 (units: a1 row x pixel half; this wave's channel half) -------------
+    // ---- P2: conv1 -> W1 (units: a1 row x pixel half; this wave's G1 channel groups) ---------
 #pragma unroll 1
-    for (int u = w >> 1; u < NA1 * 2; u += NWAVE / 2) {
+    for (int u = w / NCH1; u < NA1 * 2; u += NW / NCH1) {
       const int row1 = u >> 1, pxh = u & 1;
       const int y1 = 2 * r0 - 1 + row1;
       const int x = 16 * pxh + c16;
-      char* dst = s_w1 + (row1 * W1C + w1_slot(x)) * PXB + 32 * chh + 8 * g16;
+      char* pix = s_w1 + (row1 * W1C + w1_slot(x)) * PXB;
       if (y1 < 0 || y1 >= 32) {  // zero padding row of a1
-        *reinterpret_cast<uint2*>(dst) = make_uint2(0, 0);
-        *reinterpret_cast<uint2*>(dst + 64) = make_uint2(0, 0);
+#pragma unroll
+        for (int g = 0; g < G1; ++g) {
+          char* dst = pix + 32 * (cs1 * G1 + g) + 8 * g16;
+          *reinterpret_cast<uint2*>(dst) = make_uint2(0, 0);
+          *reinterpret_cast<uint2*>(dst + 64) = make_uint2(0, 0);
+        }
         continue;
       }
-      f32x4v acc = {};
+      f32x4v acc[G1];
+#pragma unroll
+      for (int g = 0; g < G1; ++g) acc[g] = f32x4v{};
       const char* src = s_w0 + (row1 * W0C + x) * PXB + 16 * g16;
-      // B fragments one tap ahead of the MFMAs (two register sets)
+      // B fragments one tap ahead of the MFMAs (two register sets); each feeds G1 groups
       uint4 bh[2], bl[2];
-      bh[0] = *reinterpret_cast<const uint4*>(src);
-      bl[0] = *reinterpret_cast<const uint4*>(src + 64);
+      bh[0] = (ABL & 16) ? make_uint4(lane, 1, 2, 3) : *reinterpret_cast<const uint4*>(src);
+      bl[0] = (ABL & 16) ? make_uint4(lane, 3, 2, 1) : *reinterpret_cast<const uint4*>(src + 64);
 #pragma unroll
       for (int tap = 0; tap < 9; ++tap) {
         if (tap + 1 < 9) {
           const char* p = src + (((tap + 1) / 3) * W0C + (tap + 1) % 3) * PXB;
-          bh[(tap + 1) & 1] = *reinterpret_cast<const uint4*>(p);
-          bl[(tap + 1) & 1] = *reinterpret_cast<const uint4*>(p + 64);
+          bh[(tap + 1) & 1] = (ABL & 16) ? make_uint4(tap, lane, 2, 3) : *reinterpret_cast<const uint4*>(p);
+          bl[(tap + 1) & 1] = (ABL & 16) ? make_uint4(lane, tap, 2, 1) : *reinterpret_cast<const uint4*>(p + 64);
         }
         __builtin_amdgcn_sched_barrier(0);  // keep the next tap's reads ahead of these MFMAs
-        if (ABL & 2) {
-          acc[0] += __builtin_bit_cast(float, bh[tap & 1].x ^ bl[tap & 1].y);
-        } else {
-          acc = mfma16(a1w[tap][1], bh[tap & 1], acc);
-          acc = mfma16(a1w[tap][0], bl[tap & 1], acc);
-          acc = mfma16(a1w[tap][0], bh[tap & 1], acc);
+#pragma unroll
+        for (int g = 0; g < G1; ++g) {
+          if (ABL & 2) {
+            acc[g][0] += __builtin_bit_cast(float, bh[tap & 1].x ^ bl[tap & 1].y);
+          } else {
+            acc[g] = mfma16(a1w[tap][g][1], bh[tap & 1], acc[g]);
+            acc[g] = mfma16(a1w[tap][g][0], bl[tap & 1], acc[g]);
+            acc[g] = mfma16(a1w[tap][g][0], bh[tap & 1], acc[g]);
+          }
         }
       }
-      acc = __builtin_elementwise_max(acc + bias1, f32x4v{});
-      // lane (c, g) holds channels 4g .. 4g+3; permlane16_swap (odd rows of vdst <-> even rows
-      // of src) leaves the even row with hi channels 4g .. 4g+7 and the odd row with lo
-      // channels 4g-4 .. 4g+3: one ds_write_b128 per lane instead of two ds_write_b64
-      uint2 lo;
-      uint2 hi = pack_bf16x4(acc[0], acc[1], acc[2], acc[3], lo);
-      {
+#pragma unroll
+      for (int g = 0; g < G1; ++g) {
+        const f32x4v r = __builtin_elementwise_max(acc[g] + bias1[g], f32x4v{});
+        // lane (c, g16) holds channels 4g16 .. +3; permlane16_swap (odd rows of vdst <-> even
+        // rows of src) leaves the even row with hi channels 4g16 .. +7 and the odd row with lo
+        // channels 4g16-4 .. +3: one ds_write_b128 per lane instead of two ds_write_b64
+        uint2 lo;
+        uint2 hi = pack_bf16x4(r[0], r[1], r[2], r[3], lo);
         const auto rx = __builtin_amdgcn_permlane16_swap(hi.x, lo.x, false, false);
         const auto ry = __builtin_amdgcn_permlane16_swap(hi.y, lo.y, false, false);
         hi.x = rx[0]; lo.x = rx[1]; hi.y = ry[0]; lo.y = ry[1];
+        char* d16 = pix + 32 * (cs1 * G1 + g) + 16 * (g16 >> 1) + 64 * (g16 & 1);
+        *reinterpret_cast<uint4*>(d16) = make_uint4(hi.x, hi.y, lo.x, lo.y);
       }
-      char* d16 = s_w1 + (row1 * W1C + w1_slot(x)) * PXB + 32 * chh + 16 * (g16 >> 1) + 64 * (g16 & 1);
-      *reinterpret_cast<uint4*>(d16) = make_uint4(hi.x, hi.y, lo.x, lo.y);
     }
     __syncthreads();
 
-    // ---- P3: conv2 (stride 2) -> a2 in HBM (units: output row; this wave's quarter) ---------
+    // ---- P3: conv2 (stride 2) -> a2 in HBM (units: output row; this wave's G2 quarters) -------
 #pragma unroll 1
-    for (int oy = w >> 2; oy < RB2; oy += NWAVE / 4) {
-      f32x4v acc = {};
+    for (int oy = w / NCH2; oy < RB2; oy += NW / NCH2) {
+      f32x4v acc[G2];
+#pragma unroll
+      for (int g = 0; g < G2; ++g) acc[g] = f32x4v{};
       // output column c16 reads a1 column 2*c16 - 1 + dx: W1 slot c16 (dx 0), 17 + c16 (dx 1),
       // c16 + 1 (dx 2); B fragments one tap ahead of the MFMAs
       const char* src = s_w1 + (2 * oy * W1C + c16) * PXB + 16 * g16;
       uint4 bh[2], bl[2];
-      bh[0] = *reinterpret_cast<const uint4*>(src);
-      bl[0] = *reinterpret_cast<const uint4*>(src + 64);
+      bh[0] = (ABL & 16) ? make_uint4(lane, 1, 2, 3) : *reinterpret_cast<const uint4*>(src);
+      bl[0] = (ABL & 16) ? make_uint4(lane, 3, 2, 1) : *reinterpret_cast<const uint4*>(src + 64);
 #pragma unroll
       for (int tap = 0; tap < 9; ++tap) {
         if (tap + 1 < 9) {
           const int dy = (tap + 1) / 3, dx = (tap + 1) % 3;
           const char* p = src + (dy * W1C + (dx == 1 ? 17 : (dx >> 1))) * PXB;
-          bh[(tap + 1) & 1] = *reinterpret_cast<const uint4*>(p);
-          bl[(tap + 1) & 1] = *reinterpret_cast<const uint4*>(p + 64);
+          bh[(tap + 1) & 1] = (ABL & 16) ? make_uint4(tap, lane, 2, 3) : *reinterpret_cast<const uint4*>(p);
+          bl[(tap + 1) & 1] = (ABL & 16) ? make_uint4(lane, tap, 2, 1) : *reinterpret_cast<const uint4*>(p + 64);
         }
         __builtin_amdgcn_sched_barrier(0);
-        if (ABL & 4) {
-          acc[0] += __builtin_bit_cast(float, bh[tap & 1].x ^ bl[tap & 1].y);
-        } else {
-          acc = mfma16(a2w[tap][1], bh[tap & 1], acc);
-          acc = mfma16(a2w[tap][0], bl[tap & 1], acc);
-          acc = mfma16(a2w[tap][0], bh[tap & 1], acc);
+#pragma unroll
+        for (int g = 0; g < G2; ++g) {
+          if (ABL & 4) {
+            acc[g][0] += __builtin_bit_cast(float, bh[tap & 1].x ^ bl[tap & 1].y);
+          } else {
+            acc[g] = mfma16(a2w[tap][g][1], bh[tap & 1], acc[g]);
+            acc[g] = mfma16(a2w[tap][g][0], bl[tap & 1], acc[g]);
+            acc[g] = mfma16(a2w[tap][g][0], bh[tap & 1], acc[g]);
+          }
         }
       }
-      acc = __builtin_elementwise_max(acc + bias2, f32x4v{});
-      float* o = out + ((patch * 16 + r0 + oy) * 16 + c16) * 64 + 16 * chq + 4 * g16;
-      *reinterpret_cast<f32x4v*>(o) = acc;
+      float* o = out + ((patch * 16 + r0 + oy) * 16 + c16) * 64 + 4 * g16;
+#pragma unroll
+      for (int g = 0; g < G2; ++g)
+        *reinterpret_cast<f32x4v*>(o + 16 * (cs2 * G2 + g)) =
+            __builtin_elementwise_max(acc[g] + bias2[g], f32x4v{});
     }
     // no barrier: the next band's P1 writes only W0, which P3 does not read; its first
     // barrier orders this P3's W1 reads before the next P2's W1 writes
@@ -276,32 +317,39 @@ __global__ __launch_bounds__(NWAVE * 64) void k_c12(
 hipError_t hn_launch_c12(const float* in, float* out, const HardnetDev& d, int P, float eps,
                          hipStream_t st) {
   if (P <= 0) return hipSuccess;
-  static int abl = -1;
-  if (abl < 0) abl = std::getenv("HN_C12_ABL") ? std::atoi(std::getenv("HN_C12_ABL")) & 7 : 0;
-  static int resident = 0;
-  if (!resident) {
+  static int abl = -1, nw = 0;
+  if (abl < 0) abl = std::getenv("HN_C12_ABL") ? std::atoi(std::getenv("HN_C12_ABL")) & 31 : 0;
+  // 8 waves (two per SIMD) measured faster than the 4-wave / 512-register build (22.0 vs
+  // 30.4 ms per 262,144 patches); HN_C12_NW=4 selects the latter (ablation builds: 4-wave only)
+  if (!nw) nw = std::getenv("HN_C12_NW") && std::atoi(std::getenv("HN_C12_NW")) == 4 ? 4 : 8;
+  static int resident[2] = {0, 0};
+  const int ri = nw == 8;
+  if (!resident[ri]) {
     int per_cu = 0, dev = 0, cus = 0;
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &per_cu, reinterpret_cast<const void*>(&k_c12<0>), NWAVE * 64, 0);
+    const void* fn = nw == 8 ? reinterpret_cast<const void*>(&k_c12<0, 8>)
+                             : reinterpret_cast<const void*>(&k_c12<0, 4>);
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, nw * 64, 0);
     if (e != hipSuccess) return e;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    resident = std::max(1, per_cu) * std::max(1, cus);
+    resident[ri] = std::max(1, per_cu) * std::max(1, cus);
   }
-  const int grid = (int)std::min<long>((long)P * 4, resident);
-#define HN_C12_GO(A)                                                                              \
-  hipLaunchKernelGGL(k_c12<A>, dim3(grid), dim3(NWAVE * 64), 0, st, in, out, d.stem_w, d.stem_b,  \
+  const int grid = (int)std::min<long>((long)P * 4, resident[ri]);
+#define HN_C12_GO(A, W)                                                                          \
+  hipLaunchKernelGGL((k_c12<A, W>), dim3(grid), dim3(W * 64), 0, st, in, out, d.stem_w, d.stem_b, \
                      static_cast<const uint4*>(d.c12_w1), d.bias[1],                              \
                      static_cast<const uint4*>(d.c12_w2), d.bias[2], P, eps)
-  switch (abl) {
-    case 0: HN_C12_GO(0); break;
-    case 1: HN_C12_GO(1); break;
-    case 2: HN_C12_GO(2); break;
-    case 3: HN_C12_GO(3); break;
-    case 4: HN_C12_GO(4); break;
-    case 5: HN_C12_GO(5); break;
-    case 6: HN_C12_GO(6); break;
-    default: HN_C12_GO(7); break;
+  if (nw == 8) {
+    if (abl) return hipErrorInvalidValue;  // ablations are built for the 4-wave kernel only (HN_C12_NW=4)
+    HN_C12_GO(0, 8);
+  } else {
+    switch (abl) {
+      case 0: HN_C12_GO(0, 4); break;
+      case 7: HN_C12_GO(7, 4); break;
+      case 8: HN_C12_GO(8, 4); break;
+      case 22: HN_C12_GO(22, 4); break;
+      default: HN_C12_GO(31, 4); break;
+    }
   }
 #undef HN_C12_GO
   return hipGetLastError();

@@ -109,6 +109,16 @@ def test_fused_c12_is_default_and_matches_layerwise(cuda_device, monkeypatch):
         assert np.abs(nm(x[:b]).cpu().numpy() - lw(x[:b]).cpu().numpy()).max() <= 2e-5
 
 
+def test_c12_four_wave_variant_matches(cuda_device, monkeypatch):
+    """HN_C12_NW=4: the one-wave-per-SIMD k_c12 build (two output groups per wave)."""
+    from hardnetnas_amd._native import NativeModel
+    m, fx, _ = build_module("hardnet")
+    monkeypatch.setenv("HN_C12_NW", "4")
+    x = torch.from_numpy(golden_inputs(fx)).to(cuda_device)
+    y = NativeModel.from_module(m, cuda_device)(x).cpu().numpy()
+    assert np.abs(y - fx["y"]).max() <= TOL["hardnet"]
+
+
 def test_unfused_stem_matches(cuda_device, monkeypatch):
     from hardnetnas_amd._native import NativeModel
     m, fx, _ = build_module("hardnet")

@@ -3,7 +3,7 @@
 # sys/runtime tracing) over a small bench workload.  Output: gpurun_out/pmc/<tag>/...
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
-mkdir -p gpurun_out/pmc
+rm -rf gpurun_out/pmc; mkdir -p gpurun_out/pmc
 MODEL=${MODEL:-hardnet}
 ARGS="--no-cpu-baseline --steps 1 --warmup 1 --batch ${PMC_BATCH:-32768} --model $MODEL"
 timeout -k 10 120 rocprofv3 -L > gpurun_out/pmc/counters.txt 2>&1 || true
