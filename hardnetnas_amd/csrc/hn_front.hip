@@ -22,6 +22,8 @@
 #include "hn_common.h"
 #include "hn_internal.h"
 
+#include <cstdlib>
+
 namespace {
 
 constexpr int FRONT_IRF = 0, FRONT_MAXPOOL = 1;
@@ -37,7 +39,9 @@ __constant__ unsigned char kDwLane[64] = {
     22, 23, 30, 31, 38, 39, 36, 37, 44, 45, 52, 53, 54, 55, 58, 59, 60, 61, 62, 63, 24, 25,
     16, 17, 18, 19, 32, 33, 40, 41, 26, 27, 34, 35, 42, 43, 50, 51, 48, 49, 56, 57};
 
-template <int K, int MID, int MODE, bool NORM>
+// ABL: ablation builds for profiling only (0 in production): bit 0 skips the stem MFMA and
+// epilogue, bit 1 the pw MFMA + LDS stores, bit 2 the depthwise loop, bit 3 the pwl MFMA.
+template <int K, int MID, int MODE, bool NORM, int ABL = 0>
 __global__ __launch_bounds__(256) void k_front(const float* __restrict__ in,
                                                float* __restrict__ out,
                                                const uint4* __restrict__ spack,  // stem A operand
@@ -128,6 +132,10 @@ __global__ __launch_bounds__(256) void k_front(const float* __restrict__ in,
       const int tap = 8 * h + j;  // h = 1 holds tap 8 and zeros
       tp[j] = tap < 9 ? s_in[(y + tap / 3) * 34 + px + tap % 3] : 0.f;
     }
+    if (ABL & 1) {
+      bh[i][0] = bh[i][1] = bl[i][0] = bl[i][1] = make_uint4(__float_as_uint(tp[0]), lane, 0, 0);
+      continue;
+    }
     uint4 xh, xl;
     split8_f16(make_float4(tp[0], tp[1], tp[2], tp[3]), make_float4(tp[4], tp[5], tp[6], tp[7]), xh, xl);
     f32x16 c = {};
@@ -189,7 +197,7 @@ __global__ __launch_bounds__(256) void k_front(const float* __restrict__ in,
 #pragma unroll
     for (int i = 0; i < NT; ++i) {
       const int ri = w + 4 * i, y = row0 + ri;
-      if (ri >= IR || y < 0 || y >= 32) continue;
+      if (ri >= IR || y < 0 || y >= 32 || (ABL & 2)) continue;
       f32x16 acc = {};
       acc = mfma3_f16(ah0, al0, as_f16x8(bh[i][0]), as_f16x8(bl[i][0]), acc);
       acc = mfma3_f16(ah1, al1, as_f16x8(bh[i][1]), as_f16x8(bl[i][1]), acc);
@@ -209,7 +217,7 @@ __global__ __launch_bounds__(256) void k_front(const float* __restrict__ in,
       f32x4 a0 = *reinterpret_cast<const f32x4*>(s_dw + KK * KK * 32 + c0);
       f32x4 a1 = *reinterpret_cast<const f32x4*>(s_dw + KK * KK * 32 + c0 + 4);
 #pragma unroll DYU
-      for (int dy = 0; dy < KK; ++dy)
+      for (int dy = 0; dy < ((ABL & 4) ? 0 : KK); ++dy)
 #pragma unroll
         for (int dx = 0; dx < KK; ++dx) {
           const float* wp = s_dw + (dy * KK + dx) * 32 + c0;
@@ -222,7 +230,10 @@ __global__ __launch_bounds__(256) void k_front(const float* __restrict__ in,
       uint4 xh, xl;
       split8_f16(make_float4(a0.x, a0.y, a0.z, a0.w), make_float4(a1.x, a1.y, a1.z, a1.w), xh, xl);
       const uint4* lp = pwl_a + ((size_t)(2 * m + (w >> 1)) * 2) * 64 + lane;
-      oacc = mfma3_f16(as_f16x8(lp[0]), as_f16x8(lp[64]), as_f16x8(xh), as_f16x8(xl), oacc);
+      if (ABL & 8)
+        oacc[0] += __uint_as_float(xh.x ^ xl.y);
+      else
+        oacc = mfma3_f16(as_f16x8(lp[0]), as_f16x8(lp[64]), as_f16x8(xh), as_f16x8(xl), oacc);
     }
     __syncthreads();  // s_pw / s_dw are rewritten by the next chunk
   }
@@ -257,12 +268,25 @@ __global__ __launch_bounds__(256) void k_front(const float* __restrict__ in,
 template <int K, int MID, int MODE>
 hipError_t front_launch(const HnFrontArgs& a, int P, bool norm, float eps, hipStream_t st) {
   const dim3 grid((unsigned)((P + 7) / 8) * 32), block(256);
-  if (norm)
-    hipLaunchKernelGGL((k_front<K, MID, MODE, true>), grid, block, 0, st, a.in, a.out, a.spack, a.stem_b,
-                       a.apack, a.pw_b, a.dw_w, a.dw_b, a.pwl_a, a.pwl_b, P, eps);
-  else
-    hipLaunchKernelGGL((k_front<K, MID, MODE, false>), grid, block, 0, st, a.in, a.out, a.spack, a.stem_b,
-                       a.apack, a.pw_b, a.dw_w, a.dw_b, a.pwl_a, a.pwl_b, P, eps);
+  static int abl = -1;
+  if (abl < 0) abl = std::getenv("HN_FRONT_ABL") ? std::atoi(std::getenv("HN_FRONT_ABL")) & 15 : 0;
+#define HN_FRONT_GO(NRM, A)                                                                        \
+  hipLaunchKernelGGL((k_front<K, MID, MODE, NRM, A>), grid, block, 0, st, a.in, a.out, a.spack,    \
+                     a.stem_b, a.apack, a.pw_b, a.dw_w, a.dw_b, a.pwl_a, a.pwl_b, P, eps)
+  if (norm) {
+    HN_FRONT_GO(true, 0);
+  } else if (K == 3 && MID == 32 && MODE == FRONT_IRF && abl) {
+    switch (abl) {  // ablation builds (profiling only)
+      case 1: HN_FRONT_GO(false, 1); break;
+      case 2: HN_FRONT_GO(false, 2); break;
+      case 4: HN_FRONT_GO(false, 4); break;
+      case 8: HN_FRONT_GO(false, 8); break;
+      default: HN_FRONT_GO(false, 15); break;
+    }
+  } else {
+    HN_FRONT_GO(false, 0);
+  }
+#undef HN_FRONT_GO
   return hipGetLastError();
 }
 
