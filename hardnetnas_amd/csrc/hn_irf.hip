@@ -148,7 +148,9 @@ __global__ __launch_bounds__(256) void k_irf(const float* __restrict__ x, float*
     // ---- dw: thread item = (run of R output pixels in one row, channel quad q) -----------
 #pragma unroll 1
     for (int it = t; it < RUNS * 8; it += 256) {
-      const int q = it & 7, run = it >> 3;
+      // lane -> (run, channel quad): each 16-lane ds_read_b128 group holds 4 runs x 4 quads,
+      // whose window reads land in 16 distinct bank slots (slot = 4 run + q + 9 dx mod 16)
+      const int q = (lane & 3) | ((lane >> 5) << 2), run = (it >> 6) * 8 + ((lane >> 2) & 7);
       const int o0 = run * R;  // first output pixel (tile-local)
       const int pl = o0 / (HOUT * HOUT), oy = (o0 / HOUT) % HOUT, ox0 = o0 % HOUT;
       const f32x4 b4 = reinterpret_cast<const f32x4*>(s_w + K * K * 32)[q];

@@ -117,3 +117,25 @@ def test_front_pw_epilogue_writes_conflict_free():
         for q in range(4):
             slots = {(((lane & 31) * 36 + 4 * (2 * q + (lane >> 5))) * 4 // 16) % 16 for lane in g}
             assert len(slots) == 16
+
+
+@pytest.mark.parametrize("hin,s", [(16, 1), (16, 2), (8, 1), (8, 2), (4, 1)])
+def test_irf_dw_window_reads_conflict_free(hin, s):
+    """hn_irf.hip dw window reads: lane -> (run, quad) = ((l >> 2) & 7, (l & 3) | (l >> 5) << 2),
+    run = R output pixels of one row (R = 4 at stride 1, 2 at stride 2), pixel stride 36
+    floats; every ds_read_b128 group hits 16 distinct 16-byte slots for every window column
+    (8x8 at stride 2, where a run spans a quarter of an input row pair: at most 2-way)."""
+    r = 4 if s == 1 else 2
+    hout = hin // s
+    for it0 in range(0, 512, 64):
+        for c in range(8):  # window column
+            for g in GROUPS:
+                slots = set()
+                for lane in g:
+                    q = (lane & 3) | ((lane >> 5) << 2)
+                    run = (it0 >> 6) * 8 + ((lane >> 2) & 7)
+                    o0 = run * r
+                    pl, oy, ox0 = o0 // (hout * hout), (o0 // hout) % hout, o0 % hout
+                    pix = (pl * hin + oy * s) * hin + ox0 * s + c
+                    slots.add(((pix * 36 + 4 * q) * 4 // 16) % 16)
+                assert len(slots) >= (8 if (hin, s) == (8, 2) else 16)
