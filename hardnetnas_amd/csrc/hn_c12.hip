@@ -2,20 +2,21 @@
 // one kernel, so the two 128 KB/patch activations a0 and a1 never reach HBM: the kernel reads
 // the 4 KB patch and writes a2 (64 KB/patch, [P,16,16,64] fp32 NHWC).
 //
-// Persistent workgroups of 8 waves walk a contiguous range of (patch, band) items; a band is
-// 4 rows of conv2 output.  Per band:
-//   P1 stem : the 11 a0 rows the band needs (halo recomputed by the neighbour band) on the
-//             MFMA (32x32x16 bf16x3, K = 9 taps), BN+ReLU, split to bf16 hi/lo -> LDS window W0.
-//   P2 conv1: the 9 a1 rows as 16x16x32 bf16x3 MFMA tiles (16 pixels x 16 channels, K = 32
+// Persistent workgroups of 8 waves walk a contiguous range of whole patches, each in 4 bands
+// of 4 conv2 output rows, in order.  a0 and a1 live in LDS ring buffers of 10 / 9 rows, so a
+// band computes only its 8 new a0 rows and 8 new a1 rows (no halo recompute).  Per band:
+//   P1 stem : the new a0 rows on the MFMA (32x32x16 bf16x3, K = 9 taps), BN+ReLU, split to
+//             bf16 hi/lo -> ring W0.
+//   P2 conv1: the new a1 rows as 16x16x32 bf16x3 MFMA tiles (16 pixels x 16 channels, K = 32
 //             channels per tap), each wave owning one 16-channel half with its 9 taps of
-//             weights resident in VGPRs; BN+ReLU, split -> LDS window W1 (even/odd columns
-//             split for the stride-2 reads of conv2).
+//             weights resident in VGPRs; BN+ReLU, split -> ring W1 (even/odd columns split for
+//             the stride-2 reads of conv2).
 //   P3 conv2: 4 rows x 16 pixels x 64 channels as 16x16x32 tiles, each wave owning one
 //             16-channel quarter (weights resident); BN+ReLU -> float4 stores of a2.
 // LDS pixel stride 160 B (bf16 hi 64 B | lo 64 B | pad 32 B): every ds_read_b128 of a
 // 16x16x32 operand (lane: pixel l & 15, channels 8 (l >> 4) ..) hits 16 distinct 16-byte
-// slots per 16-lane group (tests/test_lds_banks.py::test_c12_windows).
-// Two barriers per band: P3 of band b overlaps P1 of band b+1 across waves.
+// slots per 16-lane group (tests/test_lds_banks.py).  Window stores are widened to b128 with
+// permlane swaps.  Two barriers per band: P3 of band b overlaps P1 of band b+1 across waves.
 #include "hn_common.h"
 #include "hn_internal.h"
 
@@ -27,8 +28,8 @@ namespace {
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 
 constexpr int RB2 = 4;                  // conv2 output rows per band
-constexpr int NA0 = 2 * RB2 + 3;        // a0 rows per band (11)
-constexpr int NA1 = 2 * RB2 + 1;        // a1 rows per band (9)
+constexpr int NA0 = 2 * RB2 + 2;        // a0 ring rows (10): a band's conv1 reads 10 a0 rows
+constexpr int NA1 = 2 * RB2 + 1;        // a1 ring rows (9): a band's conv2 reads 9 a1 rows
 constexpr int PXB = 160;                // bytes per pixel in W0 / W1
 constexpr int W0C = 34, W1C = 33;       // columns (x = -1 .. 32 / -1 .. 31)
 constexpr int W0B = NA0 * W0C * PXB;    // 59,840
@@ -77,11 +78,12 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1, NW /
   const int r32 = lane & 31, h32 = lane >> 5;  // 32x32x16 lane roles (stem)
   const int c16 = lane & 15, g16 = lane >> 4;  // 16x16x32 lane roles (conv1/conv2)
 
-  const long nitems = (long)P * 4;
-  const long per = (nitems + gridDim.x - 1) / gridDim.x;
-  const long ib = (long)xcd_remap(blockIdx.x, gridDim.x) * per;
-  const long ie = min(nitems, ib + per);
-  if (ib >= ie) return;  // workgroup-uniform
+  // whole patches per workgroup (contiguous), their 4 bands in order: consecutive bands
+  // share a0 / a1 rows, which stay in the LDS ring buffers (no halo recompute)
+  const long per = ((long)P + gridDim.x - 1) / gridDim.x;
+  const long pb = (long)xcd_remap(blockIdx.x, gridDim.x) * per;
+  const long pe = min((long)P, pb + per);
+  if (pb >= pe) return;  // workgroup-uniform
 
   // ---- one-time init: zero both windows (borders and never-written slots stay zero) ----
   for (int i = t; i < W0B / 16; i += NW * 64) reinterpret_cast<uint4*>(s_w0)[i] = make_uint4(0, 0, 0, 0);
@@ -120,19 +122,15 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1, NW /
     bias2[g] = *reinterpret_cast<const f32x4v*>(b2 + 16 * chq + 4 * g16);
   }
 
-  long cur_patch = -1;
-  // the next patch's pixels are fetched one patch ahead (2 floats per thread)
+  // the next patch's pixels are fetched one patch ahead
   constexpr int PPT = 1024 / (NW * 64);  // patch pixels per thread (2 or 4)
   typedef float pxv __attribute__((ext_vector_type(PPT)));
-  pxv vnext = reinterpret_cast<const pxv*>(in + (ib >> 2) * 1024)[t];
+  pxv vnext = reinterpret_cast<const pxv*>(in + pb * 1024)[t];
 #pragma unroll 1
-  for (long item = ib; item < ie; ++item) {
-    const long patch = item >> 2;
-    const int r0 = (int)(item & 3) * RB2;
-    if (patch != cur_patch) {  // workgroup-uniform
-      cur_patch = patch;
+  for (long patch = pb; patch < pe; ++patch) {
+    {
       const pxv v = vnext;
-      if (((patch + 1) << 2) < ie) vnext = reinterpret_cast<const pxv*>(in + (patch + 1) * 1024)[t];
+      if (patch + 1 < pe) vnext = reinterpret_cast<const pxv*>(in + (patch + 1) * 1024)[t];
       float mean = 0.f, sd = 1.f;
       if (eps >= 0.f) {  // input_norm: (x - mean) / (std_unbiased + eps), HardNet.py:306-310
         float a = 0.f;
@@ -140,7 +138,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1, NW /
         for (int j = 0; j < PPT; ++j) a += v[j];
         const float s = wave_sum(a);
         if (lane == 0) red[w] = s;
-        __syncthreads();
+        __syncthreads();  // (also: every wave is past the previous patch's P1 reads of s_in)
         a = 0.f;
 #pragma unroll
         for (int i = 0; i < NW; ++i) a += red[i];
@@ -155,6 +153,8 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1, NW /
 #pragma unroll
         for (int i = 0; i < NW; ++i) a += red[NW + i];
         sd = sqrtf(a * (1.f / 1023.f)) + eps;
+      } else {
+        __syncthreads();
       }
       const float inv = 1.f / sd;  // as k_conv_ws's stem: (x - mean) * (1/sd)
       const int q0 = PPT * t, y = q0 >> 5, x = q0 & 31;
@@ -162,13 +162,16 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1, NW /
       for (int j = 0; j < PPT; ++j) s_in[(y + 1) * 34 + x + 1 + j] = (v[j] - mean) * inv;
       __syncthreads();
     }
-
-    // ---- P1: stem rows -> W0 ---------------------------------------------------------------
-    const int y0base = 2 * r0 - 2;
 #pragma unroll 1
-    for (int ri = w; ri < ((ABL & 8) ? 0 : NA0); ri += NW) {
-      const int y = y0base + ri;  // a0 row
-      char* rowp = s_w0 + ri * W0C * PXB;
+  for (int band = 0; band < 4; ++band) {
+    const int r0 = band * RB2;
+    // ---- P1: the band's new a0 rows -> W0 ring (slot (y + 1) % NA0) ------------------------
+    // band 0: rows -1 .. 8 (row -1 is conv1's zero padding); band b: rows 8b+1 .. 8b+8
+    const int ybeg = band == 0 ? -1 : 8 * band + 1, nrows = band == 0 ? 10 : 8;
+#pragma unroll 1
+    for (int ri = w; ri < ((ABL & 8) ? 0 : nrows); ri += NW) {
+      const int y = ybeg + ri;  // a0 row
+      char* rowp = s_w0 + ((y + 1) % NA0) * W0C * PXB;
       if (y < 0 || y >= 32) {  // zero padding row (interior columns)
         for (int i = lane; i < 32 * (PXB / 16); i += 64)
           reinterpret_cast<uint4*>(rowp + PXB)[i] = make_uint4(0, 0, 0, 0);
@@ -209,14 +212,15 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1, NW /
     }
     __syncthreads();
 
-    // ---- P2: conv1 -> W1 (units: a1 row x pixel half; this wave's G1 channel groups) ---------
+    // ---- P2: conv1 -> W1 ring (units: new a1 row x pixel half; this wave's G1 groups) --------
+    // band 0: a1 rows -1 (zero padding of conv2) .. 7; band b: 8b .. 8b+7
+    const int y1beg = band == 0 ? -1 : 8 * band, n1 = band == 0 ? 9 : 8;
 #pragma unroll 1
-    for (int u = w / NCH1; u < NA1 * 2; u += NW / NCH1) {
-      const int row1 = u >> 1, pxh = u & 1;
-      const int y1 = 2 * r0 - 1 + row1;
+    for (int u = w / NCH1; u < n1 * 2; u += NW / NCH1) {
+      const int y1 = y1beg + (u >> 1), pxh = u & 1;
       const int x = 16 * pxh + c16;
-      char* pix = s_w1 + (row1 * W1C + w1_slot(x)) * PXB;
-      if (y1 < 0 || y1 >= 32) {  // zero padding row of a1
+      char* pix = s_w1 + (((y1 + 1) % NA1) * W1C + w1_slot(x)) * PXB;
+      if (y1 < 0) {  // zero padding row of a1
 #pragma unroll
         for (int g = 0; g < G1; ++g) {
           char* dst = pix + 32 * (cs1 * G1 + g) + 8 * g16;
@@ -228,15 +232,18 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1, NW /
       f32x4v acc[G1];
 #pragma unroll
       for (int g = 0; g < G1; ++g) acc[g] = f32x4v{};
-      const char* src = s_w0 + (row1 * W0C + x) * PXB + 16 * g16;
+      // the 3 a0 rows y1 - 1 .. y1 + 1 sit in ring slots (y1 + dy) % NA0
+      const char* srow[3];
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy) srow[dy] = s_w0 + (((y1 + dy) % NA0) * W0C + x) * PXB + 16 * g16;
       // B fragments one tap ahead of the MFMAs (two register sets); each feeds G1 groups
       uint4 bh[2], bl[2];
-      bh[0] = (ABL & 16) ? make_uint4(lane, 1, 2, 3) : *reinterpret_cast<const uint4*>(src);
-      bl[0] = (ABL & 16) ? make_uint4(lane, 3, 2, 1) : *reinterpret_cast<const uint4*>(src + 64);
+      bh[0] = (ABL & 16) ? make_uint4(lane, 1, 2, 3) : *reinterpret_cast<const uint4*>(srow[0]);
+      bl[0] = (ABL & 16) ? make_uint4(lane, 3, 2, 1) : *reinterpret_cast<const uint4*>(srow[0] + 64);
 #pragma unroll
       for (int tap = 0; tap < 9; ++tap) {
         if (tap + 1 < 9) {
-          const char* p = src + (((tap + 1) / 3) * W0C + (tap + 1) % 3) * PXB;
+          const char* p = srow[(tap + 1) / 3] + ((tap + 1) % 3) * PXB;
           bh[(tap + 1) & 1] = (ABL & 16) ? make_uint4(tap, lane, 2, 3) : *reinterpret_cast<const uint4*>(p);
           bl[(tap + 1) & 1] = (ABL & 16) ? make_uint4(lane, tap, 2, 1) : *reinterpret_cast<const uint4*>(p + 64);
         }
@@ -277,15 +284,19 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1, NW /
       for (int g = 0; g < G2; ++g) acc[g] = f32x4v{};
       // output column c16 reads a1 column 2*c16 - 1 + dx: W1 slot c16 (dx 0), 17 + c16 (dx 1),
       // c16 + 1 (dx 2); B fragments one tap ahead of the MFMAs
-      const char* src = s_w1 + (2 * oy * W1C + c16) * PXB + 16 * g16;
+      // a1 rows 2 (r0 + oy) - 1 + dy sit in ring slots (2 (r0 + oy) + dy) % NA1
+      const char* srow[3];
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy)
+        srow[dy] = s_w1 + (((2 * (r0 + oy) + dy) % NA1) * W1C + c16) * PXB + 16 * g16;
       uint4 bh[2], bl[2];
-      bh[0] = (ABL & 16) ? make_uint4(lane, 1, 2, 3) : *reinterpret_cast<const uint4*>(src);
-      bl[0] = (ABL & 16) ? make_uint4(lane, 3, 2, 1) : *reinterpret_cast<const uint4*>(src + 64);
+      bh[0] = (ABL & 16) ? make_uint4(lane, 1, 2, 3) : *reinterpret_cast<const uint4*>(srow[0]);
+      bl[0] = (ABL & 16) ? make_uint4(lane, 3, 2, 1) : *reinterpret_cast<const uint4*>(srow[0] + 64);
 #pragma unroll
       for (int tap = 0; tap < 9; ++tap) {
         if (tap + 1 < 9) {
           const int dy = (tap + 1) / 3, dx = (tap + 1) % 3;
-          const char* p = src + (dy * W1C + (dx == 1 ? 17 : (dx >> 1))) * PXB;
+          const char* p = srow[dy] + (dx == 1 ? 17 : (dx >> 1)) * PXB;
           bh[(tap + 1) & 1] = (ABL & 16) ? make_uint4(tap, lane, 2, 3) : *reinterpret_cast<const uint4*>(p);
           bl[(tap + 1) & 1] = (ABL & 16) ? make_uint4(lane, tap, 2, 1) : *reinterpret_cast<const uint4*>(p + 64);
         }
@@ -309,7 +320,8 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1, NW /
     }
     // no barrier: the next band's P1 writes only W0, which P3 does not read; its first
     // barrier orders this P3's W1 reads before the next P2's W1 writes
-  }
+  }  // band
+  }  // patch
 }
 
 }  // namespace
@@ -334,7 +346,7 @@ hipError_t hn_launch_c12(const float* in, float* out, const HardnetDev& d, int P
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     resident[ri] = std::max(1, per_cu) * std::max(1, cus);
   }
-  const int grid = (int)std::min<long>((long)P * 4, resident[ri]);
+  const int grid = (int)std::min<long>((long)P, resident[ri]);
 #define HN_C12_GO(A, W)                                                                          \
   hipLaunchKernelGGL((k_c12<A, W>), dim3(grid), dim3(W * 64), 0, st, in, out, d.stem_w, d.stem_b, \
                      static_cast<const uint4*>(d.c12_w1), d.bias[1],                              \
