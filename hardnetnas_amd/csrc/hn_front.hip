@@ -9,8 +9,9 @@
 //   MODE FRONT_MAXPOOL: the "skip" op at stride 2 = MaxPool2d(3, 2, 1)
 //                       (fbnet_builder.py:202-228); writes [P,16,16,32].
 //
-// One workgroup (4 waves) owns a band of 4 output rows of one patch.  The band's
-// 2*3+k pw rows (halo recomputed by the neighbouring band) are produced row by row: a wave
+// Persistent workgroups (4 waves) walk whole patches, each in 4 bands of 4 output rows; for
+// MID = 32 the pw rows live in an LDS ring shared by consecutive bands (8 new rows per band),
+// for wider MID a band's 2*3+k rows are recomputed.  Rows are produced one per wave: a wave
 // computes the stem for one image row (32 pixels) as one fp16x3 MFMA tile whose output
 // layout (lane = pixel, 16 channels per lane) is directly the pw B operand, keeps it in
 // registers, and runs
@@ -22,6 +23,7 @@
 #include "hn_common.h"
 #include "hn_internal.h"
 
+#include <algorithm>
 #include <cstdlib>
 
 namespace {
@@ -39,9 +41,10 @@ __constant__ unsigned char kDwLane[64] = {
     22, 23, 30, 31, 38, 39, 36, 37, 44, 45, 52, 53, 54, 55, 58, 59, 60, 61, 62, 63, 24, 25,
     16, 17, 18, 19, 32, 33, 40, 41, 26, 27, 34, 35, 42, 43, 50, 51, 48, 49, 56, 57};
 
-// ABL: ablation builds for profiling only (0 in production): bit 0 skips the stem MFMA and
-// epilogue, bit 1 the pw MFMA + LDS stores, bit 2 the depthwise loop, bit 3 the pwl MFMA.
-template <int K, int MID, int MODE, bool NORM, int ABL = 0>
+// RING (MID = 32 and the maxpool form): the chunk's pw rows live in an LDS ring of IR rows
+// (slot (y + PAD) % IR) that persists across the 4 bands of a patch, so a band computes only
+// its 8 new stem/pw rows.  MID > 32 recomputes the band's halo rows for every chunk.
+template <int K, int MID, int MODE, bool NORM>
 __global__ __launch_bounds__(256) void k_front(const float* __restrict__ in,
                                                float* __restrict__ out,
                                                const uint4* __restrict__ spack,  // stem A operand
@@ -55,11 +58,13 @@ __global__ __launch_bounds__(256) void k_front(const float* __restrict__ in,
                                                int P, float eps) {
   constexpr int KK = MODE == FRONT_MAXPOOL ? 3 : K;
   constexpr int PAD = KK / 2;
-  constexpr int IR = 2 * (RB - 1) + KK;  // pw rows of the band
+  constexpr int IR = 2 * (RB - 1) + KK;  // pw rows a band reads (ring size)
   constexpr int PC = 32 + 2 * PAD;       // columns incl. zero padding
-  constexpr int NT = (IR + 3) / 4;       // row tiles per wave
+  constexpr int NT = (IR + 3) / 4;       // row tiles per wave (at most)
   constexpr int OC = 32;  // layer-0 output channels (SEARCH_SPACE2[0] = (32, 32, 2))
   constexpr int DYU = KK == 3 ? 3 : 1;  // k5: rolled dy loop keeps VGPRs (and occupancy) in check
+  constexpr bool RING = MID == 32;
+  static_assert(IR >= 8, "ring holds a band's 8 new rows");
   __shared__ float s_in[34 * 34];
   __shared__ __attribute__((aligned(16))) float s_pw[IR * PC * PS];
   __shared__ __attribute__((aligned(16))) float s_dw[KK * KK * 32 + 32];
@@ -67,227 +72,236 @@ __global__ __launch_bounds__(256) void k_front(const float* __restrict__ in,
 
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int px = lane & 31, h = lane >> 5;
-  // XCD-aware: workgroups b, b+8, b+16, b+24 (dispatched round-robin to the same XCD) are
-  // the 4 bands of one patch, so the patch is read from HBM once and then hits that L2
-  const long patch = (long)(blockIdx.x >> 5) * 8 + (blockIdx.x & 7);
-  const int r0 = ((blockIdx.x >> 3) & 3) * RB;
-  if (patch >= P) return;  // grid is padded to a multiple of 32 workgroups
-  const int row0 = 2 * r0 - PAD;
+  // persistent: whole patches per workgroup, their 4 bands in order
+  const long per = ((long)P + gridDim.x - 1) / gridDim.x;
+  const long pb = (long)xcd_remap(blockIdx.x, gridDim.x) * per;
+  const long pe = min((long)P, pb + per);
+  if (pb >= pe) return;  // workgroup-uniform
 
-  // ---- phase 0: patch (+ input_norm) to LDS; zero the pw band's padding -----------------
-  const float4 v = reinterpret_cast<const float4*>(in + patch * 1024)[t];
+  // ---- one-time init: zero s_in (its frame stays zero) and the pw pad columns ---------------
   for (int i = t; i < 34 * 34; i += 256) s_in[i] = 0.f;
   for (int i = t; i < IR * 2 * PAD * (PS / 4); i += 256) {  // left/right pad columns
     const int ri = i / (2 * PAD * (PS / 4)), rem = i % (2 * PAD * (PS / 4)), c = rem / (PS / 4);
     reinterpret_cast<float4*>(s_pw)[(ri * PC + (c < PAD ? c : 32 + c)) * (PS / 4) + rem % (PS / 4)] =
         make_float4(0.f, 0.f, 0.f, 0.f);
   }
-#pragma unroll
-  for (int ri = 0; ri < IR; ++ri) {  // rows outside the image (first / last band only)
-    if (row0 + ri >= 0 && row0 + ri < 32) continue;
-    for (int i = t; i < 32 * (PS / 4); i += 256)
-      reinterpret_cast<float4*>(s_pw)[(ri * PC + PAD) * (PS / 4) + i] = make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-  float mean = 0.f, sd = 1.f;
-  if (NORM) {  // (x - mean) / (std_unbiased + eps), as k_stem
-    const float s = wave_sum(v.x + v.y + v.z + v.w);
-    if (lane == 0) red[w] = s;
-    __syncthreads();
-    mean = (red[0] + red[1] + red[2] + red[3]) * (1.f / 1024.f);
-    const float d0 = v.x - mean, d1 = v.y - mean, d2 = v.z - mean, d3 = v.w - mean;
-    const float q = wave_sum(d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3);
-    if (lane == 0) red[4 + w] = q;
-    __syncthreads();
-    sd = sqrtf((red[4] + red[5] + red[6] + red[7]) * (1.f / 1023.f)) + eps;
-  }
-  __syncthreads();
-  {
-    const int q = 4 * t, y = q >> 5, x = q & 31;
-    float* d = s_in + (y + 1) * 34 + x + 1;
-    if (NORM) {
-      d[0] = (v.x - mean) / sd; d[1] = (v.y - mean) / sd;
-      d[2] = (v.z - mean) / sd; d[3] = (v.w - mean) / sd;
-    } else {
-      d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
-    }
-  }
-  __syncthreads();
-
-  // ---- phase A: stem rows on the MFMA ---------------------------------------------------
-  // A = stem weights [32 ch][16 = 9 taps + 0], B = im2col of one image row (lane: pixel px,
-  // taps 8h..8h+7).  C leaves channel 4h + 8q + r (i = 4q + r) of pixel px in acc[i]; that
-  // order is used as-is as the pw contraction index (pw weights are packed to match).
   const f16x8 sah = as_f16x8(spack[lane]), sal = as_f16x8(spack[64 + lane]);
   float4 sb[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) sb[q] = *reinterpret_cast<const float4*>(stem_b + 8 * q + 4 * h);
-  uint4 bh[NT][2], bl[NT][2];
-#pragma unroll
-  for (int i = 0; i < NT; ++i) {
-    const int ri = w + 4 * i, y = row0 + ri;
-    if (ri >= IR || y < 0 || y >= 32) continue;  // wave-uniform; such tiles are never read
-    float tp[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int tap = 8 * h + j;  // h = 1 holds tap 8 and zeros
-      tp[j] = tap < 9 ? s_in[(y + tap / 3) * 34 + px + tap % 3] : 0.f;
-    }
-    if (ABL & 1) {
-      bh[i][0] = bh[i][1] = bl[i][0] = bl[i][1] = make_uint4(__float_as_uint(tp[0]), lane, 0, 0);
-      continue;
-    }
-    uint4 xh, xl;
-    split8_f16(make_float4(tp[0], tp[1], tp[2], tp[3]), make_float4(tp[4], tp[5], tp[6], tp[7]), xh, xl);
-    f32x16 c = {};
-    c = mfma3_f16(sah, sal, as_f16x8(xh), as_f16x8(xl), c);
-    float4 o[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      o[q] = make_float4(fmaxf(c[4 * q] + sb[q].x, 0.f), fmaxf(c[4 * q + 1] + sb[q].y, 0.f),
-                         fmaxf(c[4 * q + 2] + sb[q].z, 0.f), fmaxf(c[4 * q + 3] + sb[q].w, 0.f));
-    if (MODE == FRONT_MAXPOOL) {
-      float4* d = reinterpret_cast<float4*>(s_pw + (ri * PC + PAD + px) * PS);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) d[2 * q + h] = o[q];
-    } else {
-      split8_f16(o[0], o[1], bh[i][0], bl[i][0]);
-      split8_f16(o[2], o[3], bh[i][1], bl[i][1]);
-    }
-  }
-
   const int lm = kDwLane[lane], dq = lm & 7, dox = lm >> 3;
-  if (MODE == FRONT_MAXPOOL) {
-    __syncthreads();
-    // MaxPool2d(3, 2, 1): padding never wins since every window holds a ReLU output >= 0
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int p = 8 * (w + 4 * j) + dox, orr = p >> 4, ox = p & 15;
-      float4 m = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-      for (int dy = 0; dy < 3; ++dy)
-#pragma unroll
-        for (int dx = 0; dx < 3; ++dx) {
-          const float4 a = *reinterpret_cast<const float4*>(s_pw + ((2 * orr + dy) * PC + 2 * ox + dx) * PS + 4 * dq);
-          m.x = fmaxf(m.x, a.x); m.y = fmaxf(m.y, a.y); m.z = fmaxf(m.z, a.z); m.w = fmaxf(m.w, a.w);
-        }
-      *reinterpret_cast<float4*>(out + ((patch * 16 + r0 + orr) * 16 + ox) * 32 + 4 * dq) = m;
-    }
-    return;
-  }
+  auto slot_of = [](int y) { return (y + PAD + IR) % IR; };  // ring slot of pw row y
 
-  // ---- phases B/C/D per 32-channel chunk of MID -----------------------------------------
-  f32x16 oacc = {};
+  float4 vnext = reinterpret_cast<const float4*>(in + pb * 1024)[t];
 #pragma unroll 1
-  for (int m = 0; m < MID / 32; ++m) {
-    // dw weights + bias of the chunk
-    for (int i = t; i < KK * KK * 8 + 8; i += 256) {
-      float4 wv;
-      if (i < KK * KK * 8)
-        wv = *reinterpret_cast<const float4*>(dw_w + (i >> 3) * MID + 32 * m + 4 * (i & 7));
-      else
-        wv = *reinterpret_cast<const float4*>(dw_b + 32 * m + 4 * (i - KK * KK * 8));
-      reinterpret_cast<float4*>(s_dw)[i] = wv;
+  for (long patch = pb; patch < pe; ++patch) {
+    // ---- patch (+ input_norm) to LDS; the next patch's pixels are prefetched ---------------
+    const float4 v = vnext;
+    if (patch + 1 < pe) vnext = reinterpret_cast<const float4*>(in + (patch + 1) * 1024)[t];
+    float mean = 0.f, sd = 1.f;
+    if (NORM) {  // (x - mean) / (std_unbiased + eps), as k_stem
+      const float s = wave_sum(v.x + v.y + v.z + v.w);
+      if (lane == 0) red[w] = s;
+      __syncthreads();
+      mean = (red[0] + red[1] + red[2] + red[3]) * (1.f / 1024.f);
+      const float d0 = v.x - mean, d1 = v.y - mean, d2 = v.z - mean, d3 = v.w - mean;
+      const float q = wave_sum(d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3);
+      if (lane == 0) red[4 + w] = q;
+      __syncthreads();
+      sd = sqrtf((red[4] + red[5] + red[6] + red[7]) * (1.f / 1023.f)) + eps;
     }
-    const uint4* ap = apack + (size_t)m * 4 * 64 + lane;
-    const f16x8 ah0 = as_f16x8(ap[0]), al0 = as_f16x8(ap[64]);
-    const f16x8 ah1 = as_f16x8(ap[128]), al1 = as_f16x8(ap[192]);
-    float4 bias[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) bias[q] = *reinterpret_cast<const float4*>(pw_b + 32 * m + 8 * q + 4 * h);
-#pragma unroll
-    for (int i = 0; i < NT; ++i) {
-      const int ri = w + 4 * i, y = row0 + ri;
-      if (ri >= IR || y < 0 || y >= 32 || (ABL & 2)) continue;
-      f32x16 acc = {};
-      acc = mfma3_f16(ah0, al0, as_f16x8(bh[i][0]), as_f16x8(bl[i][0]), acc);
-      acc = mfma3_f16(ah1, al1, as_f16x8(bh[i][1]), as_f16x8(bl[i][1]), acc);
-      float4* d = reinterpret_cast<float4*>(s_pw + (ri * PC + PAD + px) * PS);
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        d[2 * q + h] = make_float4(fmaxf(acc[4 * q] + bias[q].x, 0.f), fmaxf(acc[4 * q + 1] + bias[q].y, 0.f),
-                                   fmaxf(acc[4 * q + 2] + bias[q].z, 0.f), fmaxf(acc[4 * q + 3] + bias[q].w, 0.f));
+    __syncthreads();  // the previous patch is done with s_in and the ring
+    {
+      const int q = 4 * t, y = q >> 5, x = q & 31;
+      float* d = s_in + (y + 1) * 34 + x + 1;
+      if (NORM) {
+        d[0] = (v.x - mean) / sd; d[1] = (v.y - mean) / sd;
+        d[2] = (v.z - mean) / sd; d[3] = (v.w - mean) / sd;
+      } else {
+        d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+      }
     }
     __syncthreads();
-    // dw straight into the pwl B-operand layout: wave w owns band pixel tile (w & 1) and
-    // K-step (w >> 1) of this chunk; lane (px, h) computes channels 16*(w>>1) + 8h .. +7 of
-    // band pixel 32*(w&1) + px, splits them and multiplies with the pwl weights of that
-    // K-step.  Waves 2/3 hold partial sums over the odd K-steps, folded in at the end.
-    {
-      const int p = 32 * (w & 1) + px, orr = p >> 4, ox = p & 15, c0 = 16 * (w >> 1) + 8 * h;
-      f32x4 a0 = *reinterpret_cast<const f32x4*>(s_dw + KK * KK * 32 + c0);
-      f32x4 a1 = *reinterpret_cast<const f32x4*>(s_dw + KK * KK * 32 + c0 + 4);
-#pragma unroll DYU
-      for (int dy = 0; dy < ((ABL & 4) ? 0 : KK); ++dy)
+
+#pragma unroll 1
+    for (int band = 0; band < 4; ++band) {
+      const int r0 = band * RB;
+      // pw rows this band computes: all IR rows 2 r0 - PAD .. (band 0 / no ring), or the 8
+      // rows after the previous band's last one (ring)
+      const int ylast = 2 * r0 + 6 + PAD;
+      const int ybeg = (RING && band > 0) ? ylast - 7 : 2 * r0 - PAD;
+      const int nrows = ylast + 1 - ybeg;
+
+      // ---- phase A: stem rows on the MFMA ------------------------------------------------
+      // A = stem weights [32 ch][16 = 9 taps + 0], B = im2col of one image row (lane: pixel
+      // px, taps 8h..8h+7).  C leaves channel 4h + 8q + r (i = 4q + r) of pixel px in acc[i];
+      // that order is used as-is as the pw contraction index (pw weights are packed to match).
+      uint4 bh[NT][2], bl[NT][2];
 #pragma unroll
-        for (int dx = 0; dx < KK; ++dx) {
-          const float* wp = s_dw + (dy * KK + dx) * 32 + c0;
-          const float* ip = s_pw + ((2 * orr + dy) * PC + 2 * ox + dx) * PS + c0;
-          a0 = __builtin_elementwise_fma(*reinterpret_cast<const f32x4*>(wp), *reinterpret_cast<const f32x4*>(ip), a0);
-          a1 = __builtin_elementwise_fma(*reinterpret_cast<const f32x4*>(wp + 4), *reinterpret_cast<const f32x4*>(ip + 4), a1);
+      for (int i = 0; i < NT; ++i) {
+        const int ri = w + 4 * i, y = ybeg + ri;
+        if (ri >= nrows) continue;  // wave-uniform; such tiles are never read
+        if (y < 0 || y >= 32) {     // zero padding row of the pw output
+          float4* d = reinterpret_cast<float4*>(s_pw + (slot_of(y) * PC + PAD) * PS);
+          for (int j = lane; j < 32 * (PS / 4); j += 64) d[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+          continue;
         }
-      a0 = __builtin_elementwise_max(a0, f32x4{});
-      a1 = __builtin_elementwise_max(a1, f32x4{});
-      uint4 xh, xl;
-      split8_f16(make_float4(a0.x, a0.y, a0.z, a0.w), make_float4(a1.x, a1.y, a1.z, a1.w), xh, xl);
-      const uint4* lp = pwl_a + ((size_t)(2 * m + (w >> 1)) * 2) * 64 + lane;
-      if (ABL & 8)
-        oacc[0] += __uint_as_float(xh.x ^ xl.y);
-      else
-        oacc = mfma3_f16(as_f16x8(lp[0]), as_f16x8(lp[64]), as_f16x8(xh), as_f16x8(xl), oacc);
-    }
-    __syncthreads();  // s_pw / s_dw are rewritten by the next chunk
-  }
-  // fold the odd-K-step partial sums of waves 2/3 into waves 0/1 (s_pw is free now)
-  if (w >= 2) {
-    float4* d = reinterpret_cast<float4*>(s_pw) + ((w - 2) * 64 + lane) * 4;
+        float tp[8];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) d[q] = make_float4(oacc[4 * q], oacc[4 * q + 1], oacc[4 * q + 2], oacc[4 * q + 3]);
-  }
-  __syncthreads();
-  if (w < 2) {
-    const float4* d = reinterpret_cast<const float4*>(s_pw) + (w * 64 + lane) * 4;
+        for (int j = 0; j < 8; ++j) {
+          const int tap = 8 * h + j;  // h = 1 holds tap 8 and zeros
+          tp[j] = tap < 9 ? s_in[(y + tap / 3) * 34 + px + tap % 3] : 0.f;
+        }
+        uint4 xh, xl;
+        split8_f16(make_float4(tp[0], tp[1], tp[2], tp[3]), make_float4(tp[4], tp[5], tp[6], tp[7]), xh, xl);
+        f32x16 c = {};
+        c = mfma3_f16(sah, sal, as_f16x8(xh), as_f16x8(xl), c);
+        float4 o[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float4 v = d[q];
-      oacc[4 * q] += v.x; oacc[4 * q + 1] += v.y; oacc[4 * q + 2] += v.z; oacc[4 * q + 3] += v.w;
-    }
-  }
-  if (w < 2) {  // output pixel 32w + px of the band = row r0 + (32w + px) / 16
-    const int p = 32 * w + px;
-    float* dst = out + ((patch * 16 + r0 + (p >> 4)) * 16 + (p & 15)) * OC;
+        for (int q = 0; q < 4; ++q)
+          o[q] = make_float4(fmaxf(c[4 * q] + sb[q].x, 0.f), fmaxf(c[4 * q + 1] + sb[q].y, 0.f),
+                             fmaxf(c[4 * q + 2] + sb[q].z, 0.f), fmaxf(c[4 * q + 3] + sb[q].w, 0.f));
+        if (MODE == FRONT_MAXPOOL) {
+          float4* d = reinterpret_cast<float4*>(s_pw + (slot_of(y) * PC + PAD + px) * PS);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float4 b = *reinterpret_cast<const float4*>(pwl_b + 8 * q + 4 * h);
-      *reinterpret_cast<float4*>(dst + 8 * q + 4 * h) =
-          make_float4(oacc[4 * q] + b.x, oacc[4 * q + 1] + b.y, oacc[4 * q + 2] + b.z, oacc[4 * q + 3] + b.w);
+          for (int q = 0; q < 4; ++q) d[2 * q + h] = o[q];
+        } else {
+          split8_f16(o[0], o[1], bh[i][0], bl[i][0]);
+          split8_f16(o[2], o[3], bh[i][1], bl[i][1]);
+        }
+      }
+
+      if (MODE == FRONT_MAXPOOL) {
+        __syncthreads();
+        // MaxPool2d(3, 2, 1): padding never wins since every window holds a ReLU output >= 0
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int p = 8 * (w + 4 * j) + dox, orr = p >> 4, ox = p & 15;
+          float4 m = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+          for (int dy = 0; dy < 3; ++dy) {
+            const float* rp = s_pw + slot_of(2 * (r0 + orr) - 1 + dy) * PC * PS;
+#pragma unroll
+            for (int dx = 0; dx < 3; ++dx) {
+              const float4 a = *reinterpret_cast<const float4*>(rp + (2 * ox + dx) * PS + 4 * dq);
+              m.x = fmaxf(m.x, a.x); m.y = fmaxf(m.y, a.y); m.z = fmaxf(m.z, a.z); m.w = fmaxf(m.w, a.w);
+            }
+          }
+          *reinterpret_cast<float4*>(out + ((patch * 16 + r0 + orr) * 16 + ox) * 32 + 4 * dq) = m;
+        }
+        __syncthreads();  // reads done before the next band's rows overwrite ring slots
+        continue;
+      }
+
+      // ---- phases B/C/D per 32-channel chunk of MID -------------------------------------
+      f32x16 oacc = {};
+#pragma unroll 1
+      for (int m = 0; m < MID / 32; ++m) {
+        // dw weights + bias of the chunk
+        for (int i = t; i < KK * KK * 8 + 8; i += 256) {
+          float4 wv;
+          if (i < KK * KK * 8)
+            wv = *reinterpret_cast<const float4*>(dw_w + (i >> 3) * MID + 32 * m + 4 * (i & 7));
+          else
+            wv = *reinterpret_cast<const float4*>(dw_b + 32 * m + 4 * (i - KK * KK * 8));
+          reinterpret_cast<float4*>(s_dw)[i] = wv;
+        }
+        const uint4* ap = apack + (size_t)m * 4 * 64 + lane;
+        const f16x8 ah0 = as_f16x8(ap[0]), al0 = as_f16x8(ap[64]);
+        const f16x8 ah1 = as_f16x8(ap[128]), al1 = as_f16x8(ap[192]);
+        float4 bias[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) bias[q] = *reinterpret_cast<const float4*>(pw_b + 32 * m + 8 * q + 4 * h);
+#pragma unroll
+        for (int i = 0; i < NT; ++i) {
+          const int ri = w + 4 * i, y = ybeg + ri;
+          if (ri >= nrows || y < 0 || y >= 32) continue;
+          f32x16 acc = {};
+          acc = mfma3_f16(ah0, al0, as_f16x8(bh[i][0]), as_f16x8(bl[i][0]), acc);
+          acc = mfma3_f16(ah1, al1, as_f16x8(bh[i][1]), as_f16x8(bl[i][1]), acc);
+          float4* d = reinterpret_cast<float4*>(s_pw + (slot_of(y) * PC + PAD + px) * PS);
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            d[2 * q + h] = make_float4(fmaxf(acc[4 * q] + bias[q].x, 0.f), fmaxf(acc[4 * q + 1] + bias[q].y, 0.f),
+                                       fmaxf(acc[4 * q + 2] + bias[q].z, 0.f), fmaxf(acc[4 * q + 3] + bias[q].w, 0.f));
+        }
+        __syncthreads();
+        // dw straight into the pwl B-operand layout: wave w owns band pixel tile (w & 1) and
+        // K-step (w >> 1) of this chunk; lane (px, h) computes channels 16*(w>>1) + 8h .. +7
+        // of band pixel 32*(w&1) + px, splits them and multiplies with the pwl weights of
+        // that K-step.  Waves 2/3 hold partial sums over the odd K-steps, folded in below.
+        {
+          const int p = 32 * (w & 1) + px, orr = p >> 4, ox = p & 15, c0 = 16 * (w >> 1) + 8 * h;
+          f32x4 a0 = *reinterpret_cast<const f32x4*>(s_dw + KK * KK * 32 + c0);
+          f32x4 a1 = *reinterpret_cast<const f32x4*>(s_dw + KK * KK * 32 + c0 + 4);
+#pragma unroll DYU
+          for (int dy = 0; dy < KK; ++dy) {
+            const float* rp = s_pw + slot_of(2 * (r0 + orr) - PAD + dy) * PC * PS + c0;
+#pragma unroll
+            for (int dx = 0; dx < KK; ++dx) {
+              const float* wp = s_dw + (dy * KK + dx) * 32 + c0;
+              const float* ip = rp + (2 * ox + dx) * PS;
+              a0 = __builtin_elementwise_fma(*reinterpret_cast<const f32x4*>(wp), *reinterpret_cast<const f32x4*>(ip), a0);
+              a1 = __builtin_elementwise_fma(*reinterpret_cast<const f32x4*>(wp + 4), *reinterpret_cast<const f32x4*>(ip + 4), a1);
+            }
+          }
+          a0 = __builtin_elementwise_max(a0, f32x4{});
+          a1 = __builtin_elementwise_max(a1, f32x4{});
+          uint4 xh, xl;
+          split8_f16(make_float4(a0.x, a0.y, a0.z, a0.w), make_float4(a1.x, a1.y, a1.z, a1.w), xh, xl);
+          const uint4* lp = pwl_a + ((size_t)(2 * m + (w >> 1)) * 2) * 64 + lane;
+          oacc = mfma3_f16(as_f16x8(lp[0]), as_f16x8(lp[64]), as_f16x8(xh), as_f16x8(xl), oacc);
+        }
+        __syncthreads();  // s_dw (and, without the ring, s_pw) is rewritten next
+      }
+      // fold the odd-K-step partial sums of waves 2/3 into waves 0/1 through the interior
+      // of the ring slots of rows ybeg, ybeg + 1 (recomputed by the next band, never the
+      // rows it keeps; the pad columns stay zero)
+      if (w >= 2) {
+        float4* d = reinterpret_cast<float4*>(s_pw + (slot_of(ybeg + (w - 2)) * PC + PAD) * PS) + lane * 4;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) d[q] = make_float4(oacc[4 * q], oacc[4 * q + 1], oacc[4 * q + 2], oacc[4 * q + 3]);
+      }
+      __syncthreads();
+      if (w < 2) {  // output pixel 32w + px of the band = row r0 + (32w + px) / 16
+        const float4* d = reinterpret_cast<const float4*>(s_pw + (slot_of(ybeg + w) * PC + PAD) * PS) + lane * 4;
+        const int p = 32 * w + px;
+        float* dst = out + ((patch * 16 + r0 + (p >> 4)) * 16 + (p & 15)) * OC;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float4 v4 = d[q];
+          const float4 b = *reinterpret_cast<const float4*>(pwl_b + 8 * q + 4 * h);
+          *reinterpret_cast<float4*>(dst + 8 * q + 4 * h) =
+              make_float4(oacc[4 * q] + v4.x + b.x, oacc[4 * q + 1] + v4.y + b.y,
+                          oacc[4 * q + 2] + v4.z + b.z, oacc[4 * q + 3] + v4.w + b.w);
+        }
+      }
+      __syncthreads();  // fold reads done before the next band rewrites those ring slots
     }
   }
 }
 
+template <int K, int MID, int MODE, bool NORM>
+hipError_t front_launch_t(const HnFrontArgs& a, int P, float eps, hipStream_t st) {
+  static int resident = 0;  // persistent grid: every workgroup resident at once
+  if (!resident) {
+    int per_cu = 0, dev = 0, cus = 0;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &per_cu, reinterpret_cast<const void*>(&k_front<K, MID, MODE, NORM>), 256, 0);
+    if (e != hipSuccess) return e;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    resident = std::max(1, per_cu) * std::max(1, cus);
+  }
+  hipLaunchKernelGGL((k_front<K, MID, MODE, NORM>), dim3(std::min(P, resident)), dim3(256), 0, st, a.in,
+                     a.out, a.spack, a.stem_b, a.apack, a.pw_b, a.dw_w, a.dw_b, a.pwl_a, a.pwl_b, P, eps);
+  return hipGetLastError();
+}
 
 template <int K, int MID, int MODE>
 hipError_t front_launch(const HnFrontArgs& a, int P, bool norm, float eps, hipStream_t st) {
-  const dim3 grid((unsigned)((P + 7) / 8) * 32), block(256);
-  static int abl = -1;
-  if (abl < 0) abl = std::getenv("HN_FRONT_ABL") ? std::atoi(std::getenv("HN_FRONT_ABL")) & 15 : 0;
-#define HN_FRONT_GO(NRM, A)                                                                        \
-  hipLaunchKernelGGL((k_front<K, MID, MODE, NRM, A>), grid, block, 0, st, a.in, a.out, a.spack,    \
-                     a.stem_b, a.apack, a.pw_b, a.dw_w, a.dw_b, a.pwl_a, a.pwl_b, P, eps)
-  if (norm) {
-    HN_FRONT_GO(true, 0);
-  } else if (K == 3 && MID == 32 && MODE == FRONT_IRF && abl) {
-    switch (abl) {  // ablation builds (profiling only)
-      case 1: HN_FRONT_GO(false, 1); break;
-      case 2: HN_FRONT_GO(false, 2); break;
-      case 4: HN_FRONT_GO(false, 4); break;
-      case 8: HN_FRONT_GO(false, 8); break;
-      default: HN_FRONT_GO(false, 15); break;
-    }
-  } else {
-    HN_FRONT_GO(false, 0);
-  }
-#undef HN_FRONT_GO
-  return hipGetLastError();
+  return norm ? front_launch_t<K, MID, MODE, true>(a, P, eps, st)
+              : front_launch_t<K, MID, MODE, false>(a, P, eps, st);
 }
 
 }  // namespace
