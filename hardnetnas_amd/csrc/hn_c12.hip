@@ -70,7 +70,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1, NW /
   __shared__ __attribute__((aligned(16))) char s_w1[W1B];
   __shared__ float s_in[34 * 34];
   __shared__ float red[2 * NW];
-  constexpr int G1 = 8 / NW, G2 = 8 / NW;     // conv1 / conv2 output groups per wave
+  constexpr int G1 = 2, G2 = 8 / NW;          // conv1 / conv2 output groups per wave
   constexpr int NCH1 = 2 / G1, NCH2 = 4 / G2;  // waves sharing a P2 unit / a P3 row
 
   const int t = threadIdx.x, lane = t & 63;
@@ -101,8 +101,16 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1, NW /
   }
   // conv1 / conv2 A operands resident in registers: [tap][group][plane]
   const int cs1 = w % NCH1, cs2 = w % NCH2;
-  uint4 a1w[9][G1][2], a2w[9][G2][2];
-  f32x4v bias1[G1], bias2[G2];
+  uint4 a1w[9][G1][2];
+  // biases in LDS (read in the epilogues; frees their registers)
+  // (the stem bias too: a global load in P1 would queue behind the previous P3's output
+  // stores in the in-order vmcnt counter)
+  __shared__ __attribute__((aligned(16))) float s_b0[32], s_b1[32], s_b2[64];
+  for (int i = t; i < 128; i += NW * 64) {
+    if (i < 32) s_b0[i] = stem_b[i];
+    else if (i < 64) s_b1[i - 32] = b1[i - 32];
+    else s_b2[i - 64] = b2[i - 64];
+  }
 #pragma unroll
   for (int g = 0; g < G1; ++g) {
     const int chh = cs1 * G1 + g;
@@ -110,17 +118,14 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1, NW /
     for (int tap = 0; tap < 9; ++tap)
 #pragma unroll
       for (int pl = 0; pl < 2; ++pl) a1w[tap][g][pl] = w1p[((tap * 2 + chh) * 2 + pl) * 64 + lane];
-    bias1[g] = *reinterpret_cast<const f32x4v*>(b1 + 16 * chh + 4 * g16);
   }
-#pragma unroll
-  for (int g = 0; g < G2; ++g) {
-    const int chq = cs2 * G2 + g;
-#pragma unroll
-    for (int tap = 0; tap < 9; ++tap)
-#pragma unroll
-      for (int pl = 0; pl < 2; ++pl) a2w[tap][g][pl] = w2p[((tap * 4 + chq) * 2 + pl) * 64 + lane];
-    bias2[g] = *reinterpret_cast<const f32x4v*>(b2 + 16 * chq + 4 * g16);
-  }
+  // conv2 A fragments are streamed from L2 per tap (2 taps ahead): the register file holds
+  // both conv1 groups instead, so each P2 B fragment feeds two output groups
+  auto w2_frag = [&](int tap, int g, int pl) {
+    int i = ((tap * 4 + cs2 * G2 + g) * 2 + pl) * 64 + lane;
+    asm volatile("" : "+v"(i));  // keep the load here (not hoisted out of the patch loop)
+    return w2p[i];
+  };
 
   // the next patch's pixels are fetched one patch ahead
   constexpr int PPT = 1024 / (NW * 64);  // patch pixels per thread (2 or 4)
@@ -192,7 +197,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1, NW /
       uint2 hi[4], lo[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const float4 b = *reinterpret_cast<const float4*>(stem_b + 8 * q + 4 * h32);
+        const float4 b = *reinterpret_cast<const float4*>(s_b0 + 8 * q + 4 * h32);
         hi[q] = pack_bf16x4(fmaxf(c0[4 * q] + b.x, 0.f), fmaxf(c0[4 * q + 1] + b.y, 0.f),
                             fmaxf(c0[4 * q + 2] + b.z, 0.f), fmaxf(c0[4 * q + 3] + b.w, 0.f), lo[q]);
       }
@@ -212,111 +217,148 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1, NW /
     }
     __syncthreads();
 
-    // ---- P2: conv1 -> W1 ring (units: new a1 row x pixel half; this wave's G1 groups) --------
-    // band 0: a1 rows -1 (zero padding of conv2) .. 7; band b: 8b .. 8b+7
-    const int y1beg = band == 0 ? -1 : 8 * band, n1 = band == 0 ? 9 : 8;
-#pragma unroll 1
-    for (int u = w / NCH1; u < n1 * 2; u += NW / NCH1) {
-      const int y1 = y1beg + (u >> 1), pxh = u & 1;
-      const int x = 16 * pxh + c16;
-      char* pix = s_w1 + (((y1 + 1) % NA1) * W1C + w1_slot(x)) * PXB;
-      if (y1 < 0) {  // zero padding row of a1
+    // ---- P2: conv1 -> W1 ring (units: new a1 row, both 16-pixel halves; G1 groups) ----------
+    // band b: a1 rows 8b .. 8b+7 (+ row -1, conv2's zero padding, in band 0).  The two halves
+    // are independent accumulator chains interleaved on the MFMA pipe (a single chain of
+    // dependent 16x16x32 MFMAs issues at ~half rate).
+    const int y1beg = 8 * band;
+    if (band == 0 && w < NCH1) {  // zero padding row -1 of a1: this wave's channel groups
+      char* zrow = s_w1 + (0 * W1C) * PXB;
+#pragma unroll
+      for (int hx = 0; hx < 2; ++hx)
 #pragma unroll
         for (int g = 0; g < G1; ++g) {
-          char* dst = pix + 32 * (cs1 * G1 + g) + 8 * g16;
+          char* dst = zrow + w1_slot(16 * hx + c16) * PXB + 32 * (cs1 * G1 + g) + 8 * g16;
           *reinterpret_cast<uint2*>(dst) = make_uint2(0, 0);
           *reinterpret_cast<uint2*>(dst + 64) = make_uint2(0, 0);
         }
-        continue;
-      }
-      f32x4v acc[G1];
+    }
+#pragma unroll 1
+    for (int u = w / NCH1; u < 8; u += NW / NCH1) {
+      const int y1 = y1beg + u;
+      f32x4v acc[2][G1];
 #pragma unroll
-      for (int g = 0; g < G1; ++g) acc[g] = f32x4v{};
-      // the 3 a0 rows y1 - 1 .. y1 + 1 sit in ring slots (y1 + dy) % NA0
+      for (int g = 0; g < G1; ++g) acc[0][g] = acc[1][g] = f32x4v{};
+      // the 3 a0 rows y1 - 1 .. y1 + 1 sit in ring slots (y1 + dy) % NA0; half 1 is 16 columns on
       const char* srow[3];
 #pragma unroll
-      for (int dy = 0; dy < 3; ++dy) srow[dy] = s_w0 + (((y1 + dy) % NA0) * W0C + x) * PXB + 16 * g16;
-      // B fragments one tap ahead of the MFMAs (two register sets); each feeds G1 groups
+      for (int dy = 0; dy < 3; ++dy) srow[dy] = s_w0 + (((y1 + dy) % NA0) * W0C + c16) * PXB + 16 * g16;
+      // steps j = (tap, half): B fragments one step ahead (two register sets); each feeds
+      // the G1 groups, and consecutive steps alternate between the two halves' chains
       uint4 bh[2], bl[2];
-      bh[0] = (ABL & 16) ? make_uint4(lane, 1, 2, 3) : *reinterpret_cast<const uint4*>(srow[0]);
-      bl[0] = (ABL & 16) ? make_uint4(lane, 3, 2, 1) : *reinterpret_cast<const uint4*>(srow[0] + 64);
+      bh[0] = *reinterpret_cast<const uint4*>(srow[0]);
+      bl[0] = *reinterpret_cast<const uint4*>(srow[0] + 64);
 #pragma unroll
-      for (int tap = 0; tap < 9; ++tap) {
-        if (tap + 1 < 9) {
-          const char* p = srow[(tap + 1) / 3] + ((tap + 1) % 3) * PXB;
-          bh[(tap + 1) & 1] = (ABL & 16) ? make_uint4(tap, lane, 2, 3) : *reinterpret_cast<const uint4*>(p);
-          bl[(tap + 1) & 1] = (ABL & 16) ? make_uint4(lane, tap, 2, 1) : *reinterpret_cast<const uint4*>(p + 64);
+      for (int j = 0; j < 18; ++j) {
+        const int tap = j >> 1, hx = j & 1;
+        if (j + 1 < 18) {
+          const int tn = (j + 1) >> 1, hn = (j + 1) & 1;
+          const char* p = srow[tn / 3] + (tn % 3 + 16 * hn) * PXB;
+          bh[(j + 1) & 1] = *reinterpret_cast<const uint4*>(p);
+          bl[(j + 1) & 1] = *reinterpret_cast<const uint4*>(p + 64);
         }
-        __builtin_amdgcn_sched_barrier(0);  // keep the next tap's reads ahead of these MFMAs
+        __builtin_amdgcn_sched_barrier(0);  // keep the next step's reads ahead of these MFMAs
 #pragma unroll
         for (int g = 0; g < G1; ++g) {
           if (ABL & 2) {
-            acc[g][0] += __builtin_bit_cast(float, bh[tap & 1].x ^ bl[tap & 1].y);
+            acc[hx][g][0] += __builtin_bit_cast(float, bh[j & 1].x ^ bl[j & 1].y);
           } else {
-            acc[g] = mfma16(a1w[tap][g][1], bh[tap & 1], acc[g]);
-            acc[g] = mfma16(a1w[tap][g][0], bl[tap & 1], acc[g]);
-            acc[g] = mfma16(a1w[tap][g][0], bh[tap & 1], acc[g]);
+            acc[hx][g] = mfma16(a1w[tap][g][1], bh[j & 1], acc[hx][g]);
+            acc[hx][g] = mfma16(a1w[tap][g][0], bl[j & 1], acc[hx][g]);
+            acc[hx][g] = mfma16(a1w[tap][g][0], bh[j & 1], acc[hx][g]);
           }
         }
       }
+      char* prow = s_w1 + ((y1 + 1) % NA1) * W1C * PXB;
 #pragma unroll
-      for (int g = 0; g < G1; ++g) {
-        const f32x4v r = __builtin_elementwise_max(acc[g] + bias1[g], f32x4v{});
-        // lane (c, g16) holds channels 4g16 .. +3; permlane16_swap (odd rows of vdst <-> even
-        // rows of src) leaves the even row with hi channels 4g16 .. +7 and the odd row with lo
-        // channels 4g16-4 .. +3: one ds_write_b128 per lane instead of two ds_write_b64
-        uint2 lo;
-        uint2 hi = pack_bf16x4(r[0], r[1], r[2], r[3], lo);
-        const auto rx = __builtin_amdgcn_permlane16_swap(hi.x, lo.x, false, false);
-        const auto ry = __builtin_amdgcn_permlane16_swap(hi.y, lo.y, false, false);
-        hi.x = rx[0]; lo.x = rx[1]; hi.y = ry[0]; lo.y = ry[1];
-        char* d16 = pix + 32 * (cs1 * G1 + g) + 16 * (g16 >> 1) + 64 * (g16 & 1);
-        *reinterpret_cast<uint4*>(d16) = make_uint4(hi.x, hi.y, lo.x, lo.y);
+      for (int hx = 0; hx < 2; ++hx) {
+        char* pix = prow + w1_slot(16 * hx + c16) * PXB;
+#pragma unroll
+        for (int g = 0; g < G1; ++g) {
+          const f32x4v bias = *reinterpret_cast<const f32x4v*>(s_b1 + 16 * (cs1 * G1 + g) + 4 * g16);
+          const f32x4v r = __builtin_elementwise_max(acc[hx][g] + bias, f32x4v{});
+          // lane (c, g16) holds channels 4g16 .. +3; permlane16_swap (odd rows of vdst <-> even
+          // rows of src) leaves the even row with hi channels 4g16 .. +7 and the odd row with lo
+          // channels 4g16-4 .. +3: one ds_write_b128 per lane instead of two ds_write_b64
+          uint2 lo;
+          uint2 hi = pack_bf16x4(r[0], r[1], r[2], r[3], lo);
+          const auto rx = __builtin_amdgcn_permlane16_swap(hi.x, lo.x, false, false);
+          const auto ry = __builtin_amdgcn_permlane16_swap(hi.y, lo.y, false, false);
+          hi.x = rx[0]; lo.x = rx[1]; hi.y = ry[0]; lo.y = ry[1];
+          char* d16 = pix + 32 * (cs1 * G1 + g) + 16 * (g16 >> 1) + 64 * (g16 & 1);
+          *reinterpret_cast<uint4*>(d16) = make_uint4(hi.x, hi.y, lo.x, lo.y);
+        }
       }
     }
+    // the first two taps of this wave's conv2 fragments, in flight across the barrier
+    uint4 wq[3][G2][2];
+#pragma unroll
+    for (int tap = 0; tap < 2; ++tap)
+#pragma unroll
+      for (int g = 0; g < G2; ++g)
+#pragma unroll
+        for (int pl = 0; pl < 2; ++pl) wq[tap][g][pl] = w2_frag(tap, g, pl);
     __syncthreads();
 
-    // ---- P3: conv2 (stride 2) -> a2 in HBM (units: output row; this wave's G2 quarters) -------
-#pragma unroll 1
-    for (int oy = w / NCH2; oy < RB2; oy += NW / NCH2) {
-      f32x4v acc[G2];
+    // ---- P3: conv2 (stride 2) -> a2 in HBM (units: output rows oy and oy + 2 together; this
+    // wave's G2 quarters) ----------------------------------------------------------------------
+    static_assert(NW / NCH2 == 2, "two P3 wave sets, each taking rows oy and oy + 2");
+    {
+      const int oy0 = w / NCH2;
+      f32x4v acc[2][G2];
 #pragma unroll
-      for (int g = 0; g < G2; ++g) acc[g] = f32x4v{};
+      for (int g = 0; g < G2; ++g) acc[0][g] = acc[1][g] = f32x4v{};
       // output column c16 reads a1 column 2*c16 - 1 + dx: W1 slot c16 (dx 0), 17 + c16 (dx 1),
-      // c16 + 1 (dx 2); B fragments one tap ahead of the MFMAs
-      // a1 rows 2 (r0 + oy) - 1 + dy sit in ring slots (2 (r0 + oy) + dy) % NA1
-      const char* srow[3];
+      // c16 + 1 (dx 2); a1 rows 2 (r0 + oy) - 1 + dy sit in ring slots (2 (r0 + oy) + dy) % NA1
+      const char* srow[2][3];
 #pragma unroll
-      for (int dy = 0; dy < 3; ++dy)
-        srow[dy] = s_w1 + (((2 * (r0 + oy) + dy) % NA1) * W1C + c16) * PXB + 16 * g16;
+      for (int ry = 0; ry < 2; ++ry)
+#pragma unroll
+        for (int dy = 0; dy < 3; ++dy)
+          srow[ry][dy] = s_w1 + (((2 * (r0 + oy0 + 2 * ry) + dy) % NA1) * W1C + c16) * PXB + 16 * g16;
+      // steps j = (tap, row): B fragments one step ahead; conv2 fragments 2 taps ahead
       uint4 bh[2], bl[2];
-      bh[0] = (ABL & 16) ? make_uint4(lane, 1, 2, 3) : *reinterpret_cast<const uint4*>(srow[0]);
-      bl[0] = (ABL & 16) ? make_uint4(lane, 3, 2, 1) : *reinterpret_cast<const uint4*>(srow[0] + 64);
+      bh[0] = *reinterpret_cast<const uint4*>(srow[0][0]);
+      bl[0] = *reinterpret_cast<const uint4*>(srow[0][0] + 64);
 #pragma unroll
-      for (int tap = 0; tap < 9; ++tap) {
-        if (tap + 1 < 9) {
-          const int dy = (tap + 1) / 3, dx = (tap + 1) % 3;
-          const char* p = srow[dy] + (dx == 1 ? 17 : (dx >> 1)) * PXB;
-          bh[(tap + 1) & 1] = (ABL & 16) ? make_uint4(tap, lane, 2, 3) : *reinterpret_cast<const uint4*>(p);
-          bl[(tap + 1) & 1] = (ABL & 16) ? make_uint4(lane, tap, 2, 1) : *reinterpret_cast<const uint4*>(p + 64);
+      for (int j = 0; j < 18; ++j) {
+        const int tap = j >> 1, ry = j & 1;
+        if (ry == 0 && tap + 2 < 9) {
+#pragma unroll
+          for (int g = 0; g < G2; ++g)
+#pragma unroll
+            for (int pl = 0; pl < 2; ++pl) wq[(tap + 2) % 3][g][pl] = w2_frag(tap + 2, g, pl);
+        }
+        if (j + 1 < 18) {
+          const int tn = (j + 1) >> 1, rn = (j + 1) & 1;
+          const int dy = tn / 3, dx = tn % 3;
+          const char* p = srow[rn][dy] + (dx == 1 ? 17 : (dx >> 1)) * PXB;
+          bh[(j + 1) & 1] = *reinterpret_cast<const uint4*>(p);
+          bl[(j + 1) & 1] = *reinterpret_cast<const uint4*>(p + 64);
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int g = 0; g < G2; ++g) {
           if (ABL & 4) {
-            acc[g][0] += __builtin_bit_cast(float, bh[tap & 1].x ^ bl[tap & 1].y);
+            acc[ry][g][0] += __builtin_bit_cast(float, bh[j & 1].x ^ bl[j & 1].y);
           } else {
-            acc[g] = mfma16(a2w[tap][g][1], bh[tap & 1], acc[g]);
-            acc[g] = mfma16(a2w[tap][g][0], bl[tap & 1], acc[g]);
-            acc[g] = mfma16(a2w[tap][g][0], bh[tap & 1], acc[g]);
+            const uint4* wc = wq[tap % 3][g];
+            acc[ry][g] = mfma16(wc[1], bh[j & 1], acc[ry][g]);
+            acc[ry][g] = mfma16(wc[0], bl[j & 1], acc[ry][g]);
+            acc[ry][g] = mfma16(wc[0], bh[j & 1], acc[ry][g]);
           }
         }
       }
-      float* o = out + ((patch * 16 + r0 + oy) * 16 + c16) * 64 + 4 * g16;
 #pragma unroll
-      for (int g = 0; g < G2; ++g)
-        *reinterpret_cast<f32x4v*>(o + 16 * (cs2 * G2 + g)) =
-            __builtin_elementwise_max(acc[g] + bias2[g], f32x4v{});
+      for (int ry = 0; ry < 2; ++ry) {
+        float* o = out + ((patch * 16 + r0 + oy0 + 2 * ry) * 16 + c16) * 64 + 4 * g16;
+#pragma unroll
+        for (int g = 0; g < G2; ++g)
+          *reinterpret_cast<f32x4v*>(o + 16 * (cs2 * G2 + g)) =
+              __builtin_elementwise_max(
+                  acc[ry][g] + *reinterpret_cast<const f32x4v*>(s_b2 + 16 * (cs2 * G2 + g) + 4 * g16),
+                  f32x4v{});
+      }
     }
     // no barrier: the next band's P1 writes only W0, which P3 does not read; its first
     // barrier orders this P3's W1 reads before the next P2's W1 writes
@@ -352,8 +394,15 @@ hipError_t hn_launch_c12(const float* in, float* out, const HardnetDev& d, int P
                      static_cast<const uint4*>(d.c12_w1), d.bias[1],                              \
                      static_cast<const uint4*>(d.c12_w2), d.bias[2], P, eps)
   if (nw == 8) {
-    if (abl) return hipErrorInvalidValue;  // ablations are built for the 4-wave kernel only (HN_C12_NW=4)
-    HN_C12_GO(0, 8);
+    switch (abl) {
+      case 0: HN_C12_GO(0, 8); break;
+      case 1: HN_C12_GO(1, 8); break;
+      case 2: HN_C12_GO(2, 8); break;
+      case 4: HN_C12_GO(4, 8); break;
+      case 6: HN_C12_GO(6, 8); break;
+      case 8: HN_C12_GO(8, 8); break;
+      default: return hipErrorInvalidValue;
+    }
   } else {
     switch (abl) {
       case 0: HN_C12_GO(0, 4); break;

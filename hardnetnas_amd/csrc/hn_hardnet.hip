@@ -704,6 +704,7 @@ struct WsCfg : ConvCfg<CIN, COUT, HIN, S, NP, TR, WM, WN> {
   static constexpr int BUF = B::LDS;
   static constexpr int PBUF = 34 * 34 * 4;  // one private normalised patch per producer wave
   static constexpr int SMEM = 2 * BUF + (STEM ? NWP * PBUF : 0);
+  static constexpr bool DEEP = !STEM && UPT <= 6;  // two stages of loads in flight
   static_assert(SMEM <= 160 * 1024, "LDS");
 };
 
@@ -711,7 +712,7 @@ struct WsCfg : ConvCfg<CIN, COUT, HIN, S, NP, TR, WM, WN> {
 // normalised patch into their own LDS copy (no cross-wave hand-off) and run conv0 on the
 // MFMA straight into the next window (input_norm + conv0 + BN + ReLU, HardNet.py:281-283,
 // 306-310).
-template <int CIN, int COUT, int HIN, int S, int NP, int TR, int WM, int WN, bool STEM>
+template <int CIN, int COUT, int HIN, int S, int NP, int TR, int WM, int WN, bool STEM, int ABL = 0>
 __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_ws(
     const float* __restrict__ in, float* __restrict__ out, const uint4* __restrict__ wp,
     const float* __restrict__ bias, int P, const float* __restrict__ stem_w,
@@ -742,8 +743,8 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_ws(
   };
   // ---- producer side ----
   const int ptid = tid - C::NWC * 64;
-  float4 pf[C::UPT][2];
-  auto produce_loads = [&](int s) {
+  float4 pf[C::UPT][2], pf2[C::UPT][2];  // two stages in flight (non-STEM)
+  auto produce_loads = [&](int s, float4 (&pf)[C::UPT][2]) {
     int p0, y0;
     tile_of(s, p0, y0);
     const int cc = s % C::NCC;
@@ -764,7 +765,7 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_ws(
       }
     }
   };
-  auto produce_write = [&](char* dst) {
+  auto produce_write = [&](char* dst, const float4 (&pf)[C::UPT][2]) {
 #pragma unroll
     for (int k = 0; k < C::UPT; ++k) {
       const int u = ptid + k * C::PTHR;
@@ -881,25 +882,49 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_ws(
       stem_loads(0);
       stem_write(0, buf0);
     } else {
-      produce_loads(0);
-      produce_write(buf0);
+      produce_loads(0, pf);
+      produce_write(buf0, pf);
+      if (NS > 1) produce_loads(1, pf);
     }
   }
   __syncthreads();
 
   if (producer) {
+    if constexpr ((ABL & 32) != 0) {  // timing only: no barriers at all
+    } else if constexpr ((ABL & 8) != 0) {  // timing only: idle producers
 #pragma unroll 1
-    for (int s = 0; s < NS; ++s) {
-      if (s + 1 < NS) {
-        if constexpr (STEM) {
+      for (int s = 0; s < NS; ++s) __syncthreads();
+    } else if constexpr (STEM) {
+#pragma unroll 1
+      for (int s = 0; s < NS; ++s) {
+        if (s + 1 < NS) {
           stem_loads(s + 1);
           stem_write(s + 1, (s & 1) ? buf0 : buf1);
-        } else {
-          produce_loads(s + 1);
-          produce_write((s & 1) ? buf0 : buf1);
         }
+        __syncthreads();
       }
-      __syncthreads();
+    } else if constexpr (!C::DEEP) {
+#pragma unroll 1
+      for (int s = 0; s < NS; ++s) {
+        if (s + 1 < NS) {
+          produce_write((s & 1) ? buf0 : buf1, pf);
+          if (s + 2 < NS) produce_loads(s + 2, pf);
+        }
+        __syncthreads();
+      }
+    } else {
+      // stage s + 2's loads are issued before stage s + 1 is written, so each load has two
+      // stages of MFMA work to land in
+#pragma unroll 1
+      for (int s = 0; s < NS; s += 2) {
+        if (s + 2 < NS) produce_loads(s + 2, pf2);
+        if (s + 1 < NS) produce_write(buf1, pf);
+        __syncthreads();
+        if (s + 1 >= NS) break;
+        if (s + 3 < NS) produce_loads(s + 3, pf);
+        if (s + 2 < NS) produce_write(buf0, pf2);
+        __syncthreads();
+      }
     }
     return;
   }
@@ -923,24 +948,30 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_ws(
 #pragma unroll
     for (int nt = 0; nt < C::NT; ++nt) acc[mt][nt] = f32x16{};
 
+  constexpr int NKS = 18;
+  static_assert(NKS % 3 == 0, "the weight ring runs on across stages");
+  // weight fragments of K-step k of channel chunk cc; a stage's first two K-steps are
+  // fetched during the previous stage's last two, i.e. before its epilogue stores, which
+  // would otherwise sit in front of them in the in-order vmcnt queue
+  auto load_b = [&](int cc, int ksx, uint4 (&dst)[C::NT][2]) {
+#pragma unroll
+    for (int nt = 0; nt < C::NT; ++nt) {
+      const unsigned k = cc * CHUNK_BYTES +
+                         (((ABL & 1) ? 0 : ksx) * C::NTOT + nt) * 2 * 64 * 16;  // ABL 1: timing only
+      dst[nt][0] = buf_load16(wr_, wvoff, k);
+      dst[nt][1] = buf_load16(wr_, wvoff, k + 64 * 16);
+    }
+  };
+  uint4 bq[3][C::NT][2];
+  load_b(0, 0, bq[0]);
+  load_b(0, 1, bq[1]);
 #pragma unroll 1
   for (int s = 0; s < NS; ++s) {
     const char* cur = (s & 1) ? buf1 : buf0;
-    const int cc = s % C::NCC;
-    const unsigned wsoff = cc * CHUNK_BYTES;
-    constexpr int NKS = 18;
-    uint4 bq[3][C::NT][2];
+    const int cc = s % C::NCC, ccn = (s + 1) % C::NCC;
     uint4 aq[2][C::MT][2];
-    auto load_b = [&](int ksx, uint4 (&dst)[C::NT][2]) {
-#pragma unroll
-      for (int nt = 0; nt < C::NT; ++nt) {
-        const unsigned k = ((ksx * C::NTOT + nt) * 2) * 64 * 16;
-        dst[nt][0] = buf_load16(wr_, wvoff, wsoff + k);
-        dst[nt][1] = buf_load16(wr_, wvoff, wsoff + k + 64 * 16);
-      }
-    };
     auto load_a = [&](int ksx, uint4 (&dst)[C::MT][2]) {
-      const int tap = ksx >> 1, ks = ksx & 1;
+      const int tap = (ABL & 2) ? 0 : ksx >> 1, ks = (ABL & 2) ? 0 : ksx & 1;  // ABL 2: timing only
       const int toff = (tap / 3) * C::RS + C::colofs(tap % 3) * 80 + ks * 32;
 #pragma unroll
       for (int mt = 0; mt < C::MT; ++mt) {
@@ -948,21 +979,27 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_ws(
         dst[mt][1] = *reinterpret_cast<const uint4*>(cur + C::PLANE + abase[mt] + toff);
       }
     };
-    load_b(0, bq[0]);
-    load_b(1, bq[1]);
     load_a(0, aq[0]);
 #pragma unroll
     for (int ksx = 0; ksx < NKS; ++ksx) {
-      if (ksx + 2 < NKS) load_b(ksx + 2, bq[(ksx + 2) % 3]);
+      if (ksx + 2 < NKS)
+        load_b(cc, ksx + 2, bq[(ksx + 2) % 3]);
+      else if (s + 1 < NS)
+        load_b(ccn, ksx + 2 - NKS, bq[(ksx + 2) % 3]);
       if (ksx + 1 < NKS) load_a(ksx + 1, aq[(ksx + 1) & 1]);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int mt = 0; mt < C::MT; ++mt) {
         const bf16x8 xh = as_bf16x8(aq[ksx & 1][mt][0]), xl = as_bf16x8(aq[ksx & 1][mt][1]);
 #pragma unroll
-        for (int nt = 0; nt < C::NT; ++nt)
-          acc[mt][nt] = mfma3(as_bf16x8(bq[ksx % 3][nt][0]), as_bf16x8(bq[ksx % 3][nt][1]), xh, xl,
-                              acc[mt][nt]);
+        for (int nt = 0; nt < C::NT; ++nt) {
+          if constexpr (ABL & 16)  // timing only: no MFMA, operands kept live
+            acc[mt][nt][0] += __builtin_bit_cast(float, aq[ksx & 1][mt][0].x ^ aq[ksx & 1][mt][1].y ^
+                                                           bq[ksx % 3][nt][0].z ^ bq[ksx % 3][nt][1].w);
+          else
+            acc[mt][nt] = mfma3(as_bf16x8(bq[ksx % 3][nt][0]), as_bf16x8(bq[ksx % 3][nt][1]), xh,
+                                xl, acc[mt][nt]);
+        }
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -988,14 +1025,15 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_ws(
               v.y = fmaxf(acc[mt][nt][4 * q + 1] + bv[q].y, 0.f);
               v.z = fmaxf(acc[mt][nt][4 * q + 2] + bv[q].z, 0.f);
               v.w = fmaxf(acc[mt][nt][4 * q + 3] + bv[q].w, 0.f);
-              *reinterpret_cast<float4*>(obase + (size_t)mt * 32 * COUT + nt * 32 + 8 * q) = v;
+              if (!(ABL & 4) || v.x == 1234.5f)  // ABL 4: timing only, no stores
+                *reinterpret_cast<float4*>(obase + (size_t)mt * 32 * COUT + nt * 32 + 8 * q) = v;
             }
           }
           acc[mt][nt] = f32x16{};
         }
       }
     }
-    __syncthreads();
+    if constexpr (!(ABL & 32)) __syncthreads();
   }
 }
 
@@ -1269,13 +1307,14 @@ HN_PIPE_A(pipe3_a4, false, 64, 64, 16, 1, 1, 8, 2, 2, 4)
 HN_PIPE_A(pipe3_a7, false, 64, 64, 16, 1, 1, 8, 2, 2, 7)
 
 #define HN_WS(NAME, CIN, COUT, HIN, S, NP, TR, WM, WN) HN_WS_S(NAME, false, CIN, COUT, HIN, S, NP, TR, WM, WN)
-#define HN_WS_S(NAME, STEM, CIN, COUT, HIN, S, NP, TR, WM, WN)                             \
+#define HN_WS_S(NAME, STEM, CIN, COUT, HIN, S, NP, TR, WM, WN) HN_WS_A(NAME, STEM, CIN, COUT, HIN, S, NP, TR, WM, WN, 0)
+#define HN_WS_A(NAME, STEM, CIN, COUT, HIN, S, NP, TR, WM, WN, ABL)                      \
   using NAME##_cfg = WsCfg<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM>;                       \
   static hipError_t NAME(const float* in, float* out, const void* wp, const float* bias,   \
                          int P, const float* sw, const float* sb, float eps, hipStream_t st) { \
     constexpr int lds = NAME##_cfg::SMEM;                                                  \
     const void* fn =                                                                       \
-        reinterpret_cast<const void*>(&k_conv_ws<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM>); \
+        reinterpret_cast<const void*>(&k_conv_ws<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM, ABL>); \
     static int resident = 0;                                                               \
     if (!resident) {                                                                       \
       hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds); \
@@ -1289,7 +1328,7 @@ HN_PIPE_A(pipe3_a7, false, 64, 64, 16, 1, 1, 8, 2, 2, 7)
     }                                                                                      \
     const int tiles = (P + NP - 1) / NP * NAME##_cfg::RT;                                  \
     const int grid = std::min(tiles, resident);                                            \
-    hipLaunchKernelGGL((k_conv_ws<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM>), dim3(grid),   \
+    hipLaunchKernelGGL((k_conv_ws<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM, ABL>), dim3(grid),   \
                        dim3(NAME##_cfg::NTHR), lds, st, in, out,                           \
                        static_cast<const uint4*>(wp), bias, P, sw, sb, eps);               \
     return hipGetLastError();                                                              \
@@ -1305,6 +1344,20 @@ HN_WS(ws4, 64, 128, 16, 2, 1, 4, 1, 4)
 HN_WS(ws4_t8, 64, 128, 16, 2, 1, 8, 1, 4)
 HN_WS(ws5, 128, 128, 8, 1, 1, 8, 1, 4)
 HN_WS(ws5_np2, 128, 128, 8, 1, 2, 8, 1, 4)
+// wider N tiles (fewer A-fragment reads, weights shared through L1)
+HN_WS(ws3_w8, 64, 64, 16, 1, 1, 16, 4, 1)
+HN_WS(ws4_w8, 64, 128, 16, 2, 1, 8, 2, 2)
+HN_WS(ws5_w8, 128, 128, 8, 1, 2, 8, 2, 2)
+// ablation builds (timing only, wrong results): weights fetched once per stage
+HN_WS_A(ws3_a1, false, 64, 64, 16, 1, 1, 16, 2, 2, 45)
+HN_WS_A(ws4_a1, false, 64, 128, 16, 2, 1, 8, 1, 4, 45)
+HN_WS_A(ws5_a1, false, 128, 128, 8, 1, 2, 8, 1, 4, 45)
+HN_WS_A(ws3_a2, false, 64, 64, 16, 1, 1, 16, 2, 2, 8)
+HN_WS_A(ws4_a2, false, 64, 128, 16, 2, 1, 8, 1, 4, 8)
+HN_WS_A(ws5_a2, false, 128, 128, 8, 1, 2, 8, 1, 4, 8)
+HN_WS_A(ws3_a3, false, 64, 64, 16, 1, 1, 16, 2, 2, 40)
+HN_WS_A(ws4_a3, false, 64, 128, 16, 2, 1, 8, 1, 4, 40)
+HN_WS_A(ws5_a3, false, 128, 128, 8, 1, 2, 8, 1, 4, 40)
 
 hipError_t hn_launch_stem(const float* in, float* out, const float* w, const float* b, int P,
                           bool norm, float eps, hipStream_t st) {
@@ -1319,6 +1372,23 @@ hipError_t hn_launch_stem(const float* in, float* out, const float* w, const flo
 hipError_t hn_launch_hardnet_conv(int layer, int variant, const HardnetDev& d, const float* in,
                                   float* out, int P, float eps, hipStream_t st) {
   const bool v1 = variant == 1;
+  if (variant == 8 || variant == 9 || variant == 4) {  // ablation (timing only)
+    const int a = variant == 8 ? 1 : variant == 9 ? 2 : 3;
+    switch (layer) {
+      case 3: return (a == 1 ? ws3_a1 : a == 2 ? ws3_a2 : ws3_a3)(in, out, d.wpack[3], d.bias[3], P, nullptr, nullptr, 0.f, st);
+      case 4: return (a == 1 ? ws4_a1 : a == 2 ? ws4_a2 : ws4_a3)(in, out, d.wpack[4], d.bias[4], P, nullptr, nullptr, 0.f, st);
+      case 5: return (a == 1 ? ws5_a1 : a == 2 ? ws5_a2 : ws5_a3)(in, out, d.wpack[5], d.bias[5], P, nullptr, nullptr, 0.f, st);
+    }
+    return hipErrorInvalidValue;
+  }
+  if (variant == 7) {  // warp-specialised, NT = 2
+    switch (layer) {
+      case 3: return ws3_w8(in, out, d.wpack[3], d.bias[3], P, nullptr, nullptr, 0.f, st);
+      case 4: return ws4_w8(in, out, d.wpack[4], d.bias[4], P, nullptr, nullptr, 0.f, st);
+      case 5: return ws5_w8(in, out, d.wpack[5], d.bias[5], P, nullptr, nullptr, 0.f, st);
+    }
+    return hipErrorInvalidValue;
+  }
   if (variant == 5 || variant == 6) {  // warp-specialised: 5 = smaller tile, 6 = larger
     const bool big = variant == 6;
     switch (layer) {
