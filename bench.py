@@ -159,13 +159,15 @@ def cpu_baseline(name: str, model, seconds: float = 12.0):
                       f"{len(rates)} batches (~{seconds:.0f} s), {threads} threads, median"}
 
 
-def read_traffic(name: str, stage: str):
+def read_traffic(name: str, stage: str, patches_per_launch: float):
+    """PMC-measured HBM bytes per launch of `stage` (profiles/pmc_traffic_<name>.json holds
+    bytes per patch from tools/pmc.sh + tools/pmc_traffic.py), or None."""
     f = os.path.join(ROOT, "profiles", f"pmc_traffic_{name}.json")
     if not os.path.exists(f):
         return None
     try:
-        d = json.load(open(f))
-        return d.get(stage)
+        e = json.load(open(f)).get(stage)
+        return int(e["bytes_per_patch"] * patches_per_launch) if e else None
     except Exception:
         return None
 
@@ -254,7 +256,7 @@ def main():
             alg = per_patch * b / launches_per_step
             bound, peak, unit = "hbm", PEAK_HBM, "GB/s"
             achieved = per_patch * b * args.steps / (dom_ms * 1e-3) / 1e9
-        traffic = read_traffic(args.model, dom)
+        traffic = read_traffic(args.model, dom, b / launches_per_step)
         roof = {"bound": bound, "kernel": dom,
                 "achieved": round(achieved, 2) if achieved is not None else None,
                 "peak": round(peak, 1), "unit": unit,

@@ -4,7 +4,9 @@ launch per bench stage -> profiles/pmc_traffic_<model>.json (read by bench.py).
 gfx950 correction (MI355X_MICROARCH.md, HBM): FETCH_SIZE reports exactly half of the bytes
 of a wide coalesced streaming read, so read bytes = 2 * FETCH_SIZE * 1024; WRITE_SIZE is
 exact for 16-B-per-lane streaming stores: write bytes = WRITE_SIZE * 1024.
-usage: python tools/pmc_traffic.py <pmc dir> <model> [out.json]
+usage: python tools/pmc_traffic.py <pmc dir> <model> <patches processed in the profiled run> [out.json]
+Output per stage: HBM bytes per patch (read + write, summed over every launch of the stage), so
+bench.py can scale it to its own launch size.
 """
 import csv
 import glob
@@ -37,8 +39,8 @@ def stage_of(name: str):
 
 
 def main():
-    d, model = sys.argv[1], sys.argv[2]
-    out = sys.argv[3] if len(sys.argv) > 3 else os.path.join("profiles", f"pmc_traffic_{model}.json")
+    d, model, patches = sys.argv[1], sys.argv[2], int(sys.argv[3])
+    out = sys.argv[4] if len(sys.argv) > 4 else os.path.join("profiles", f"pmc_traffic_{model}.json")
     tot = defaultdict(lambda: defaultdict(float))
     cnt = defaultdict(lambda: defaultdict(set))
     for f in glob.glob(os.path.join(d, "p*", "run_counter_collection.csv")):
@@ -49,15 +51,15 @@ def main():
             c = r["Counter_Name"]
             tot[st][c] += float(r["Counter_Value"])
             cnt[st][c].add(r["Dispatch_Id"])
-    res = {}
+    res = {"patches_profiled": patches}
     for st, cs in tot.items():
         if "FETCH_SIZE" in cs and "WRITE_SIZE" in cs:
-            nf, nw = len(cnt[st]["FETCH_SIZE"]), len(cnt[st]["WRITE_SIZE"])
-            rd = 2 * cs["FETCH_SIZE"] * 1024 / nf
-            wr = cs["WRITE_SIZE"] * 1024 / nw
-            res[st] = int(rd + wr)
-            res[st + ".detail"] = {"read_bytes_per_launch": int(rd), "write_bytes_per_launch": int(wr),
-                                   "launches": nf, "fetch_correction": 2.0}
+            rd = 2 * cs["FETCH_SIZE"] * 1024
+            wr = cs["WRITE_SIZE"] * 1024
+            res[st] = {"bytes_per_patch": round((rd + wr) / patches, 1),
+                       "read_bytes_per_patch": round(rd / patches, 1),
+                       "write_bytes_per_patch": round(wr / patches, 1),
+                       "dispatches": len(cnt[st]["FETCH_SIZE"]), "fetch_correction": 2.0}
     json.dump(res, open(out, "w"), indent=1, sort_keys=True)
     print(json.dumps(res, indent=1, sort_keys=True))
 
