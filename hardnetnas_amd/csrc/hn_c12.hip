@@ -27,13 +27,16 @@ namespace {
 
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 
-constexpr int RB2 = 4;                  // conv2 output rows per band
-constexpr int NA0 = 2 * RB2 + 2;        // a0 ring rows (10): a band's conv1 reads 10 a0 rows
-constexpr int NA1 = 2 * RB2 + 1;        // a1 ring rows (9): a band's conv2 reads 9 a1 rows
 constexpr int PXB = 160;                // bytes per pixel in W0 / W1
 constexpr int W0C = 34, W1C = 33;       // columns (x = -1 .. 32 / -1 .. 31)
-constexpr int W0B = NA0 * W0C * PXB;    // 59,840
-constexpr int W1B = NA1 * W1C * PXB;    // 47,520
+// ring geometry for RB2 conv2 output rows per band
+template <int RB2>
+struct C12Ring {
+  static constexpr int NA0 = 2 * RB2 + 2;      // a0 ring rows: a band's conv1 reads 2 RB2 + 2 a0 rows
+  static constexpr int NA1 = 2 * RB2 + 1;      // a1 ring rows: a band's conv2 reads 2 RB2 + 1 a1 rows
+  static constexpr int W0B = NA0 * W0C * PXB;  // RB2 4: 59,840   RB2 2: 32,640
+  static constexpr int W1B = NA1 * W1C * PXB;  // RB2 4: 47,520   RB2 2: 26,400
+};
 
 HN_DEV f32x4v mfma16(const uint4& a, const uint4& b, f32x4v c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a), as_bf16x8(b), c, 0, 0, 0);
@@ -56,22 +59,31 @@ HN_DEV int w1_slot(int x) { return ((x + 1) & 1) ? 17 + (x >> 1) : (x + 1) >> 1;
 // bit 4 skips the P2/P3 B-fragment LDS reads; bit 0 skips P1's MFMA work,
 // bit 1 skips P2's, bit 2 skips P3's (the phases still run their LDS traffic and barriers).
 //
-// NW = 8: two waves per SIMD, each wave holds one conv1 16-channel group and one conv2
-//         group (144 VGPRs of weights).
-// NW = 4: one wave per SIMD with the 512-register file: each wave holds both conv1 groups and
-//         two conv2 groups (288 registers of weights), so every B fragment read from LDS feeds
-//         two output groups (half the LDS reads per MFMA).
-template <int ABL, int NW>
-__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1, NW / 4))) void k_c12(
+// Every wave holds both conv1 16-channel groups (144 VGPRs of weights), so each P2 B fragment
+// feeds two output groups.  Configurations (NW waves, RB2 rows per band, WPE waves per SIMD):
+//   <8, 4, 2>: one workgroup per CU (107 KB of rings), two waves per SIMD;
+//   <4, 4, 1>: one workgroup per CU, one wave per SIMD (512-register file);
+//   <4, 2, 2>: two workgroups per CU (59 KB of rings each) with independent barriers, so one
+//              workgroup's MFMA phases run while the other waits at a barrier.
+// P3I: P3 walks taps, each with both output rows' B fragments (one tap ahead) and the two rows'
+// accumulator chains interleaved MFMA by MFMA; conv2 fragments WA taps ahead (P3I = 0: steps
+// of one (tap, row), fragments 2 taps ahead).
+template <int ABL, int NW, int RB2, int WPE, bool P3I = false, int WA = 2>
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void k_c12(
     const float* __restrict__ in, float* __restrict__ out, const float* __restrict__ stem_w,
     const float* __restrict__ stem_b, const uint4* __restrict__ w1p, const float* __restrict__ b1,
     const uint4* __restrict__ w2p, const float* __restrict__ b2, int P, float eps) {
+  constexpr int NA0 = C12Ring<RB2>::NA0, NA1 = C12Ring<RB2>::NA1;
+  constexpr int W0B = C12Ring<RB2>::W0B, W1B = C12Ring<RB2>::W1B;
   __shared__ __attribute__((aligned(16))) char s_w0[W0B];
   __shared__ __attribute__((aligned(16))) char s_w1[W1B];
   __shared__ float s_in[34 * 34];
   __shared__ float red[2 * NW];
-  constexpr int G1 = 2, G2 = 8 / NW;          // conv1 / conv2 output groups per wave
-  constexpr int NCH1 = 2 / G1, NCH2 = 4 / G2;  // waves sharing a P2 unit / a P3 row
+  // P3: RB2 / 2 wave sets, each taking two output rows (set s: rows s and s + RB2 / 2); the
+  // NCH2 waves of a set split the 4 16-channel quarters, G2 each
+  constexpr int NSET = RB2 / 2, NCH2 = NW / NSET, G2 = 4 / NCH2;
+  constexpr int G1 = 2, NCH1 = 2 / G1;  // conv1 output groups per wave / waves sharing a P2 unit
+  static_assert(NSET * NCH2 == NW && G2 * NCH2 == 4, "P3 work split");
 
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -91,13 +103,19 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1, NW /
   for (int i = t; i < 34 * 34; i += NW * 64) s_in[i] = 0.f;
 
   // stem A operand (32x32x16): lane (channel r32, taps 8*h32 ..), bf16 hi/lo
-  bf16x8 sah, sal;
+  // (kept in LDS, [lane][hi|lo], read once per P1 row: frees 8 VGPRs for the P3 pipeline)
+  __shared__ __attribute__((aligned(16))) uint4 s_stem[64][2];
+  if (t < 64) {
+    bf16x8 sah, sal;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int tap = 8 * h32 + j;
-    const float v = tap < 9 ? stem_w[tap * 32 + r32] : 0.f;
-    sah[j] = (__bf16)v;
-    sal[j] = (__bf16)(v - (float)sah[j]);
+    for (int j = 0; j < 8; ++j) {
+      const int tap = 8 * h32 + j;
+      const float v = tap < 9 ? stem_w[tap * 32 + r32] : 0.f;
+      sah[j] = (__bf16)v;
+      sal[j] = (__bf16)(v - (float)sah[j]);
+    }
+    s_stem[lane][0] = __builtin_bit_cast(uint4, sah);
+    s_stem[lane][1] = __builtin_bit_cast(uint4, sal);
   }
   // conv1 / conv2 A operands resident in registers: [tap][group][plane]
   const int cs1 = w % NCH1, cs2 = w % NCH2;
@@ -168,11 +186,11 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1, NW /
       __syncthreads();
     }
 #pragma unroll 1
-  for (int band = 0; band < 4; ++band) {
+  for (int band = 0; band < 16 / RB2; ++band) {
     const int r0 = band * RB2;
     // ---- P1: the band's new a0 rows -> W0 ring (slot (y + 1) % NA0) ------------------------
     // band 0: rows -1 .. 8 (row -1 is conv1's zero padding); band b: rows 8b+1 .. 8b+8
-    const int ybeg = band == 0 ? -1 : 8 * band + 1, nrows = band == 0 ? 10 : 8;
+    const int ybeg = band == 0 ? -1 : 2 * RB2 * band + 1, nrows = band == 0 ? 2 * RB2 + 2 : 2 * RB2;
 #pragma unroll 1
     for (int ri = w; ri < ((ABL & 8) ? 0 : nrows); ri += NW) {
       const int y = ybeg + ri;  // a0 row
@@ -190,7 +208,9 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1, NW /
         xh[j] = (__bf16)v;
         xl[j] = (__bf16)(v - (float)xh[j]);
       }
-      const f32x16 c0 = (ABL & 1) ? f32x16{} : mfma3(sah, sal, xh, xl, f32x16{});
+      const f32x16 c0 = (ABL & 1) ? f32x16{}
+                                  : mfma3(as_bf16x8(s_stem[lane][0]), as_bf16x8(s_stem[lane][1]), xh, xl,
+                                          f32x16{});
       // lane (px, h) holds channels 8q + 4h .. +3; permlane32_swap pairs (q, q+1) so that
       // lanes 0-31 hold channels 8q .. 8q+7 and lanes 32-63 channels 8q+8 .. 8q+15 of the
       // same pixel (T21): 4 ds_write_b128 instead of 8 ds_write_b64
@@ -218,10 +238,10 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1, NW /
     __syncthreads();
 
     // ---- P2: conv1 -> W1 ring (units: new a1 row, both 16-pixel halves; G1 groups) ----------
-    // band b: a1 rows 8b .. 8b+7 (+ row -1, conv2's zero padding, in band 0).  The two halves
+    // band b: a1 rows 2 RB2 b .. + 2 RB2 - 1 (+ row -1, conv2's zero padding, in band 0).  The two halves
     // are independent accumulator chains interleaved on the MFMA pipe (a single chain of
     // dependent 16x16x32 MFMAs issues at ~half rate).
-    const int y1beg = 8 * band;
+    const int y1beg = 2 * RB2 * band;
     if (band == 0 && w < NCH1) {  // zero padding row -1 of a1: this wave's channel groups
       char* zrow = s_w1 + (0 * W1C) * PXB;
 #pragma unroll
@@ -234,7 +254,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1, NW /
         }
     }
 #pragma unroll 1
-    for (int u = w / NCH1; u < 8; u += NW / NCH1) {
+    for (int u = w / NCH1; u < 2 * RB2; u += NW / NCH1) {
       const int y1 = y1beg + u;
       f32x4v acc[2][G1];
 #pragma unroll
@@ -290,10 +310,10 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1, NW /
         }
       }
     }
-    // the first two taps of this wave's conv2 fragments, in flight across the barrier
-    uint4 wq[3][G2][2];
+    // the first WA taps of this wave's conv2 fragments, in flight across the barrier
+    uint4 wq[WA + 1][G2][2];
 #pragma unroll
-    for (int tap = 0; tap < 2; ++tap)
+    for (int tap = 0; tap < WA; ++tap)
 #pragma unroll
       for (int g = 0; g < G2; ++g)
 #pragma unroll
@@ -302,9 +322,8 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1, NW /
 
     // ---- P3: conv2 (stride 2) -> a2 in HBM (units: output rows oy and oy + 2 together; this
     // wave's G2 quarters) ----------------------------------------------------------------------
-    static_assert(NW / NCH2 == 2, "two P3 wave sets, each taking rows oy and oy + 2");
     {
-      const int oy0 = w / NCH2;
+      const int oy0 = w / NCH2;  // rows oy0 and oy0 + NSET
       f32x4v acc[2][G2];
 #pragma unroll
       for (int g = 0; g < G2; ++g) acc[0][g] = acc[1][g] = f32x4v{};
@@ -315,7 +334,48 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1, NW /
       for (int ry = 0; ry < 2; ++ry)
 #pragma unroll
         for (int dy = 0; dy < 3; ++dy)
-          srow[ry][dy] = s_w1 + (((2 * (r0 + oy0 + 2 * ry) + dy) % NA1) * W1C + c16) * PXB + 16 * g16;
+          srow[ry][dy] = s_w1 + (((2 * (r0 + oy0 + NSET * ry) + dy) % NA1) * W1C + c16) * PXB + 16 * g16;
+      if constexpr (P3I) {
+        // taps: both rows' B fragments one tap ahead; conv2 fragments WA taps ahead
+        auto bptr = [&](int tn, int rn) {
+          const int dy = tn / 3, dx = tn % 3;
+          return srow[rn][dy] + (dx == 1 ? 17 : (dx >> 1)) * PXB;
+        };
+        uint4 bf[2][2][2];  // [buffer][row][plane]
+#pragma unroll
+        for (int rn = 0; rn < 2; ++rn) {
+          bf[0][rn][0] = *reinterpret_cast<const uint4*>(bptr(0, rn));
+          bf[0][rn][1] = *reinterpret_cast<const uint4*>(bptr(0, rn) + 64);
+        }
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) {
+          if (tap + WA < 9) {
+#pragma unroll
+            for (int g = 0; g < G2; ++g)
+#pragma unroll
+              for (int pl = 0; pl < 2; ++pl) wq[(tap + WA) % (WA + 1)][g][pl] = w2_frag(tap + WA, g, pl);
+          }
+          if (tap + 1 < 9) {
+#pragma unroll
+            for (int rn = 0; rn < 2; ++rn) {
+              bf[(tap + 1) & 1][rn][0] = *reinterpret_cast<const uint4*>(bptr(tap + 1, rn));
+              bf[(tap + 1) & 1][rn][1] = *reinterpret_cast<const uint4*>(bptr(tap + 1, rn) + 64);
+            }
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          const uint4(&b)[2][2] = bf[tap & 1];
+#pragma unroll
+          for (int g = 0; g < G2; ++g) {
+            const uint4* wc = wq[tap % (WA + 1)][g];
+            acc[0][g] = mfma16(wc[1], b[0][0], acc[0][g]);
+            acc[1][g] = mfma16(wc[1], b[1][0], acc[1][g]);
+            acc[0][g] = mfma16(wc[0], b[0][1], acc[0][g]);
+            acc[1][g] = mfma16(wc[0], b[1][1], acc[1][g]);
+            acc[0][g] = mfma16(wc[0], b[0][0], acc[0][g]);
+            acc[1][g] = mfma16(wc[0], b[1][0], acc[1][g]);
+          }
+        }
+      } else {
       // steps j = (tap, row): B fragments one step ahead; conv2 fragments 2 taps ahead
       uint4 bh[2], bl[2];
       bh[0] = *reinterpret_cast<const uint4*>(srow[0][0]);
@@ -323,11 +383,11 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1, NW /
 #pragma unroll
       for (int j = 0; j < 18; ++j) {
         const int tap = j >> 1, ry = j & 1;
-        if (ry == 0 && tap + 2 < 9) {
+        if (ry == 0 && tap + WA < 9) {
 #pragma unroll
           for (int g = 0; g < G2; ++g)
 #pragma unroll
-            for (int pl = 0; pl < 2; ++pl) wq[(tap + 2) % 3][g][pl] = w2_frag(tap + 2, g, pl);
+            for (int pl = 0; pl < 2; ++pl) wq[(tap + WA) % (WA + 1)][g][pl] = w2_frag(tap + WA, g, pl);
         }
         if (j + 1 < 18) {
           const int tn = (j + 1) >> 1, rn = (j + 1) & 1;
@@ -342,16 +402,17 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1, NW /
           if (ABL & 4) {
             acc[ry][g][0] += __builtin_bit_cast(float, bh[j & 1].x ^ bl[j & 1].y);
           } else {
-            const uint4* wc = wq[tap % 3][g];
+            const uint4* wc = wq[tap % (WA + 1)][g];
             acc[ry][g] = mfma16(wc[1], bh[j & 1], acc[ry][g]);
             acc[ry][g] = mfma16(wc[0], bl[j & 1], acc[ry][g]);
             acc[ry][g] = mfma16(wc[0], bh[j & 1], acc[ry][g]);
           }
         }
       }
+      }
 #pragma unroll
       for (int ry = 0; ry < 2; ++ry) {
-        float* o = out + ((patch * 16 + r0 + oy0 + 2 * ry) * 16 + c16) * 64 + 4 * g16;
+        float* o = out + ((patch * 16 + r0 + oy0 + NSET * ry) * 16 + c16) * 64 + 4 * g16;
 #pragma unroll
         for (int g = 0; g < G2; ++g)
           *reinterpret_cast<f32x4v*>(o + 16 * (cs2 * G2 + g)) =
@@ -368,48 +429,72 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1, NW /
 
 }  // namespace
 
+// HN_C12_CFG variants (A/B and ablation builds; 0 is production):
+//   0 <8 waves, 4-row bands, 2 waves/SIMD>   1 <4, 4, 1> (512-register file)
+//   2 <4 waves, 2-row bands, 2 workgroups/CU>
+//   3 / 4: 0 with tap-interleaved P3, conv2 fragments 2 / 3 taps ahead;  5 / 6: the same for 2
+#define HN_C12_CFGS(X)                                                                   \
+  X(0, 8, 4, 2, false, 2) X(1, 4, 4, 1, false, 2) X(2, 4, 2, 2, false, 2)                 \
+  X(3, 8, 4, 2, true, 2) X(4, 8, 4, 2, true, 3) X(5, 4, 2, 2, true, 2) X(6, 4, 2, 2, true, 3)
+constexpr int kC12Cfgs = 7;
+
 hipError_t hn_launch_c12(const float* in, float* out, const HardnetDev& d, int P, float eps,
                          hipStream_t st) {
   if (P <= 0) return hipSuccess;
-  static int abl = -1, nw = 0;
-  if (abl < 0) abl = std::getenv("HN_C12_ABL") ? std::atoi(std::getenv("HN_C12_ABL")) & 31 : 0;
-  // 8 waves (two per SIMD) measured faster than the 4-wave / 512-register build (22.0 vs
-  // 30.4 ms per 262,144 patches); HN_C12_NW=4 selects the latter (ablation builds: 4-wave only)
-  if (!nw) nw = std::getenv("HN_C12_NW") && std::atoi(std::getenv("HN_C12_NW")) == 4 ? 4 : 8;
-  static int resident[2] = {0, 0};
-  const int ri = nw == 8;
-  if (!resident[ri]) {
+  // read per launch (tests switch them between models): HN_C12_ABL ablation bits (cfg 0 and 2)
+  const char* ea = std::getenv("HN_C12_ABL");
+  const int abl = ea ? std::atoi(ea) & 31 : 0;
+  const char* ec = std::getenv("HN_C12_CFG");
+  const int cfg = ec ? std::atoi(ec) : 0;
+  if (cfg < 0 || cfg >= kC12Cfgs) return hipErrorInvalidValue;
+  static int resident[kC12Cfgs] = {};
+  static const void* const fns[kC12Cfgs] = {
+#define HN_C12_FN(C, W, R, E, I, A) reinterpret_cast<const void*>(&k_c12<0, W, R, E, I, A>),
+      HN_C12_CFGS(HN_C12_FN)
+#undef HN_C12_FN
+  };
+  static const int nws[kC12Cfgs] = {
+#define HN_C12_NWS(C, W, R, E, I, A) W,
+      HN_C12_CFGS(HN_C12_NWS)
+#undef HN_C12_NWS
+  };
+  const int nw = nws[cfg];
+  if (!resident[cfg]) {
     int per_cu = 0, dev = 0, cus = 0;
-    const void* fn = nw == 8 ? reinterpret_cast<const void*>(&k_c12<0, 8>)
-                             : reinterpret_cast<const void*>(&k_c12<0, 4>);
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, nw * 64, 0);
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fns[cfg], nw * 64, 0);
     if (e != hipSuccess) return e;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    resident[ri] = std::max(1, per_cu) * std::max(1, cus);
+    resident[cfg] = std::max(1, per_cu) * std::max(1, cus);
   }
-  const int grid = (int)std::min<long>((long)P, resident[ri]);
-#define HN_C12_GO(A, W)                                                                          \
-  hipLaunchKernelGGL((k_c12<A, W>), dim3(grid), dim3(W * 64), 0, st, in, out, d.stem_w, d.stem_b, \
-                     static_cast<const uint4*>(d.c12_w1), d.bias[1],                              \
+  const int grid = (int)std::min<long>((long)P, resident[cfg]);
+#define HN_C12_GO(A, W, R, E, I, WA)                                                             \
+  hipLaunchKernelGGL((k_c12<A, W, R, E, I, WA>), dim3(grid), dim3(W * 64), 0, st, in, out,      \
+                     d.stem_w, d.stem_b, static_cast<const uint4*>(d.c12_w1), d.bias[1],        \
                      static_cast<const uint4*>(d.c12_w2), d.bias[2], P, eps)
-  if (nw == 8) {
-    switch (abl) {
-      case 0: HN_C12_GO(0, 8); break;
-      case 1: HN_C12_GO(1, 8); break;
-      case 2: HN_C12_GO(2, 8); break;
-      case 4: HN_C12_GO(4, 8); break;
-      case 6: HN_C12_GO(6, 8); break;
-      case 8: HN_C12_GO(8, 8); break;
-      default: return hipErrorInvalidValue;
+  if (abl) {
+    if (cfg == 0) {
+      switch (abl) {
+        case 1: HN_C12_GO(1, 8, 4, 2, false, 2); break;
+        case 6: HN_C12_GO(6, 8, 4, 2, false, 2); break;
+        case 8: HN_C12_GO(8, 8, 4, 2, false, 2); break;
+        default: return hipErrorInvalidValue;
+      }
+    } else if (cfg == 2) {
+      switch (abl) {
+        case 6: HN_C12_GO(6, 4, 2, 2, false, 2); break;
+        case 8: HN_C12_GO(8, 4, 2, 2, false, 2); break;
+        default: return hipErrorInvalidValue;
+      }
+    } else {
+      return hipErrorInvalidValue;
     }
   } else {
-    switch (abl) {
-      case 0: HN_C12_GO(0, 4); break;
-      case 7: HN_C12_GO(7, 4); break;
-      case 8: HN_C12_GO(8, 4); break;
-      case 22: HN_C12_GO(22, 4); break;
-      default: HN_C12_GO(31, 4); break;
+    switch (cfg) {
+#define HN_C12_CASE(C, W, R, E, I, A) \
+  case C: HN_C12_GO(0, W, R, E, I, A); break;
+      HN_C12_CFGS(HN_C12_CASE)
+#undef HN_C12_CASE
     }
   }
 #undef HN_C12_GO

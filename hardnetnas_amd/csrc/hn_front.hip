@@ -41,6 +41,13 @@ __constant__ unsigned char kDwLane[64] = {
     22, 23, 30, 31, 38, 39, 36, 37, 44, 45, 52, 53, 54, 55, 58, 59, 60, 61, 62, 63, 24, 25,
     16, 17, 18, 19, 32, 33, 40, 41, 26, 27, 34, 35, 42, 43, 50, 51, 48, 49, 56, 57};
 
+// LDS pw row layout (IRF form): columns c (pad included) split even / odd -- even c at position
+// c / 2, odd c at HALF + c / 2 -- so the dw's stride-2 window reads of consecutive output
+// pixels hit consecutive positions (pixel stride PS = 36 floats = 9 slots: 16 distinct 16-byte
+// slots per ds_read_b128 group), and the row stride is a multiple of 64 floats so the two
+// output rows a 16-lane group mixes see the same slot pattern (tests/test_lds_banks.py).  The
+// maxpool form keeps the plain column order (its lane map kDwLane is built for it).
+//
 // RING (MID = 32 and the maxpool form): the chunk's pw rows live in an LDS ring of IR rows
 // (slot (y + PAD) % IR) that persists across the 4 bands of a patch, so a band computes only
 // its 8 new stem/pw rows.  MID > 32 recomputes the band's halo rows for every chunk.
@@ -64,9 +71,12 @@ __global__ __launch_bounds__(256) void k_front(const float* __restrict__ in,
   constexpr int OC = 32;  // layer-0 output channels (SEARCH_SPACE2[0] = (32, 32, 2))
   constexpr int DYU = KK == 3 ? 3 : 1;  // k5: rolled dy loop keeps VGPRs (and occupancy) in check
   constexpr bool RING = MID == 32;
+  constexpr bool SPLIT = MODE == FRONT_IRF;                  // even/odd column split
+  constexpr int HALF = (PC + 1) / 2;                         // first odd-column position
+  constexpr int RS = SPLIT ? (PC * PS + 63) / 64 * 64 : PC * PS;  // row stride (floats)
   static_assert(IR >= 8, "ring holds a band's 8 new rows");
   __shared__ float s_in[34 * 34];
-  __shared__ __attribute__((aligned(16))) float s_pw[IR * PC * PS];
+  __shared__ __attribute__((aligned(16))) float s_pw[IR * RS];
   __shared__ __attribute__((aligned(16))) float s_dw[KK * KK * 32 + 32];
   __shared__ float red[8];
 
@@ -78,11 +88,13 @@ __global__ __launch_bounds__(256) void k_front(const float* __restrict__ in,
   const long pe = min((long)P, pb + per);
   if (pb >= pe) return;  // workgroup-uniform
 
+  // position of padded column c in a pw row
+  auto colpos = [](int c) { return SPLIT ? ((c & 1) ? HALF + (c >> 1) : c >> 1) : c; };
   // ---- one-time init: zero s_in (its frame stays zero) and the pw pad columns ---------------
   for (int i = t; i < 34 * 34; i += 256) s_in[i] = 0.f;
   for (int i = t; i < IR * 2 * PAD * (PS / 4); i += 256) {  // left/right pad columns
     const int ri = i / (2 * PAD * (PS / 4)), rem = i % (2 * PAD * (PS / 4)), c = rem / (PS / 4);
-    reinterpret_cast<float4*>(s_pw)[(ri * PC + (c < PAD ? c : 32 + c)) * (PS / 4) + rem % (PS / 4)] =
+    reinterpret_cast<float4*>(s_pw)[(ri * RS + colpos(c < PAD ? c : 32 + c) * PS) / 4 + rem % (PS / 4)] =
         make_float4(0.f, 0.f, 0.f, 0.f);
   }
   const f16x8 sah = as_f16x8(spack[lane]), sal = as_f16x8(spack[64 + lane]);
@@ -141,9 +153,9 @@ __global__ __launch_bounds__(256) void k_front(const float* __restrict__ in,
       for (int i = 0; i < NT; ++i) {
         const int ri = w + 4 * i, y = ybeg + ri;
         if (ri >= nrows) continue;  // wave-uniform; such tiles are never read
-        if (y < 0 || y >= 32) {     // zero padding row of the pw output
-          float4* d = reinterpret_cast<float4*>(s_pw + (slot_of(y) * PC + PAD) * PS);
-          for (int j = lane; j < 32 * (PS / 4); j += 64) d[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (y < 0 || y >= 32) {     // zero padding row of the pw output (whole row)
+          float4* d = reinterpret_cast<float4*>(s_pw + slot_of(y) * RS);
+          for (int j = lane; j < RS / 4; j += 64) d[j] = make_float4(0.f, 0.f, 0.f, 0.f);
           continue;
         }
         float tp[8];
@@ -162,7 +174,7 @@ __global__ __launch_bounds__(256) void k_front(const float* __restrict__ in,
           o[q] = make_float4(fmaxf(c[4 * q] + sb[q].x, 0.f), fmaxf(c[4 * q + 1] + sb[q].y, 0.f),
                              fmaxf(c[4 * q + 2] + sb[q].z, 0.f), fmaxf(c[4 * q + 3] + sb[q].w, 0.f));
         if (MODE == FRONT_MAXPOOL) {
-          float4* d = reinterpret_cast<float4*>(s_pw + (slot_of(y) * PC + PAD + px) * PS);
+          float4* d = reinterpret_cast<float4*>(s_pw + slot_of(y) * RS + colpos(PAD + px) * PS);
 #pragma unroll
           for (int q = 0; q < 4; ++q) d[2 * q + h] = o[q];
         } else {
@@ -180,7 +192,7 @@ __global__ __launch_bounds__(256) void k_front(const float* __restrict__ in,
           float4 m = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
           for (int dy = 0; dy < 3; ++dy) {
-            const float* rp = s_pw + slot_of(2 * (r0 + orr) - 1 + dy) * PC * PS;
+            const float* rp = s_pw + slot_of(2 * (r0 + orr) - 1 + dy) * RS;
 #pragma unroll
             for (int dx = 0; dx < 3; ++dx) {
               const float4 a = *reinterpret_cast<const float4*>(rp + (2 * ox + dx) * PS + 4 * dq);
@@ -219,7 +231,7 @@ __global__ __launch_bounds__(256) void k_front(const float* __restrict__ in,
           f32x16 acc = {};
           acc = mfma3_f16(ah0, al0, as_f16x8(bh[i][0]), as_f16x8(bl[i][0]), acc);
           acc = mfma3_f16(ah1, al1, as_f16x8(bh[i][1]), as_f16x8(bl[i][1]), acc);
-          float4* d = reinterpret_cast<float4*>(s_pw + (slot_of(y) * PC + PAD + px) * PS);
+          float4* d = reinterpret_cast<float4*>(s_pw + slot_of(y) * RS + colpos(PAD + px) * PS);
 #pragma unroll
           for (int q = 0; q < 4; ++q)
             d[2 * q + h] = make_float4(fmaxf(acc[4 * q] + bias[q].x, 0.f), fmaxf(acc[4 * q + 1] + bias[q].y, 0.f),
@@ -236,11 +248,12 @@ __global__ __launch_bounds__(256) void k_front(const float* __restrict__ in,
           f32x4 a1 = *reinterpret_cast<const f32x4*>(s_dw + KK * KK * 32 + c0 + 4);
 #pragma unroll DYU
           for (int dy = 0; dy < KK; ++dy) {
-            const float* rp = s_pw + slot_of(2 * (r0 + orr) - PAD + dy) * PC * PS + c0;
+            const float* rp = s_pw + slot_of(2 * (r0 + orr) - PAD + dy) * RS + c0;
 #pragma unroll
             for (int dx = 0; dx < KK; ++dx) {
               const float* wp = s_dw + (dy * KK + dx) * 32 + c0;
-              const float* ip = rp + (2 * ox + dx) * PS;
+              // column 2 ox + dx: position ox + dx / 2 (even dx) or HALF + ox + dx / 2 (odd)
+              const float* ip = rp + ((dx & 1) ? HALF + ox + (dx >> 1) : ox + (dx >> 1)) * PS;
               a0 = __builtin_elementwise_fma(*reinterpret_cast<const f32x4*>(wp), *reinterpret_cast<const f32x4*>(ip), a0);
               a1 = __builtin_elementwise_fma(*reinterpret_cast<const f32x4*>(wp + 4), *reinterpret_cast<const f32x4*>(ip + 4), a1);
             }
@@ -256,15 +269,20 @@ __global__ __launch_bounds__(256) void k_front(const float* __restrict__ in,
       }
       // fold the odd-K-step partial sums of waves 2/3 into waves 0/1 through the interior
       // of the ring slots of rows ybeg, ybeg + 1 (recomputed by the next band, never the
-      // rows it keeps; the pad columns stay zero)
+      // rows it keeps; the pad columns stay zero): lanes 0-31 use the 16 interior even-column
+      // positions 1 .., lanes 32-63 the 16 interior odd-column positions HALF + PAD - 1 ..
+      auto fold_at = [&](int row) {
+        return reinterpret_cast<float4*>(s_pw + slot_of(row) * RS + (h ? HALF + PAD - 1 : 1) * PS) + px * 4;
+      };
+      static_assert(16 * PS >= 32 * 16, "a half-wave's partial sums fit 16 interior positions");
       if (w >= 2) {
-        float4* d = reinterpret_cast<float4*>(s_pw + (slot_of(ybeg + (w - 2)) * PC + PAD) * PS) + lane * 4;
+        float4* d = fold_at(ybeg + (w - 2));
 #pragma unroll
         for (int q = 0; q < 4; ++q) d[q] = make_float4(oacc[4 * q], oacc[4 * q + 1], oacc[4 * q + 2], oacc[4 * q + 3]);
       }
       __syncthreads();
       if (w < 2) {  // output pixel 32w + px of the band = row r0 + (32w + px) / 16
-        const float4* d = reinterpret_cast<const float4*>(s_pw + (slot_of(ybeg + w) * PC + PAD) * PS) + lane * 4;
+        const float4* d = fold_at(ybeg + w);
         const int p = 32 * w + px;
         float* dst = out + ((patch * 16 + r0 + (p >> 4)) * 16 + (p & 15)) * OC;
 #pragma unroll

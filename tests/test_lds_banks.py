@@ -139,3 +139,51 @@ def test_irf_dw_window_reads_conflict_free(hin, s):
                     pix = (pl * hin + oy * s) * hin + ox0 * s + c
                     slots.add(((pix * 36 + 4 * q) * 4 // 16) % 16)
                 assert len(slots) >= (8 if (hin, s) == (8, 2) else 16)
+
+
+@pytest.mark.parametrize("kk", [3, 5])
+def test_front_irf_dw_reads_conflict_free(kk):
+    """hn_front.hip IRF-form dw window reads: wave w, lane (px = l & 31, h = l >> 5) reads band
+    pixel p = 32 (w & 1) + px (output row p >> 4, column ox = p & 15), channels
+    16 (w >> 1) + 8 h (+4), at padded input column 2 ox + dx of ring row
+    2 (r0 + row) - PAD + dy.  Columns are split even / odd (position c / 2 or HALF + c / 2),
+    pixel stride 36 floats, row stride RS = PC * 36 rounded up to 64 floats: every
+    ds_read_b128 group hits 16 distinct 16-byte slots for every band, dy and dx."""
+    pad, rb = kk // 2, 4
+    ir = 2 * (rb - 1) + kk
+    pc = 32 + 2 * pad
+    half = (pc + 1) // 2
+    rs = (pc * 36 + 63) // 64 * 64
+    assert half + pc // 2 <= rs // 36  # positions fit the row
+    for w in range(4):
+        for band in range(4):
+            r0 = band * rb
+            for dy in range(kk):
+                for dx in range(kk):
+                    for j in range(2):
+                        for g in GROUPS:
+                            slots = set()
+                            for lane in g:
+                                px, h = lane & 31, lane >> 5
+                                p = 32 * (w & 1) + px
+                                orr, ox = p >> 4, p & 15
+                                c0 = 16 * (w >> 1) + 8 * h + 4 * j
+                                slot = (2 * (r0 + orr) - pad + dy + pad + ir) % ir
+                                pos = half + ox + (dx >> 1) if dx & 1 else ox + (dx >> 1)
+                                slots.add(((slot * rs + pos * 36 + c0) * 4 // 16) % 16)
+                            assert len(slots) == 16, (kk, w, band, dy, dx, g[0])
+
+
+@pytest.mark.parametrize("kk", [3, 5])
+def test_front_irf_fold_positions_are_interior(kk):
+    """The pwl partial-sum fold uses the 16 interior even positions from 1 and the 16 interior
+    odd positions from HALF + PAD - 1: never a zero pad column."""
+    pad = kk // 2
+    pc = 32 + 2 * pad
+    half = (pc + 1) // 2
+    pos = {c: (half + c // 2 if c & 1 else c // 2) for c in range(pc)}
+    padpos = {pos[c] for c in range(pc) if c < pad or c >= 32 + pad}
+    for start in (1, half + pad - 1):
+        span = set(range(start, start + 16))
+        assert not span & padpos
+        assert (start + 15) * 36 + 36 <= (pc * 36 + 63) // 64 * 64 or start + 15 < pc
