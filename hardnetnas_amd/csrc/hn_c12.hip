@@ -429,7 +429,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, WP
 
 }  // namespace
 
-// HN_C12_CFG variants (A/B and ablation builds; 0 is production):
+// HN_C12_CFG variants (A/B and ablation builds; 2 is production):
 //   0 <8 waves, 4-row bands, 2 waves/SIMD>   1 <4, 4, 1> (512-register file)
 //   2 <4 waves, 2-row bands, 2 workgroups/CU>
 //   3 / 4: 0 with tap-interleaved P3, conv2 fragments 2 / 3 taps ahead;  5 / 6: the same for 2
@@ -445,7 +445,7 @@ hipError_t hn_launch_c12(const float* in, float* out, const HardnetDev& d, int P
   const char* ea = std::getenv("HN_C12_ABL");
   const int abl = ea ? std::atoi(ea) & 31 : 0;
   const char* ec = std::getenv("HN_C12_CFG");
-  const int cfg = ec ? std::atoi(ec) : 0;
+  const int cfg = ec ? std::atoi(ec) : 2;  // 2: 4.5 % faster than 0 (same-box A/B)
   if (cfg < 0 || cfg >= kC12Cfgs) return hipErrorInvalidValue;
   static int resident[kC12Cfgs] = {};
   static const void* const fns[kC12Cfgs] = {

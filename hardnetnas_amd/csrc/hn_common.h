@@ -40,6 +40,8 @@ HN_DEV bf16x8 as_bf16x8(const uint4& v) { return __builtin_bit_cast(bf16x8, v); 
 // dropped lo*lo term is ~2^-22 relative -- used where activations are range-bounded (the
 // NAS front: no input_norm, ReLU outputs of O(1)); same MFMA rate as bf16.
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+// (v_fma_mix{lo,hi}_f16 for the lo half -- one instruction per value -- measured slower on
+// gfx950: k_irf 12.3 -> 13.7 ms)
 HN_DEV void split8_f16(const float4& a, const float4& b, uint4& hi, uint4& lo) {
   const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
   f16x8 h, l;

@@ -98,9 +98,14 @@ __global__ __launch_bounds__(256) void k_front(const float* __restrict__ in,
         make_float4(0.f, 0.f, 0.f, 0.f);
   }
   const f16x8 sah = as_f16x8(spack[lane]), sal = as_f16x8(spack[64 + lane]);
-  float4 sb[4];
+  // stem bias as the MFMA's initial accumulator (lane (px, h): acc[4q + r] = channel
+  // 4h + 8q + r), so the epilogue is ReLU only
+  f32x16 sb;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) sb[q] = *reinterpret_cast<const float4*>(stem_b + 8 * q + 4 * h);
+  for (int q = 0; q < 4; ++q) {
+    const float4 b = *reinterpret_cast<const float4*>(stem_b + 8 * q + 4 * h);
+    sb[4 * q] = b.x; sb[4 * q + 1] = b.y; sb[4 * q + 2] = b.z; sb[4 * q + 3] = b.w;
+  }
   const int lm = kDwLane[lane], dq = lm & 7, dox = lm >> 3;
   auto slot_of = [](int y) { return (y + PAD + IR) % IR; };  // ring slot of pw row y
 
@@ -166,13 +171,12 @@ __global__ __launch_bounds__(256) void k_front(const float* __restrict__ in,
         }
         uint4 xh, xl;
         split8_f16(make_float4(tp[0], tp[1], tp[2], tp[3]), make_float4(tp[4], tp[5], tp[6], tp[7]), xh, xl);
-        f32x16 c = {};
-        c = mfma3_f16(sah, sal, as_f16x8(xh), as_f16x8(xl), c);
+        const f32x16 c = mfma3_f16(sah, sal, as_f16x8(xh), as_f16x8(xl), sb);
         float4 o[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-          o[q] = make_float4(fmaxf(c[4 * q] + sb[q].x, 0.f), fmaxf(c[4 * q + 1] + sb[q].y, 0.f),
-                             fmaxf(c[4 * q + 2] + sb[q].z, 0.f), fmaxf(c[4 * q + 3] + sb[q].w, 0.f));
+          o[q] = make_float4(fmaxf(c[4 * q], 0.f), fmaxf(c[4 * q + 1], 0.f), fmaxf(c[4 * q + 2], 0.f),
+                             fmaxf(c[4 * q + 3], 0.f));
         if (MODE == FRONT_MAXPOOL) {
           float4* d = reinterpret_cast<float4*>(s_pw + slot_of(y) * RS + colpos(PAD + px) * PS);
 #pragma unroll
@@ -221,21 +225,23 @@ __global__ __launch_bounds__(256) void k_front(const float* __restrict__ in,
         const uint4* ap = apack + (size_t)m * 4 * 64 + lane;
         const f16x8 ah0 = as_f16x8(ap[0]), al0 = as_f16x8(ap[64]);
         const f16x8 ah1 = as_f16x8(ap[128]), al1 = as_f16x8(ap[192]);
-        float4 bias[4];
+        f32x16 bias;  // pw bias as the initial accumulator
 #pragma unroll
-        for (int q = 0; q < 4; ++q) bias[q] = *reinterpret_cast<const float4*>(pw_b + 32 * m + 8 * q + 4 * h);
+        for (int q = 0; q < 4; ++q) {
+          const float4 b = *reinterpret_cast<const float4*>(pw_b + 32 * m + 8 * q + 4 * h);
+          bias[4 * q] = b.x; bias[4 * q + 1] = b.y; bias[4 * q + 2] = b.z; bias[4 * q + 3] = b.w;
+        }
 #pragma unroll
         for (int i = 0; i < NT; ++i) {
           const int ri = w + 4 * i, y = ybeg + ri;
           if (ri >= nrows || y < 0 || y >= 32) continue;
-          f32x16 acc = {};
-          acc = mfma3_f16(ah0, al0, as_f16x8(bh[i][0]), as_f16x8(bl[i][0]), acc);
+          f32x16 acc = mfma3_f16(ah0, al0, as_f16x8(bh[i][0]), as_f16x8(bl[i][0]), bias);
           acc = mfma3_f16(ah1, al1, as_f16x8(bh[i][1]), as_f16x8(bl[i][1]), acc);
           float4* d = reinterpret_cast<float4*>(s_pw + slot_of(y) * RS + colpos(PAD + px) * PS);
 #pragma unroll
           for (int q = 0; q < 4; ++q)
-            d[2 * q + h] = make_float4(fmaxf(acc[4 * q] + bias[q].x, 0.f), fmaxf(acc[4 * q + 1] + bias[q].y, 0.f),
-                                       fmaxf(acc[4 * q + 2] + bias[q].z, 0.f), fmaxf(acc[4 * q + 3] + bias[q].w, 0.f));
+            d[2 * q + h] = make_float4(fmaxf(acc[4 * q], 0.f), fmaxf(acc[4 * q + 1], 0.f),
+                                       fmaxf(acc[4 * q + 2], 0.f), fmaxf(acc[4 * q + 3], 0.f));
         }
         __syncthreads();
         // dw straight into the pwl B-operand layout: wave w owns band pixel tile (w & 1) and

@@ -105,9 +105,18 @@ __global__ __launch_bounds__(256) void k_irf(const float* __restrict__ x, float*
     for (int s = 0; s < KS; ++s) split8_f16(pa[i][s], pb[i][s], bh[i][s], bl[i][s]);
   if (PREF && tile + 1 < tend) HN_IRF_LOAD(tile + 1)
 
+  // pwl accumulators start at the pwl bias (lane (px, h): acc[4q + r] = channel 8q + 4h + r
+  // of the tile's 32 output channels), so the epilogue is stores only
   f32x16 acc[TW];
 #pragma unroll
-  for (int i = 0; i < TW; ++i) acc[i] = f32x16{};
+  for (int i = 0; i < TW; ++i) {
+    const int ct = (4 * i + w) / NOT;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 b = *reinterpret_cast<const float4*>(pwl_b + 32 * ct + 8 * q + 4 * h);
+      acc[i][4 * q] = b.x; acc[i][4 * q + 1] = b.y; acc[i][4 * q + 2] = b.z; acc[i][4 * q + 3] = b.w;
+    }
+  }
 
 #pragma unroll 1
   for (int m = 0; m < MID / 32; ++m) {
@@ -122,12 +131,15 @@ __global__ __launch_bounds__(256) void k_irf(const float* __restrict__ x, float*
     }
     // ---- pw --------------------------------------------------------------------------
     {
-      float4 bias[4];
+      f32x16 bias;  // pw bias as the initial accumulator (epilogue: ReLU only)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) bias[q] = *reinterpret_cast<const float4*>(pw_b + 32 * m + 8 * q + 4 * h);
+      for (int q = 0; q < 4; ++q) {
+        const float4 b = *reinterpret_cast<const float4*>(pw_b + 32 * m + 8 * q + 4 * h);
+        bias[4 * q] = b.x; bias[4 * q + 1] = b.y; bias[4 * q + 2] = b.z; bias[4 * q + 3] = b.w;
+      }
       f32x16 c[TI];
 #pragma unroll
-      for (int i = 0; i < TI; ++i) c[i] = f32x16{};
+      for (int i = 0; i < TI; ++i) c[i] = bias;
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
         const uint4* ap = pw_a + ((size_t)(m * KS + s) * 2) * 64 + lane;
@@ -140,8 +152,8 @@ __global__ __launch_bounds__(256) void k_irf(const float* __restrict__ x, float*
         float4* d = reinterpret_cast<float4*>(s_pw + ((4 * i + w) * 32 + px) * PS);
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-          d[2 * q + h] = make_float4(fmaxf(c[i][4 * q] + bias[q].x, 0.f), fmaxf(c[i][4 * q + 1] + bias[q].y, 0.f),
-                                     fmaxf(c[i][4 * q + 2] + bias[q].z, 0.f), fmaxf(c[i][4 * q + 3] + bias[q].w, 0.f));
+          d[2 * q + h] = make_float4(fmaxf(c[i][4 * q], 0.f), fmaxf(c[i][4 * q + 1], 0.f),
+                                     fmaxf(c[i][4 * q + 2], 0.f), fmaxf(c[i][4 * q + 3], 0.f));
       }
     }
     __syncthreads();
@@ -216,7 +228,7 @@ __global__ __launch_bounds__(256) void k_irf(const float* __restrict__ x, float*
     }
   }
 
-  // ---- epilogue: bias, float4 stores -------------------------------------------------------
+  // ---- epilogue: float4 stores (the bias is in the accumulators) ------------------------------
 #pragma unroll
   for (int i = 0; i < TW; ++i) {
     const int tile = 4 * i + w, pt = tile % NOT, ct = tile / NOT;
@@ -226,9 +238,8 @@ __global__ __launch_bounds__(256) void k_irf(const float* __restrict__ x, float*
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int c0 = 8 * q + 4 * h;
-      const float4 b = *reinterpret_cast<const float4*>(pwl_b + 32 * ct + c0);
-      *reinterpret_cast<float4*>(dst + c0) = make_float4(acc[i][4 * q] + b.x, acc[i][4 * q + 1] + b.y,
-                                                         acc[i][4 * q + 2] + b.z, acc[i][4 * q + 3] + b.w);
+      *reinterpret_cast<float4*>(dst + c0) =
+          make_float4(acc[i][4 * q], acc[i][4 * q + 1], acc[i][4 * q + 2], acc[i][4 * q + 3]);
     }
   }
   }  // tile loop
