@@ -5,7 +5,8 @@
 // Persistent workgroups of 8 waves walk a contiguous range of whole patches, each in 4 bands
 // of 4 conv2 output rows, in order.  a0 and a1 live in LDS ring buffers of 10 / 9 rows, so a
 // band computes only its 8 new a0 rows and 8 new a1 rows (no halo recompute).  Per band:
-//   P1 stem : the new a0 rows on the MFMA (32x32x16 bf16x3, K = 9 taps), BN+ReLU, split to
+//   P1 stem : the new a0 rows on the MFMA (32x32x16 bf16x3, K = 9 taps + the bias in K slot 9
+//             against a constant-1 input), ReLU, split to
 //             bf16 hi/lo -> ring W0.
 //   P2 conv1: the new a1 rows as 16x16x32 bf16x3 MFMA tiles (16 pixels x 16 channels, K = 32
 //             channels per tap), each wave owning one 16-channel half with its 9 taps of
@@ -108,9 +109,9 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, WP
   if (t < 64) {
     bf16x8 sah, sal;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < 8; ++j) {  // K slot 9 carries the bias (its B input is 1.0)
       const int tap = 8 * h32 + j;
-      const float v = tap < 9 ? stem_w[tap * 32 + r32] : 0.f;
+      const float v = tap < 9 ? stem_w[tap * 32 + r32] : (tap == 9 ? stem_b[r32] : 0.f);
       sah[j] = (__bf16)v;
       sal[j] = (__bf16)(v - (float)sah[j]);
     }
@@ -204,7 +205,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, WP
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int tap = 8 * h32 + j;
-        const float v = tap < 9 ? s_in[(y + tap / 3) * 34 + r32 + tap % 3] : 0.f;
+        const float v = tap < 9 ? s_in[(y + tap / 3) * 34 + r32 + tap % 3] : (tap == 9 ? 1.f : 0.f);
         xh[j] = (__bf16)v;
         xl[j] = (__bf16)(v - (float)xh[j]);
       }
@@ -216,11 +217,9 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, WP
       // same pixel (T21): 4 ds_write_b128 instead of 8 ds_write_b64
       uint2 hi[4], lo[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float4 b = *reinterpret_cast<const float4*>(s_b0 + 8 * q + 4 * h32);
-        hi[q] = pack_bf16x4(fmaxf(c0[4 * q] + b.x, 0.f), fmaxf(c0[4 * q + 1] + b.y, 0.f),
-                            fmaxf(c0[4 * q + 2] + b.z, 0.f), fmaxf(c0[4 * q + 3] + b.w, 0.f), lo[q]);
-      }
+      for (int q = 0; q < 4; ++q)  // (the bias came in through K slot 9)
+        hi[q] = pack_bf16x4(fmaxf(c0[4 * q], 0.f), fmaxf(c0[4 * q + 1], 0.f), fmaxf(c0[4 * q + 2], 0.f),
+                            fmaxf(c0[4 * q + 3], 0.f), lo[q]);
       char* o = rowp + (r32 + 1) * PXB + 16 * h32;
 #pragma unroll
       for (int k = 0; k < 4; k += 2) {
