@@ -257,7 +257,8 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, WP
       const int y1 = y1beg + u;
       f32x4v acc[2][G1];
 #pragma unroll
-      for (int g = 0; g < G1; ++g) acc[0][g] = acc[1][g] = f32x4v{};
+      for (int g = 0; g < G1; ++g)  // the bias is the chains' initial accumulator
+        acc[0][g] = acc[1][g] = *reinterpret_cast<const f32x4v*>(s_b1 + 16 * (cs1 * G1 + g) + 4 * g16);
       // the 3 a0 rows y1 - 1 .. y1 + 1 sit in ring slots (y1 + dy) % NA0; half 1 is 16 columns on
       const char* srow[3];
 #pragma unroll
@@ -294,8 +295,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, WP
         char* pix = prow + w1_slot(16 * hx + c16) * PXB;
 #pragma unroll
         for (int g = 0; g < G1; ++g) {
-          const f32x4v bias = *reinterpret_cast<const f32x4v*>(s_b1 + 16 * (cs1 * G1 + g) + 4 * g16);
-          const f32x4v r = __builtin_elementwise_max(acc[hx][g] + bias, f32x4v{});
+          const f32x4v r = __builtin_elementwise_max(acc[hx][g], f32x4v{});
           // lane (c, g16) holds channels 4g16 .. +3; permlane16_swap (odd rows of vdst <-> even
           // rows of src) leaves the even row with hi channels 4g16 .. +7 and the odd row with lo
           // channels 4g16-4 .. +3: one ds_write_b128 per lane instead of two ds_write_b64
@@ -325,7 +325,8 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, WP
       const int oy0 = w / NCH2;  // rows oy0 and oy0 + NSET
       f32x4v acc[2][G2];
 #pragma unroll
-      for (int g = 0; g < G2; ++g) acc[0][g] = acc[1][g] = f32x4v{};
+      for (int g = 0; g < G2; ++g)  // the bias is the chains' initial accumulator
+        acc[0][g] = acc[1][g] = *reinterpret_cast<const f32x4v*>(s_b2 + 16 * (cs2 * G2 + g) + 4 * g16);
       // output column c16 reads a1 column 2*c16 - 1 + dx: W1 slot c16 (dx 0), 17 + c16 (dx 1),
       // c16 + 1 (dx 2); a1 rows 2 (r0 + oy) - 1 + dy sit in ring slots (2 (r0 + oy) + dy) % NA1
       const char* srow[2][3];
@@ -416,7 +417,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, WP
         for (int g = 0; g < G2; ++g)
           *reinterpret_cast<f32x4v*>(o + 16 * (cs2 * G2 + g)) =
               __builtin_elementwise_max(
-                  acc[ry][g] + *reinterpret_cast<const f32x4v*>(s_b2 + 16 * (cs2 * G2 + g) + 4 * g16),
+                  acc[ry][g],
                   f32x4v{});
       }
     }
