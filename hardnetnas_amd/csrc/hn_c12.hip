@@ -69,7 +69,13 @@ HN_DEV int w1_slot(int x) { return ((x + 1) & 1) ? 17 + (x >> 1) : (x + 1) >> 1;
 // P3I: P3 walks taps, each with both output rows' B fragments (one tap ahead) and the two rows'
 // accumulator chains interleaved MFMA by MFMA; conv2 fragments WA taps ahead (P3I = 0: steps
 // of one (tap, row), fragments 2 taps ahead).
-template <int ABL, int NW, int RB2, int WPE, bool P3I = false, int WA = 2>
+// P2I: P2 walks taps with both 16-pixel halves' B fragments one tap ahead, so the 4 accumulator
+// chains (2 halves x 2 groups) interleave MFMA by MFMA (P2I = 0: steps of one (tap, half), 2
+// chains at a time).
+// Tried and removed (same-box A/B): P1's operands read during the previous P3 (-1.3 % vs 7,
+// nothing on top of PRIO); P1's row computed inside the previous P3 with its MFMAs spread over
+// P3's steps (+5-10 %: the register file then holds conv2 fragments only one tap ahead).
+template <int ABL, int NW, int RB2, int WPE, bool P3I = false, int WA = 2, bool P2I = false, int PRIO = 0>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void k_c12(
     const float* __restrict__ in, float* __restrict__ out, const float* __restrict__ stem_w,
     const float* __restrict__ stem_b, const uint4* __restrict__ w1p, const float* __restrict__ b1,
@@ -146,6 +152,41 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, WP
     return w2p[i];
   };
 
+  // P1 operands of a0 row y: the im2col taps (K slot 9 = 1.0 carries the bias) and the stem A
+  auto p1_fetch = [&](int y, float (&xv)[8], uint4& sa0, uint4& sa1) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int tap = 8 * h32 + j;
+      xv[j] = tap < 9 ? s_in[(y + tap / 3) * 34 + r32 + tap % 3] : (tap == 9 ? 1.f : 0.f);
+    }
+    sa0 = s_stem[lane][0];
+    sa1 = s_stem[lane][1];
+  };
+  // P1 epilogue: ReLU, split to bf16 hi/lo, a0 row y -> its W0 ring slot
+  auto p1_store = [&](int y, const f32x16& c0) {
+    char* rowp = s_w0 + ((y + 1) % NA0) * W0C * PXB;
+    // lane (px, h) holds channels 8q + 4h .. +3; permlane32_swap pairs (q, q+1) so that
+    // lanes 0-31 hold channels 8q .. 8q+7 and lanes 32-63 channels 8q+8 .. 8q+15 of the
+    // same pixel (T21): 4 ds_write_b128 instead of 8 ds_write_b64
+    uint2 hi[4], lo[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)  // (the bias came in through K slot 9)
+      hi[q] = pack_bf16x4(fmaxf(c0[4 * q], 0.f), fmaxf(c0[4 * q + 1], 0.f), fmaxf(c0[4 * q + 2], 0.f),
+                          fmaxf(c0[4 * q + 3], 0.f), lo[q]);
+    char* o = rowp + (r32 + 1) * PXB + 16 * h32;
+#pragma unroll
+    for (int k = 0; k < 4; k += 2) {
+      auto sw = [](uint2& a, uint2& b) {
+        const auto rx = __builtin_amdgcn_permlane32_swap(a.x, b.x, false, false);
+        const auto ry = __builtin_amdgcn_permlane32_swap(a.y, b.y, false, false);
+        a.x = rx[0]; b.x = rx[1]; a.y = ry[0]; b.y = ry[1];
+      };
+      sw(hi[k], hi[k + 1]);
+      sw(lo[k], lo[k + 1]);
+      *reinterpret_cast<uint4*>(o + 16 * k) = make_uint4(hi[k].x, hi[k].y, hi[k + 1].x, hi[k + 1].y);
+      *reinterpret_cast<uint4*>(o + 64 + 16 * k) = make_uint4(lo[k].x, lo[k].y, lo[k + 1].x, lo[k + 1].y);
+    }
+  };
   // the next patch's pixels are fetched one patch ahead
   constexpr int PPT = 1024 / (NW * 64);  // patch pixels per thread (2 or 4)
   typedef float pxv __attribute__((ext_vector_type(PPT)));
@@ -189,6 +230,11 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, WP
 #pragma unroll 1
   for (int band = 0; band < 16 / RB2; ++band) {
     const int r0 = band * RB2;
+    // PRIO & 3: wave priority raised over P1 -- a short serial latency chain that every wave of
+    // the workgroup waits for at the next barrier -- so its VALU and MFMA issue ahead of the
+    // other workgroup's waves on the same SIMD (MI355X_MICROARCH.md, two waves per SIMD, item 4);
+    // PRIO & 4: over P3 as well (P3 -> P1 -> barrier)
+    if constexpr ((PRIO & 3) != 0) __builtin_amdgcn_s_setprio(PRIO & 3);
     // ---- P1: the band's new a0 rows -> W0 ring (slot (y + 1) % NA0) ------------------------
     // band 0: rows -1 .. 8 (row -1 is conv1's zero padding); band b: rows 8b+1 .. 8b+8
     const int ybeg = band == 0 ? -1 : 2 * RB2 * band + 1, nrows = band == 0 ? 2 * RB2 + 2 : 2 * RB2;
@@ -201,39 +247,19 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, WP
           reinterpret_cast<uint4*>(rowp + PXB)[i] = make_uint4(0, 0, 0, 0);
         continue;
       }
+      float xv[8];
+      uint4 sa0, sa1;
+      p1_fetch(y, xv, sa0, sa1);
       bf16x8 xh, xl;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const int tap = 8 * h32 + j;
-        const float v = tap < 9 ? s_in[(y + tap / 3) * 34 + r32 + tap % 3] : (tap == 9 ? 1.f : 0.f);
-        xh[j] = (__bf16)v;
-        xl[j] = (__bf16)(v - (float)xh[j]);
+        xh[j] = (__bf16)xv[j];
+        xl[j] = (__bf16)(xv[j] - (float)xh[j]);
       }
-      const f32x16 c0 = (ABL & 1) ? f32x16{}
-                                  : mfma3(as_bf16x8(s_stem[lane][0]), as_bf16x8(s_stem[lane][1]), xh, xl,
-                                          f32x16{});
-      // lane (px, h) holds channels 8q + 4h .. +3; permlane32_swap pairs (q, q+1) so that
-      // lanes 0-31 hold channels 8q .. 8q+7 and lanes 32-63 channels 8q+8 .. 8q+15 of the
-      // same pixel (T21): 4 ds_write_b128 instead of 8 ds_write_b64
-      uint2 hi[4], lo[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q)  // (the bias came in through K slot 9)
-        hi[q] = pack_bf16x4(fmaxf(c0[4 * q], 0.f), fmaxf(c0[4 * q + 1], 0.f), fmaxf(c0[4 * q + 2], 0.f),
-                            fmaxf(c0[4 * q + 3], 0.f), lo[q]);
-      char* o = rowp + (r32 + 1) * PXB + 16 * h32;
-#pragma unroll
-      for (int k = 0; k < 4; k += 2) {
-        auto sw = [](uint2& a, uint2& b) {
-          const auto rx = __builtin_amdgcn_permlane32_swap(a.x, b.x, false, false);
-          const auto ry = __builtin_amdgcn_permlane32_swap(a.y, b.y, false, false);
-          a.x = rx[0]; b.x = rx[1]; a.y = ry[0]; b.y = ry[1];
-        };
-        sw(hi[k], hi[k + 1]);
-        sw(lo[k], lo[k + 1]);
-        *reinterpret_cast<uint4*>(o + 16 * k) = make_uint4(hi[k].x, hi[k].y, hi[k + 1].x, hi[k + 1].y);
-        *reinterpret_cast<uint4*>(o + 64 + 16 * k) = make_uint4(lo[k].x, lo[k].y, lo[k + 1].x, lo[k + 1].y);
-      }
+      const f32x16 c0 = (ABL & 1) ? f32x16{} : mfma3(as_bf16x8(sa0), as_bf16x8(sa1), xh, xl, f32x16{});
+      p1_store(y, c0);
     }
+    if constexpr (PRIO != 0) __builtin_amdgcn_s_setprio(0);
     __syncthreads();
 
     // ---- P2: conv1 -> W1 ring (units: new a1 row, both 16-pixel halves; G1 groups) ----------
@@ -263,6 +289,48 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, WP
       const char* srow[3];
 #pragma unroll
       for (int dy = 0; dy < 3; ++dy) srow[dy] = s_w0 + (((y1 + dy) % NA0) * W0C + c16) * PXB + 16 * g16;
+      if constexpr (P2I) {
+        // taps: both halves' B fragments one tap ahead; the 2 x G1 accumulator chains are
+        // interleaved MFMA by MFMA (dependent distance 2 G1 instead of G1)
+        uint4 bq[2][2][2];  // [buffer][half][plane]
+        auto bptr = [&](int tn, int hn) { return srow[tn / 3] + (tn % 3 + 16 * hn) * PXB; };
+#pragma unroll
+        for (int hn = 0; hn < 2; ++hn) {
+          bq[0][hn][0] = *reinterpret_cast<const uint4*>(bptr(0, hn));
+          bq[0][hn][1] = *reinterpret_cast<const uint4*>(bptr(0, hn) + 64);
+        }
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) {
+          if (tap + 1 < 9) {
+#pragma unroll
+            for (int hn = 0; hn < 2; ++hn) {
+              bq[(tap + 1) & 1][hn][0] = *reinterpret_cast<const uint4*>(bptr(tap + 1, hn));
+              bq[(tap + 1) & 1][hn][1] = *reinterpret_cast<const uint4*>(bptr(tap + 1, hn) + 64);
+            }
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          const uint4(&b)[2][2] = bq[tap & 1];
+          if constexpr ((ABL & 2) != 0) {
+#pragma unroll
+            for (int g = 0; g < G1; ++g)
+#pragma unroll
+              for (int hx = 0; hx < 2; ++hx) acc[hx][g][0] += __builtin_bit_cast(float, b[hx][0].x ^ b[hx][1].y);
+            continue;
+          }
+#pragma unroll
+          for (int g = 0; g < G1; ++g)
+#pragma unroll
+            for (int hx = 0; hx < 2; ++hx) acc[hx][g] = mfma16(a1w[tap][g][1], b[hx][0], acc[hx][g]);
+#pragma unroll
+          for (int g = 0; g < G1; ++g)
+#pragma unroll
+            for (int hx = 0; hx < 2; ++hx) acc[hx][g] = mfma16(a1w[tap][g][0], b[hx][1], acc[hx][g]);
+#pragma unroll
+          for (int g = 0; g < G1; ++g)
+#pragma unroll
+            for (int hx = 0; hx < 2; ++hx) acc[hx][g] = mfma16(a1w[tap][g][0], b[hx][0], acc[hx][g]);
+        }
+      } else {
       // steps j = (tap, half): B fragments one step ahead (two register sets); each feeds
       // the G1 groups, and consecutive steps alternate between the two halves' chains
       uint4 bh[2], bl[2];
@@ -288,6 +356,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, WP
             acc[hx][g] = mfma16(a1w[tap][g][0], bh[j & 1], acc[hx][g]);
           }
         }
+      }
       }
       char* prow = s_w1 + ((y1 + 1) % NA1) * W1C * PXB;
 #pragma unroll
@@ -319,6 +388,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, WP
         for (int pl = 0; pl < 2; ++pl) wq[tap][g][pl] = w2_frag(tap, g, pl);
     __syncthreads();
 
+    if constexpr ((PRIO & 4) != 0) __builtin_amdgcn_s_setprio(PRIO & 3);  // P3 too (P3 -> P1 -> barrier)
     // ---- P3: conv2 (stride 2) -> a2 in HBM (units: output rows oy and oy + 2 together; this
     // wave's G2 quarters) ----------------------------------------------------------------------
     {
@@ -429,14 +499,19 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, WP
 
 }  // namespace
 
-// HN_C12_CFG variants (A/B and ablation builds; 2 is production):
+// HN_C12_CFG variants (A/B and ablation builds; 12 is production):
 //   0 <8 waves, 4-row bands, 2 waves/SIMD>   1 <4, 4, 1> (512-register file)
 //   2 <4 waves, 2-row bands, 2 workgroups/CU>
 //   3 / 4: 0 with tap-interleaved P3, conv2 fragments 2 / 3 taps ahead;  5 / 6: the same for 2
+//   7 / 8: 2 / 5 with the tap-interleaved P2 (both halves' chains MFMA by MFMA);  9: 0 with it
+//   10 / 11: 7 with the P1 wave priority raised to 1 / 3;  12: 7 with P3 and P1 at priority 1
 #define HN_C12_CFGS(X)                                                                   \
-  X(0, 8, 4, 2, false, 2) X(1, 4, 4, 1, false, 2) X(2, 4, 2, 2, false, 2)                 \
-  X(3, 8, 4, 2, true, 2) X(4, 8, 4, 2, true, 3) X(5, 4, 2, 2, true, 2) X(6, 4, 2, 2, true, 3)
-constexpr int kC12Cfgs = 7;
+  X(0, 8, 4, 2, false, 2, false, 0) X(1, 4, 4, 1, false, 2, false, 0) X(2, 4, 2, 2, false, 2, false, 0) \
+  X(3, 8, 4, 2, true, 2, false, 0) X(4, 8, 4, 2, true, 3, false, 0) X(5, 4, 2, 2, true, 2, false, 0)     \
+  X(6, 4, 2, 2, true, 3, false, 0) X(7, 4, 2, 2, false, 2, true, 0) X(8, 4, 2, 2, true, 2, true, 0)      \
+  X(9, 8, 4, 2, false, 2, true, 0) X(10, 4, 2, 2, false, 2, true, 1) X(11, 4, 2, 2, false, 2, true, 3) \
+  X(12, 4, 2, 2, false, 2, true, 5)
+constexpr int kC12Cfgs = 13;
 
 hipError_t hn_launch_c12(const float* in, float* out, const HardnetDev& d, int P, float eps,
                          hipStream_t st) {
@@ -445,16 +520,16 @@ hipError_t hn_launch_c12(const float* in, float* out, const HardnetDev& d, int P
   const char* ea = std::getenv("HN_C12_ABL");
   const int abl = ea ? std::atoi(ea) & 31 : 0;
   const char* ec = std::getenv("HN_C12_CFG");
-  const int cfg = ec ? std::atoi(ec) : 2;  // 2: 4.5 % faster than 0 (same-box A/B)
+  const int cfg = ec ? std::atoi(ec) : 12;  // same-box A/Bs: 12 2-4 % < 7 1.5 % < 2 4.5 % < 0
   if (cfg < 0 || cfg >= kC12Cfgs) return hipErrorInvalidValue;
   static int resident[kC12Cfgs] = {};
   static const void* const fns[kC12Cfgs] = {
-#define HN_C12_FN(C, W, R, E, I, A) reinterpret_cast<const void*>(&k_c12<0, W, R, E, I, A>),
+#define HN_C12_FN(C, W, R, E, I, A, Q, PR) reinterpret_cast<const void*>(&k_c12<0, W, R, E, I, A, Q, PR>),
       HN_C12_CFGS(HN_C12_FN)
 #undef HN_C12_FN
   };
   static const int nws[kC12Cfgs] = {
-#define HN_C12_NWS(C, W, R, E, I, A) W,
+#define HN_C12_NWS(C, W, R, E, I, A, Q, PR) W,
       HN_C12_CFGS(HN_C12_NWS)
 #undef HN_C12_NWS
   };
@@ -468,22 +543,29 @@ hipError_t hn_launch_c12(const float* in, float* out, const HardnetDev& d, int P
     resident[cfg] = std::max(1, per_cu) * std::max(1, cus);
   }
   const int grid = (int)std::min<long>((long)P, resident[cfg]);
-#define HN_C12_GO(A, W, R, E, I, WA)                                                             \
-  hipLaunchKernelGGL((k_c12<A, W, R, E, I, WA>), dim3(grid), dim3(W * 64), 0, st, in, out,      \
+#define HN_C12_GO(A, W, R, E, I, WA, Q, PR)                                                      \
+  hipLaunchKernelGGL((k_c12<A, W, R, E, I, WA, Q, PR>), dim3(grid), dim3(W * 64), 0, st, in, out,      \
                      d.stem_w, d.stem_b, static_cast<const uint4*>(d.c12_w1), d.bias[1],        \
                      static_cast<const uint4*>(d.c12_w2), d.bias[2], P, eps)
   if (abl) {
     if (cfg == 0) {
       switch (abl) {
-        case 1: HN_C12_GO(1, 8, 4, 2, false, 2); break;
-        case 6: HN_C12_GO(6, 8, 4, 2, false, 2); break;
-        case 8: HN_C12_GO(8, 8, 4, 2, false, 2); break;
+        case 1: HN_C12_GO(1, 8, 4, 2, false, 2, false, 0); break;
+        case 6: HN_C12_GO(6, 8, 4, 2, false, 2, false, 0); break;
+        case 8: HN_C12_GO(8, 8, 4, 2, false, 2, false, 0); break;
         default: return hipErrorInvalidValue;
       }
     } else if (cfg == 2) {
       switch (abl) {
-        case 6: HN_C12_GO(6, 4, 2, 2, false, 2); break;
-        case 8: HN_C12_GO(8, 4, 2, 2, false, 2); break;
+        case 6: HN_C12_GO(6, 4, 2, 2, false, 2, false, 0); break;
+        case 8: HN_C12_GO(8, 4, 2, 2, false, 2, false, 0); break;
+        default: return hipErrorInvalidValue;
+      }
+    } else if (cfg == 12) {
+      switch (abl) {
+        case 1: HN_C12_GO(1, 4, 2, 2, false, 2, true, 5); break;
+        case 6: HN_C12_GO(6, 4, 2, 2, false, 2, true, 5); break;
+        case 8: HN_C12_GO(8, 4, 2, 2, false, 2, true, 5); break;
         default: return hipErrorInvalidValue;
       }
     } else {
@@ -491,8 +573,8 @@ hipError_t hn_launch_c12(const float* in, float* out, const HardnetDev& d, int P
     }
   } else {
     switch (cfg) {
-#define HN_C12_CASE(C, W, R, E, I, A) \
-  case C: HN_C12_GO(0, W, R, E, I, A); break;
+#define HN_C12_CASE(C, W, R, E, I, A, Q, PR) \
+  case C: HN_C12_GO(0, W, R, E, I, A, Q, PR); break;
       HN_C12_CFGS(HN_C12_CASE)
 #undef HN_C12_CASE
     }
