@@ -580,6 +580,7 @@ extern "C" int hn_create(const hn_arch_desc* desc, const float* host_params, siz
     int i = 0;
     for (const char* c = e; *c && i < 6; ++c)
       if (*c >= '0' && *c <= '9') m->variant[i++] = *c - '0';
+      else if (*c >= 'a' && *c <= 'f') m->variant[i++] = 10 + (*c - 'a');
   }
   (void)hipGetDevice(&m->device);
   Cursor cur{host_params, n_params};
