@@ -74,7 +74,9 @@ HN_DEV int w1_slot(int x) { return ((x + 1) & 1) ? 17 + (x >> 1) : (x + 1) >> 1;
 // chains at a time).
 // Tried and removed (same-box A/B): P1's operands read during the previous P3 (-1.3 % vs 7,
 // nothing on top of PRIO); P1's row computed inside the previous P3 with its MFMAs spread over
-// P3's steps (+5-10 %: the register file then holds conv2 fragments only one tap ahead).
+// P3's steps (+5-10 %: the register file then holds conv2 fragments only one tap ahead); the
+// 29 split-stem products K-packed into two independent MFMAs instead of the dependent mfma3
+// chain (+1 %: P1 is not bound by its MFMA latency).
 template <int ABL, int NW, int RB2, int WPE, bool P3I = false, int WA = 2, bool P2I = false, int PRIO = 0>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void k_c12(
     const float* __restrict__ in, float* __restrict__ out, const float* __restrict__ stem_w,
