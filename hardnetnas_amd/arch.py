@@ -141,6 +141,33 @@ def nas_macs(arch) -> int:
     return total
 
 
+# FDLNet's hand-instantiated NAS descriptors (HardNetNeiMask,
+# FDLNet-master/latency/NASNet/model/des.py:8-55 and latency/NASNet_0.1/model/des.py:10-55):
+# a fixed front on the 32x32 patch to 8x8x64, then three IRFBlocks from the same op vocabulary
+# (latency/NASNet/model/operations.py:205-320 == fbnet_builder.IRFBlock), the 4x4 head and
+# torch.norm L2.  The variants differ only in the front:
+#   "NASNet":     Conv 3x3 (bias) -> BN(affine=False) -> [Conv 1x1 s2 -> BN -> ReLU] x 2 (32, 64)
+#   "NASNet_0.1": Conv 3x3 (bias) -> MaxPool(3, 2, 1) -> Identity -> ConvBNRelu 1x1 s2 (64)
+FDL_VARIANTS = ("NASNet", "NASNet_0.1")
+FDL_LAYERS: List[Tuple[int, int, int]] = [(64, 64, 1), (64, 128, 2), (128, 128, 1)]
+FDL_OPS: List[str] = ["ir_k5_e1", "ir_k3_e3", "ir_k5_s2"]  # IRFBlock(64,64,1,1,k5), (64,128,3,2,k3), (128,128,1,1,k5,mid,g2)
+FDL_INPUT_NORM_EPS = 1e-8
+
+
+def fdl_macs(variant: str) -> int:
+    """MACs per patch of the FDLNet descriptor as the reference computes it (full 32x32 stem)."""
+    total = 9 * 32 * 32 * 32                       # stem
+    if variant == "NASNet":
+        total += 32 * 32 * 16 * 16 + 32 * 64 * 8 * 8  # two 1x1 stride-2 convs
+    else:
+        total += 32 * 64 * 8 * 8                     # 1x1 stride-2 conv after the maxpool
+    hw = 8
+    for (ci, co, s), op in zip(FDL_LAYERS, FDL_OPS):
+        total += layer_macs(ci, co, s, op, hw)
+        hw //= s
+    return total + 128 * DESC_DIM * HEAD_KERNEL * HEAD_KERNEL
+
+
 # Stock HardNet conv stack (hardnet/HardNet.py:280-302): (C_in, C_out, k, stride, pad, relu)
 HARDNET_CONVS: List[Tuple[int, int, int, int, int, bool]] = [
     (1, 32, 3, 1, 1, True),

@@ -232,6 +232,63 @@ def make_op(name: str, c_in: int, c_out: int, stride: int) -> nn.Module:
                     pw_group=spec.pw_group, shuffle=spec.shuffle, se=spec.se)
 
 
+class FDLIdentity(nn.Module):
+    """FDLNet's ``Identity`` (latency/NASNet/model/operations.py, class Identity): a 1x1
+    ConvBNRelu with the block's stride when C or the resolution changes, else nothing
+    (unlike fbnet_builder's, no max-pool)."""
+
+    def __init__(self, c_in, c_out, stride):
+        super().__init__()
+        self.conv = (ConvBNRelu(c_in, c_out, 1, stride, 0, relu=True)
+                     if c_in != c_out or stride != 1 else None)
+
+    def forward(self, x):
+        return self.conv(x) if self.conv is not None else x
+
+
+class HardNetNeiMask(_NativeMixin, nn.Module):
+    """FDLNet's hand-instantiated NAS descriptor ``HardNetNeiMask``:
+    ``variant="NASNet"`` = FDLNet-master/latency/NASNet/model/des.py:8-55,
+    ``variant="NASNet_0.1"`` = latency/NASNet_0.1/model/des.py:10-55.  Same ``.features``
+    indices / state_dict keys as the reference; input_norm eps 1e-8 (des.py:40-47); L2 by
+    ``torch.norm`` without eps (des.py:49-53).  The neighbour-mask training loss is not
+    part of the descriptor forward and is not restated here."""
+
+    def __init__(self, MARGIN: float = 1.0, C: float = 1.0, variant: str = "NASNet"):
+        super().__init__()
+        if variant not in A.FDL_VARIANTS:
+            raise ValueError(f"variant must be one of {A.FDL_VARIANTS}")
+        self.MARGIN, self.C, self.variant = MARGIN, C, variant
+        if variant == "NASNet":
+            front = [nn.Conv2d(1, 32, kernel_size=3, stride=1, padding=1),
+                     nn.BatchNorm2d(32, affine=False),
+                     nn.Conv2d(32, 32, kernel_size=1, stride=2, padding=0, bias=False),
+                     nn.BatchNorm2d(32), nn.ReLU(inplace=True),
+                     nn.Conv2d(32, 64, kernel_size=1, stride=2, padding=0, bias=False),
+                     nn.BatchNorm2d(64), nn.ReLU(inplace=True)]
+        else:
+            front = [nn.Conv2d(1, 32, kernel_size=3, stride=1, padding=1),
+                     nn.MaxPool2d(kernel_size=3, stride=2, padding=1),
+                     FDLIdentity(32, 32, 1), FDLIdentity(32, 64, 2)]
+        blocks = [make_op(op, ci, co, s) for op, (ci, co, s) in zip(A.FDL_OPS, A.FDL_LAYERS)]
+        head = [nn.Conv2d(128, 128, kernel_size=4, bias=False), nn.BatchNorm2d(128, affine=False)]
+        self.features = nn.Sequential(*front, *blocks, *head)
+        self.input_norm_eps = A.FDL_INPUT_NORM_EPS
+
+    def input_norm(self, x):
+        flat = x.view(x.size(0), -1)
+        mp = torch.mean(flat, dim=1)
+        sp = torch.std(flat, dim=1) + self.input_norm_eps
+        return (x - mp.detach().view(-1, 1, 1, 1)) / sp.detach().view(-1, 1, 1, 1)
+
+    def forward(self, input):
+        if _native_eligible(self, input):
+            return self._native_forward(input)
+        x_features = self.features(self.input_norm(input))
+        x = x_features.view(x_features.size(0), -1)
+        return x / torch.norm(x, p=2, dim=-1, keepdim=True)
+
+
 class HardNetNAS(_NativeMixin, nn.Module):
     """Sampled hardnetNAS descriptor (model_supernet.py:53-85, argmax op per layer).
 

@@ -159,6 +159,41 @@ def nas_forward(p: Dict[str, torch.Tensor], ops: Sequence[str], x: torch.Tensor,
     return (out, acts) if return_layers else out
 
 
+# ---- FDLNet hand-instantiated NAS descriptors (SURVEY 2 row 16, 8(c) fixture plan) ----
+FDL_LAYERS = [(64, 64, 1), (64, 128, 2), (128, 128, 1)]
+FDL_OPS = ["ir_k5_e1", "ir_k3_e3", "ir_k5_s2"]
+FDL_INPUT_NORM_EPS = 1e-8  # latency/NASNet/model/des.py:40-47
+
+
+def fdl_forward(p: Dict[str, torch.Tensor], variant: str, x: torch.Tensor, dtype=torch.float32):
+    """HardNetNeiMask.forward, FDLNet-master/latency/NASNet/model/des.py:49-53 (variant
+    "NASNet": features at des.py:13-36) and latency/NASNet_0.1/model/des.py:17-29
+    ("NASNet_0.1").  input_norm with eps 1e-8 after the unbiased std; the stem conv has a
+    bias; the IRFBlocks are latency/NASNet/model/operations.py:205-320 (= fbnet_builder's);
+    L2 by torch.norm without eps."""
+    y = input_norm(x.to(dtype), FDL_INPUT_NORM_EPS)
+    y = F.conv2d(y, _t(p, "features.0.weight", dtype), _t(p, "features.0.bias", dtype), 1, 1)
+    if variant == "NASNet":
+        y = _bn(y, p, "features.1", dtype, affine=False)
+        for conv, bn in ((2, 3), (5, 6)):  # Conv 1x1 s2 (no bias) + BN + ReLU
+            y = F.conv2d(y, _t(p, f"features.{conv}.weight", dtype), None, 2)
+            y = F.relu(_bn(y, p, f"features.{bn}", dtype, affine=True))
+        first, head = 8, 11
+    elif variant == "NASNet_0.1":
+        y = F.max_pool2d(y, 3, 2, 1)
+        # Identity(32, 32, 1) is the identity; Identity(32, 64, 2) = ConvBNRelu 1x1 stride 2
+        y = _cbr(y, p, "features.3.conv", dtype, 2, 0, 1, True)
+        first, head = 4, 7
+    else:
+        raise ValueError(variant)
+    for i, (op, (ci, co, s)) in enumerate(zip(FDL_OPS, FDL_LAYERS)):
+        y = nas_layer(y, p, f"features.{first + i}", op, ci, co, s, dtype)
+    y = F.conv2d(y, _t(p, f"features.{head}.weight", dtype))
+    y = _bn(y, p, f"features.{head + 1}", dtype, affine=False)
+    y = y.reshape(y.size(0), -1)
+    return y / torch.norm(y, p=2, dim=-1, keepdim=True)
+
+
 # ---- losses / metrics (SURVEY 8(f) rows 1-2) ----------------------------------------
 def distance_matrix_vector(anchor, positive):
     """hardnet/Losses.py:5-13."""

@@ -12,6 +12,8 @@ outputs, checksums) is written into tests/golden/*.npz.
 * hardnetNAS: ``FBNet_Stochastic_SuperNet`` (model_supernet.py) and ``PRIMITIVES``
   (fbnet_builder.py) are imported directly; the sampled net is the supernet with
   each MixedOperation replaced by ``ops[CANDIDATE_BLOCKS.index(op)]``.
+* FDLNet ``HardNetNeiMask`` (latency/NASNet{,_0.1}/model/des.py) is imported directly with
+  the variant's directory as the package root.
 * losses/metrics: ``distance_matrix_vector`` / ``loss_HardNet`` (hardnet/Losses.py)
   and ``ErrorRateAt95Recall`` (hardnet/EvalMetrics.py) are AST-extracted.  The
   reference loss calls ``.cuda()`` on an eye matrix; for CPU fixture generation
@@ -217,6 +219,54 @@ def make_nas(name, ops):
     print("nas", name, y.shape, float(np.abs(y - y64).max()))
 
 
+def make_fdl(variant):
+    """FDLNet HardNetNeiMask (latency/<variant>/model/des.py), imported from the reference with
+    its own package root on sys.path (both variants use the package names model/ and utils/)."""
+    from hardnetnas_amd.model import HardNetNeiMask
+    for k in [k for k in sys.modules if k.split(".")[0] in ("model", "utils")]:
+        del sys.modules[k]
+    sys.path.insert(0, os.path.join(REF, "FDLNet-master", "latency", variant))
+    try:
+        from model.des import HardNetNeiMask as RefNet
+    finally:
+        sys.path.pop(0)
+    torch.manual_seed(0)
+    model = RefNet(1.0, 1.0)
+    sd = model.state_dict()
+    tmpl = {k: tuple(v.shape) for k, v in HardNetNeiMask(variant=variant).state_dict().items()}
+    assert tmpl == {k: tuple(v.shape) for k, v in sd.items()}, "state_dict layout differs"
+    w = synth.synth_state_dict(tmpl, WEIGHT_SEED)
+    sd.update({k: torch.from_numpy(v) for k, v in w.items()})
+    model.load_state_dict(sd)
+    xc = torch.from_numpy(synth.synth_patches(N_CALIB, CALIB_SEED))
+    _calibrate(model, model, xc)
+    x = torch.from_numpy(synth.synth_patches(N_TEST, TEST_SEED))
+    xe = torch.from_numpy(edge_patches())
+    with torch.no_grad():
+        y = model(x).numpy()
+        ye = model(xe).numpy()
+        m64 = model.double()
+        y64 = m64(x.double()).numpy()
+        ye64 = m64(xe.double()).numpy()
+    sd = {k: v.float().numpy() for k, v in model.state_dict().items()
+          if not k.endswith("num_batches_tracked")}
+    out = {
+        "meta": json.dumps({"model": "fdl", "variant": variant, "weight_seed": WEIGHT_SEED,
+                            "test_seed": TEST_SEED, "n_test": N_TEST,
+                            "weights_sha256": {k: synth.sha256_f32(v) for k, v in w.items()
+                                               if "running" not in k},
+                            "source": "FDLNet-master/latency/%s/model/des.py HardNetNeiMask "
+                                      "(imported, torch %s CPU)" % (variant, torch.__version__)}),
+        "x_edge": xe.numpy(), "y": y, "y_edge": ye, "y64": y64, "y_edge64": ye64,
+    }
+    for k, v in sd.items():
+        if "running" in k:
+            out["bn/" + k] = v
+    tag = variant.replace(".", "")
+    np.savez_compressed(os.path.join(HERE, f"fdl_{tag}.npz"), **out)
+    print("fdl", variant, y.shape, float(np.abs(y - y64).max()))
+
+
 def make_losses():
     ns = _ns()
     exec(_extract(os.path.join(REF, "hardnet/Losses.py"),
@@ -271,3 +321,5 @@ if __name__ == "__main__":
     for name, ops in NAS_FIXTURES.items():
         make_nas(name, ops)
     make_losses()
+    for v in A.FDL_VARIANTS:
+        make_fdl(v)

@@ -4,7 +4,7 @@ import numpy as np
 import pytest
 import torch
 
-from fixtures import NAS_NAMES, build_module, load, params_for, golden_inputs
+from fixtures import FDL_NAMES, NAS_NAMES, build_module, load, params_for, golden_inputs
 from oracle import hardnet_oracle as O
 
 TOL = 1e-5   # fp32 vs fp32 of the same ATen ops: only summation-order noise
@@ -14,11 +14,13 @@ def _oracle(name, p, x, dtype=torch.float32):
     t = {k: torch.from_numpy(v) for k, v in p.items()}
     if name == "hardnet":
         return O.hardnet_forward(t, torch.from_numpy(x), dtype).numpy()
+    if name.startswith("fdl_"):
+        return O.fdl_forward(t, load(name)["meta"]["variant"], torch.from_numpy(x), dtype).numpy()
     ops = load("nas_" + name)["meta"]["ops"]
     return O.nas_forward(t, ops, torch.from_numpy(x), dtype).numpy()
 
 
-@pytest.mark.parametrize("name", ["hardnet"] + NAS_NAMES)
+@pytest.mark.parametrize("name", ["hardnet"] + NAS_NAMES + FDL_NAMES)
 def test_oracle_matches_reference_vectors(name):
     m, fx, p = build_module(name)
     x = golden_inputs(fx)
@@ -30,14 +32,14 @@ def test_oracle_matches_reference_vectors(name):
     assert np.abs(ye - fx["y_edge"]).max() <= TOL
 
 
-@pytest.mark.parametrize("name", ["hardnet", "wang2", "cov_b"])
+@pytest.mark.parametrize("name", ["hardnet", "wang2", "cov_b"] + FDL_NAMES)
 def test_oracle_fp64_matches_reference_fp64(name):
     m, fx, p = build_module(name)
     y = _oracle(name, p, golden_inputs(fx)[:64], torch.float64)
     assert np.abs(y - fx["y64"][:64]).max() <= 1e-12
 
 
-@pytest.mark.parametrize("name", ["hardnet"] + NAS_NAMES)
+@pytest.mark.parametrize("name", ["hardnet"] + NAS_NAMES + FDL_NAMES)
 def test_module_torch_path_matches_reference(name):
     m, fx, _ = build_module(name)
     with torch.no_grad():
@@ -114,3 +116,25 @@ def test_fpr95_known_answers():
     assert got == pytest.approx(1.0 / 3.0) and got == float(fx["fpr_kat"])
     got = O.error_rate_at_95_recall(fx["fpr_labels"], 1.0 / (fx["fpr_dists"] + 1e-8))
     assert got == float(fx["fpr"])
+
+
+@pytest.mark.parametrize("name", FDL_NAMES)
+def test_fdl_edge_outputs_finite(name):
+    """Zero / constant patches (std == 0) stay finite through input_norm's eps and the
+    eps-free torch.norm (the head's output is never the zero vector)."""
+    fx = load(name)
+    assert np.isfinite(fx["y_edge"]).all() and np.isfinite(fx["y"]).all()
+
+
+def test_state_dict_layout_fdl():
+    """Index layout of HardNetNeiMask.features (latency/NASNet/model/des.py:13-36,
+    latency/NASNet_0.1/model/des.py:17-29)."""
+    from hardnetnas_amd.model import HardNetNeiMask
+    k1 = list(HardNetNeiMask(variant="NASNet").state_dict().keys())
+    assert k1[:4] == ["features.0.weight", "features.0.bias", "features.1.running_mean",
+                      "features.1.running_var"]
+    assert "features.8.pw.conv.weight" in k1 and "features.11.weight" in k1
+    assert "features.12.running_var" in k1 and "features.11.bias" not in k1
+    k2 = list(HardNetNeiMask(variant="NASNet_0.1").state_dict().keys())
+    assert k2[2] == "features.3.conv.conv.weight" and "features.7.weight" in k2
+    assert "features.10.pwl.bn.running_var" not in k2 and "features.6.pwl.bn.running_var" in k2
