@@ -16,7 +16,7 @@ Extra objects on the JSON line:
   cpu_baseline  the torch-CPU restatement of the same forward (oracle/), rank 0 at
                 N = 1 only, on a bounded sample.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--model hardnet|wang2|...]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--model hardnet|wang2|...|fdl_NASNet|fdl_NASNet_01]
 For N > 1 launch with torch.distributed.run (one process per GPU).
 """
 from __future__ import annotations
@@ -38,7 +38,7 @@ sys.path.insert(0, ROOT)
 from hardnetnas_amd import arch as A  # noqa: E402
 from hardnetnas_amd import synth  # noqa: E402
 from hardnetnas_amd._native import NativeModel  # noqa: E402
-from hardnetnas_amd.model import HardNet, HardNetNAS  # noqa: E402
+from hardnetnas_amd.model import HardNet, HardNetNAS, HardNetNeiMask  # noqa: E402
 
 METRIC = "Mpatches/s (32×32→128-D) at 1/2/4/8 MI355X; HPatches FPR95 parity"
 PEAK_MFMA_BF16 = 2500.0           # TFLOP/s dense bf16 (MI355X_MICROARCH.md)
@@ -99,12 +99,29 @@ def nas_stage_bytes(ops) -> dict:
     return out
 
 
+# FDLNet HardNetNeiMask descriptors (bench --model fdl_NASNet | fdl_NASNet_01)
+FDL_MODELS = {"fdl_NASNet": "NASNet", "fdl_NASNet_01": "NASNet_0.1"}
+
+
+def fdl_stage_bytes(name: str) -> dict:
+    """Algorithmic HBM bytes per patch of each FDL stage: the fused front (patch in, 8x8x64
+    out), the three fused IRF blocks (x in + y out), the head (4x4x128 in, 128 out)."""
+    irf, hw = 0, 8
+    for ci, co, s in A.FDL_LAYERS:
+        irf += 4 * (ci * hw * hw + co * (hw // s) ** 2)
+        hw //= s
+    return {"front": 4096 + 4 * 64 * 64, "irf": irf, "head": 4 * (128 * 16 + 128)}
+
+
 def build_model(name: str):
     """Synthetic weights (splitmix64 seed 1234) + the calibrated BN statistics committed
     with the golden fixtures (tests/golden/*.npz, data only)."""
-    m = HardNet() if name == "hardnet" else HardNetNAS(name)
-    fx = np.load(os.path.join(ROOT, "tests", "golden",
-                              ("hardnet" if name == "hardnet" else "nas_" + name) + ".npz"))
+    if name in FDL_MODELS:
+        m, fxname = HardNetNeiMask(variant=FDL_MODELS[name]), name
+    else:
+        m = HardNet() if name == "hardnet" else HardNetNAS(name)
+        fxname = "hardnet" if name == "hardnet" else "nas_" + name
+    fx = np.load(os.path.join(ROOT, "tests", "golden", fxname + ".npz"))
     sd = m.state_dict()
     tmpl = {k: tuple(v.shape) for k, v in sd.items()}
     w = synth.synth_state_dict(tmpl, 1234)
@@ -126,6 +143,8 @@ def synth_input_on_device(b: int, device, seed: int) -> torch.Tensor:
 
 
 def flop_per_patch(name: str) -> int:
+    if name in FDL_MODELS:
+        return 2 * A.fdl_macs(FDL_MODELS[name])
     return 2 * (A.hardnet_macs() if name == "hardnet" else A.nas_macs(name))
 
 
@@ -143,6 +162,8 @@ def cpu_baseline(name: str, model, seconds: float = 12.0):
         with torch.no_grad():
             if name == "hardnet":
                 O.hardnet_forward(p, x)
+            elif name in FDL_MODELS:
+                O.fdl_forward(p, FDL_MODELS[name], x)
             else:
                 O.nas_forward(p, model.arch_ops, x)
 
@@ -252,7 +273,8 @@ def main():
         else:
             # NAS: HBM-bound fp32 kernels; a stage class aggregates its launches (e.g. every
             # pw of the 6 blocks), so use its summed algorithmic bytes / summed device time
-            per_patch = nas_stage_bytes(args.model).get(dom, 0)
+            per_patch = (fdl_stage_bytes(args.model) if args.model in FDL_MODELS
+                         else nas_stage_bytes(args.model)).get(dom, 0)
             alg = per_patch * b / launches_per_step
             bound, peak, unit = "hbm", PEAK_HBM, "GB/s"
             achieved = per_patch * b * args.steps / (dom_ms * 1e-3) / 1e9
@@ -275,6 +297,8 @@ def main():
             "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": ("Stock HardNet forward" if args.model == "hardnet"
+                                    else f"FDLNet HardNetNeiMask {FDL_MODELS[args.model]} forward"
+                                    if args.model in FDL_MODELS
                                     else f"hardnetNAS {args.model} forward")
                        + f", {b} synthetic 32x32 patches per GPU"
                        + (" (BASELINE config 4 per-rank shard)" if world > 1 and b == CONFIG4_PER_RANK else "")
@@ -282,7 +306,8 @@ def main():
                        "model": args.model, "global_batch": b * world, "per_gpu_batch": b,
                        "parallelism": f"dp{world}",
                        "precision": "bf16x3 split-precision MFMA, fp32 accumulate" if args.model == "hardnet"
-                       else "fp16x3 split-precision MFMA for 1x1 convs and head, fp32 VALU depthwise",
+                       else "fp16x3 split-precision MFMA for 1x1 convs and head, fp32 VALU depthwise"
+                       + (" and front" if args.model in FDL_MODELS else ""),
                        "flop_per_patch": flop_per_patch(args.model)},
             "roofline": roof,
             "cpu_baseline": None,

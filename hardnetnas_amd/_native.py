@@ -25,6 +25,8 @@ _lib_lock = threading.Lock()
 
 HN_KIND_HARDNET = 0
 HN_KIND_NAS = 1
+HN_KIND_FDL_NASNET = 2
+HN_KIND_FDL_NASNET01 = 3
 HN_MAX_LAYERS = 8
 
 
@@ -125,22 +127,34 @@ def nas_desc(ops: List[str], layers=None, input_norm_eps: float = -1.0,
     return d
 
 
+def fdl_desc(variant: str = "NASNet") -> HnArchDesc:
+    """FDLNet HardNetNeiMask (latency/NASNet{,_0.1}/model/des.py): the fixed front is implied
+    by the kind; the three IRFBlocks are described like NAS layers."""
+    d = nas_desc(A.FDL_OPS, A.FDL_LAYERS, input_norm_eps=A.FDL_INPUT_NORM_EPS, l2_eps=0.0)
+    d.kind = HN_KIND_FDL_NASNET if variant == "NASNet" else HN_KIND_FDL_NASNET01
+    return d
+
+
 def state_dict_blob(sd: Dict[str, torch.Tensor]) -> np.ndarray:
     """Concatenate every float tensor of a state_dict in state_dict order, skipping
     ``num_batches_tracked``.  This is exactly the order hn_create parses:
       HardNet: features.{0,3,...,19}.weight followed by the BN running_mean/var;
       NAS:     first.conv/bn(w,b,mean,var), per block pw/dw/pwl ConvBNRelu (and
                se4.op.{1,3}.{weight,bias}) or the skip's 1x1 ConvBNRelu, then
-               last_stages.conv_k1.weight + last_stages.batchnorm running stats."""
+               last_stages.conv_k1.weight + last_stages.batchnorm running stats;
+      FDL:     features.0.{weight,bias}, the front's BN stats / 1x1 ConvBN(Relu)s, the
+               IRFBlocks as for NAS, the head conv weight + BN running stats."""
     parts = [v.detach().to("cpu", torch.float32).contiguous().reshape(-1).numpy()
              for k, v in sd.items() if not k.endswith("num_batches_tracked")]
     return np.ascontiguousarray(np.concatenate(parts), dtype=np.float32)
 
 
 def desc_for_module(module) -> HnArchDesc:
-    from .model import HardNet, HardNetNAS
+    from .model import HardNet, HardNetNAS, HardNetNeiMask
     if isinstance(module, HardNet):
         return hardnet_desc(module.input_norm_eps, module.l2_eps)
+    if isinstance(module, HardNetNeiMask):
+        return fdl_desc(module.variant)
     if isinstance(module, HardNetNAS):
         return nas_desc(module.arch_ops, module.layers)
     raise TypeError(type(module))

@@ -152,6 +152,7 @@ struct hn_model {
   std::vector<void*> allocs;
   HardnetDev hd;
   float *stem_w = nullptr, *stem_b = nullptr;  // NAS stem
+  float *fdl_w1 = nullptr, *fdl_b1 = nullptr, *fdl_w2 = nullptr, *fdl_b2 = nullptr;  // FDL front 1x1s
   std::vector<NasLayer> layers;
   float *head_w = nullptr, *head_b = nullptr;  // NAS head
   uint16_t* head_pack = nullptr;               // NAS head as fp16x3 MFMA B operand (K = 2048)
@@ -191,10 +192,11 @@ struct hn_model {
 static int check_desc(const hn_arch_desc* d) {
   if (!d) return fail(HN_ERR_ARG, "desc is NULL");
   if (d->kind == HN_KIND_HARDNET) return HN_OK;
-  if (d->kind != HN_KIND_NAS) return fail(HN_ERR_ARG, "unknown desc->kind");
+  const bool fdl = d->kind == HN_KIND_FDL_NASNET || d->kind == HN_KIND_FDL_NASNET01;
+  if (d->kind != HN_KIND_NAS && !fdl) return fail(HN_ERR_ARG, "unknown desc->kind");
   if (d->n_layers < 1 || d->n_layers > HN_MAX_LAYERS)
     return fail(HN_ERR_ARG, "n_layers out of range");
-  int hw = 32, c = 32;
+  int hw = fdl ? 8 : 32, c = fdl ? 64 : 32;  // FDL: the fixed front leaves 8x8x64
   for (int i = 0; i < d->n_layers; ++i) {
     if (d->op[i] < 0 || d->op[i] >= 17) return fail(HN_ERR_ARG, "op index out of range");
     if (d->c_in[i] != c) return fail(HN_ERR_ARG, "c_in does not chain");
@@ -205,6 +207,7 @@ static int check_desc(const hn_arch_desc* d) {
     c = d->c_out[i];
   }
   if (hw != 4) return fail(HN_ERR_ARG, "NAS head expects a 4x4 final map (SEARCH_SPACE2)");
+  if (fdl && c != 128) return fail(HN_ERR_ARG, "FDL head expects 128 channels (des.py)");
   return HN_OK;
 }
 
@@ -233,6 +236,10 @@ extern "C" int hn_param_count(const hn_arch_desc* desc, size_t* n_out) {
     return HN_OK;
   }
   size_t n = 32 * 9 + 4 * 32;  // first: ConvBNRelu(1, 32, 3)
+  if (desc->kind == HN_KIND_FDL_NASNET)  // des.py:14-24: stem (+bias) + BN stats, 1x1 32 + BN, 1x1 64 + BN
+    n = 32 * 9 + 32 + 2 * 32 + 32 * 32 + 4 * 32 + 64 * 32 + 4 * 64;
+  else if (desc->kind == HN_KIND_FDL_NASNET01)  // stem (+bias), Identity(32, 64, 2) ConvBNRelu
+    n = 32 * 9 + 32 + 64 * 32 + 4 * 64;
   for (int i = 0; i < desc->n_layers; ++i) n += nas_layer_params(desc, i);
   n += (size_t)128 * desc->c_out[desc->n_layers - 1] * 16 + 2 * 128;  // head conv + BN stats
   *n_out = n;
@@ -438,21 +445,73 @@ static int take_cbr(hn_model* m, Cursor& cur, int cout, size_t per_out, Folded* 
   return HN_OK;
 }
 
+static int build_nas_layers(hn_model* m, Cursor& cur, int hw, size_t maxf);
+
+// stem [32][9] -> [tap][32] for the VALU stem / front kernels
+static std::vector<float> stem_taps(const std::vector<float>& w) {
+  std::vector<float> sw(9 * 32);
+  for (int n = 0; n < 32; ++n)
+    for (int t = 0; t < 9; ++t) sw[t * 32 + n] = w[n * 9 + t];
+  return sw;
+}
+
 static int build_nas(hn_model* m, Cursor& cur) {
-  const hn_arch_desc& d = m->desc;
   int rc;
   Folded f;
   if ((rc = take_cbr(m, cur, 32, 9, &f))) return rc;
-  {
-    std::vector<float> sw(9 * 32);
-    for (int n = 0; n < 32; ++n)
-      for (int t = 0; t < 9; ++t) sw[t * 32 + n] = f.w[n * 9 + t];
-    if ((rc = m->upload(sw, &m->stem_w))) return rc;
-    if ((rc = m->upload(f.b, &m->stem_b))) return rc;
-    if (!m->no_front && (rc = m->upload(pack_front_stem(f), &m->front_spack))) return rc;
+  if ((rc = m->upload(stem_taps(f.w), &m->stem_w))) return rc;
+  if ((rc = m->upload(f.b, &m->stem_b))) return rc;
+  if (!m->no_front && (rc = m->upload(pack_front_stem(f), &m->front_spack))) return rc;
+  return build_nas_layers(m, cur, 32, 32 * 32 * 32);
+}
+
+// FDLNet HardNetNeiMask (des.py): the front's parameters in state_dict order, BN folded
+// (in double) into the conv before it; the stem keeps its conv bias.
+static int build_fdl(hn_model* m, Cursor& cur) {
+  const bool v0 = m->desc.kind == HN_KIND_FDL_NASNET;
+  const float* w0 = cur.take(32 * 9);
+  const float* b0 = cur.take(32);
+  if (!cur.ok) return fail(HN_ERR_ARG, "host_params too short");
+  Folded s;
+  if (v0) {  // features.1: BatchNorm2d(32, affine=False) on conv + bias
+    const float* mu = cur.take(32);
+    const float* var = cur.take(32);
+    if (!cur.ok) return fail(HN_ERR_ARG, "host_params too short");
+    s = fold(w0, 9, 32, nullptr, nullptr, mu, var, m->desc.bn_eps);
+    for (int c = 0; c < 32; ++c)  // bias: (b - mu) * sc, in double
+      s.b[c] = (float)(((double)b0[c] - (double)mu[c]) / std::sqrt((double)var[c] + (double)m->desc.bn_eps));
+  } else {
+    s.w.assign(w0, w0 + 32 * 9);
+    s.b.assign(b0, b0 + 32);
   }
-  size_t maxf = 32 * 32 * 32;
-  int hw = 32;
+  int rc;
+  if ((rc = m->upload(stem_taps(s.w), &m->stem_w))) return rc;
+  if ((rc = m->upload(s.b, &m->stem_b))) return rc;
+  Folded f;
+  if (v0) {
+    // features.2 (Conv 1x1 s2 32 -> 32) + features.3 (BN): weight, then gamma, beta, mean, var
+    const float* w = cur.take(32 * 32);
+    const float* g = cur.take(32);
+    const float* be = cur.take(32);
+    const float* mu = cur.take(32);
+    const float* var = cur.take(32);
+    if (!cur.ok) return fail(HN_ERR_ARG, "host_params too short");
+    f = fold(w, 32, 32, g, be, mu, var, m->desc.bn_eps);
+    if ((rc = m->upload(transpose_pw(f.w, 32, 32), &m->fdl_w1))) return rc;
+    if ((rc = m->upload(f.b, &m->fdl_b1))) return rc;
+  }
+  // NASNet: features.5 + features.6; NASNet_0.1: features.3.conv.{conv,bn} -- same order
+  if ((rc = take_cbr(m, cur, 64, 32, &f))) return rc;
+  if ((rc = m->upload(transpose_pw(f.w, 64, 32), &m->fdl_w2))) return rc;
+  if ((rc = m->upload(f.b, &m->fdl_b2))) return rc;
+  return build_nas_layers(m, cur, 8, 8 * 8 * 64);
+}
+
+static int build_nas_layers(hn_model* m, Cursor& cur, int hw, size_t maxf) {
+  const hn_arch_desc& d = m->desc;
+  const bool fdl = d.kind != HN_KIND_NAS;
+  int rc;
+  Folded f;
   for (int i = 0; i < d.n_layers; ++i) {
     NasLayer L;
     const OpSpec& s = kOps[d.op[i]];
@@ -492,7 +551,8 @@ static int build_nas(hn_model* m, Cursor& cur) {
         if ((rc = m->upload(b, &L.front_b))) return rc;
         m->front = 1;
       }
-      const bool irf = i > 0 && !m->no_irf && hn_irf_supported(L.cin, L.cout, L.hin, L.stride, L.k, L.mid);
+      const bool irf = (i > 0 || fdl) && !m->no_irf &&
+                       hn_irf_supported(L.cin, L.cout, L.hin, L.stride, L.k, L.mid);
       if (irf) {
         const int g = L.g, cg = L.mid / g;
         auto src = [&](int d) { return g > 1 ? (d % g) * cg + d / g : d; };  // ChannelShuffle
@@ -584,7 +644,9 @@ extern "C" int hn_create(const hn_arch_desc* desc, const float* host_params, siz
   }
   (void)hipGetDevice(&m->device);
   Cursor cur{host_params, n_params};
-  rc = desc->kind == HN_KIND_HARDNET ? build_hardnet(m, cur) : build_nas(m, cur);
+  rc = desc->kind == HN_KIND_HARDNET ? build_hardnet(m, cur)
+       : desc->kind == HN_KIND_NAS    ? build_nas(m, cur)
+                                      : build_fdl(m, cur);
   if (!rc && cur.i != n_params) rc = fail(HN_ERR_ARG, "host_params not fully consumed");
   if (rc) {
     delete m;
@@ -665,7 +727,10 @@ static int forward_nas(hn_model* m, const float* in, int P, float* out, float* w
   float* y = ws + 3 * per;
   const float ineps = m->desc.input_norm_eps;
   size_t first = 0;
-  if (m->front) {
+  if (m->desc.kind != HN_KIND_NAS) {  // FDLNet front (des.py) -> 8x8x64
+    const HnFdlFrontArgs fa{in, x, m->stem_w, m->stem_b, m->fdl_w1, m->fdl_b1, m->fdl_w2, m->fdl_b2};
+    STAGE("front", hn_launch_fdl_front(fa, P, m->desc.kind == HN_KIND_FDL_NASNET ? 0 : 1, ineps, st));
+  } else if (m->front) {
     const NasLayer& L = m->layers[0];
     const bool mp = m->front == 2;
     const HnFrontArgs fa{in, x, reinterpret_cast<const uint4*>(m->front_spack), m->stem_b,

@@ -54,6 +54,15 @@ struct HnFrontArgs {
 bool hn_front_supported(int k, int mid);
 hipError_t hn_launch_front(const HnFrontArgs& a, int P, int k, int mid, bool maxpool, bool norm,
                            float eps, hipStream_t st);
+// FDLNet HardNetNeiMask front (32x32 patch -> 8x8x64), hn_fdl.hip; mode 0 = NASNet, 1 = NASNet_0.1
+struct HnFdlFrontArgs {
+  const float* in;
+  float* out;
+  const float *stem_w, *stem_b;  // [9][32], [32]
+  const float *w1, *b1;          // [32][32], [32] (mode 0)
+  const float *w2, *b2;          // [32][64], [64]
+};
+hipError_t hn_launch_fdl_front(const HnFdlFrontArgs& a, int P, int mode, float eps, hipStream_t st);
 // fused IRF block (pw -> dw -> pwl [+ residual]) for layers 1..5, hn_irf.hip
 struct HnIrfArgs {
   const float* x;

@@ -43,8 +43,10 @@ enum hn_status {
 };
 
 enum hn_kind {
-  HN_KIND_HARDNET = 0, /* stock HardNet, hardnet/HardNet.py:275-304 */
-  HN_KIND_NAS = 1      /* sampled hardnetNAS net, model_supernet.py:53-85 */
+  HN_KIND_HARDNET = 0,      /* stock HardNet, hardnet/HardNet.py:275-304 */
+  HN_KIND_NAS = 1,          /* sampled hardnetNAS net, model_supernet.py:53-85 */
+  HN_KIND_FDL_NASNET = 2,   /* FDLNet HardNetNeiMask, FDLNet-master/latency/NASNet/model/des.py:8-55 */
+  HN_KIND_FDL_NASNET01 = 3  /* FDLNet HardNetNeiMask, FDLNet-master/latency/NASNet_0.1/model/des.py:10-55 */
 };
 
 #define HN_MAX_LAYERS 8
@@ -53,6 +55,9 @@ enum hn_kind {
  *  HardNet: only kind, input_norm_eps, l2_eps, bn_eps are read.
  *  NAS:     op[i] = index into CANDIDATE_BLOCKS (lookup_table_builder.py:18-20);
  *           c_in/c_out/stride from SEARCH_SPACE2 (lookup_table_builder.py:22-45).
+ *  FDL:     a fixed front (des.py) to 8x8x64, then op/c_in/c_out/stride of its IRFBlocks in the
+ *           same CANDIDATE_BLOCKS vocabulary (NASNet: ir_k5_e1 64->64, ir_k3_e3 64->128 s2,
+ *           ir_k5_s2 128->128), then the 4x4 head; input_norm_eps 1e-8, l2_eps 0.
  *  input_norm_eps < 0 disables input_norm (the NAS nets have none);
  *  l2_eps: HardNet 1e-10 inside the sqrt (Utils.py:18); NAS 0 (torch.norm, model_supernet.py:84). */
 typedef struct hn_arch_desc {
@@ -76,7 +81,7 @@ int hn_param_count(const hn_arch_desc* desc, size_t* n_out);
  * host_params is the concatenation, in state_dict order, of every conv weight and
  * BatchNorm tensor of the module (HardNet: for each of the 7 convs
  *   features.{c}.weight, features.{b}.running_mean, features.{b}.running_var;
- * NAS: see hardnetnas_amd/_native.py::state_dict_blob, which documents the order).
+ * NAS / FDL: see hardnetnas_amd/_native.py::state_dict_blob, which documents the order).
  * BatchNorm (eval) is folded into the conv weights/bias here, once. */
 int hn_create(const hn_arch_desc* desc, const float* host_params, size_t n_params,
               hn_model** out);

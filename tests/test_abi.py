@@ -49,6 +49,21 @@ def test_param_count_nas_matches_state_dict(name):
     assert n.value == blob.size
 
 
+@pytest.mark.parametrize("variant", A.FDL_VARIANTS)
+def test_param_count_fdl_matches_state_dict(variant):
+    """FDLNet HardNetNeiMask: the front + IRFBlock + head parameters hn_create parses equal
+    the module's state_dict blob (reference layout, tests/test_oracle_golden.py)."""
+    from hardnetnas_amd.model import HardNetNeiMask
+    m = HardNetNeiMask(variant=variant)
+    n = ctypes.c_size_t()
+    d = N.desc_for_module(m)
+    assert d.kind == (N.HN_KIND_FDL_NASNET if variant == "NASNet" else N.HN_KIND_FDL_NASNET01)
+    assert N.load_library().hn_param_count(ctypes.byref(d), ctypes.byref(n)) == 0
+    assert n.value == N.state_dict_blob(m.state_dict()).size
+    d.c_in[0] = 32  # the FDL front leaves 64 channels
+    assert N.load_library().hn_param_count(ctypes.byref(d), ctypes.byref(n)) == 1
+
+
 def test_every_candidate_op_param_count():
     """Single-op archs for each of the 17 CANDIDATE_BLOCKS at every layer slot."""
     from hardnetnas_amd.model import HardNetNAS

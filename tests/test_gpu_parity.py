@@ -3,6 +3,7 @@
 Tolerances (BASELINE.json north_star: <= 1e-4 max abs on the 128-D descriptor):
   HardNet  -- bf16x3 split-precision MFMA: 1e-4 max abs vs the reference fp32 forward.
   NAS      -- fp16x3 MFMA 1x1 convs/head + fp32 depthwise: 2e-5 max abs (the old exact-fp32 budget).
+  FDL      -- FDLNet HardNetNeiMask: fp32 VALU front + the NAS kernels: 2e-5 max abs.
 """
 import os
 
@@ -10,7 +11,7 @@ import numpy as np
 import pytest
 import torch
 
-from fixtures import NAS_NAMES, build_module, load, golden_inputs
+from fixtures import FDL_NAMES, NAS_NAMES, build_module, load, golden_inputs
 from oracle import hardnet_oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -28,7 +29,7 @@ def _native_lib_loaded():
     return "libhardnet_mi355x.so" in maps
 
 
-@pytest.mark.parametrize("name", ["hardnet"] + NAS_NAMES)
+@pytest.mark.parametrize("name", ["hardnet"] + NAS_NAMES + FDL_NAMES)
 def test_forward_matches_reference_vectors(name, cuda_device):
     m, fx, _ = build_module(name)
     m = m.to(cuda_device)
@@ -46,7 +47,7 @@ def test_forward_matches_reference_vectors(name, cuda_device):
     assert np.abs(ye - fx["y_edge"]).max() <= _tol(name)
 
 
-@pytest.mark.parametrize("name", ["hardnet", "wang2"])
+@pytest.mark.parametrize("name", ["hardnet", "wang2", "fdl_NASNet_01"])
 @pytest.mark.parametrize("b", [1, 3, 63, 65, 130, 255])
 def test_ragged_batches(name, b, cuda_device):
     m, fx, _ = build_module(name)
@@ -333,3 +334,27 @@ def test_nas_unfused_irf_matches(name, cuda_device, monkeypatch):
     y = nm(x).cpu().numpy()
     assert "irf" not in nm.stage_times()
     assert np.abs(y - fx["y"]).max() <= NAS_TOL
+
+
+@pytest.mark.parametrize("name", FDL_NAMES)
+def test_fdl_runs_front_irf_head_and_matches_layerwise(name, cuda_device, monkeypatch):
+    """The FDL descriptor runs its fused front, the fused IRF blocks and the MFMA head; the
+    layer-by-layer pw/dw/pwl kernels (HN_NO_IRF=1) agree; a 3 000-patch run matches the
+    oracle on a sample."""
+    from hardnetnas_amd._native import NativeModel
+    m, fx, p = build_module(name)
+    x = torch.from_numpy(golden_inputs(fx)).to(cuda_device)
+    nm = NativeModel.from_module(m, cuda_device)
+    nm.set_profiling(True)
+    y = nm(x).cpu().numpy()
+    assert set(nm.stage_times()) == {"front", "irf", "head"}
+    assert np.abs(y - fx["y"]).max() <= NAS_TOL
+    monkeypatch.setenv("HN_NO_IRF", "1")
+    lw = NativeModel.from_module(m, cuda_device)
+    assert np.abs(lw(x).cpu().numpy() - y).max() <= NAS_TOL
+    from hardnetnas_amd import synth
+    xb = torch.from_numpy(synth.synth_patches(3000, 11))
+    yb = nm(xb.to(cuda_device)).cpu()
+    t = {k: torch.from_numpy(v) for k, v in p.items()}
+    ref = O.fdl_forward(t, fx["meta"]["variant"], xb[-200:])
+    assert float((yb[-200:] - ref).abs().max()) <= NAS_TOL
