@@ -664,24 +664,26 @@ extern "C" int hn_workspace_bytes(const hn_model* m, int64_t batch, size_t* byte
 }
 
 // Launch one stage; with profiling on, bracket it by a hipEvent pair on the same stream.
-#define STAGE(NAME, CALL)                                                                  \
+#define STAGE_ON(SS, NAME, CALL)                                                           \
   do {                                                                                     \
     hipEvent_t a_ = nullptr;                                                               \
     if (m->prof.on) {                                                                      \
       a_ = m->prof.get();                                                                  \
-      HIPCHK(hipEventRecord(a_, st));                                                      \
+      HIPCHK(hipEventRecord(a_, SS));                                                      \
     }                                                                                      \
     HIPCHK(CALL);                                                                          \
     if (m->prof.on) {                                                                      \
       hipEvent_t b_ = m->prof.get();                                                       \
-      HIPCHK(hipEventRecord(b_, st));                                                      \
+      HIPCHK(hipEventRecord(b_, SS));                                                      \
       m->prof.pend.push_back({m->prof.stage_id(NAME), a_, b_});                            \
     }                                                                                      \
   } while (0)
+#define STAGE(NAME, CALL) STAGE_ON(st, NAME, CALL)
 
-static int forward_hardnet(hn_model* m, const float* in, int P, float* out, float* ws,
+// pmax: the largest chunk of this call; the buffers keep the same offsets for every chunk
+static int forward_hardnet(hn_model* m, const float* in, int P, int pmax, float* out, float* ws,
                            hipStream_t st) {
-  const size_t per = m->ws_floats_per_patch * (size_t)P;
+  const size_t per = m->ws_floats_per_patch * (size_t)pmax;
   float* a0 = ws;
   float* a1 = ws + per;
   float* a2 = ws + 2 * per;
@@ -718,9 +720,9 @@ static int forward_hardnet(hn_model* m, const float* in, int P, float* out, floa
   return HN_OK;
 }
 
-static int forward_nas(hn_model* m, const float* in, int P, float* out, float* ws,
+static int forward_nas(hn_model* m, const float* in, int P, int pmax, float* out, float* ws,
                        hipStream_t st) {
-  const size_t per = m->ws_floats_per_patch * (size_t)P;
+  const size_t per = m->ws_floats_per_patch * (size_t)pmax;
   float* x = ws;
   float* t1 = ws + per;
   float* t2 = ws + 2 * per;
@@ -809,8 +811,9 @@ extern "C" int hn_forward(hn_model* m, const float* d_in, int64_t batch, float* 
     const float* in = d_in + off * 1024;
     float* out = d_out + off * 128;
     float* ws = static_cast<float*>(d_workspace);
-    const int rc = m->desc.kind == HN_KIND_HARDNET ? forward_hardnet(m, in, P, out, ws, st)
-                                                   : forward_nas(m, in, P, out, ws, st);
+    const int pmax = (int)std::min<int64_t>(m->chunk, batch);
+    const int rc = m->desc.kind == HN_KIND_HARDNET ? forward_hardnet(m, in, P, pmax, out, ws, st)
+                                                   : forward_nas(m, in, P, pmax, out, ws, st);
     if (rc) return rc;
   }
   return HN_OK;

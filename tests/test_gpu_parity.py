@@ -358,3 +358,4 @@ def test_fdl_runs_front_irf_head_and_matches_layerwise(name, cuda_device, monkey
     t = {k: torch.from_numpy(v) for k, v in p.items()}
     ref = O.fdl_forward(t, fx["meta"]["variant"], xb[-200:])
     assert float((yb[-200:] - ref).abs().max()) <= NAS_TOL
+
