@@ -56,7 +56,8 @@ HN_DEV uint2 pack_bf16x4(float a, float b, float c, float d, uint2& lo) {
 // W1 column slot of a1 column x (x = -1 .. 31): even (x + 1) -> (x + 1) / 2, odd -> 17 + x / 2
 HN_DEV int w1_slot(int x) { return ((x + 1) & 1) ? 17 + (x >> 1) : (x + 1) >> 1; }
 
-// ABL (ablation builds for profiling only; 0 in production): bit 3 skips P1 entirely,
+// ABL (ablation builds for profiling only; 0 in production): bit 5 reads every conv2 fragment
+// from tap 0 (L1-resident weights), bit 3 skips P1 entirely,
 // bit 4 skips the P2/P3 B-fragment LDS reads; bit 0 skips P1's MFMA work,
 // bit 1 skips P2's, bit 2 skips P3's (the phases still run their LDS traffic and barriers).
 //
@@ -149,6 +150,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, WP
   // conv2 A fragments are streamed from L2 per tap (2 taps ahead): the register file holds
   // both conv1 groups instead, so each P2 B fragment feeds two output groups
   auto w2_frag = [&](int tap, int g, int pl) {
+    if constexpr ((ABL & 32) != 0) tap = 0;  // timing only: L1-resident conv2 fragments
     int i = ((tap * 4 + cs2 * G2 + g) * 2 + pl) * 64 + lane;
     asm volatile("" : "+v"(i));  // keep the load here (not hoisted out of the patch loop)
     return w2p[i];
@@ -520,7 +522,7 @@ hipError_t hn_launch_c12(const float* in, float* out, const HardnetDev& d, int P
   if (P <= 0) return hipSuccess;
   // read per launch (tests switch them between models): HN_C12_ABL ablation bits (cfg 0 and 2)
   const char* ea = std::getenv("HN_C12_ABL");
-  const int abl = ea ? std::atoi(ea) & 31 : 0;
+  const int abl = ea ? std::atoi(ea) & 63 : 0;
   const char* ec = std::getenv("HN_C12_CFG");
   const int cfg = ec ? std::atoi(ec) : 12;  // same-box A/Bs: 12 2-4 % < 7 1.5 % < 2 4.5 % < 0
   if (cfg < 0 || cfg >= kC12Cfgs) return hipErrorInvalidValue;
@@ -568,6 +570,7 @@ hipError_t hn_launch_c12(const float* in, float* out, const HardnetDev& d, int P
         case 1: HN_C12_GO(1, 4, 2, 2, false, 2, true, 5); break;
         case 6: HN_C12_GO(6, 4, 2, 2, false, 2, true, 5); break;
         case 8: HN_C12_GO(8, 4, 2, 2, false, 2, true, 5); break;
+        case 32: HN_C12_GO(32, 4, 2, 2, false, 2, true, 5); break;
         default: return hipErrorInvalidValue;
       }
     } else {
