@@ -359,3 +359,48 @@ def test_fdl_runs_front_irf_head_and_matches_layerwise(name, cuda_device, monkey
     ref = O.fdl_forward(t, fx["meta"]["variant"], xb[-200:])
     assert float((yb[-200:] - ref).abs().max()) <= NAS_TOL
 
+
+
+@pytest.mark.parametrize("name,model", [("hardnet", "hardnet"), ("fdl_NASNet", "fdl_nasnet"),
+                                        ("wang2", "nas:1,4,14,13,4,0")])
+def test_c_abi_demo_program(name, model, tmp_path):
+    """hardnetnas_amd/lib/hn_cabi_demo (built by `make`): the forward driven through the C ABI
+    alone (hn_param_count / hn_create / hn_workspace_bytes / hn_forward + hipMalloc), in a
+    child process with no Python or torch -- the boundary a non-Python host would bind."""
+    import subprocess
+    from hardnetnas_amd import _native as N
+    exe = os.path.join(os.path.dirname(N.lib_path()), "hn_cabi_demo")
+    assert os.path.exists(exe), "build the library first (make -C hardnetnas_amd/csrc)"
+    m, fx, _ = build_module(name)
+    x = golden_inputs(fx)[:100]
+    N.state_dict_blob(m.state_dict()).tofile(tmp_path / "p.f32")
+    np.ascontiguousarray(x, dtype=np.float32).tofile(tmp_path / "x.f32")
+    r = subprocess.run([exe, model, str(tmp_path / "p.f32"), str(tmp_path / "x.f32"), "100",
+                        str(tmp_path / "y.f32")], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    y = np.fromfile(tmp_path / "y.f32", dtype=np.float32).reshape(100, 128)
+    assert np.abs(y - fx["y"][:100]).max() <= _tol(name)
+
+
+def test_forward_is_graph_capturable(cuda_device):
+    """The header's promise: hn_forward neither allocates nor synchronises, so a whole forward
+    (several chunks) can be captured once into a HIP graph and replayed on new inputs."""
+    from hardnetnas_amd._native import NativeModel
+    m, fx, _ = build_module("hardnet")
+    x = torch.from_numpy(golden_inputs(fx)).to(cuda_device)
+    nm = NativeModel.from_module(m, cuda_device)
+    ref = nm(x).clone()
+    static_x = torch.zeros_like(x)
+    out = torch.empty((x.shape[0], 128), device=cuda_device)
+    ws = torch.empty(nm.workspace_bytes(x.shape[0]), device=cuda_device, dtype=torch.uint8)
+    nm.forward(static_x, out=out, workspace=ws)  # warm-up: one-time launch attributes
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream(device=cuda_device)
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            nm.forward(static_x, out=out, workspace=ws)
+    static_x.copy_(x)
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
