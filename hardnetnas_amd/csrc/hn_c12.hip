@@ -56,7 +56,8 @@ HN_DEV uint2 pack_bf16x4(float a, float b, float c, float d, uint2& lo) {
 // W1 column slot of a1 column x (x = -1 .. 31): even (x + 1) -> (x + 1) / 2, odd -> 17 + x / 2
 HN_DEV int w1_slot(int x) { return ((x + 1) & 1) ? 17 + (x >> 1) : (x + 1) >> 1; }
 
-// ABL (ablation builds for profiling only; 0 in production): bit 5 reads every conv2 fragment
+// ABL (ablation builds for profiling only; 0 in production): bit 6 = phase time stamps (below),
+// bit 5 reads every conv2 fragment
 // from tap 0 (L1-resident weights), bit 3 skips P1 entirely,
 // bit 4 skips the P2/P3 B-fragment LDS reads; bit 0 skips P1's MFMA work,
 // bit 1 skips P2's, bit 2 skips P3's (the phases still run their LDS traffic and barriers).
@@ -191,12 +192,23 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, WP
       *reinterpret_cast<uint4*>(o + 64 + 16 * k) = make_uint4(lo[k].x, lo[k].y, lo[k + 1].x, lo[k + 1].y);
     }
   };
+  // ABL bit 6 (timing only): per-wave s_memtime stamps at the phase boundaries of every band of
+  // the workgroup's third patch, written past the launch's a2 output (out + P * 16384 floats: the
+  // workspace buffer holds 32768 floats per patch); tools/c12_timeline.py
+  long long* const dbg =
+      reinterpret_cast<long long*>(out + (long)P * 16384) + ((long)blockIdx.x * NW + w) * 128;
+  long patch_ts = -1;
+#define HN_C12_TS(K)                                                                        \
+  if constexpr ((ABL & 64) != 0) {                                                          \
+    if (patch == patch_ts && lane == 0) dbg[band * 6 + (K)] = (long long)__builtin_amdgcn_s_memtime(); \
+  }
   // the next patch's pixels are fetched one patch ahead
   constexpr int PPT = 1024 / (NW * 64);  // patch pixels per thread (2 or 4)
   typedef float pxv __attribute__((ext_vector_type(PPT)));
   pxv vnext = reinterpret_cast<const pxv*>(in + pb * 1024)[t];
 #pragma unroll 1
   for (long patch = pb; patch < pe; ++patch) {
+    if constexpr ((ABL & 64) != 0) patch_ts = pb + 2;
     {
       const pxv v = vnext;
       if (patch + 1 < pe) vnext = reinterpret_cast<const pxv*>(in + (patch + 1) * 1024)[t];
@@ -233,6 +245,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, WP
     }
 #pragma unroll 1
   for (int band = 0; band < 16 / RB2; ++band) {
+    HN_C12_TS(0);
     const int r0 = band * RB2;
     // PRIO & 3: wave priority raised over P1 -- a short serial latency chain that every wave of
     // the workgroup waits for at the next barrier -- so its VALU and MFMA issue ahead of the
@@ -263,8 +276,10 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, WP
       const f32x16 c0 = (ABL & 1) ? f32x16{} : mfma3(as_bf16x8(sa0), as_bf16x8(sa1), xh, xl, f32x16{});
       p1_store(y, c0);
     }
+    HN_C12_TS(1);
     if constexpr (PRIO != 0) __builtin_amdgcn_s_setprio(0);
     __syncthreads();
+    HN_C12_TS(2);
 
     // ---- P2: conv1 -> W1 ring (units: new a1 row, both 16-pixel halves; G1 groups) ----------
     // band b: a1 rows 2 RB2 b .. + 2 RB2 - 1 (+ row -1, conv2's zero padding, in band 0).  The two halves
@@ -382,6 +397,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, WP
         }
       }
     }
+    HN_C12_TS(3);
     // the first WA taps of this wave's conv2 fragments, in flight across the barrier
     uint4 wq[WA + 1][G2][2];
 #pragma unroll
@@ -391,6 +407,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, WP
 #pragma unroll
         for (int pl = 0; pl < 2; ++pl) wq[tap][g][pl] = w2_frag(tap, g, pl);
     __syncthreads();
+    HN_C12_TS(4);
 
     if constexpr ((PRIO & 4) != 0) __builtin_amdgcn_s_setprio(PRIO & 3);  // P3 too (P3 -> P1 -> barrier)
     // ---- P3: conv2 (stride 2) -> a2 in HBM (units: output rows oy and oy + 2 together; this
@@ -490,11 +507,10 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, WP
 #pragma unroll
         for (int g = 0; g < G2; ++g)
           *reinterpret_cast<f32x4v*>(o + 16 * (cs2 * G2 + g)) =
-              __builtin_elementwise_max(
-                  acc[ry][g],
-                  f32x4v{});
+              __builtin_elementwise_max(acc[ry][g], f32x4v{});
       }
     }
+    HN_C12_TS(5);
     // no barrier: the next band's P1 writes only W0, which P3 does not read; its first
     // barrier orders this P3's W1 reads before the next P2's W1 writes
   }  // band
@@ -522,7 +538,7 @@ hipError_t hn_launch_c12(const float* in, float* out, const HardnetDev& d, int P
   if (P <= 0) return hipSuccess;
   // read per launch (tests switch them between models): HN_C12_ABL ablation bits (cfg 0 and 2)
   const char* ea = std::getenv("HN_C12_ABL");
-  const int abl = ea ? std::atoi(ea) & 63 : 0;
+  const int abl = ea ? std::atoi(ea) & 127 : 0;
   const char* ec = std::getenv("HN_C12_CFG");
   const int cfg = ec ? std::atoi(ec) : 12;  // same-box A/Bs: 12 2-4 % < 7 1.5 % < 2 4.5 % < 0
   if (cfg < 0 || cfg >= kC12Cfgs) return hipErrorInvalidValue;
@@ -571,6 +587,7 @@ hipError_t hn_launch_c12(const float* in, float* out, const HardnetDev& d, int P
         case 6: HN_C12_GO(6, 4, 2, 2, false, 2, true, 5); break;
         case 8: HN_C12_GO(8, 4, 2, 2, false, 2, true, 5); break;
         case 32: HN_C12_GO(32, 4, 2, 2, false, 2, true, 5); break;
+        case 64: HN_C12_GO(64, 4, 2, 2, false, 2, true, 5); break;
         default: return hipErrorInvalidValue;
       }
     } else {

@@ -1,0 +1,44 @@
+"""k_c12 phase timeline from the HN_C12_ABL=64 timing build (s_memtime stamps per wave at the
+band phase boundaries of each workgroup's third patch).  Prints the median cycles per phase.
+usage (MI355X): python tools/c12_timeline.py"""
+import os
+import sys
+
+os.environ["HN_C12_ABL"] = "64"
+os.environ.setdefault("HN_C12_CFG", "12")
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from hardnetnas_amd._native import NativeModel  # noqa: E402
+
+P = 16384  # one sub-chunk = one k_c12 launch
+dev = torch.device("cuda:0")
+nm = NativeModel.from_module(bench.build_model("hardnet"), dev)
+x = bench.synth_input_on_device(P, dev, 5)
+ws = torch.zeros(nm.workspace_bytes(P), dtype=torch.uint8, device=dev)
+out = torch.empty((P, 128), device=dev)
+for _ in range(2):
+    nm.forward(x, out=out, workspace=ws)
+torch.cuda.synchronize()
+per = 32768 * P                      # floats per workspace buffer (ws_floats_per_patch * P)
+off = (2 * per + P * 16384) * 4      # a2 + the launch's c12 output
+nwg, nw = 512, 4
+raw = ws[off: off + nwg * nw * 128 * 8].view(torch.int64).cpu().numpy().reshape(nwg, nw, 128)
+t = raw[:, :, :48].reshape(nwg, nw, 8, 6).astype(np.float64)
+ok = (t > 0).all(axis=(1, 2, 3))
+t = t[ok]
+names = ["P1", "barrier 1", "P2 (+epilogue)", "conv2 frag loads + barrier 2", "P3 (+stores)"]
+d = np.diff(t, axis=3)                           # [wg, wave, band, 5]
+nxt = t[:, :, 1:, 0] - t[:, :, :-1, 5]           # P3 end -> next band start
+print(f"{ok.sum()} workgroups; median cycles per band per wave (s_memtime):")
+for i, n in enumerate(names):
+    print(f"  {n:32s} {np.median(d[..., i]):8.0f}   (p90 {np.percentile(d[..., i], 90):8.0f})")
+print(f"  {'band end -> next band':32s} {np.median(nxt):8.0f}")
+band = t[:, :, 1:, 0] - t[:, :, :-1, 0]
+print(f"  {'band total':32s} {np.median(band):8.0f}")
+print("per band index (median over workgroups, wave 0):")
+for b in range(8):
+    print("  band", b, " ".join(f"{np.median(d[:, 0, b, i]):7.0f}" for i in range(5)))
