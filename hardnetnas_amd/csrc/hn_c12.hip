@@ -199,8 +199,12 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, WP
       reinterpret_cast<long long*>(out + (long)P * 16384) + ((long)blockIdx.x * NW + w) * 128;
   long patch_ts = -1;
 #define HN_C12_TS(K)                                                                        \
-  if constexpr ((ABL & 64) != 0) {                                                          \
+  if constexpr ((ABL & 192) != 0) {                                                          \
     if (patch == patch_ts && lane == 0) dbg[band * 6 + (K)] = (long long)__builtin_amdgcn_s_memtime(); \
+  }
+#define HN_C12_TS2(K)                                                                       \
+  if constexpr ((ABL & 128) != 0) {                                                         \
+    if (patch == patch_ts && lane == 0) dbg[48 + band * 4 + (K)] = (long long)__builtin_amdgcn_s_memtime(); \
   }
   // the next patch's pixels are fetched one patch ahead
   constexpr int PPT = 1024 / (NW * 64);  // patch pixels per thread (2 or 4)
@@ -208,7 +212,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, WP
   pxv vnext = reinterpret_cast<const pxv*>(in + pb * 1024)[t];
 #pragma unroll 1
   for (long patch = pb; patch < pe; ++patch) {
-    if constexpr ((ABL & 64) != 0) patch_ts = pb + 2;
+    if constexpr ((ABL & 192) != 0) patch_ts = pb + 2;
     {
       const pxv v = vnext;
       if (patch + 1 < pe) vnext = reinterpret_cast<const pxv*>(in + (patch + 1) * 1024)[t];
@@ -273,8 +277,19 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, WP
         xh[j] = (__bf16)xv[j];
         xl[j] = (__bf16)(xv[j] - (float)xh[j]);
       }
+      if constexpr ((ABL & 128) != 0) {  // sub-stamp a: operands read and split
+        asm volatile("" ::"v"(xh[0]), "v"(xl[7]));
+        HN_C12_TS2(0);
+      }
       const f32x16 c0 = (ABL & 1) ? f32x16{} : mfma3(as_bf16x8(sa0), as_bf16x8(sa1), xh, xl, f32x16{});
+      if constexpr ((ABL & 128) != 0) {  // sub-stamp b: the MFMA chain's result is available
+        float z = c0[0] + c0[15];
+        asm volatile("" : "+v"(z));
+        if (z == 1234.5f) dbg[127] = 0;
+        HN_C12_TS2(1);
+      }
       p1_store(y, c0);
+      HN_C12_TS2(2);  // sub-stamp c: epilogue issued (the stamp's wait also drains the LDS stores)
     }
     HN_C12_TS(1);
     if constexpr (PRIO != 0) __builtin_amdgcn_s_setprio(0);
@@ -538,7 +553,7 @@ hipError_t hn_launch_c12(const float* in, float* out, const HardnetDev& d, int P
   if (P <= 0) return hipSuccess;
   // read per launch (tests switch them between models): HN_C12_ABL ablation bits (cfg 0 and 2)
   const char* ea = std::getenv("HN_C12_ABL");
-  const int abl = ea ? std::atoi(ea) & 127 : 0;
+  const int abl = ea ? std::atoi(ea) & 255 : 0;
   const char* ec = std::getenv("HN_C12_CFG");
   const int cfg = ec ? std::atoi(ec) : 12;  // same-box A/Bs: 12 2-4 % < 7 1.5 % < 2 4.5 % < 0
   if (cfg < 0 || cfg >= kC12Cfgs) return hipErrorInvalidValue;
@@ -588,6 +603,7 @@ hipError_t hn_launch_c12(const float* in, float* out, const HardnetDev& d, int P
         case 8: HN_C12_GO(8, 4, 2, 2, false, 2, true, 5); break;
         case 32: HN_C12_GO(32, 4, 2, 2, false, 2, true, 5); break;
         case 64: HN_C12_GO(64, 4, 2, 2, false, 2, true, 5); break;
+        case 64 + 128: HN_C12_GO(192, 4, 2, 2, false, 2, true, 5); break;
         default: return hipErrorInvalidValue;
       }
     } else {

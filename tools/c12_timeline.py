@@ -4,7 +4,7 @@ usage (MI355X): python tools/c12_timeline.py"""
 import os
 import sys
 
-os.environ["HN_C12_ABL"] = "64"
+os.environ["HN_C12_ABL"] = os.environ.get("HN_C12_ABL", "64")
 os.environ.setdefault("HN_C12_CFG", "12")
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -42,3 +42,12 @@ print(f"  {'band total':32s} {np.median(band):8.0f}")
 print("per band index (median over workgroups, wave 0):")
 for b in range(8):
     print("  band", b, " ".join(f"{np.median(d[:, 0, b, i]):7.0f}" for i in range(5)))
+
+if os.environ["HN_C12_ABL"] == "192":  # P1 sub-stamps: band start, a, b, c, P1 end
+    raw2 = ws[off: off + nwg * nw * 128 * 8].view(torch.int64).cpu().numpy().reshape(nwg, nw, 128)
+    sub = raw2[:, :, 48:80].reshape(nwg, nw, 8, 4)[ok][:, :, 1:, :3].astype(np.float64)
+    t0 = t[:, :, 1:, 0]
+    marks = np.concatenate([t0[..., None], sub], axis=3)
+    dd = np.diff(marks, axis=3)
+    for i, n in enumerate(["P1 operands read + split", "P1 MFMA chain", "P1 epilogue + stores"]):
+        print(f"  {n:32s} {np.median(dd[..., i]):8.0f}")
