@@ -93,17 +93,25 @@ constexpr int conv_row_stride(int ncols, int wout, int s) {
   return rs;
 }
 
-template <int CIN, int COUT, int HIN, int S, int NP, int TR, int WM, int WN>
+// PX: bytes per window pixel per plane.  80 = 64 data + 16 pad (conflict-free by padding); 64 =
+// no pad, the 16-byte channel chunk q of window row wr stored at chunk q ^ ((wr / S) & 3), which
+// keeps the 32x32x16 operand reads and the producer stores conflict-free when a 32-pixel tile is
+// 4 output rows of 8 (its rows read window rows S yl + ky: distinct swizzles) -- 20 % less LDS.
+template <int CIN, int COUT, int HIN, int S, int NP, int TR, int WM, int WN, int PX = 80>
 struct ConvCfg {
   static constexpr int HOUT = HIN / S, WOUT = HOUT;
   static constexpr int RIN = (S == 1) ? TR + 2 : 2 * TR + 1;
   static constexpr int NCOLS = (S == 1) ? HIN + 2 : HIN + 1;
-  static constexpr int HALF = (NCOLS + 1) / 2;
+  // (64-byte layout: one spare slot between the even and odd columns, so that a producer store
+  // group's odd / even pixel pair never lands 512 bytes apart)
+  static constexpr int HALF = PX == 80 ? (NCOLS + 1) / 2 : (NCOLS + 1) / 2 + 1;
   static constexpr int BM = NP * TR * WOUT;
   static constexpr int RT = HOUT / TR;
   static constexpr int MT = BM / WM / 32, NT = COUT / WN / 32;
   static constexpr int NTOT = COUT / 32, NCC = CIN / 32;
-  static constexpr int RS = conv_row_stride(NCOLS, WOUT, S);
+  static_assert(PX == 80 || (PX == 64 && (S == 2 || HIN / S == 8)),
+                "the 64-byte swizzled layout: stride 2, or 8-wide output rows");
+  static constexpr int RS = PX == 80 ? conv_row_stride(NCOLS, WOUT, S) : (HALF + NCOLS / 2) * PX;
   static constexpr int PS = RIN * RS;
   static constexpr int PLANE = NP * PS;
   static constexpr int LDS = 2 * PLANE;
@@ -695,9 +703,9 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void k_conv_pipe(
 // barrier per stage.  For the HBM-heavy stride-2 layers this keeps ~UNITS*32 B per
 // workgroup in flight instead of one unit per K-step.
 // ------------------------------------------------------------------------------------
-template <int CIN, int COUT, int HIN, int S, int NP, int TR, int WM, int WN, bool STEM = false>
-struct WsCfg : ConvCfg<CIN, COUT, HIN, S, NP, TR, WM, WN> {
-  using B = ConvCfg<CIN, COUT, HIN, S, NP, TR, WM, WN>;
+template <int CIN, int COUT, int HIN, int S, int NP, int TR, int WM, int WN, bool STEM = false, int PX = 80>
+struct WsCfg : ConvCfg<CIN, COUT, HIN, S, NP, TR, WM, WN, PX> {
+  using B = ConvCfg<CIN, COUT, HIN, S, NP, TR, WM, WN, PX>;
   static constexpr int NWC = WM * WN, NWP = 4, NTHR = (NWC + NWP) * 64, PTHR = NWP * 64;
   static constexpr int UNITS = NP * B::RIN * B::NCOLS * 4;
   static constexpr int UPT = STEM ? 1 : (UNITS + PTHR - 1) / PTHR;
@@ -712,12 +720,14 @@ struct WsCfg : ConvCfg<CIN, COUT, HIN, S, NP, TR, WM, WN> {
 // normalised patch into their own LDS copy (no cross-wave hand-off) and run conv0 on the
 // MFMA straight into the next window (input_norm + conv0 + BN + ReLU, HardNet.py:281-283,
 // 306-310).
-template <int CIN, int COUT, int HIN, int S, int NP, int TR, int WM, int WN, bool STEM, int ABL = 0>
+template <int CIN, int COUT, int HIN, int S, int NP, int TR, int WM, int WN, bool STEM, int ABL = 0,
+          int PX = 80>
 __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_ws(
     const float* __restrict__ in, float* __restrict__ out, const uint4* __restrict__ wp,
     const float* __restrict__ bias, int P, const float* __restrict__ stem_w,
     const float* __restrict__ stem_b, float eps) {
-  using C = WsCfg<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM>;
+  using C = WsCfg<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM, PX>;
+  static_assert(PX == 80 || !STEM, "the stem producer writes the 80-byte layout");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -776,7 +786,8 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_ws(
         uint4 hi, lo;
         split8(pf[k][0], pf[k][1], hi, lo);
         const int pc = (S == 1) ? wc : ((wc & 1) ? C::HALF + (wc >> 1) : (wc >> 1));
-        const int off = np * C::PS + wr * C::RS + pc * 80 + g * 16;
+        const int gs = PX == 80 ? g : g ^ ((wr / S) & 3);  // swizzled chunk (64-byte layout)
+        const int off = np * C::PS + wr * C::RS + pc * PX + gs * 16;
         *reinterpret_cast<uint4*>(dst + off) = hi;
         *reinterpret_cast<uint4*>(dst + C::PLANE + off) = lo;
       }
@@ -931,13 +942,14 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_ws(
 
   // ---- compute side ----
   const int wm = wave / WN, wn = wave % WN;
-  int abase[C::MT];
+  int abase[C::MT], ylr[C::MT];
 #pragma unroll
   for (int mt = 0; mt < C::MT; ++mt) {
     const int m = (wm * C::MT + mt) * 32 + r;
     const int np = m / (TR * C::WOUT), rem = m % (TR * C::WOUT);
     const int yl = rem / C::WOUT, xo = rem % C::WOUT;
-    abase[mt] = np * C::PS + yl * S * C::RS + xo * 80 + h * 16;
+    abase[mt] = np * C::PS + yl * S * C::RS + xo * PX + (PX == 80 ? h * 16 : 0);
+    ylr[mt] = yl;
   }
   constexpr unsigned CHUNK_BYTES = 9 * 2 * C::NTOT * 2 * 64 * 16;
   const __amdgpu_buffer_rsrc_t wr_ = make_rsrc(wp, C::NCC * CHUNK_BYTES);
@@ -972,11 +984,13 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_ws(
     uint4 aq[2][C::MT][2];
     auto load_a = [&](int ksx, uint4 (&dst)[C::MT][2]) {
       const int tap = (ABL & 2) ? 0 : ksx >> 1, ks = (ABL & 2) ? 0 : ksx & 1;  // ABL 2: timing only
-      const int toff = (tap / 3) * C::RS + C::colofs(tap % 3) * 80 + ks * 32;
+      const int toff = (tap / 3) * C::RS + C::colofs(tap % 3) * PX + (PX == 80 ? ks * 32 : 0);
 #pragma unroll
       for (int mt = 0; mt < C::MT; ++mt) {
-        dst[mt][0] = *reinterpret_cast<const uint4*>(cur + abase[mt] + toff);
-        dst[mt][1] = *reinterpret_cast<const uint4*>(cur + C::PLANE + abase[mt] + toff);
+        // 64-byte layout: chunk 2 ks + h of window row 2 yl + ky sits at (2 ks + h) ^ ((yl + ky / 2) & 3)
+        const int co = PX == 80 ? 0 : 16 * ((2 * ks + h) ^ ((ylr[mt] + (tap / 3) / S) & 3));
+        dst[mt][0] = *reinterpret_cast<const uint4*>(cur + abase[mt] + toff + co);
+        dst[mt][1] = *reinterpret_cast<const uint4*>(cur + C::PLANE + abase[mt] + toff + co);
       }
     };
     load_a(0, aq[0]);
@@ -1308,13 +1322,14 @@ HN_PIPE_A(pipe3_a7, false, 64, 64, 16, 1, 1, 8, 2, 2, 7)
 
 #define HN_WS(NAME, CIN, COUT, HIN, S, NP, TR, WM, WN) HN_WS_S(NAME, false, CIN, COUT, HIN, S, NP, TR, WM, WN)
 #define HN_WS_S(NAME, STEM, CIN, COUT, HIN, S, NP, TR, WM, WN) HN_WS_A(NAME, STEM, CIN, COUT, HIN, S, NP, TR, WM, WN, 0)
-#define HN_WS_A(NAME, STEM, CIN, COUT, HIN, S, NP, TR, WM, WN, ABL)                      \
-  using NAME##_cfg = WsCfg<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM>;                       \
+#define HN_WS_A(NAME, STEM, CIN, COUT, HIN, S, NP, TR, WM, WN, ABL) HN_WS_X(NAME, STEM, CIN, COUT, HIN, S, NP, TR, WM, WN, ABL, 80)
+#define HN_WS_X(NAME, STEM, CIN, COUT, HIN, S, NP, TR, WM, WN, ABL, PX)                  \
+  using NAME##_cfg = WsCfg<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM, PX>;                   \
   static hipError_t NAME(const float* in, float* out, const void* wp, const float* bias,   \
                          int P, const float* sw, const float* sb, float eps, hipStream_t st) { \
     constexpr int lds = NAME##_cfg::SMEM;                                                  \
     const void* fn =                                                                       \
-        reinterpret_cast<const void*>(&k_conv_ws<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM, ABL>); \
+        reinterpret_cast<const void*>(&k_conv_ws<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM, ABL, PX>); \
     static int resident = 0;                                                               \
     if (!resident) {                                                                       \
       hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds); \
@@ -1328,7 +1343,7 @@ HN_PIPE_A(pipe3_a7, false, 64, 64, 16, 1, 1, 8, 2, 2, 7)
     }                                                                                      \
     const int tiles = (P + NP - 1) / NP * NAME##_cfg::RT;                                  \
     const int grid = std::min(tiles, resident);                                            \
-    hipLaunchKernelGGL((k_conv_ws<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM, ABL>), dim3(grid),   \
+    hipLaunchKernelGGL((k_conv_ws<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM, ABL, PX>), dim3(grid), \
                        dim3(NAME##_cfg::NTHR), lds, st, in, out,                           \
                        static_cast<const uint4*>(wp), bias, P, sw, sb, eps);               \
     return hipGetLastError();                                                              \
@@ -1344,6 +1359,12 @@ HN_WS(ws4, 64, 128, 16, 2, 1, 4, 1, 4)
 HN_WS(ws4_t8, 64, 128, 16, 2, 1, 8, 1, 4)
 HN_WS(ws5, 128, 128, 8, 1, 1, 8, 1, 4)
 HN_WS(ws5_np2, 128, 128, 8, 1, 2, 8, 1, 4)
+// conv4 with the 64-byte swizzled window: two patches per stage (twice the weight reuse of ws4_t8)
+// -- HN_VARIANT digit d -- and the same layout at one patch (digit e)
+HN_WS_X(ws4_np2s, false, 64, 128, 16, 2, 2, 8, 1, 4, 0, 64)
+HN_WS_X(ws4_s, false, 64, 128, 16, 2, 1, 8, 1, 4, 0, 64)
+HN_WS_X(ws4_np2s22, false, 64, 128, 16, 2, 2, 8, 2, 2, 0, 64)  // digit f: 2 x 2 waves
+
 // wider N tiles (fewer A-fragment reads, weights shared through L1)
 HN_WS(ws3_w8, 64, 64, 16, 1, 1, 16, 4, 1)
 HN_WS(ws4_w8, 64, 128, 16, 2, 1, 8, 2, 2)
@@ -1380,6 +1401,11 @@ hipError_t hn_launch_hardnet_conv(int layer, int variant, const HardnetDev& d, c
       case 5: return (a == 1 ? ws5_a1 : a == 2 ? ws5_a2 : ws5_a3)(in, out, d.wpack[5], d.bias[5], P, nullptr, nullptr, 0.f, st);
     }
     return hipErrorInvalidValue;
+  }
+  if (variant >= 13 && variant <= 15) {  // conv4, 64-byte swizzled window (2 / 1 / 2 patches per stage)
+    if (layer != 4) return hipErrorInvalidValue;
+    return (variant == 13 ? ws4_np2s : variant == 14 ? ws4_s : ws4_np2s22)(in, out, d.wpack[4], d.bias[4], P,
+                                                                          nullptr, nullptr, 0.f, st);
   }
   if (variant == 7) {  // warp-specialised, NT = 2
     switch (layer) {

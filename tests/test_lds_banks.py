@@ -187,3 +187,58 @@ def test_front_irf_fold_positions_are_interior(kk):
         span = set(range(start, start + 16))
         assert not span & padpos
         assert (start + 15) * 36 + 36 <= (pc * 36 + 63) // 64 * 64 or start + 15 < pc
+
+
+# 64-byte swizzled window layout of k_conv_ws (hn_hardnet.hip ConvCfg PX = 64, stride 2):
+# chunk q (16 B = 8 channels) of window row wr at slot q ^ ((wr // S) & 3), no pixel pad, one
+# spare column slot between the even and the odd half
+SWZ_CONFIGS = {"4np2": (64, 128, 16, 2, 2, 8, 1, 4), "4": (64, 128, 16, 2, 1, 8, 1, 4),
+               "4np2w22": (64, 128, 16, 2, 2, 8, 2, 2)}
+
+
+@pytest.mark.parametrize("layer", sorted(SWZ_CONFIGS))
+def test_swizzled_window_reads_and_writes_conflict_free(layer):
+    cin, cout, hin, s, np_, tr, wm, wn = SWZ_CONFIGS[layer]
+    hout = hin // s
+    rin, ncols = 2 * tr + 1, hin + 1
+    half = (ncols + 1) // 2 + 1
+    rs = (half + ncols // 2) * 64
+    ps = rin * rs
+    mt_n = np_ * tr * hout // wm // 32
+    assert 2 * 2 * np_ * ps <= 160 * 1024  # double-buffered hi + lo planes
+
+    def colofs(kx):
+        return half + (kx >> 1) if kx & 1 else kx >> 1
+
+    for w in range(wm):
+        for mt in range(mt_n):
+            for tap in range(9):
+                ky, kx = divmod(tap, 3)
+                for ks in range(2):
+                    addrs = []
+                    for lane in range(64):
+                        r, h = lane & 31, lane >> 5
+                        m = (w * mt_n + mt) * 32 + r
+                        npi, rem = divmod(m, tr * hout)
+                        yl, xo = divmod(rem, hout)
+                        wr = yl * s + ky
+                        q = (2 * ks + h) ^ ((wr // s) & 3)
+                        addrs.append(npi * ps + wr * rs + (colofs(kx) + xo) * 64 + 16 * q)
+                    for grp in GROUPS:
+                        slots = {(addrs[l] // 16) % 16 for l in grp}
+                        assert len(slots) == 16, (layer, w, mt, tap, ks, grp[0])
+    # producer stores: unit u = (pixel, 8-channel group g); ds_write_b128 lanes in groups of 8
+    units = np_ * rin * ncols * 4
+    addr = []
+    for u in range(units):
+        g, pix = u & 3, u >> 2
+        wc, t2 = pix % ncols, pix // ncols
+        wr, npi = t2 % rin, t2 // rin
+        pc = (wc >> 1) + half if wc & 1 else wc >> 1
+        addr.append(npi * ps + wr * rs + pc * 64 + 16 * (g ^ ((wr // s) & 3)))
+    assert len(set(addr)) == units
+    for k in range(0, units - 7, 8):
+        if (k // 64) != ((k + 7) // 64):
+            continue
+        slots = {(a // 16) % 16 for a in addr[k:k + 8]}
+        assert len(slots) == 8, (layer, k)
