@@ -111,7 +111,8 @@ struct ConvCfg {
   static constexpr int NTOT = COUT / 32, NCC = CIN / 32;
   static_assert(PX == 80 || (PX == 64 && (S == 2 || HIN / S == 8)),
                 "the 64-byte swizzled layout: stride 2, or 8-wide output rows");
-  static constexpr int RS = PX == 80 ? conv_row_stride(NCOLS, WOUT, S) : (HALF + NCOLS / 2) * PX;
+  static constexpr int RS = PX == 80 ? conv_row_stride(NCOLS, WOUT, S)
+                                     : (S == 1 ? NCOLS : HALF + NCOLS / 2) * PX;
   static constexpr int PS = RIN * RS;
   static constexpr int PLANE = NP * PS;
   static constexpr int LDS = 2 * PLANE;

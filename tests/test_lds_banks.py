@@ -193,21 +193,24 @@ def test_front_irf_fold_positions_are_interior(kk):
 # chunk q (16 B = 8 channels) of window row wr at slot q ^ ((wr // S) & 3), no pixel pad, one
 # spare column slot between the even and the odd half
 SWZ_CONFIGS = {"4np2": (64, 128, 16, 2, 2, 8, 1, 4), "4": (64, 128, 16, 2, 1, 8, 1, 4),
-               "4np2w22": (64, 128, 16, 2, 2, 8, 2, 2)}
+               "4np2w22": (64, 128, 16, 2, 2, 8, 2, 2),
+               "5np4a": (128, 128, 8, 1, 4, 8, 4, 2), "5np4b": (128, 128, 8, 1, 4, 8, 2, 2)}
 
 
 @pytest.mark.parametrize("layer", sorted(SWZ_CONFIGS))
 def test_swizzled_window_reads_and_writes_conflict_free(layer):
     cin, cout, hin, s, np_, tr, wm, wn = SWZ_CONFIGS[layer]
     hout = hin // s
-    rin, ncols = 2 * tr + 1, hin + 1
+    rin, ncols = (2 * tr + 1, hin + 1) if s == 2 else (tr + 2, hin + 2)
     half = (ncols + 1) // 2 + 1
-    rs = (half + ncols // 2) * 64
+    rs = (half + ncols // 2) * 64 if s == 2 else ncols * 64
     ps = rin * rs
     mt_n = np_ * tr * hout // wm // 32
     assert 2 * 2 * np_ * ps <= 160 * 1024  # double-buffered hi + lo planes
 
     def colofs(kx):
+        if s == 1:
+            return kx
         return half + (kx >> 1) if kx & 1 else kx >> 1
 
     for w in range(wm):
@@ -234,7 +237,7 @@ def test_swizzled_window_reads_and_writes_conflict_free(layer):
         g, pix = u & 3, u >> 2
         wc, t2 = pix % ncols, pix // ncols
         wr, npi = t2 % rin, t2 // rin
-        pc = (wc >> 1) + half if wc & 1 else wc >> 1
+        pc = wc if s == 1 else ((wc >> 1) + half if wc & 1 else wc >> 1)
         addr.append(npi * ps + wr * rs + pc * 64 + 16 * (g ^ ((wr // s) & 3)))
     assert len(set(addr)) == units
     for k in range(0, units - 7, 8):
