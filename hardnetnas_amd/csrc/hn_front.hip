@@ -67,7 +67,14 @@ __global__ __launch_bounds__(256) void k_front(const float* __restrict__ in,
   constexpr int PAD = KK / 2;
   constexpr int IR = 2 * (RB - 1) + KK;  // pw rows a band reads (ring size)
   constexpr int PC = 32 + 2 * PAD;       // columns incl. zero padding
-  constexpr int NT = (IR + 3) / 4;       // row tiles per wave (at most)
+  // LEAN (k3 IRF, MID = 32): the waves take only the band's real (non-padding) stem/pw rows
+  // -- at most 8, two row tiles per wave instead of three -- and the stem / pw biases are read
+  // from LDS where used instead of held in 32 VGPRs: 162 instead of 210 registers, three
+  // workgroups per CU instead of two (wang2 front 6.7 -> 6.1 ms).  Elsewhere the extra LDS
+  // round trips on the row's latency chain cost more than they free (k5: register-bound at two
+  // workgroups either way; maxpool: LDS-bound at three).
+  constexpr bool LEAN = MODE == FRONT_IRF && K == 3 && MID == 32;
+  constexpr int NT = LEAN ? 2 : (IR + 3) / 4;  // row tiles per wave (at most)
   constexpr int OC = 32;  // layer-0 output channels (SEARCH_SPACE2[0] = (32, 32, 2))
   constexpr int DYU = KK == 3 ? 3 : 1;  // k5: rolled dy loop keeps VGPRs (and occupancy) in check
   constexpr bool RING = MID == 32;
@@ -79,6 +86,8 @@ __global__ __launch_bounds__(256) void k_front(const float* __restrict__ in,
   __shared__ __attribute__((aligned(16))) float s_pw[IR * RS];
   __shared__ __attribute__((aligned(16))) float s_dw[KK * KK * 32 + 32];
   __shared__ float red[8];
+  // stem bias and (MID = 32: the single chunk's) pw bias, read where used (fewer live VGPRs)
+  __shared__ __attribute__((aligned(16))) float s_sb[32], s_pwb[32];
 
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int px = lane & 31, h = lane >> 5;
@@ -98,14 +107,23 @@ __global__ __launch_bounds__(256) void k_front(const float* __restrict__ in,
         make_float4(0.f, 0.f, 0.f, 0.f);
   }
   const f16x8 sah = as_f16x8(spack[lane]), sal = as_f16x8(spack[64 + lane]);
-  // stem bias as the MFMA's initial accumulator (lane (px, h): acc[4q + r] = channel
-  // 4h + 8q + r), so the epilogue is ReLU only
-  f32x16 sb;
+  constexpr bool LDSB = LEAN;
+  if (t < 32) s_sb[t] = stem_b[t];
+  else if (t < 64 && MID == 32) s_pwb[t - 32] = pw_b[t - 32];
+  // (visible after the first patch's barriers)
+  // 32 channels of a bias vector in the MFMA accumulator order (lane (px, h): acc[4q + r] =
+  // channel 4h + 8q + r) -- the initial accumulator, so the epilogues are ReLU only
+  auto bias16 = [&](const float* b) {
+    f32x16 v;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const float4 b = *reinterpret_cast<const float4*>(stem_b + 8 * q + 4 * h);
-    sb[4 * q] = b.x; sb[4 * q + 1] = b.y; sb[4 * q + 2] = b.z; sb[4 * q + 3] = b.w;
-  }
+    for (int q = 0; q < 4; ++q) {
+      const float4 x = *reinterpret_cast<const float4*>(b + 8 * q + 4 * h);
+      v[4 * q] = x.x; v[4 * q + 1] = x.y; v[4 * q + 2] = x.z; v[4 * q + 3] = x.w;
+    }
+    return v;
+  };
+  f32x16 sbr = {};  // !LDSB: the stem bias in registers
+  if constexpr (!LDSB) sbr = bias16(stem_b);
   const int lm = kDwLane[lane], dq = lm & 7, dox = lm >> 3;
   auto slot_of = [](int y) { return (y + PAD + IR) % IR; };  // ring slot of pw row y
 
@@ -147,20 +165,29 @@ __global__ __launch_bounds__(256) void k_front(const float* __restrict__ in,
       // rows after the previous band's last one (ring)
       const int ylast = 2 * r0 + 6 + PAD;
       const int ybeg = (RING && band > 0) ? ylast - 7 : 2 * r0 - PAD;
-      const int nrows = ylast + 1 - ybeg;
+      // LEAN: the real rows yr0 .. go to the waves round-robin and the padding rows are
+      // zero-filled apart; otherwise all rows ybeg .. ylast round-robin
+      const int yr0 = LEAN ? max(ybeg, 0) : ybeg;
+      const int nreal = LEAN ? min(ylast, 31) + 1 - yr0 : ylast + 1 - ybeg;
 
       // ---- phase A: stem rows on the MFMA ------------------------------------------------
       // A = stem weights [32 ch][16 = 9 taps + 0], B = im2col of one image row (lane: pixel
       // px, taps 8h..8h+7).  C leaves channel 4h + 8q + r (i = 4q + r) of pixel px in acc[i];
       // that order is used as-is as the pw contraction index (pw weights are packed to match).
+      auto zero_row = [&](int y) {  // zero padding row of the pw output (whole row)
+        float4* d = reinterpret_cast<float4*>(s_pw + slot_of(y) * RS);
+        for (int j = lane; j < RS / 4; j += 64) d[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+      };
+      if constexpr (LEAN)
+        for (int y = ybeg + w; y <= ylast; y += 4)
+          if (y < 0 || y >= 32) zero_row(y);
       uint4 bh[NT][2], bl[NT][2];
 #pragma unroll
       for (int i = 0; i < NT; ++i) {
-        const int ri = w + 4 * i, y = ybeg + ri;
-        if (ri >= nrows) continue;  // wave-uniform; such tiles are never read
-        if (y < 0 || y >= 32) {     // zero padding row of the pw output (whole row)
-          float4* d = reinterpret_cast<float4*>(s_pw + slot_of(y) * RS);
-          for (int j = lane; j < RS / 4; j += 64) d[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+        const int ri = w + 4 * i, y = yr0 + ri;
+        if (ri >= nreal) continue;  // wave-uniform; such tiles are never read
+        if (!LEAN && (y < 0 || y >= 32)) {
+          zero_row(y);
           continue;
         }
         float tp[8];
@@ -171,7 +198,7 @@ __global__ __launch_bounds__(256) void k_front(const float* __restrict__ in,
         }
         uint4 xh, xl;
         split8_f16(make_float4(tp[0], tp[1], tp[2], tp[3]), make_float4(tp[4], tp[5], tp[6], tp[7]), xh, xl);
-        const f32x16 c = mfma3_f16(sah, sal, as_f16x8(xh), as_f16x8(xl), sb);
+        const f32x16 c = mfma3_f16(sah, sal, as_f16x8(xh), as_f16x8(xl), LDSB ? bias16(s_sb) : sbr);
         float4 o[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q)
@@ -225,16 +252,13 @@ __global__ __launch_bounds__(256) void k_front(const float* __restrict__ in,
         const uint4* ap = apack + (size_t)m * 4 * 64 + lane;
         const f16x8 ah0 = as_f16x8(ap[0]), al0 = as_f16x8(ap[64]);
         const f16x8 ah1 = as_f16x8(ap[128]), al1 = as_f16x8(ap[192]);
-        f32x16 bias;  // pw bias as the initial accumulator
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float4 b = *reinterpret_cast<const float4*>(pw_b + 32 * m + 8 * q + 4 * h);
-          bias[4 * q] = b.x; bias[4 * q + 1] = b.y; bias[4 * q + 2] = b.z; bias[4 * q + 3] = b.w;
-        }
+        f32x16 bias;  // pw bias as the initial accumulator (LDSB: read per row from LDS)
+        if constexpr (!LDSB) bias = bias16(pw_b + 32 * m);
 #pragma unroll
         for (int i = 0; i < NT; ++i) {
-          const int ri = w + 4 * i, y = ybeg + ri;
-          if (ri >= nrows || y < 0 || y >= 32) continue;
+          const int ri = w + 4 * i, y = yr0 + ri;
+          if (ri >= nreal || y < 0 || y >= 32) continue;
+          if constexpr (LDSB) bias = bias16(s_pwb);
           f32x16 acc = mfma3_f16(ah0, al0, as_f16x8(bh[i][0]), as_f16x8(bl[i][0]), bias);
           acc = mfma3_f16(ah1, al1, as_f16x8(bh[i][1]), as_f16x8(bl[i][1]), acc);
           float4* d = reinterpret_cast<float4*>(s_pw + slot_of(y) * RS + colpos(PAD + px) * PS);
