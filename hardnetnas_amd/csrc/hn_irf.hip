@@ -34,7 +34,7 @@ struct IrfTile {
 };
 
 // The 64 -> 128 stride-2 blocks are held to 168 VGPRs, three workgroups per CU (their LDS
-// allows three; k5 spills 20 dwords outside the MFMA loops): wang2 / wang4 irf -1 %.
+// allows three; the k5 form spills 20 dwords and still gains): wang2 / wang4 irf -1 %.
 template <int CIN, int COUT, int HIN, int S, int K, int MID>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((CIN == 64 && S == 2) ? 3 : 1))) void k_irf(const float* __restrict__ x, float* __restrict__ y,
                                              const uint4* __restrict__ pw_a,   // [MID/32][CIN/16][2][64]
