@@ -33,10 +33,12 @@ struct IrfTile {
   static constexpr int NI = NPB * HIN * HIN;  // input pixels per workgroup
 };
 
-// The 64 -> 128 stride-2 blocks are held to 168 VGPRs, three workgroups per CU (their LDS
-// allows three; the k5 form spills 20 dwords and still gains): wang2 / wang4 irf -1 %.
+// The 64 -> 128 stride-2 and the 128-channel (4x4) blocks are held to 168 VGPRs, three
+// workgroups per CU (their LDS allows three; the k5 forms spill 20-25 dwords and still gain):
+// wang2 / wang4 / FDLNet irf -1 to -2 %.  The 32 -> 64 stride-2 blocks lose with the same cap
+// (+6 % irf: their register prefetch of the next tile spills).
 template <int CIN, int COUT, int HIN, int S, int K, int MID>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((CIN == 64 && S == 2) ? 3 : 1))) void k_irf(const float* __restrict__ x, float* __restrict__ y,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((CIN == 64 && S == 2) || CIN == 128 ? 3 : 1))) void k_irf(const float* __restrict__ x, float* __restrict__ y,
                                              const uint4* __restrict__ pw_a,   // [MID/32][CIN/16][2][64]
                                              const float* __restrict__ pw_b,   // [MID] dw order
                                              const float* __restrict__ dw_w,   // [K*K][MID]
