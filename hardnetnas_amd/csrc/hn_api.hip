@@ -751,6 +751,12 @@ static int forward_nas(hn_model* m, const float* in, int P, int pmax, float* out
     const long npix_out = (long)P * L.hout * L.hout;
     if (L.skip) {
       const float* src = x;
+      const bool nofuse = std::getenv("HN_NO_SKIPFUSE") != nullptr;  // (A/B, layerwise tests)
+      if (L.stride == 2 && L.skip_conv && !nofuse && hn_skip_s2_supported(L.hin, L.cin, L.cout)) {
+        STAGE("skip", hn_launch_skip_s2(x, y, L.pw_w, L.pw_b, P, L.hin, L.cin, L.cout, st));
+        std::swap(x, y);
+        continue;
+      }
       if (L.stride == 2) {
         STAGE("maxpool", hn_launch_maxpool(x, t1, P, L.hin, L.cin, st));
         src = t1;

@@ -29,6 +29,10 @@ hipError_t hn_launch_pw(const float* in, float* out, const float* wt, const floa
 hipError_t hn_launch_dw(const float* in, float* out, const float* wd, const float* bias, int P,
                         int hin, int c, int k, int s, hipStream_t st);
 hipError_t hn_launch_maxpool(const float* in, float* out, int P, int hin, int c, hipStream_t st);
+// fused MaxPool2d(3, 2, 1) + ConvBNRelu 1x1 of the channel-changing "skip" op (hn_nas.hip)
+bool hn_skip_s2_supported(int hin, int cin, int cout);
+hipError_t hn_launch_skip_s2(const float* in, float* out, const float* wt, const float* bias, int P, int hin,
+                             int cin, int cout, hipStream_t st);
 hipError_t hn_launch_se(float* y, const float* w1, const float* b1, const float* w2,
                         const float* b2, int P, int hw, int c, int mid, hipStream_t st);
 hipError_t hn_launch_nas_head(const float* a, float* out, const float* wt, const float* bias,

@@ -287,6 +287,100 @@ __global__ __launch_bounds__(256) void k_maxpool(const float* __restrict__ in, f
   *reinterpret_cast<float4*>(out + (((p * hout) + yo) * (long)hout + xo) * c + c4) = m;
 }
 
+// k_skip_s2: the "skip" op where the channel count changes (fbnet_builder.py:202-228) --
+// MaxPool2d(3, 2, 1) then ConvBNRelu 1x1 CIN -> COUT -- in one pass, so the pooled tensor never
+// reaches HBM.  32-pixel tiles of the flattened [P, HOUT, HOUT] output; the 4 waves of a
+// workgroup cover COUT / 32 channel tiles x PT = 128 / COUT pixel tiles.  The workgroup first
+// pools the PT tiles into their MFMA B fragments (K-step of 16 input channels: lane (pixel, h)
+// holds channels 16 ks + 8 h .. + 7), split to fp16 hi / lo in LDS; after a barrier each wave
+// runs its channel tile's 32x32x16 fp16x3 MFMA K-loop with the weights (BN folded) resident in
+// registers, bias + ReLU, float4 stores.
+template <int HIN, int CIN, int COUT>
+__global__ __launch_bounds__(256) void k_skip_s2(const float* __restrict__ in, float* __restrict__ out,
+                                                 const float* __restrict__ wt,    // [CIN][COUT]
+                                                 const float* __restrict__ bias,  // [COUT]
+                                                 int P) {
+  constexpr int HOUT = HIN / 2, NT = COUT / 32, PT = 4 / NT, KS = CIN / 16;
+  static_assert(NT * PT == 4, "4 waves");
+  __shared__ uint4 s_b[PT][KS][2][64];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int nt = w % NT, pt = w / NT;  // this wave's MFMA work
+  // A operand: row = output channel 32 nt + r, K-step ks = input channels 16 ks + 8 h + j
+  f16x8 ah[KS], al[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float v = wt[(16 * ks + 8 * h + j) * COUT + 32 * nt + r];
+      ah[ks][j] = (_Float16)v;
+      al[ks][j] = (_Float16)(v - (float)ah[ks][j]);
+    }
+  }
+  f32x16 b0;  // bias in the accumulator order (channel 8q + 4h + r' at i = 4q + r')
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float4 x = *reinterpret_cast<const float4*>(bias + 32 * nt + 8 * q + 4 * h);
+    b0[4 * q] = x.x; b0[4 * q + 1] = x.y; b0[4 * q + 2] = x.z; b0[4 * q + 3] = x.w;
+  }
+  const long npix = (long)P * HOUT * HOUT;
+  const long ntile = (npix + 31) / 32;
+#pragma unroll 1
+  for (long g = (long)blockIdx.x * PT; g < ntile; g += (long)gridDim.x * PT) {  // workgroup-uniform
+    // pool the PT tiles cooperatively: item = (pixel, channel quad), consecutive threads on
+    // consecutive quads of one pixel (coalesced 256-byte rows); the padding row / column -1 is
+    // replaced by row / column 0, in the same window (a repeat does not change a max) -- no
+    // branches, all 9 loads in flight.  The quad lands in its B-fragment slot: K-step c4 / 4,
+    // lane half (c4 / 2) & 1, 8-byte half c4 & 1 of the lane's 16-byte entry.
+#pragma unroll
+    for (int it = t; it < 32 * PT * (CIN / 4); it += 256) {
+      const int c4 = it % (CIN / 4), pxl = it / (CIN / 4), tp = pxl / 32, px = pxl % 32;
+      const long op = (g + tp) * 32 + px;
+      float4 m = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (op < npix) {
+        const long p = op / (HOUT * HOUT);
+        const int rem = (int)(op % (HOUT * HOUT)), oy = rem / HOUT, ox = rem % HOUT;
+        const float* base = in + p * HIN * HIN * CIN + 4 * c4;
+        m = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky) {
+          const int y = max(2 * oy - 1 + ky, 0);  // (rows / columns 2 o + 1 stay inside)
+#pragma unroll
+          for (int kx = 0; kx < 3; ++kx) {
+            const int x = max(2 * ox - 1 + kx, 0);
+            const float4 a = *reinterpret_cast<const float4*>(base + (y * HIN + x) * CIN);
+            m.x = fmaxf(m.x, a.x); m.y = fmaxf(m.y, a.y); m.z = fmaxf(m.z, a.z); m.w = fmaxf(m.w, a.w);
+          }
+        }
+      }
+      typedef _Float16 f16x4_t __attribute__((ext_vector_type(4)));
+      f16x4_t hi, lo;
+      hi[0] = (_Float16)m.x; lo[0] = (_Float16)(m.x - (float)hi[0]);
+      hi[1] = (_Float16)m.y; lo[1] = (_Float16)(m.y - (float)hi[1]);
+      hi[2] = (_Float16)m.z; lo[2] = (_Float16)(m.z - (float)hi[2]);
+      hi[3] = (_Float16)m.w; lo[3] = (_Float16)(m.w - (float)hi[3]);
+      const int ks = c4 >> 2, ln = ((c4 >> 1) & 1) * 32 + px, half = c4 & 1;
+      reinterpret_cast<uint2*>(&s_b[tp][ks][0][ln])[half] = __builtin_bit_cast(uint2, hi);
+      reinterpret_cast<uint2*>(&s_b[tp][ks][1][ln])[half] = __builtin_bit_cast(uint2, lo);
+    }
+    __syncthreads();
+    f32x16 c = b0;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+      c = mfma3_f16(ah[ks], al[ks], as_f16x8(s_b[pt][ks][0][lane]), as_f16x8(s_b[pt][ks][1][lane]), c);
+    const long op = (g + pt) * 32 + r;
+    if (op < npix) {
+      float* dst = out + op * COUT + 32 * nt + 4 * h;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        *reinterpret_cast<float4*>(dst + 8 * q) =
+            make_float4(fmaxf(c[4 * q], 0.f), fmaxf(c[4 * q + 1], 0.f), fmaxf(c[4 * q + 2], 0.f),
+                        fmaxf(c[4 * q + 3], 0.f));
+    }
+    __syncthreads();  // s_b is rewritten by the next tile group
+  }
+}
+
 // SE in place on y [P][hw][c]; one 256-thread workgroup per patch (c <= 256).
 __global__ __launch_bounds__(256) void k_se(float* __restrict__ y, const float* __restrict__ w1,
                                             const float* __restrict__ b1,  // [mid][c], [mid]
@@ -407,6 +501,38 @@ hipError_t hn_launch_dw(const float* in, float* out, const float* wd, const floa
   else
     return hipErrorInvalidValue;
   return hipGetLastError();
+}
+
+template <int HIN, int CIN, int COUT>
+static hipError_t skip_s2_launch(const float* in, float* out, const float* wt, const float* bias, int P,
+                                 hipStream_t st) {
+  static int resident = 0;  // persistent grid
+  if (!resident) {
+    int per_cu = 0, dev = 0, cus = 0;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &per_cu, reinterpret_cast<const void*>(&k_skip_s2<HIN, CIN, COUT>), 256, 0);
+    if (e != hipSuccess) return e;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    resident = (per_cu > 1 ? per_cu : 1) * (cus > 1 ? cus : 1);
+  }
+  constexpr int PT = 4 / (COUT / 32);
+  const long groups = (((long)P * (HIN / 2) * (HIN / 2) + 31) / 32 + PT - 1) / PT;
+  const int grid = (int)(groups < resident ? groups : resident);
+  hipLaunchKernelGGL((k_skip_s2<HIN, CIN, COUT>), dim3(grid), dim3(256), 0, st, in, out, wt, bias, P);
+  return hipGetLastError();
+}
+
+bool hn_skip_s2_supported(int hin, int cin, int cout) {
+  return (hin == 16 && cin == 32 && cout == 64) || (hin == 8 && cin == 64 && cout == 128);
+}
+
+hipError_t hn_launch_skip_s2(const float* in, float* out, const float* wt, const float* bias, int P, int hin,
+                             int cin, int cout, hipStream_t st) {
+  if (P <= 0) return hipSuccess;
+  if (hin == 16 && cin == 32 && cout == 64) return skip_s2_launch<16, 32, 64>(in, out, wt, bias, P, st);
+  if (hin == 8 && cin == 64 && cout == 128) return skip_s2_launch<8, 64, 128>(in, out, wt, bias, P, st);
+  return hipErrorInvalidValue;
 }
 
 hipError_t hn_launch_maxpool(const float* in, float* out, int P, int hin, int c, hipStream_t st) {

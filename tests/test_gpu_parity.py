@@ -404,3 +404,25 @@ def test_forward_is_graph_capturable(cuda_device):
     g.replay()
     torch.cuda.synchronize()
     assert torch.equal(out, ref)
+
+
+@pytest.mark.parametrize("name", ["wang3", "cov_c"])
+def test_nas_fused_skip_s2_matches_unfused(name, cuda_device, monkeypatch):
+    """The channel-changing stride-2 "skip" (MaxPool2d(3, 2, 1) + ConvBNRelu 1x1,
+    fbnet_builder.py:202-228) runs as one kernel (stage "skip", fp16x3 MFMA); it matches the
+    reference vectors, and the maxpool + fp32 pw kernels (HN_NO_SKIPFUSE=1) on ragged batches."""
+    from hardnetnas_amd._native import NativeModel
+    m, fx, _ = build_module(name)
+    x = torch.from_numpy(golden_inputs(fx)).to(cuda_device)
+    nm = NativeModel.from_module(m, cuda_device)
+    nm.set_profiling(True)
+    y = nm(x).cpu().numpy()
+    st = nm.stage_times()
+    assert "skip" in st and "maxpool" not in st
+    assert np.abs(y - fx["y"]).max() <= NAS_TOL
+    monkeypatch.setenv("HN_NO_SKIPFUSE", "1")
+    lw = NativeModel.from_module(m, cuda_device)
+    lw.set_profiling(True)
+    for b in (1, 3, 37, 256):
+        assert np.abs(lw(x[:b]).cpu().numpy() - y[:b]).max() <= NAS_TOL
+    assert "maxpool" in lw.stage_times() and "skip" not in lw.stage_times()
