@@ -704,7 +704,8 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void k_conv_pipe(
 // barrier per stage.  For the HBM-heavy stride-2 layers this keeps ~UNITS*32 B per
 // workgroup in flight instead of one unit per K-step.
 // ------------------------------------------------------------------------------------
-template <int CIN, int COUT, int HIN, int S, int NP, int TR, int WM, int WN, bool STEM = false, int PX = 80>
+template <int CIN, int COUT, int HIN, int S, int NP, int TR, int WM, int WN, bool STEM = false, int PX = 80,
+          bool CST = false>
 struct WsCfg : ConvCfg<CIN, COUT, HIN, S, NP, TR, WM, WN, PX> {
   using B = ConvCfg<CIN, COUT, HIN, S, NP, TR, WM, WN, PX>;
   static constexpr int NWC = WM * WN, NWP = 4, NTHR = (NWC + NWP) * 64, PTHR = NWP * 64;
@@ -712,7 +713,9 @@ struct WsCfg : ConvCfg<CIN, COUT, HIN, S, NP, TR, WM, WN, PX> {
   static constexpr int UPT = STEM ? 1 : (UNITS + PTHR - 1) / PTHR;
   static constexpr int BUF = B::LDS;
   static constexpr int PBUF = 34 * 34 * 4;  // one private normalised patch per producer wave
-  static constexpr int SMEM = 2 * BUF + (STEM ? NWP * PBUF : 0);
+  static constexpr int SROW = 36;                   // CST: floats per pixel row of the scratch
+  static constexpr int SCR = 32 * SROW * 4;          // CST: one 32 x 32 tile per MFMA wave
+  static constexpr int SMEM = 2 * BUF + (STEM ? NWP * PBUF : 0) + (CST ? NWC * SCR : 0);
   static constexpr bool DEEP = !STEM && UPT <= 6;  // two stages of loads in flight
   static_assert(SMEM <= 160 * 1024, "LDS");
 };
@@ -721,13 +724,17 @@ struct WsCfg : ConvCfg<CIN, COUT, HIN, S, NP, TR, WM, WN, PX> {
 // normalised patch into their own LDS copy (no cross-wave hand-off) and run conv0 on the
 // MFMA straight into the next window (input_norm + conv0 + BN + ReLU, HardNet.py:281-283,
 // 306-310).
+// CST: the epilogue transposes each 32-pixel x 32-channel tile through a per-wave LDS scratch
+// so that every store instruction writes 8 whole 128-byte pixel rows (8 lanes per row) instead
+// of 32 pixels x 32 bytes.
 template <int CIN, int COUT, int HIN, int S, int NP, int TR, int WM, int WN, bool STEM, int ABL = 0,
-          int PX = 80>
+          int PX = 80, bool CST = false>
 __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_ws(
     const float* __restrict__ in, float* __restrict__ out, const uint4* __restrict__ wp,
     const float* __restrict__ bias, int P, const float* __restrict__ stem_w,
     const float* __restrict__ stem_b, float eps) {
-  using C = WsCfg<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM, PX>;
+  using C = WsCfg<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM, PX, CST>;
+  static_assert(!CST || NP == 1, "CST: single-patch tiles (no ragged pixel rows)");
   static_assert(PX == 80 || !STEM, "the stem producer writes the 80-byte layout");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1040,9 +1047,28 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_ws(
               v.y = fmaxf(acc[mt][nt][4 * q + 1] + bv[q].y, 0.f);
               v.z = fmaxf(acc[mt][nt][4 * q + 2] + bv[q].z, 0.f);
               v.w = fmaxf(acc[mt][nt][4 * q + 3] + bv[q].w, 0.f);
-              if (!(ABL & 4) || v.x == 1234.5f)  // ABL 4: timing only, no stores
+              if constexpr (CST) {
+                float* scr = reinterpret_cast<float*>(smem + 2 * C::BUF) + wave * (C::SCR / 4);
+                *reinterpret_cast<float4*>(scr + r * C::SROW + 8 * q + 4 * h) = v;
+              } else if (!(ABL & 4) || v.x == 1234.5f) {  // ABL 4: timing only, no stores
                 *reinterpret_cast<float4*>(obase + (size_t)mt * 32 * COUT + nt * 32 + 8 * q) = v;
+              }
             }
+          }
+          if constexpr (CST) {  // same wave: its LDS accesses execute in order
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("" ::: "memory");
+            const float* scr = reinterpret_cast<const float*>(smem + 2 * C::BUF) + wave * (C::SCR / 4);
+            float* ob = out + ((size_t)(p0 * C::HOUT + y0) * C::WOUT + (wm * C::MT + mt) * 32) * COUT +
+                        (wn * C::NT + nt) * 32;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              const int pl = 8 * k + (lane >> 3), c4 = lane & 7;
+              *reinterpret_cast<float4*>(ob + (size_t)pl * COUT + 4 * c4) =
+                  *reinterpret_cast<const float4*>(scr + pl * C::SROW + 4 * c4);
+            }
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("" ::: "memory");
           }
           acc[mt][nt] = f32x16{};
         }
@@ -1324,13 +1350,14 @@ HN_PIPE_A(pipe3_a7, false, 64, 64, 16, 1, 1, 8, 2, 2, 7)
 #define HN_WS(NAME, CIN, COUT, HIN, S, NP, TR, WM, WN) HN_WS_S(NAME, false, CIN, COUT, HIN, S, NP, TR, WM, WN)
 #define HN_WS_S(NAME, STEM, CIN, COUT, HIN, S, NP, TR, WM, WN) HN_WS_A(NAME, STEM, CIN, COUT, HIN, S, NP, TR, WM, WN, 0)
 #define HN_WS_A(NAME, STEM, CIN, COUT, HIN, S, NP, TR, WM, WN, ABL) HN_WS_X(NAME, STEM, CIN, COUT, HIN, S, NP, TR, WM, WN, ABL, 80)
-#define HN_WS_X(NAME, STEM, CIN, COUT, HIN, S, NP, TR, WM, WN, ABL, PX)                  \
-  using NAME##_cfg = WsCfg<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM, PX>;                   \
+#define HN_WS_X(NAME, STEM, CIN, COUT, HIN, S, NP, TR, WM, WN, ABL, PX) HN_WS_C(NAME, STEM, CIN, COUT, HIN, S, NP, TR, WM, WN, ABL, PX, false)
+#define HN_WS_C(NAME, STEM, CIN, COUT, HIN, S, NP, TR, WM, WN, ABL, PX, CST)             \
+  using NAME##_cfg = WsCfg<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM, PX, CST>;                   \
   static hipError_t NAME(const float* in, float* out, const void* wp, const float* bias,   \
                          int P, const float* sw, const float* sb, float eps, hipStream_t st) { \
     constexpr int lds = NAME##_cfg::SMEM;                                                  \
     const void* fn =                                                                       \
-        reinterpret_cast<const void*>(&k_conv_ws<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM, ABL, PX>); \
+        reinterpret_cast<const void*>(&k_conv_ws<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM, ABL, PX, CST>); \
     static int resident = 0;                                                               \
     if (!resident) {                                                                       \
       hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds); \
@@ -1344,7 +1371,7 @@ HN_PIPE_A(pipe3_a7, false, 64, 64, 16, 1, 1, 8, 2, 2, 7)
     }                                                                                      \
     const int tiles = (P + NP - 1) / NP * NAME##_cfg::RT;                                  \
     const int grid = std::min(tiles, resident);                                            \
-    hipLaunchKernelGGL((k_conv_ws<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM, ABL, PX>), dim3(grid), \
+    hipLaunchKernelGGL((k_conv_ws<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM, ABL, PX, CST>), dim3(grid), \
                        dim3(NAME##_cfg::NTHR), lds, st, in, out,                           \
                        static_cast<const uint4*>(wp), bias, P, sw, sb, eps);               \
     return hipGetLastError();                                                              \
@@ -1365,6 +1392,10 @@ HN_WS(ws5_np2, 128, 128, 8, 1, 2, 8, 1, 4)
 HN_WS_X(ws4_np2s, false, 64, 128, 16, 2, 2, 8, 1, 4, 0, 64)
 HN_WS_X(ws4_s, false, 64, 128, 16, 2, 1, 8, 1, 4, 0, 64)
 HN_WS_X(ws4_np2s22, false, 64, 128, 16, 2, 2, 8, 2, 2, 0, 64)  // digit f: 2 x 2 waves
+// conv3 / conv4 (one patch per stage) with the epilogue transposed through LDS for whole-row
+// stores (CST): HN_VARIANT digit g
+HN_WS_C(ws3_cst, false, 64, 64, 16, 1, 1, 16, 2, 2, 0, 80, true)
+HN_WS_C(ws4_cst, false, 64, 128, 16, 2, 1, 8, 1, 4, 0, 80, true)
 
 // wider N tiles (fewer A-fragment reads, weights shared through L1)
 HN_WS(ws3_w8, 64, 64, 16, 1, 1, 16, 4, 1)
@@ -1407,6 +1438,13 @@ hipError_t hn_launch_hardnet_conv(int layer, int variant, const HardnetDev& d, c
     if (layer != 4) return hipErrorInvalidValue;
     return (variant == 13 ? ws4_np2s : variant == 14 ? ws4_s : ws4_np2s22)(in, out, d.wpack[4], d.bias[4], P,
                                                                           nullptr, nullptr, 0.f, st);
+  }
+  if (variant == 16) {  // coalesced epilogue stores
+    switch (layer) {
+      case 3: return ws3_cst(in, out, d.wpack[3], d.bias[3], P, nullptr, nullptr, 0.f, st);
+      case 4: return ws4_cst(in, out, d.wpack[4], d.bias[4], P, nullptr, nullptr, 0.f, st);
+    }
+    return hipErrorInvalidValue;
   }
   if (variant == 7) {  // warp-specialised, NT = 2
     switch (layer) {
