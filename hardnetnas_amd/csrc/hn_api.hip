@@ -167,7 +167,7 @@ struct hn_model {
   bool no_irf = false;    // HN_NO_IRF=1: layer-by-layer pw/dw/pwl kernels (A/B, debugging)
   // conv tiling per layer (index 0 = stem+conv1, 2..5 = conv2..5); defaults are the best
   // measured on MI355X (tools/tune_variants.py); HN_VARIANT="003303" style override
-  int variant[6] = {6, 0, 5, 16, 15, 3};  // conv3: 16 = whole-row epilogue stores; conv4: 15 = two patches per stage, 64-byte swizzled window
+  int variant[6] = {6, 0, 5, 16, 15, 16};  // 16 = epilogue stores through LDS (conv3 whole rows, conv5 64-byte rows); conv4: 15 = two patches per stage, 64-byte swizzled window
   size_t ws_floats_per_patch = 0;  // per buffer
   int n_bufs = 0;
 

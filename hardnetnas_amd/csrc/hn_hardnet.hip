@@ -375,7 +375,7 @@ __global__ __launch_bounds__(256) void k_conv3x3(const float* __restrict__ in, f
 // barrier ends the stage.  STEM (conv1): the next tile's raw patch is prefetched the same
 // way and input_norm + conv0 (MFMA) fill the next window.
 // ------------------------------------------------------------------------------------
-template <int CIN, int COUT, int HIN, int S, int NP, int TR, int WM, int WN, bool STEM>
+template <int CIN, int COUT, int HIN, int S, int NP, int TR, int WM, int WN, bool STEM, bool CST = false>
 struct PipeCfg : ConvCfg<CIN, COUT, HIN, S, NP, TR, WM, WN> {
   using B = ConvCfg<CIN, COUT, HIN, S, NP, TR, WM, WN>;
   static constexpr int NW = WM * WN, NTHR = NW * 64;
@@ -383,19 +383,24 @@ struct PipeCfg : ConvCfg<CIN, COUT, HIN, S, NP, TR, WM, WN> {
   static constexpr int UPT = (UNITS + NTHR - 1) / NTHR;
   static constexpr int BUF = B::LDS;
   static constexpr int PBUF = 2 * BUF;
-  static constexpr int SMEM = 2 * BUF + (STEM ? 34 * 34 * 4 : 0);
+  static constexpr int SROW = 20;             // CST: floats per pixel row (16 channels + pad)
+  static constexpr int SCR = 32 * SROW * 4;   // CST: one 32-pixel x 16-channel half tile per wave
+  static constexpr int SMEM = 2 * BUF + (STEM ? 34 * 34 * 4 : 0) + (CST ? NW * SCR : 0);
   static_assert(SMEM <= 160 * 1024, "LDS");
   static_assert(UPT <= 18, "prefetch fits in the K-loop");
 };
 
 // ABL (ablation builds only, never shipped): bit0 no weight loads in the K-loop, bit1 no
 // LDS fragment reads, bit2 no next-stage staging.
-template <int CIN, int COUT, int HIN, int S, int NP, int TR, int WM, int WN, bool STEM, int ABL = 0>
+// CST: the epilogue goes through a per-wave LDS scratch, 16 channels at a time, so that each
+// store instruction writes 16 pixel rows of 64 bytes instead of 32 x 32 bytes.
+template <int CIN, int COUT, int HIN, int S, int NP, int TR, int WM, int WN, bool STEM, int ABL = 0,
+          bool CST = false>
 __global__ __launch_bounds__(WM * WN * 64, 2) void k_conv_pipe(
     const float* __restrict__ in, float* __restrict__ out, const uint4* __restrict__ wp,
     const float* __restrict__ bias, int P, const float* __restrict__ stem_w,
     const float* __restrict__ stem_b, float eps) {
-  using C = PipeCfg<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM>;
+  using C = PipeCfg<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM, CST>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
@@ -669,6 +674,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void k_conv_pipe(
         for (int mt = 0; mt < C::MT; ++mt) {
           const bool ok = NP == 1 || p0 + ((wm * C::MT + mt) * 32) / (TR * C::WOUT) < P;
           if (ok) {
+            float* scr = reinterpret_cast<float*>(smem + 2 * C::BUF) + wave * (C::SCR / 4);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
               float4 v;
@@ -676,7 +682,25 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void k_conv_pipe(
               v.y = fmaxf(acc[mt][nt][4 * q + 1] + bv[q].y, 0.f);
               v.z = fmaxf(acc[mt][nt][4 * q + 2] + bv[q].z, 0.f);
               v.w = fmaxf(acc[mt][nt][4 * q + 3] + bv[q].w, 0.f);
-              *reinterpret_cast<float4*>(obase + (size_t)mt * 32 * COUT + nt * 32 + 8 * q) = v;
+              if constexpr (CST) {
+                *reinterpret_cast<float4*>(scr + r * C::SROW + 8 * (q & 1) + 4 * h) = v;
+                if (q & 1) {  // channels 16 (q / 2) .. + 15 of the tile: 16 rows of 64 bytes per store
+                  __builtin_amdgcn_wave_barrier();
+                  asm volatile("" ::: "memory");
+                  float* ob = out + ((size_t)(p0 * C::HOUT + y0) * C::WOUT + (wm * C::MT + mt) * 32) * COUT +
+                              (wn * C::NT + nt) * 32 + 16 * (q >> 1);
+#pragma unroll
+                  for (int k = 0; k < 2; ++k) {
+                    const int pl = 16 * k + (lane >> 2), c4 = lane & 3;
+                    *reinterpret_cast<float4*>(ob + (size_t)pl * COUT + 4 * c4) =
+                        *reinterpret_cast<const float4*>(scr + pl * C::SROW + 4 * c4);
+                  }
+                  __builtin_amdgcn_wave_barrier();
+                  asm volatile("" ::: "memory");
+                }
+              } else {
+                *reinterpret_cast<float4*>(obase + (size_t)mt * 32 * COUT + nt * 32 + 8 * q) = v;
+              }
             }
           }
           acc[mt][nt] = f32x16{};
@@ -734,7 +758,6 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_ws(
     const float* __restrict__ bias, int P, const float* __restrict__ stem_w,
     const float* __restrict__ stem_b, float eps) {
   using C = WsCfg<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM, PX, CST>;
-  static_assert(!CST || NP == 1, "CST: single-patch tiles (no ragged pixel rows)");
   static_assert(PX == 80 || !STEM, "the stem producer writes the 80-byte layout");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1055,7 +1078,7 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_ws(
               }
             }
           }
-          if constexpr (CST) {  // same wave: its LDS accesses execute in order
+          if (CST && ok) {  // same wave: its LDS accesses execute in order
             __builtin_amdgcn_wave_barrier();
             asm volatile("" ::: "memory");
             const float* scr = reinterpret_cast<const float*>(smem + 2 * C::BUF) + wave * (C::SCR / 4);
@@ -1304,14 +1327,15 @@ HN_CONV(conv5_v1, false, 128, 128, 8, 1, 1, 8, 1, 4)
 
 // persistent launch: grid = min(tiles, resident workgroups) (occupancy query, cached)
 #define HN_PIPE(NAME, STEM, CIN, COUT, HIN, S, NP, TR, WM, WN) HN_PIPE_A(NAME, STEM, CIN, COUT, HIN, S, NP, TR, WM, WN, 0)
-#define HN_PIPE_A(NAME, STEM, CIN, COUT, HIN, S, NP, TR, WM, WN, ABL)                      \
-  using NAME##_cfg = PipeCfg<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM>;                     \
+#define HN_PIPE_A(NAME, STEM, CIN, COUT, HIN, S, NP, TR, WM, WN, ABL) HN_PIPE_C(NAME, STEM, CIN, COUT, HIN, S, NP, TR, WM, WN, ABL, false)
+#define HN_PIPE_C(NAME, STEM, CIN, COUT, HIN, S, NP, TR, WM, WN, ABL, CST)                 \
+  using NAME##_cfg = PipeCfg<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM, CST>;                \
   static hipError_t NAME(const float* in, float* out, const void* wp, const float* bias,   \
                          int P, const float* sw, const float* sb, float eps,               \
                          hipStream_t st) {                                                 \
     constexpr int lds = NAME##_cfg::SMEM;                                                  \
     const void* fn = reinterpret_cast<const void*>(                                        \
-        &k_conv_pipe<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM, ABL>);                       \
+        &k_conv_pipe<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM, ABL, CST>);                       \
     static int resident = 0;                                                               \
     if (!resident) {                                                                       \
       hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds); \
@@ -1325,7 +1349,7 @@ HN_CONV(conv5_v1, false, 128, 128, 8, 1, 1, 8, 1, 4)
     }                                                                                      \
     const int tiles = (P + NP - 1) / NP * NAME##_cfg::RT;                                  \
     const int grid = std::min(tiles, resident);                                            \
-    hipLaunchKernelGGL((k_conv_pipe<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM, ABL>), dim3(grid), \
+    hipLaunchKernelGGL((k_conv_pipe<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM, ABL, CST>), dim3(grid), \
                        dim3(NAME##_cfg::NTHR), lds, st, in, out,                           \
                        static_cast<const uint4*>(wp), bias, P, sw, sb, eps);               \
     return hipGetLastError();                                                              \
@@ -1341,6 +1365,7 @@ HN_PIPE(pipe4, false, 64, 128, 16, 2, 1, 4, 1, 4)
 HN_PIPE(pipe4_t8, false, 64, 128, 16, 2, 1, 8, 1, 4)
 HN_PIPE(pipe5, false, 128, 128, 8, 1, 1, 8, 1, 4)
 HN_PIPE(pipe5_np2, false, 128, 128, 8, 1, 2, 8, 1, 4)
+HN_PIPE_C(pipe5_cst, false, 128, 128, 8, 1, 2, 8, 1, 4, 0, true)  // HN_VARIANT digit g at conv5
 // conv3 ablation builds (HN_VARIANT digit 4..7 for layer 3 -> ABL 1, 2, 4, 7)
 HN_PIPE_A(pipe3_a1, false, 64, 64, 16, 1, 1, 8, 2, 2, 1)
 HN_PIPE_A(pipe3_a2, false, 64, 64, 16, 1, 1, 8, 2, 2, 2)
@@ -1392,10 +1417,11 @@ HN_WS(ws5_np2, 128, 128, 8, 1, 2, 8, 1, 4)
 HN_WS_X(ws4_np2s, false, 64, 128, 16, 2, 2, 8, 1, 4, 0, 64)
 HN_WS_X(ws4_s, false, 64, 128, 16, 2, 1, 8, 1, 4, 0, 64)
 HN_WS_X(ws4_np2s22, false, 64, 128, 16, 2, 2, 8, 2, 2, 0, 64)  // digit f: 2 x 2 waves
-// conv3 / conv4 (one patch per stage) with the epilogue transposed through LDS for whole-row
-// stores (CST): HN_VARIANT digit g
+// conv3 with the epilogue transposed through LDS for whole-row stores (CST): HN_VARIANT digit g
+// (the default, conv3 12.8 -> 12.1 ms).  The same on conv4's one-patch tiling (8.49 -> 8.35 ms)
+// and conv5's k_conv_ws form (13.0 -> 12.6) stays behind their defaults; conv5's k_conv_pipe
+// gets the half-tile form (pipe5_cst, 11.9 -> 11.5 ms, the default).
 HN_WS_C(ws3_cst, false, 64, 64, 16, 1, 1, 16, 2, 2, 0, 80, true)
-HN_WS_C(ws4_cst, false, 64, 128, 16, 2, 1, 8, 1, 4, 0, 80, true)
 
 // wider N tiles (fewer A-fragment reads, weights shared through L1)
 HN_WS(ws3_w8, 64, 64, 16, 1, 1, 16, 4, 1)
@@ -1442,7 +1468,7 @@ hipError_t hn_launch_hardnet_conv(int layer, int variant, const HardnetDev& d, c
   if (variant == 16) {  // coalesced epilogue stores
     switch (layer) {
       case 3: return ws3_cst(in, out, d.wpack[3], d.bias[3], P, nullptr, nullptr, 0.f, st);
-      case 4: return ws4_cst(in, out, d.wpack[4], d.bias[4], P, nullptr, nullptr, 0.f, st);
+      case 5: return pipe5_cst(in, out, d.wpack[5], d.bias[5], P, nullptr, nullptr, 0.f, st);
     }
     return hipErrorInvalidValue;
   }
