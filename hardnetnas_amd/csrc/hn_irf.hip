@@ -232,20 +232,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((CIN == 64 
     }
   }
 
-  // ---- epilogue: float4 stores (the bias is in the accumulators) ------------------------------
+  // ---- epilogue (the bias is in the accumulators): each 32-pixel x 32-channel tile goes through
+  // a per-wave scratch in s_pw (free after the last chunk's barrier), so that every float4 store
+  // instruction writes 8 whole 128-byte pixel rows instead of 32 pixels x 32 bytes ---------------
+  float* scr = s_pw + w * 32 * PS;
+  static_assert(NI * PS >= 4 * 32 * PS, "scratch fits in s_pw");
 #pragma unroll
   for (int i = 0; i < TW; ++i) {
     const int tile = 4 * i + w, pt = tile % NOT, ct = tile / NOT;
-    const int o = pt * 32 + px;
-    if (o >= npv * HOUT * HOUT) continue;
-    float* dst = y + (p0 * (HOUT * HOUT) + o) * COUT + 32 * ct;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int c0 = 8 * q + 4 * h;
-      *reinterpret_cast<float4*>(dst + c0) =
+    for (int q = 0; q < 4; ++q)
+      *reinterpret_cast<float4*>(scr + px * PS + 8 * q + 4 * h) =
           make_float4(acc[i][4 * q], acc[i][4 * q + 1], acc[i][4 * q + 2], acc[i][4 * q + 3]);
+    __builtin_amdgcn_wave_barrier();  // (one wave: its LDS accesses execute in order)
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int pl = 8 * k + (lane >> 3), c4 = lane & 7, o = pt * 32 + pl;
+      if (o < npv * HOUT * HOUT)
+        *reinterpret_cast<float4*>(y + (p0 * (HOUT * HOUT) + o) * COUT + 32 * ct + 4 * c4) =
+            *reinterpret_cast<const float4*>(scr + pl * PS + 4 * c4);
     }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
   }
+  __syncthreads();  // the scratch (s_pw) is rewritten by the next tile's pw
   }  // tile loop
 #undef HN_IRF_LOAD
 }
