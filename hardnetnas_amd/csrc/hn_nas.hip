@@ -303,6 +303,8 @@ __global__ __launch_bounds__(256) void k_skip_s2(const float* __restrict__ in, f
   constexpr int HOUT = HIN / 2, NT = COUT / 32, PT = 4 / NT, KS = CIN / 16;
   static_assert(NT * PT == 4, "4 waves");
   __shared__ uint4 s_b[PT][KS][2][64];
+  // per-wave output tile, transposed for stores of 128-byte rows
+  __shared__ __attribute__((aligned(16))) float s_o[4][32 * 36];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int r = lane & 31, h = lane >> 5;
   const int nt = w % NT, pt = w / NT;  // this wave's MFMA work
@@ -368,14 +370,21 @@ __global__ __launch_bounds__(256) void k_skip_s2(const float* __restrict__ in, f
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks)
       c = mfma3_f16(ah[ks], al[ks], as_f16x8(s_b[pt][ks][0][lane]), as_f16x8(s_b[pt][ks][1][lane]), c);
-    const long op = (g + pt) * 32 + r;
-    if (op < npix) {
-      float* dst = out + op * COUT + 32 * nt + 4 * h;
+    float* so = s_o[w];
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        *reinterpret_cast<float4*>(dst + 8 * q) =
-            make_float4(fmaxf(c[4 * q], 0.f), fmaxf(c[4 * q + 1], 0.f), fmaxf(c[4 * q + 2], 0.f),
-                        fmaxf(c[4 * q + 3], 0.f));
+    for (int q = 0; q < 4; ++q)
+      *reinterpret_cast<float4*>(so + r * 36 + 8 * q + 4 * h) =
+          make_float4(fmaxf(c[4 * q], 0.f), fmaxf(c[4 * q + 1], 0.f), fmaxf(c[4 * q + 2], 0.f),
+                      fmaxf(c[4 * q + 3], 0.f));
+    __builtin_amdgcn_wave_barrier();  // (one wave: its LDS accesses execute in order)
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int pl = 8 * k + (lane >> 3), c4 = lane & 7;
+      const long op = (g + pt) * 32 + pl;
+      if (op < npix)
+        *reinterpret_cast<float4*>(out + op * COUT + 32 * nt + 4 * c4) =
+            *reinterpret_cast<const float4*>(so + pl * 36 + 4 * c4);
     }
     __syncthreads();  // s_b is rewritten by the next tile group
   }
