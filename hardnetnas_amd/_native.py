@@ -10,8 +10,10 @@ There is no fallback: if the library cannot be loaded, every entry point raises.
 from __future__ import annotations
 
 import ctypes
+import itertools
 import os
 import threading
+import weakref
 from typing import Dict, List, Optional
 
 import numpy as np
@@ -160,10 +162,16 @@ def desc_for_module(module) -> HnArchDesc:
     raise TypeError(type(module))
 
 
+_OP_IDS = itertools.count(1)
+_BY_ID: "weakref.WeakValueDictionary[int, NativeModel]" = weakref.WeakValueDictionary()
+
+
 class NativeModel:
     """A device model (packed, BN-folded weights) created through hn_create."""
 
     def __init__(self, desc: HnArchDesc, blob: np.ndarray, device: torch.device):
+        self.op_id = next(_OP_IDS)  # the ``handle`` argument of torch.ops.hardnet_mi355x.forward
+        _BY_ID[self.op_id] = self
         self.lib = load_library()
         self.device = torch.device(device)
         self.desc = desc
@@ -196,7 +204,14 @@ class NativeModel:
         b = x.shape[0]
         if out is None:
             out = torch.empty((b, 128), device=self.device, dtype=torch.float32)
+        elif (tuple(out.shape) != (b, 128) or out.dtype != torch.float32 or out.device != self.device
+              or not out.is_contiguous()):
+            raise ValueError(f"out must be a contiguous fp32 [{b},128] tensor on {self.device}, got "
+                             f"{out.dtype} {tuple(out.shape)} on {out.device}")
         ws_bytes = self.workspace_bytes(b)
+        if workspace is not None and (workspace.dtype != torch.uint8 or workspace.device != self.device
+                                      or not workspace.is_contiguous()):
+            raise ValueError(f"workspace must be a contiguous uint8 tensor on {self.device}")
         if workspace is None or workspace.numel() < ws_bytes:
             workspace = torch.empty(max(ws_bytes, 16), device=self.device, dtype=torch.uint8)
         stream = torch.cuda.current_stream(self.device).cuda_stream
@@ -309,3 +324,25 @@ def preprocess(u8: torch.Tensor, resize: str = "cv2", normalize: bool = True,
         _check(lib.hn_preprocess(x.data_ptr(), n, hw, RESIZE_MODES[resize], int(normalize),
                                  mean, std, out.data_ptr(), stream), "hn_preprocess")
     return out
+
+
+# ----------------------------------------------------------------------------------
+# torch.library registration: hardnet_mi355x::forward(Tensor x, int handle) -> Tensor
+# ----------------------------------------------------------------------------------
+@torch.library.custom_op("hardnet_mi355x::forward", mutates_args=(), device_types="cuda")
+def forward_op(x: torch.Tensor, handle: int) -> torch.Tensor:
+    """Eval-mode descriptor forward of the NativeModel whose ``op_id`` is ``handle`` (the
+    drop-in for HardNet.forward, hardnet/HardNet.py:312-315, under torch.no_grad -- :454).
+    Registered as a custom op with a fake (meta) kernel so that torch.compile traces through
+    the module's forward; there is no CPU kernel (the CPU path is the module's torch layers)."""
+    nm = _BY_ID.get(int(handle))
+    if nm is None:
+        raise RuntimeError(f"hardnet_mi355x::forward: no live native model with handle {handle}")
+    return nm.forward(x)
+
+
+@forward_op.register_fake
+def _forward_fake(x, handle):
+    if x.dim() != 4 or tuple(x.shape[1:]) != (1, 32, 32):
+        raise ValueError(f"expected [B,1,32,32], got {tuple(x.shape)}")
+    return x.new_empty((x.shape[0], 128))

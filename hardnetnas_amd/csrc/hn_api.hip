@@ -11,10 +11,77 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
+#include <utility>
 #include <vector>
 
 static thread_local std::string g_err;
+
+// ---------------------------------------------------------------------------------------
+// launcher knobs and the per-device occupancy cache (hn_internal.h)
+// ---------------------------------------------------------------------------------------
+static int env_int(const char* name, int dflt) {
+  const char* e = std::getenv(name);
+  return e ? std::atoi(e) : dflt;
+}
+
+void hn_read_knobs(HnKnobs* k) {
+  *k = HnKnobs{};
+  k->c12_cfg = env_int("HN_C12_CFG", 12);
+  k->head_v1 = std::getenv("HN_HEAD_V1") != nullptr;
+  k->fdl_valu = std::getenv("HN_FDL_VALU") != nullptr;
+  k->naive_pw = std::getenv("HN_NAIVE_PW") != nullptr;
+  k->naive_dw = std::getenv("HN_NAIVE_DW") != nullptr;
+  k->no_skipfuse = std::getenv("HN_NO_SKIPFUSE") != nullptr;
+  k->pairdist_valu = std::getenv("HN_PAIRDIST_VALU") != nullptr;
+#ifdef HN_EXPERIMENTS
+  k->c12_abl = env_int("HN_C12_ABL", 0) & 255;
+  k->dbg = env_int("HN_DEBUG", 0);
+#endif
+}
+
+static thread_local const HnKnobs* tl_knobs = nullptr;
+
+const HnKnobs& hn_knobs() {
+  if (tl_knobs) return *tl_knobs;
+  static std::once_flag once;
+  static HnKnobs process;
+  std::call_once(once, [] { hn_read_knobs(&process); });
+  return process;
+}
+
+namespace {
+struct KnobScope {  // makes a model's knobs current on this thread for one API call
+  const HnKnobs* prev;
+  explicit KnobScope(const HnKnobs* k) : prev(tl_knobs) { tl_knobs = k; }
+  ~KnobScope() { tl_knobs = prev; }
+};
+}  // namespace
+
+hipError_t hn_resident_blocks(const void* fn, int nthreads, int lds, int* resident) {
+  static std::mutex mu;
+  static std::map<std::pair<const void*, int>, int> cache;
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = cache.find({fn, dev});
+  if (it != cache.end()) {
+    *resident = it->second;
+    return hipSuccess;
+  }
+  if (lds > 0 && (e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds)) != hipSuccess)
+    return e;
+  int per_cu = 0, cus = 0;
+  if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, nthreads, lds)) != hipSuccess) return e;
+  if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
+  const int r = std::max(1, per_cu) * std::max(1, cus);
+  cache[{fn, dev}] = r;
+  *resident = r;
+  return hipSuccess;
+}
 
 static int fail(int code, const std::string& msg) {
   g_err = msg;
@@ -147,6 +214,7 @@ struct Prof {
 
 struct hn_model {
   Prof prof;
+  HnKnobs knobs;  // launcher A/B switches, read once at hn_create
   hn_arch_desc desc{};
   int device = 0;
   std::vector<void*> allocs;
@@ -640,7 +708,19 @@ extern "C" int hn_create(const hn_arch_desc* desc, const float* host_params, siz
     int i = 0;
     for (const char* c = e; *c && i < 6; ++c)
       if (*c >= '0' && *c <= '9') m->variant[i++] = *c - '0';
-      else if (*c >= 'a' && *c <= 'g') m->variant[i++] = 10 + (*c - 'a');
+      else if (*c >= 'a' && *c <= 'z') m->variant[i++] = 10 + (*c - 'a');
+  }
+  hn_read_knobs(&m->knobs);
+  for (int l = 0; l < 6; ++l)
+    if (!hn_hardnet_variant_ok(l, m->variant[l])) {
+      const std::string msg = "HN_VARIANT: tiling " + std::to_string(m->variant[l]) +
+                              " is not available for layer " + std::to_string(l);
+      delete m;
+      return fail(HN_ERR_ARG, msg);
+    }
+  if (!hn_c12_cfg_ok(m->knobs.c12_cfg, m->knobs.c12_abl)) {
+    delete m;
+    return fail(HN_ERR_ARG, "HN_C12_CFG / HN_C12_ABL: no such k_c12 build in this library");
   }
   (void)hipGetDevice(&m->device);
   Cursor cur{host_params, n_params};
@@ -751,7 +831,7 @@ static int forward_nas(hn_model* m, const float* in, int P, int pmax, float* out
     const long npix_out = (long)P * L.hout * L.hout;
     if (L.skip) {
       const float* src = x;
-      const bool nofuse = std::getenv("HN_NO_SKIPFUSE") != nullptr;  // (A/B, layerwise tests)
+      const bool nofuse = m->knobs.no_skipfuse;  // (A/B, layerwise tests)
       if (L.stride == 2 && L.skip_conv && !nofuse && hn_skip_s2_supported(L.hin, L.cin, L.cout)) {
         STAGE("skip", hn_launch_skip_s2(x, y, L.pw_w, L.pw_b, P, L.hin, L.cin, L.cout, st));
         std::swap(x, y);
@@ -812,6 +892,7 @@ extern "C" int hn_forward(hn_model* m, const float* d_in, int64_t batch, float* 
   if (workspace_bytes < need)
     return fail(HN_ERR_WORKSPACE, "workspace too small: need " + std::to_string(need) + " bytes");
   hipStream_t st = static_cast<hipStream_t>(hip_stream);
+  KnobScope knobs(&m->knobs);
   for (int64_t off = 0; off < batch; off += m->chunk) {
     const int P = (int)std::min<int64_t>(m->chunk, batch - off);
     const float* in = d_in + off * 1024;

@@ -548,16 +548,26 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, WP
   X(12, 4, 2, 2, false, 2, true, 5)
 constexpr int kC12Cfgs = 13;
 
+bool hn_c12_cfg_ok(int cfg, int abl) {
+  if (cfg < 0 || cfg >= kC12Cfgs) return false;
+  if (!abl) return true;
+#ifdef HN_EXPERIMENTS
+  switch (cfg) {
+    case 0: return abl == 1 || abl == 6 || abl == 8;
+    case 2: return abl == 6 || abl == 8;
+    case 12: return abl == 1 || abl == 6 || abl == 8 || abl == 32 || abl == 64 || abl == 192;
+  }
+#endif
+  return false;
+}
+
 hipError_t hn_launch_c12(const float* in, float* out, const HardnetDev& d, int P, float eps,
                          hipStream_t st) {
   if (P <= 0) return hipSuccess;
-  // read per launch (tests switch them between models): HN_C12_ABL ablation bits (cfg 0 and 2)
-  const char* ea = std::getenv("HN_C12_ABL");
-  const int abl = ea ? std::atoi(ea) & 255 : 0;
-  const char* ec = std::getenv("HN_C12_CFG");
-  const int cfg = ec ? std::atoi(ec) : 12;  // same-box A/Bs: 12 2-4 % < 7 1.5 % < 2 4.5 % < 0
-  if (cfg < 0 || cfg >= kC12Cfgs) return hipErrorInvalidValue;
-  static int resident[kC12Cfgs] = {};
+  // the calling model's HN_C12_CFG (and, in the HN_EXPERIMENTS library, HN_C12_ABL), hn_create
+  const int cfg = hn_knobs().c12_cfg;  // same-box A/Bs: 12 2-4 % < 7 1.5 % < 2 4.5 % < 0
+  const int abl = hn_knobs().c12_abl;
+  if (!hn_c12_cfg_ok(cfg, abl)) return hipErrorInvalidValue;
   static const void* const fns[kC12Cfgs] = {
 #define HN_C12_FN(C, W, R, E, I, A, Q, PR) reinterpret_cast<const void*>(&k_c12<0, W, R, E, I, A, Q, PR>),
       HN_C12_CFGS(HN_C12_FN)
@@ -569,32 +579,26 @@ hipError_t hn_launch_c12(const float* in, float* out, const HardnetDev& d, int P
 #undef HN_C12_NWS
   };
   const int nw = nws[cfg];
-  if (!resident[cfg]) {
-    int per_cu = 0, dev = 0, cus = 0;
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fns[cfg], nw * 64, 0);
-    if (e != hipSuccess) return e;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    resident[cfg] = std::max(1, per_cu) * std::max(1, cus);
-  }
-  const int grid = (int)std::min<long>((long)P, resident[cfg]);
+  int resident = 0;
+  const hipError_t e = hn_resident_blocks(fns[cfg], nw * 64, 0, &resident);
+  if (e != hipSuccess) return e;
+  const int grid = (int)std::min<long>((long)P, resident);
 #define HN_C12_GO(A, W, R, E, I, WA, Q, PR)                                                      \
   hipLaunchKernelGGL((k_c12<A, W, R, E, I, WA, Q, PR>), dim3(grid), dim3(W * 64), 0, st, in, out,      \
                      d.stem_w, d.stem_b, static_cast<const uint4*>(d.c12_w1), d.bias[1],        \
                      static_cast<const uint4*>(d.c12_w2), d.bias[2], P, eps)
   if (abl) {
+#ifdef HN_EXPERIMENTS
     if (cfg == 0) {
       switch (abl) {
         case 1: HN_C12_GO(1, 8, 4, 2, false, 2, false, 0); break;
         case 6: HN_C12_GO(6, 8, 4, 2, false, 2, false, 0); break;
         case 8: HN_C12_GO(8, 8, 4, 2, false, 2, false, 0); break;
-        default: return hipErrorInvalidValue;
       }
     } else if (cfg == 2) {
       switch (abl) {
         case 6: HN_C12_GO(6, 4, 2, 2, false, 2, false, 0); break;
         case 8: HN_C12_GO(8, 4, 2, 2, false, 2, false, 0); break;
-        default: return hipErrorInvalidValue;
       }
     } else if (cfg == 12) {
       switch (abl) {
@@ -604,11 +608,9 @@ hipError_t hn_launch_c12(const float* in, float* out, const HardnetDev& d, int P
         case 32: HN_C12_GO(32, 4, 2, 2, false, 2, true, 5); break;
         case 64: HN_C12_GO(64, 4, 2, 2, false, 2, true, 5); break;
         case 64 + 128: HN_C12_GO(192, 4, 2, 2, false, 2, true, 5); break;
-        default: return hipErrorInvalidValue;
       }
-    } else {
-      return hipErrorInvalidValue;
     }
+#endif
   } else {
     switch (cfg) {
 #define HN_C12_CASE(C, W, R, E, I, A, Q, PR) \

@@ -329,19 +329,11 @@ __global__ __launch_bounds__(256) void k_fdl_front_mfma(const float* __restrict_
 
 hipError_t hn_launch_fdl_front(const HnFdlFrontArgs& a, int P, int mode, float eps, hipStream_t st) {
   if (P <= 0) return hipSuccess;
-  static int valu = -1;  // HN_FDL_VALU=1: the fp32 VALU form (A/B)
-  if (valu < 0) valu = std::getenv("HN_FDL_VALU") ? 1 : 0;
-  if (!valu) {
-    static int resident = 0;  // persistent grid
-    if (!resident) {
-      int per_cu = 0, dev = 0, cus = 0;
-      hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-          &per_cu, reinterpret_cast<const void*>(&k_fdl_front_mfma<0>), 256, 0);
-      if (e != hipSuccess) return e;
-      (void)hipGetDevice(&dev);
-      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-      resident = std::max(1, per_cu) * std::max(1, cus);
-    }
+  if (!hn_knobs().fdl_valu) {  // HN_FDL_VALU=1: the fp32 VALU form (A/B)
+    int resident = 0;  // persistent grid
+    const hipError_t e =
+        hn_resident_blocks(reinterpret_cast<const void*>(&k_fdl_front_mfma<0>), 256, 0, &resident);
+    if (e != hipSuccess) return e;
     const int grid = std::min((P + 3) / 4, resident);
     if (mode == 0)
       hipLaunchKernelGGL(k_fdl_front_mfma<0>, dim3(grid), dim3(256), 0, st, a.in, a.out, a.stem_w, a.stem_b,

@@ -331,16 +331,10 @@ __global__ __launch_bounds__(256) void k_front(const float* __restrict__ in,
 
 template <int K, int MID, int MODE, bool NORM>
 hipError_t front_launch_t(const HnFrontArgs& a, int P, float eps, hipStream_t st) {
-  static int resident = 0;  // persistent grid: every workgroup resident at once
-  if (!resident) {
-    int per_cu = 0, dev = 0, cus = 0;
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &per_cu, reinterpret_cast<const void*>(&k_front<K, MID, MODE, NORM>), 256, 0);
-    if (e != hipSuccess) return e;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    resident = std::max(1, per_cu) * std::max(1, cus);
-  }
+  int resident = 0;  // persistent grid: every workgroup resident at once
+  const hipError_t e =
+      hn_resident_blocks(reinterpret_cast<const void*>(&k_front<K, MID, MODE, NORM>), 256, 0, &resident);
+  if (e != hipSuccess) return e;
   hipLaunchKernelGGL((k_front<K, MID, MODE, NORM>), dim3(std::min(P, resident)), dim3(256), 0, st, a.in,
                      a.out, a.spack, a.stem_b, a.apack, a.pw_b, a.dw_w, a.dw_b, a.pwl_a, a.pwl_b, P, eps);
   return hipGetLastError();

@@ -329,6 +329,7 @@ __global__ __launch_bounds__(256) void k_conv3x3(const float* __restrict__ in, f
   // patches when NP > 1), so tile pixel m is output pixel (p0*HOUT + y0)*WOUT + m.
   float* obase = out + ((size_t)(p0 * C::HOUT + y0) * C::WOUT + wm * C::MT * 32 + r) * COUT +
                  wn * C::NT * 32 + 4 * h;
+#ifdef HN_EXPERIMENTS
   if (dbg & 1) {  // ablation: keep the accumulators live, one store per lane
     float sum = 0.f;
 #pragma unroll
@@ -340,6 +341,7 @@ __global__ __launch_bounds__(256) void k_conv3x3(const float* __restrict__ in, f
     obase[0] = sum;
     return;
   }
+#endif
 #pragma unroll
   for (int nt = 0; nt < C::NT; ++nt) {
     float4 bv[4];
@@ -387,6 +389,7 @@ struct PipeCfg : ConvCfg<CIN, COUT, HIN, S, NP, TR, WM, WN> {
   static constexpr int SCR = 32 * SROW * 4;   // CST: one 32-pixel x 16-channel half tile per wave
   static constexpr int SMEM = 2 * BUF + (STEM ? 34 * 34 * 4 : 0) + (CST ? NW * SCR : 0);
   static_assert(SMEM <= 160 * 1024, "LDS");
+  static_assert(!(STEM && CST), "the CST epilogue scratch starts where the STEM buffers live");
   static_assert(UPT <= 18, "prefetch fits in the K-loop");
 };
 
@@ -742,6 +745,7 @@ struct WsCfg : ConvCfg<CIN, COUT, HIN, S, NP, TR, WM, WN, PX> {
   static constexpr int SMEM = 2 * BUF + (STEM ? NWP * PBUF : 0) + (CST ? NWC * SCR : 0);
   static constexpr bool DEEP = !STEM && UPT <= 6;  // two stages of loads in flight
   static_assert(SMEM <= 160 * 1024, "LDS");
+  static_assert(!(STEM && CST), "the CST epilogue scratch starts where the STEM buffers live");
 };
 
 // STEM (conv1 only): the producers load the raw patch, reduce mean/std per wave, write the
@@ -1277,15 +1281,6 @@ __global__ __launch_bounds__(256) void k_head2(const float* __restrict__ a, floa
 // ------------------------------------------------------------------------------------
 // host launchers
 // ------------------------------------------------------------------------------------
-static int g_dbg = -1;  // HN_DEBUG bits: 1 = skip conv epilogue stores (ablation only)
-static int dbg_flags() {
-  if (g_dbg < 0) {
-    const char* e = std::getenv("HN_DEBUG");
-    g_dbg = e ? std::atoi(e) : 0;
-  }
-  return g_dbg;
-}
-
 // stem-fused kernels carry the normalised patch (34x34 fp32) + 8 reduction floats
 template <class CFG, bool STEM>
 constexpr int conv_lds() { return CFG::LDS + (STEM ? (34 * 34 + 8) * 4 : 0); }
@@ -1296,19 +1291,15 @@ constexpr int conv_lds() { return CFG::LDS + (STEM ? (34 * 34 + 8) * 4 : 0); }
                          int P, const float* sw, const float* sb, float eps,               \
                          hipStream_t st) {                                                 \
     constexpr int lds = conv_lds<NAME##_cfg, STEM>();                                      \
-    static bool attr = false;                                                              \
-    if (!attr) {                                                                           \
-      hipError_t e = hipFuncSetAttribute(                                                  \
-          reinterpret_cast<const void*>(&k_conv3x3<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM>), \
-          hipFuncAttributeMaxDynamicSharedMemorySize, lds);                                \
-      if (e != hipSuccess) return e;                                                       \
-      attr = true;                                                                         \
-    }                                                                                      \
+    int resident = 0; /* sets the dynamic-LDS limit on this device */                     \
+    hipError_t e = hn_resident_blocks(                                                     \
+        reinterpret_cast<const void*>(&k_conv3x3<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM>), \
+        256, lds, &resident);                                                              \
+    if (e != hipSuccess) return e;                                                         \
     const int grid = (P + NP - 1) / NP * NAME##_cfg::RT;                                   \
-    (void)dbg_flags();                                                                     \
     hipLaunchKernelGGL((k_conv3x3<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM>), dim3(grid),   \
                        dim3(256), lds, st, in, out, static_cast<const uint4*>(wp), bias, P, \
-                       sw, sb, eps, g_dbg);                                                \
+                       sw, sb, eps, hn_knobs().dbg);                                       \
     return hipGetLastError();                                                              \
   }
 
@@ -1336,17 +1327,9 @@ HN_CONV(conv5_v1, false, 128, 128, 8, 1, 1, 8, 1, 4)
     constexpr int lds = NAME##_cfg::SMEM;                                                  \
     const void* fn = reinterpret_cast<const void*>(                                        \
         &k_conv_pipe<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM, ABL, CST>);                       \
-    static int resident = 0;                                                               \
-    if (!resident) {                                                                       \
-      hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds); \
-      if (e != hipSuccess) return e;                                                       \
-      int per_cu = 0, dev = 0, cus = 0;                                                    \
-      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, NAME##_cfg::NTHR, lds); \
-      if (e != hipSuccess) return e;                                                       \
-      (void)hipGetDevice(&dev);                                                            \
-      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);       \
-      resident = std::max(1, per_cu) * std::max(1, cus);                                   \
-    }                                                                                      \
+    int resident = 0;                                                                      \
+    const hipError_t e = hn_resident_blocks(fn, NAME##_cfg::NTHR, lds, &resident);         \
+    if (e != hipSuccess) return e;                                                         \
     const int tiles = (P + NP - 1) / NP * NAME##_cfg::RT;                                  \
     const int grid = std::min(tiles, resident);                                            \
     hipLaunchKernelGGL((k_conv_pipe<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM, ABL, CST>), dim3(grid), \
@@ -1366,11 +1349,6 @@ HN_PIPE(pipe4_t8, false, 64, 128, 16, 2, 1, 8, 1, 4)
 HN_PIPE(pipe5, false, 128, 128, 8, 1, 1, 8, 1, 4)
 HN_PIPE(pipe5_np2, false, 128, 128, 8, 1, 2, 8, 1, 4)
 HN_PIPE_C(pipe5_cst, false, 128, 128, 8, 1, 2, 8, 1, 4, 0, true)  // HN_VARIANT digit g at conv5
-// conv3 ablation builds (HN_VARIANT digit 4..7 for layer 3 -> ABL 1, 2, 4, 7)
-HN_PIPE_A(pipe3_a1, false, 64, 64, 16, 1, 1, 8, 2, 2, 1)
-HN_PIPE_A(pipe3_a2, false, 64, 64, 16, 1, 1, 8, 2, 2, 2)
-HN_PIPE_A(pipe3_a4, false, 64, 64, 16, 1, 1, 8, 2, 2, 4)
-HN_PIPE_A(pipe3_a7, false, 64, 64, 16, 1, 1, 8, 2, 2, 7)
 
 #define HN_WS(NAME, CIN, COUT, HIN, S, NP, TR, WM, WN) HN_WS_S(NAME, false, CIN, COUT, HIN, S, NP, TR, WM, WN)
 #define HN_WS_S(NAME, STEM, CIN, COUT, HIN, S, NP, TR, WM, WN) HN_WS_A(NAME, STEM, CIN, COUT, HIN, S, NP, TR, WM, WN, 0)
@@ -1383,17 +1361,9 @@ HN_PIPE_A(pipe3_a7, false, 64, 64, 16, 1, 1, 8, 2, 2, 7)
     constexpr int lds = NAME##_cfg::SMEM;                                                  \
     const void* fn =                                                                       \
         reinterpret_cast<const void*>(&k_conv_ws<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM, ABL, PX, CST>); \
-    static int resident = 0;                                                               \
-    if (!resident) {                                                                       \
-      hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds); \
-      if (e != hipSuccess) return e;                                                       \
-      int per_cu = 0, dev = 0, cus = 0;                                                    \
-      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, NAME##_cfg::NTHR, lds); \
-      if (e != hipSuccess) return e;                                                       \
-      (void)hipGetDevice(&dev);                                                            \
-      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);       \
-      resident = std::max(1, per_cu) * std::max(1, cus);                                   \
-    }                                                                                      \
+    int resident = 0;                                                                      \
+    const hipError_t e = hn_resident_blocks(fn, NAME##_cfg::NTHR, lds, &resident);         \
+    if (e != hipSuccess) return e;                                                         \
     const int tiles = (P + NP - 1) / NP * NAME##_cfg::RT;                                  \
     const int grid = std::min(tiles, resident);                                            \
     hipLaunchKernelGGL((k_conv_ws<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM, ABL, PX, CST>), dim3(grid), \
@@ -1427,7 +1397,9 @@ HN_WS_C(ws3_cst, false, 64, 64, 16, 1, 1, 16, 2, 2, 0, 80, true)
 HN_WS(ws3_w8, 64, 64, 16, 1, 1, 16, 4, 1)
 HN_WS(ws4_w8, 64, 128, 16, 2, 1, 8, 2, 2)
 HN_WS(ws5_w8, 128, 128, 8, 1, 2, 8, 2, 2)
-// ablation builds (timing only, wrong results): weights fetched once per stage
+#ifdef HN_EXPERIMENTS
+// ablation builds (timing only, wrong results; the HN_EXPERIMENTS library only): weights
+// fetched once per stage
 HN_WS_A(ws3_a1, false, 64, 64, 16, 1, 1, 16, 2, 2, 45)
 HN_WS_A(ws4_a1, false, 64, 128, 16, 2, 1, 8, 1, 4, 45)
 HN_WS_A(ws5_a1, false, 128, 128, 8, 1, 2, 8, 1, 4, 45)
@@ -1437,6 +1409,7 @@ HN_WS_A(ws5_a2, false, 128, 128, 8, 1, 2, 8, 1, 4, 8)
 HN_WS_A(ws3_a3, false, 64, 64, 16, 1, 1, 16, 2, 2, 40)
 HN_WS_A(ws4_a3, false, 64, 128, 16, 2, 1, 8, 1, 4, 40)
 HN_WS_A(ws5_a3, false, 128, 128, 8, 1, 2, 8, 1, 4, 40)
+#endif
 
 hipError_t hn_launch_stem(const float* in, float* out, const float* w, const float* b, int P,
                           bool norm, float eps, hipStream_t st) {
@@ -1447,10 +1420,32 @@ hipError_t hn_launch_stem(const float* in, float* out, const float* w, const flo
   return hipGetLastError();
 }
 
+// HN_VARIANT digit v is a tiling this library has for conv layer `layer` (0 = stem + conv1,
+// 1 = conv1 alone, 2..5 = conv2..conv5); mirrors the dispatch below.  Digits 4 / 8 / 9 are the
+// timing-only ablation builds of conv3..conv5 (HN_EXPERIMENTS library only).
+bool hn_hardnet_variant_ok(int layer, int v) {
+  if (layer < 0 || layer > 5) return false;
+  if (v == 4 || v == 8 || v == 9) {
+#ifdef HN_EXPERIMENTS
+    return layer >= 3;
+#else
+    return false;
+#endif
+  }
+  if (v >= 13 && v <= 15) return layer == 4;
+  if (v == 16) return layer == 3 || layer == 5;
+  if (v == 7) return layer >= 3;
+  if (v == 0 || v == 1) return true;
+  if (v == 2 || v == 3 || v == 5 || v == 6) return true;  // (layer 1 always runs conv1_launch)
+  return false;
+}
+
 // layer 0 = fused stem (input_norm + conv0) + conv1 from the raw patches
 hipError_t hn_launch_hardnet_conv(int layer, int variant, const HardnetDev& d, const float* in,
                                   float* out, int P, float eps, hipStream_t st) {
   const bool v1 = variant == 1;
+  if (!hn_hardnet_variant_ok(layer, variant)) return hipErrorInvalidValue;
+#ifdef HN_EXPERIMENTS
   if (variant == 8 || variant == 9 || variant == 4) {  // ablation (timing only)
     const int a = variant == 8 ? 1 : variant == 9 ? 2 : 3;
     switch (layer) {
@@ -1460,6 +1455,7 @@ hipError_t hn_launch_hardnet_conv(int layer, int variant, const HardnetDev& d, c
     }
     return hipErrorInvalidValue;
   }
+#endif
   if (variant >= 13 && variant <= 15) {  // conv4, 64-byte swizzled window (2 / 1 / 2 patches per stage)
     if (layer != 4) return hipErrorInvalidValue;
     return (variant == 13 ? ws4_np2s : variant == 14 ? ws4_s : ws4_np2s22)(in, out, d.wpack[4], d.bias[4], P,
@@ -1491,10 +1487,6 @@ hipError_t hn_launch_hardnet_conv(int layer, int variant, const HardnetDev& d, c
       case 5: return (big ? ws5_np2 : ws5)(in, out, d.wpack[5], d.bias[5], P, nullptr, nullptr, 0.f, st);
     }
     return hipErrorInvalidValue;
-  }
-  if (layer == 3 && variant >= 4) {
-    auto f = variant == 4 ? pipe3_a1 : variant == 5 ? pipe3_a2 : variant == 6 ? pipe3_a4 : pipe3_a7;
-    return f(in, out, d.wpack[3], d.bias[3], P, nullptr, nullptr, 0.f, st);
   }
   if (variant >= 2) {  // persistent pipelined kernels: 2 = smaller tile, 3 = larger tile
     const bool big = variant == 3;
@@ -1528,8 +1520,7 @@ hipError_t hn_launch_hardnet_conv(int layer, int variant, const HardnetDev& d, c
 hipError_t hn_launch_head(const float* a, float* out, const void* wp, const float* bias, int P,
                           int K, float l2eps, hipStream_t st, bool f16) {
   const int grid = (P + 63) / 64;
-  static int old = -1;
-  if (old < 0) old = std::getenv("HN_HEAD_V1") ? 1 : 0;
+  const bool old = hn_knobs().head_v1;
   const uint4* w = static_cast<const uint4*>(wp);
   if (K == 8192 && !f16 && old)
     hipLaunchKernelGGL(k_head<8192>, dim3(grid), dim3(256), 0, st, a, out, w, bias, P, l2eps);

@@ -2,6 +2,30 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+// A/B switches of the launchers.  Read from the environment once per model in hn_create (and
+// once per process for the model-less entry points); hn_forward makes the calling model's
+// set current for the duration of the call (thread-local), so launchers never call getenv.
+// Every switch selects a parity-tested alternative kernel; the ablation switches (c12_abl,
+// dbg: timing-only builds with wrong results) exist only in the HN_EXPERIMENTS library.
+struct HnKnobs {
+  int c12_cfg = 12;            // HN_C12_CFG: k_c12 configuration (0..12, all exact)
+  bool head_v1 = false;        // HN_HEAD_V1: the first HardNet head GEMM
+  bool fdl_valu = false;       // HN_FDL_VALU: FDLNet front as fp32 VALU
+  bool naive_pw = false;       // HN_NAIVE_PW: untiled 1x1 conv kernel
+  bool naive_dw = false;       // HN_NAIVE_DW: untiled depthwise kernel
+  bool no_skipfuse = false;    // HN_NO_SKIPFUSE: maxpool + pw instead of k_skip_s2
+  bool pairdist_valu = false;  // HN_PAIRDIST_VALU: fp32 VALU pair-distance kernel
+  int c12_abl = 0;             // HN_C12_ABL (HN_EXPERIMENTS only)
+  int dbg = 0;                 // HN_DEBUG (HN_EXPERIMENTS only)
+};
+void hn_read_knobs(HnKnobs* k);
+const HnKnobs& hn_knobs();
+
+// Resident workgroups of `fn` on the current device at `nthreads` threads and `lds` bytes of
+// dynamic LDS (also raises the function's dynamic-LDS limit to `lds` on that device).  Cached
+// per (function, device) under a mutex.
+hipError_t hn_resident_blocks(const void* fn, int nthreads, int lds, int* resident);
+
 // Device-resident, BN-folded, packed HardNet parameters.
 struct HardnetDev {
   float* stem_w = nullptr;   // [9][32]   conv0 folded
@@ -17,6 +41,8 @@ hipError_t hn_launch_c12(const float* in, float* out, const HardnetDev& d, int P
 
 hipError_t hn_launch_stem(const float* in, float* out, const float* w, const float* b, int P,
                           bool norm, float eps, hipStream_t st);
+bool hn_hardnet_variant_ok(int layer, int variant);
+bool hn_c12_cfg_ok(int cfg, int abl);
 hipError_t hn_launch_hardnet_conv(int layer, int variant, const HardnetDev& d, const float* in,
                                   float* out, int P, float eps, hipStream_t st);
 hipError_t hn_launch_head(const float* a, float* out, const void* wp, const float* bias, int P,

@@ -265,15 +265,9 @@ template <int CIN, int COUT, int HIN, int S, int K, int MID>
 hipError_t irf_launch(const HnIrfArgs& a, int P, hipStream_t st) {
   constexpr int NPB = IrfTile<CIN, HIN>::NPB;
   const void* fn = reinterpret_cast<const void*>(&k_irf<CIN, COUT, HIN, S, K, MID>);
-  static int resident = 0;  // persistent grid: every workgroup resident at once
-  if (!resident) {
-    int per_cu = 0, dev = 0, cus = 0;
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, 0);
-    if (e != hipSuccess) return e;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    resident = std::max(1, per_cu) * std::max(1, cus);
-  }
+  int resident = 0;  // persistent grid: every workgroup resident at once
+  const hipError_t e = hn_resident_blocks(fn, 256, 0, &resident);
+  if (e != hipSuccess) return e;
   const int grid = CIN == 32 ? std::min((P + NPB - 1) / NPB, resident) : (P + NPB - 1) / NPB;
   hipLaunchKernelGGL((k_irf<CIN, COUT, HIN, S, K, MID>), dim3(grid), dim3(256), 0, st, a.x, a.y, a.pw_a,
                      a.pw_b, a.dw_w, a.dw_b, a.pwl_a, a.pwl_b, P);

@@ -456,8 +456,7 @@ static inline unsigned blocks(long n, int per) { return (unsigned)((n + per - 1)
 hipError_t hn_launch_pw(const float* in, float* out, const float* wt, const float* bias,
                         const float* res, long npix, int cin, int cout, int groups, bool relu,
                         int shuffle_g, hipStream_t st) {
-  static int naive = -1;
-  if (naive < 0) naive = std::getenv("HN_NAIVE_PW") ? 1 : 0;
+  const bool naive = hn_knobs().naive_pw;
   if (naive) {
     hipLaunchKernelGGL(k_pw, dim3(blocks(npix * (cout / 4), 256)), dim3(256), 0, st, in, out, wt,
                        bias, res, npix, cin, cout, groups, relu ? 1 : 0, shuffle_g);
@@ -490,8 +489,7 @@ static hipError_t dw_lds(const float* in, float* out, const float* wd, const flo
 hipError_t hn_launch_dw(const float* in, float* out, const float* wd, const float* bias, int P,
                         int hin, int c, int k, int s, hipStream_t st) {
   const int hout = hin / s;
-  static int naive = -1;
-  if (naive < 0) naive = std::getenv("HN_NAIVE_DW") ? 1 : 0;
+  const bool naive = hn_knobs().naive_dw;
   if (!naive && c % 32 == 0) {
     // strips of T output rows: LDS <= ~60 KB for every SEARCH_SPACE2 shape
 #define HN_DWCASE(KK, SS, HH, TT) \
@@ -515,16 +513,10 @@ hipError_t hn_launch_dw(const float* in, float* out, const float* wd, const floa
 template <int HIN, int CIN, int COUT>
 static hipError_t skip_s2_launch(const float* in, float* out, const float* wt, const float* bias, int P,
                                  hipStream_t st) {
-  static int resident = 0;  // persistent grid
-  if (!resident) {
-    int per_cu = 0, dev = 0, cus = 0;
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &per_cu, reinterpret_cast<const void*>(&k_skip_s2<HIN, CIN, COUT>), 256, 0);
-    if (e != hipSuccess) return e;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    resident = (per_cu > 1 ? per_cu : 1) * (cus > 1 ? cus : 1);
-  }
+  int resident = 0;  // persistent grid
+  const hipError_t e =
+      hn_resident_blocks(reinterpret_cast<const void*>(&k_skip_s2<HIN, CIN, COUT>), 256, 0, &resident);
+  if (e != hipSuccess) return e;
   constexpr int PT = 4 / (COUT / 32);
   const long groups = (((long)P * (HIN / 2) * (HIN / 2) + 31) / 32 + PT - 1) / PT;
   const int grid = (int)(groups < resident ? groups : resident);

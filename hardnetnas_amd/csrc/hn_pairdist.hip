@@ -270,8 +270,7 @@ hipError_t hn_launch_pairdist(const float* a, const float* p, int B, int D_, int
   if (D_ != D) return hipErrorInvalidValue;
   unsigned* cm = static_cast<unsigned*>(ws);
   const unsigned g = (B + 255) / 256;
-  static int valu = -1;
-  if (valu < 0) valu = std::getenv("HN_PAIRDIST_VALU") ? 1 : 0;
+  const bool valu = hn_knobs().pairdist_valu;  // HN_PAIRDIST_VALU (A/B), read once per process
   if (!valu) {
     float* asq = reinterpret_cast<float*>(cm + ((B + 63) / 64) * 64);
     float* psq = asq + ((B + 63) / 64) * 64;

@@ -12,12 +12,14 @@ reference training / FPR95 loops and checkpoints work unchanged:
   ``ConvBNRelu`` / ``IRFBlock`` / ``Identity`` (fbnet_building_blocks/fbnet_builder.py)
   so the keys of a supernet checkpoint map 1:1 (``load_supernet_state_dict``).
 
-Eval-mode forward on a HIP tensor (fp32, contiguous ``[B,1,32,32]``) runs the
-hand-written gfx950 kernels through the C ABI (``hardnetnas_amd._native``).  There
-is no silent fallback for that case: if the native library is missing the call
-raises.  Train mode (BatchNorm batch statistics, Dropout, autograd -- SURVEY.md
-8(f) row 4, out of scope for the HIP path) and CPU tensors run the module's own
-PyTorch layers, exactly like the reference module would.
+Eval-mode forward on a HIP tensor (fp32 ``[B,1,32,32]``) with no autograd graph to record
+(under ``torch.no_grad()`` as in the reference eval loop, hardnet/HardNet.py:454, or with
+parameters frozen) runs the hand-written gfx950 kernels through the registered op
+``torch.ops.hardnet_mi355x.forward`` (C ABI, ``hardnetnas_amd._native``).  There is no silent
+fallback for that case: if the native library is missing the call raises.  Train mode
+(BatchNorm batch statistics, Dropout), autograd-recording calls and CPU tensors run the
+module's own PyTorch layers, exactly like the reference module would; ``strict=True`` turns
+an eval-mode HIP call that cannot take the native path into an error.
 """
 from __future__ import annotations
 
@@ -50,19 +52,40 @@ class Flatten(nn.Module):
         return x.reshape(x.size(0), -1)
 
 
+def _native_blocker(module: nn.Module, x: torch.Tensor):
+    """None if this call can run on the HIP kernels, else why not.  The native forward is an
+    inference kernel: it builds no autograd graph, so whenever the reference module would
+    record one (grad mode on and the input or any parameter requiring grad -- e.g. an eval-mode
+    fine-tune, or input gradients; hardnet/HardNet.py:392-423) the module's own layers run."""
+    if module.training:
+        return "module is in train mode"
+    if not x.is_cuda:
+        return "input is not a HIP tensor"
+    if x.dtype != torch.float32 or x.dim() != 4 or tuple(x.shape[1:]) != (1, 32, 32):
+        return f"input must be fp32 [B,1,32,32], got {x.dtype} {tuple(x.shape)}"
+    if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in module.parameters())):
+        return "autograd is recording (grad mode on and the input or a parameter requires grad)"
+    return None
+
+
 def _native_eligible(module: nn.Module, x: torch.Tensor) -> bool:
-    return (not module.training and x.is_cuda and x.dtype == torch.float32
-            and x.dim() == 4 and tuple(x.shape[1:]) == (1, 32, 32))
+    return _native_blocker(module, x) is None
 
 
 class _NativeMixin:
-    """Owns the packed device model; re-packs when parameters/buffers change."""
+    """Owns the packed device model; re-packs when parameters/buffers change.
+
+    ``native_strict`` (constructor keyword ``strict``): an eval-mode call on a HIP tensor that
+    cannot take the native path raises instead of running the torch layers."""
+
+    native_strict = False
 
     def _native_key(self):
         ts = list(self.parameters()) + list(self.buffers())
         return tuple((t.data_ptr(), t._version) for t in ts)
 
-    def _native_forward(self, x: torch.Tensor) -> torch.Tensor:
+    @torch.compiler.disable
+    def _native_handle(self, x: torch.Tensor) -> int:
         from . import _native
         key = (x.device.index, self._native_key())
         h = getattr(self, "_hn_handle", None)
@@ -70,7 +93,20 @@ class _NativeMixin:
             self._hn_handle = None  # release the old one first
             self._hn_handle = _native.NativeModel.from_module(self, x.device)
             self._hn_key = key
-        return self._hn_handle.forward(x)
+        return self._hn_handle.op_id
+
+    def _native_forward(self, x: torch.Tensor) -> torch.Tensor:
+        from . import _native  # noqa: F401  (registers torch.ops.hardnet_mi355x)
+        return torch.ops.hardnet_mi355x.forward(x, self._native_handle(x))
+
+    def _dispatch_native(self, x: torch.Tensor):
+        """The native descriptor if this call takes the HIP path, else None (torch layers)."""
+        why = _native_blocker(self, x)
+        if why is None:
+            return self._native_forward(x)
+        if self.native_strict and not self.training and x.is_cuda:
+            raise RuntimeError(f"{type(self).__name__}(strict=True): native forward not taken: {why}")
+        return None
 
     def __getstate__(self):
         d = dict(self.__dict__)
@@ -82,8 +118,9 @@ class _NativeMixin:
 class HardNet(_NativeMixin, nn.Module):
     """HardNet model definition (hardnet/HardNet.py:275-315)."""
 
-    def __init__(self):
+    def __init__(self, strict: bool = False):
         super().__init__()
+        self.native_strict = strict
         self.features = nn.Sequential(
             nn.Conv2d(1, 32, kernel_size=3, padding=1, bias=False),
             nn.BatchNorm2d(32, affine=False),
@@ -120,8 +157,9 @@ class HardNet(_NativeMixin, nn.Module):
         return (x - mp.detach().view(-1, 1, 1, 1)) / sp.detach().view(-1, 1, 1, 1)
 
     def forward(self, input):
-        if _native_eligible(self, input):
-            return self._native_forward(input)
+        y = self._dispatch_native(input)
+        if y is not None:
+            return y
         x_features = self.features(self.input_norm(input))
         x = x_features.view(x_features.size(0), -1)
         norm = torch.sqrt(torch.sum(x * x, dim=1) + self.l2_eps)
@@ -254,8 +292,10 @@ class HardNetNeiMask(_NativeMixin, nn.Module):
     ``torch.norm`` without eps (des.py:49-53).  The neighbour-mask training loss is not
     part of the descriptor forward and is not restated here."""
 
-    def __init__(self, MARGIN: float = 1.0, C: float = 1.0, variant: str = "NASNet"):
+    def __init__(self, MARGIN: float = 1.0, C: float = 1.0, variant: str = "NASNet",
+                 strict: bool = False):
         super().__init__()
+        self.native_strict = strict
         if variant not in A.FDL_VARIANTS:
             raise ValueError(f"variant must be one of {A.FDL_VARIANTS}")
         self.MARGIN, self.C, self.variant = MARGIN, C, variant
@@ -282,8 +322,9 @@ class HardNetNeiMask(_NativeMixin, nn.Module):
         return (x - mp.detach().view(-1, 1, 1, 1)) / sp.detach().view(-1, 1, 1, 1)
 
     def forward(self, input):
-        if _native_eligible(self, input):
-            return self._native_forward(input)
+        y = self._dispatch_native(input)
+        if y is not None:
+            return y
         x_features = self.features(self.input_norm(input))
         x = x_features.view(x_features.size(0), -1)
         return x / torch.norm(x, p=2, dim=-1, keepdim=True)
@@ -298,8 +339,9 @@ class HardNetNAS(_NativeMixin, nn.Module):
     ``y / torch.norm(y)`` with no epsilon (model_supernet.py:84).
     """
 
-    def __init__(self, arch="wang2", layers: Sequence = None):
+    def __init__(self, arch="wang2", layers: Sequence = None, strict: bool = False):
         super().__init__()
+        self.native_strict = strict
         self.arch_ops: List[str] = A.arch_ops(arch)
         self.layers = list(layers) if layers is not None else list(A.SEARCH_SPACE2)
         self.first = ConvBNRelu(1, A.STEM_CHANNELS, 3, 1, 1, relu=True)
@@ -313,8 +355,9 @@ class HardNetNAS(_NativeMixin, nn.Module):
         ]))
 
     def forward(self, x):
-        if _native_eligible(self, x):
-            return self._native_forward(x)
+        y = self._dispatch_native(x)
+        if y is not None:
+            return y
         y = self.first(x)
         for op in self.stages:
             y = op(y)

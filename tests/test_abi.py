@@ -116,3 +116,67 @@ def test_bench_knows_every_hardnet_stage():
     fwd = src[src.index("static int forward_hardnet("):src.index("static int forward_nas(")]
     names = set(re.findall(r'STAGE\("([^"]+)"', fwd))
     assert names and names <= set(bench.HARDNET_STAGE_MAC) and names <= set(bench.HARDNET_STAGE_BYTES)
+
+
+def _kernel_template_args(kernel: str):
+    """Template argument lists of every `kernel<...>` symbol in the product library (nm -C)."""
+    import subprocess
+    out = subprocess.run(["nm", "-C", "--defined-only", N.lib_path()], capture_output=True,
+                         text=True, check=True).stdout
+    return [m.split(",") for m in re.findall(kernel + r"<([^<>]*)>\(", out)]
+
+
+def test_product_library_has_no_ablation_builds():
+    """The timing-only ablation builds (wrong results by construction) live only in the
+    HN_EXPERIMENTS library: no k_conv_ws / k_conv_pipe (ABL = 10th template argument) or k_c12
+    (ABL = 1st) instantiation in libhardnet_mi355x.so carries a nonzero ABL."""
+    ws = _kernel_template_args("k_conv_ws")
+    pipe = _kernel_template_args("k_conv_pipe")
+    c12 = _kernel_template_args("k_c12")
+    assert ws and pipe and c12
+    for args in ws + pipe:
+        assert int(args[9]) == 0, args
+    for args in c12:
+        assert int(args[0]) == 0, args
+
+
+@pytest.mark.parametrize("env,val", [("HN_VARIANT", "888888"), ("HN_VARIANT", "004000"),
+                                     ("HN_VARIANT", "00000z"), ("HN_C12_CFG", "13")])
+def test_create_rejects_ablation_and_unknown_builds(env, val, monkeypatch):
+    """hn_create validates the A/B switches before touching the GPU: an ablation tiling or an
+    unknown k_c12 configuration is HN_ERR_ARG, never a silently wrong model."""
+    m, _, _ = build_module("hardnet")
+    blob = N.state_dict_blob(m.state_dict())
+    monkeypatch.setenv(env, val)
+    lib = N.load_library()
+    h = ctypes.c_void_p()
+    rc = lib.hn_create(ctypes.byref(N.hardnet_desc()), blob.ctypes.data, blob.size, ctypes.byref(h))
+    assert rc == 1, lib.hn_last_error()
+    assert env.encode() in lib.hn_last_error()
+    assert not h.value
+
+
+def test_registered_torch_op_and_fake_kernel():
+    """torch.ops.hardnet_mi355x.forward exists (registered at import) and its fake kernel gives
+    the [B,128] result shape that torch.compile traces with."""
+    import torch
+    from torch._subclasses.fake_tensor import FakeTensorMode
+    assert hasattr(torch.ops.hardnet_mi355x, "forward")
+    with FakeTensorMode():
+        y = torch.ops.hardnet_mi355x.forward(torch.empty(7, 1, 32, 32), 1)
+    assert tuple(y.shape) == (7, 128)
+
+
+def test_cpu_and_train_calls_use_the_torch_layers():
+    """CPU tensors and train mode never reach the native path (reference semantics), with or
+    without strict."""
+    import torch
+    from hardnetnas_amd.model import HardNet
+    m = HardNet(strict=True).eval()
+    x = torch.randn(3, 1, 32, 32)
+    with torch.no_grad():
+        assert m(x).shape == (3, 128)
+    m.train()
+    y = m(torch.randn(4, 1, 32, 32))
+    y.sum().backward()
+    assert getattr(m, "_hn_handle", None) is None

@@ -47,7 +47,7 @@ def test_forward_matches_reference_vectors(name, cuda_device):
     assert np.abs(ye - fx["y_edge"]).max() <= _tol(name)
 
 
-@pytest.mark.parametrize("name", ["hardnet", "wang2", "fdl_NASNet_01"])
+@pytest.mark.parametrize("name", ["hardnet", "wang2", "wang3", "fdl_NASNet", "fdl_NASNet_01"])
 @pytest.mark.parametrize("b", [1, 3, 63, 65, 130, 255])
 def test_ragged_batches(name, b, cuda_device):
     m, fx, _ = build_module(name)
@@ -120,9 +120,9 @@ def test_c12_variants_match(cuda_device, monkeypatch, cfg):
     from hardnetnas_amd._native import NativeModel
     m, fx, _ = build_module("hardnet")
     x = torch.from_numpy(golden_inputs(fx)).to(cuda_device)
+    y0 = NativeModel.from_module(m, cuda_device)(x).cpu().numpy()
+    monkeypatch.setenv("HN_C12_CFG", cfg)  # read once, by hn_create
     nm = NativeModel.from_module(m, cuda_device)
-    y0 = nm(x).cpu().numpy()
-    monkeypatch.setenv("HN_C12_CFG", cfg)
     y = nm(x).cpu().numpy()
     assert np.abs(y - fx["y"]).max() <= TOL["hardnet"]
     assert np.abs(y - y0).max() <= 2e-5
@@ -178,6 +178,50 @@ def test_large_batch_properties(name, cuda_device):
     else:
         ref = O.nas_forward(t, load("nas_" + name)["meta"]["ops"], xs)
     assert (y[idx.to(cuda_device)].cpu() - ref).abs().max().item() <= _tol(name)
+
+
+def _oracle_rows(name, p, xs):
+    t = {k: torch.from_numpy(v) for k, v in p.items()}
+    if name == "hardnet":
+        return O.hardnet_forward(t, xs)
+    if name.startswith("fdl_"):
+        return O.fdl_forward(t, load(name)["meta"]["variant"], xs)
+    return O.nas_forward(t, load("nas_" + name)["meta"]["ops"], xs)
+
+
+@pytest.mark.parametrize("name", ["wang2", "wang3", "wang4", "fdl_NASNet", "fdl_NASNet_01"])
+def test_persistent_kernels_past_one_round(name, cuda_device):
+    """65,537 patches: every persistent NAS / FDL kernel (grid = min(tiles, resident)) runs
+    several rounds per workgroup and ends on a ragged tile; a strided 256-row sample (incl.
+    the last row) equals the oracle and every row has unit norm."""
+    from hardnetnas_amd import synth
+    m, fx, p = build_module(name)
+    m = m.to(cuda_device)
+    b = 65537
+    x = torch.from_numpy(synth.synth_patches(b, seed=21)).to(cuda_device)
+    with torch.no_grad():
+        y = m(x)
+    assert (y.norm(dim=1) - 1).abs().max().item() < 1e-5
+    idx = torch.cat([torch.arange(0, b, b // 255)[:255], torch.tensor([b - 1])])
+    ref = _oracle_rows(name, p, x[idx.to(cuda_device)].cpu())
+    assert (y[idx.to(cuda_device)].cpu() - ref).abs().max().item() <= _tol(name)
+
+
+def test_hardnet_at_the_timed_size(cuda_device):
+    """BASELINE config 2's exact launch (262,144 patches, the bench's chunking and grids): a
+    strided 1,024-row sample equals the oracle to 1e-4 and every row has unit norm."""
+    from hardnetnas_amd import synth
+    m, fx, p = build_module("hardnet")
+    m = m.to(cuda_device)
+    b = 262144
+    x = torch.from_numpy(synth.synth_patches(b, seed=1000)).to(cuda_device)
+    with torch.no_grad():
+        y = m(x)
+    assert torch.isfinite(y).all()
+    assert (y.norm(dim=1) - 1).abs().max().item() < 1e-5
+    idx = torch.arange(0, b, b // 1024) + 255  # offset: rows away from chunk starts too
+    ref = _oracle_rows("hardnet", p, x[idx.to(cuda_device)].cpu())
+    assert (y[idx.to(cuda_device)].cpu() - ref).abs().max().item() <= TOL["hardnet"]
 
 
 def test_weights_update_triggers_repack(cuda_device):
