@@ -47,7 +47,8 @@ class HnArchDesc(ctypes.Structure):
 
 
 EXPORTED = ["hn_param_count", "hn_create", "hn_workspace_bytes", "hn_forward",
-            "hn_pairdist_workspace_bytes", "hn_pairdist_hardneg", "hn_fpr95_workspace_bytes",
+            "hn_pairdist_workspace_bytes", "hn_pairdist_hardneg", "hn_pairdist_rows_workspace_bytes",
+            "hn_pairdist_rows", "hn_hardnet_loss", "hn_fpr95_workspace_bytes",
             "hn_fpr95", "hn_preprocess", "hn_set_profiling",
             "hn_stage_times", "hn_destroy", "hn_last_error", "hn_abi_version"]
 
@@ -78,6 +79,9 @@ def load_library():
         lib.hn_forward.argtypes = [P, P, I64, P, P, S, P]
         lib.hn_pairdist_workspace_bytes.argtypes = [I64, ctypes.POINTER(S)]
         lib.hn_pairdist_hardneg.argtypes = [P, P, I64, I32, I32, P, P, P, S, P]
+        lib.hn_pairdist_rows_workspace_bytes.argtypes = [I64, I64, ctypes.POINTER(S)]
+        lib.hn_pairdist_rows.argtypes = [P, I64, I64, P, I64, I32, P, P, P, P, S, P]
+        lib.hn_hardnet_loss.argtypes = [P, P, P, I64, ctypes.c_float, I32, ctypes.c_float, P, P, P]
         lib.hn_fpr95_workspace_bytes.argtypes = [I64, ctypes.POINTER(S)]
         lib.hn_fpr95.argtypes = [P, P, P, I64, I32, P, P, P, S, P]
         lib.hn_preprocess.argtypes = [P, I64, I32, I32, I32, ctypes.c_float, ctypes.c_float, P, P]
@@ -90,7 +94,8 @@ def load_library():
         for name in ("hn_param_count", "hn_create", "hn_workspace_bytes", "hn_forward",
                      "hn_pairdist_workspace_bytes", "hn_pairdist_hardneg", "hn_abi_version",
                      "hn_set_profiling", "hn_stage_times", "hn_fpr95_workspace_bytes",
-                     "hn_fpr95"):
+                     "hn_fpr95", "hn_pairdist_rows_workspace_bytes", "hn_pairdist_rows",
+                     "hn_hardnet_loss"):
             getattr(lib, name).restype = ctypes.c_int
         _lib = lib
         return lib
@@ -270,6 +275,55 @@ def pairdist_hardneg(anchor: torch.Tensor, positive: torch.Tensor, anchor_swap: 
                                        pos.data_ptr(), mn.data_ptr(), ws.data_ptr(), ws.numel(),
                                        stream), "hn_pairdist_hardneg")
     return pos, mn
+
+
+def pairdist_rows(anchor_rows: torch.Tensor, row0: int, positive: torch.Tensor, col_min: bool = False):
+    """Rows [row0, row0 + n) of loss_HardNet's masked distance matrix (hardnet/Losses.py:95-108)
+    between this rank's anchors and all positives: (pos, row_min, col_min or None); col_min[j]
+    is the masked minimum of column j over these rows only (all-reduce it with MIN)."""
+    lib = load_library()
+    a = anchor_rows.contiguous().float()
+    p = positive.contiguous().float()
+    if a.dim() != 2 or p.dim() != 2 or a.shape[1] != p.shape[1] or a.device != p.device:
+        raise ValueError("expected [n,D] anchors and [B,D] positives on one device")
+    n, d = a.shape
+    b = p.shape[0]
+    sz = ctypes.c_size_t()
+    _check(lib.hn_pairdist_rows_workspace_bytes(n, b, ctypes.byref(sz)), "hn_pairdist_rows_workspace_bytes")
+    ws = torch.empty(max(sz.value, 16), device=a.device, dtype=torch.uint8)
+    pos = torch.empty(n, device=a.device, dtype=torch.float32)
+    rmin = torch.empty(n, device=a.device, dtype=torch.float32)
+    cmin = torch.empty(b, device=a.device, dtype=torch.float32) if col_min else None
+    stream = torch.cuda.current_stream(a.device).cuda_stream
+    with torch.cuda.device(a.device):
+        _check(lib.hn_pairdist_rows(a.data_ptr(), n, int(row0), p.data_ptr(), b, d, pos.data_ptr(),
+                                    rmin.data_ptr(), cmin.data_ptr() if cmin is not None else None,
+                                    ws.data_ptr(), ws.numel(), stream), "hn_pairdist_rows")
+    return pos, rmin, cmin
+
+
+LOSS_TYPES = {"triplet_margin": 0, "softmax": 1, "contrastive": 2}  # enum hn_loss_type
+
+
+def hardnet_loss(pos: torch.Tensor, row_min: torch.Tensor, col_min: Optional[torch.Tensor] = None,
+                 margin: float = 1.0, loss_type: str = "triplet_margin", scale: Optional[float] = None):
+    """scale * sum of loss_HardNet's per-row margin loss (Losses.py:142-153; scale defaults to
+    1/n = torch.mean) with min_neg = min(row_min, col_min): (loss [1], min_neg [n])."""
+    lib = load_library()
+    if loss_type not in LOSS_TYPES:
+        raise ValueError(f"loss_type must be one of {sorted(LOSS_TYPES)}")
+    n = pos.shape[0]
+    ps, rm = pos.contiguous().float(), row_min.contiguous().float()
+    cm = col_min.contiguous().float() if col_min is not None else None
+    mn = torch.empty(n, device=ps.device, dtype=torch.float32)
+    loss = torch.empty(1, device=ps.device, dtype=torch.float32)
+    stream = torch.cuda.current_stream(ps.device).cuda_stream
+    with torch.cuda.device(ps.device):
+        _check(lib.hn_hardnet_loss(ps.data_ptr(), rm.data_ptr(), cm.data_ptr() if cm is not None else None,
+                                   n, float(margin), LOSS_TYPES[loss_type],
+                                   float(1.0 / n if scale is None else scale), mn.data_ptr(),
+                                   loss.data_ptr(), stream), "hn_hardnet_loss")
+    return loss, mn
 
 
 def fpr95(out_a: torch.Tensor, out_p: torch.Tensor, labels: torch.Tensor):

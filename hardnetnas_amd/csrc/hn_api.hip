@@ -930,6 +930,45 @@ extern "C" int hn_pairdist_hardneg(const float* d_anchor, const float* d_positiv
   return HN_OK;
 }
 
+extern "C" int hn_pairdist_rows_workspace_bytes(int64_t n_rows, int64_t batch, size_t* bytes_out) {
+  if (!bytes_out || n_rows < 1 || batch < 2 || batch > (1 << 30) || n_rows > batch)
+    return fail(HN_ERR_ARG, "bad n_rows / batch");
+  *bytes_out = (size_t)((n_rows + 63) / 64 * 64 + (batch + 63) / 64 * 64) * sizeof(float);
+  return HN_OK;
+}
+
+extern "C" int hn_pairdist_rows(const float* d_anchor_rows, int64_t n_rows, int64_t row0,
+                                const float* d_positive, int64_t batch, int32_t dim, float* d_pos,
+                                float* d_row_min, float* d_col_min, void* d_workspace,
+                                size_t workspace_bytes, void* hip_stream) {
+  if (!d_anchor_rows || !d_positive || !d_pos || !d_row_min || !d_workspace)
+    return fail(HN_ERR_ARG, "NULL device pointer");
+  if (dim != 128) return fail(HN_ERR_ARG, "dim must be 128");
+  size_t need = 0;
+  int rc = hn_pairdist_rows_workspace_bytes(n_rows, batch, &need);
+  if (rc) return rc;
+  if (row0 < 0 || row0 + n_rows > batch) return fail(HN_ERR_ARG, "rows [row0, row0 + n_rows) outside the batch");
+  if (workspace_bytes < need) return fail(HN_ERR_WORKSPACE, "workspace too small");
+  if ((reinterpret_cast<uintptr_t>(d_anchor_rows) | reinterpret_cast<uintptr_t>(d_positive)) & 15)
+    return fail(HN_ERR_ARG, "descriptor pointers must be 16-byte aligned");
+  HIPCHK(hn_launch_pairdist_rows(d_anchor_rows, (int)n_rows, (int)row0, d_positive, (int)batch, d_pos,
+                                 d_row_min, d_col_min, d_workspace, static_cast<hipStream_t>(hip_stream)));
+  return HN_OK;
+}
+
+extern "C" int hn_hardnet_loss(const float* d_pos, const float* d_row_min, const float* d_col_min,
+                               int64_t n, float margin, int32_t loss_type, float scale,
+                               float* d_min_neg, float* d_loss, void* hip_stream) {
+  if (!d_pos || !d_row_min || !d_loss) return fail(HN_ERR_ARG, "NULL device pointer");
+  if (n < 1 || n > (1 << 30)) return fail(HN_ERR_ARG, "n out of range");
+  if (loss_type < HN_LOSS_TRIPLET_MARGIN || loss_type > HN_LOSS_CONTRASTIVE)
+    return fail(HN_ERR_ARG, "unknown loss_type " + std::to_string(loss_type) +
+                                " (Losses.py:142-152: triplet_margin, softmax, contrastive)");
+  HIPCHK(hn_launch_loss(d_pos, d_row_min, d_col_min, (int)n, margin, loss_type, scale, d_min_neg, d_loss,
+                        static_cast<hipStream_t>(hip_stream)));
+  return HN_OK;
+}
+
 extern "C" int hn_fpr95_workspace_bytes(int64_t n, size_t* bytes_out) {
   if (!bytes_out || n < 1 || n > (int64_t)1 << 30) return fail(HN_ERR_ARG, "n out of range");
   HIPCHK(hn_fpr95_ws_bytes(n, bytes_out));

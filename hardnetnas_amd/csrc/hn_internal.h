@@ -66,6 +66,12 @@ hipError_t hn_launch_nas_head(const float* a, float* out, const float* wt, const
 
 hipError_t hn_launch_pairdist(const float* a, const float* p, int B, int D, int swap,
                               float* pos, float* minneg, void* ws, hipStream_t st);
+// rows [row0, row0 + NA) of the B x B matrix (a = those NA anchors, p = all B positives);
+// colmin (float bits, atomicMin; may be NULL) gets the column minima over these rows
+hipError_t hn_launch_pairdist_rows(const float* a, int NA, int row0, const float* p, int B, float* pos,
+                                   float* rowmin, float* colmin, void* ws, hipStream_t st);
+hipError_t hn_launch_loss(const float* pos, const float* rmin, const float* cmin, int n, float margin,
+                          int type, float scale, float* min_neg, float* loss, hipStream_t st);
 
 hipError_t hn_fpr95_ws_bytes(int64_t n, size_t* bytes);
 // fused NAS front (stem + layer 0), hn_front.hip

@@ -11,7 +11,9 @@
 #include "hn_common.h"
 #include "hn_internal.h"
 
+#include <cmath>
 #include <cstdlib>
+#include <cstring>
 
 namespace {
 constexpr int TM = 64, TN = 64, D = 128, LDP = D + 4;
@@ -123,18 +125,24 @@ __global__ __launch_bounds__(256) void k_combine(float* rowmin, const unsigned* 
   if (i < B) rowmin[i] = fminf(rowmin[i], __uint_as_float(colmin[i]));
 }
 // ---------------------------------------------------------------------------------------
-// MFMA version.  x(i,j) = (|a_i|^2 + |p_j|^2) - 2 a_i.p_j with the dot on the bf16 MFMA in
-// bf16x3 split precision; dm = sqrt(x + 1e-6) + 1e-8 is monotone in x, so minima are
-// tracked on x: per anchor row the min over unmasked off-diagonal entries (xu) and over the
-// +10 entries (diagonal and dm < 0.008, xm); min_neg = xu exists ? dm(xu) : dm(xm) + 10 --
-// exactly the reference's min over (dm + 10*eye + 10*[dm + 10*eye < 0.008]).  pos (the
-// diagonal) is recomputed in exact fp32 by k_pos.  One workgroup = 128 anchors (4 waves x
-// 32, A fragments resident in registers) sweeping positives in double-buffered LDS tiles
-// of 64 (rows padded to 272 B: conflict-free ds_read_b128).
+// MFMA version, over a block of anchor rows (the whole matrix on one GPU, or one rank's row
+// shard of it when the batch is sharded -- SURVEY.md 8(e), config 5 at scale).
+//
+// x(i,j) = (|a_i|^2 + |p_j|^2) - 2 a_i.p_j with the dot on the bf16 MFMA in bf16x3 split
+// precision.  dm = sqrt(x + 1e-6) + 1e-8 is monotone in x, so minima are tracked on x: per
+// anchor row the min over unmasked entries (xu) and over the +10 entries (the diagonal and
+// dm < 0.008, xm); min_neg = min(dm(xu), dm(xm) + 10) -- the reference's min over
+// dm + 10*eye + 10*[dm + 10*eye < 0.008] (Losses.py:95-105).  The 0.008 test is done on x
+// against the exact float threshold X* (mask_threshold_x: dm(x) < 0.008 <=> x < X* in fp32),
+// so the epilogue has no sqrt; without anchor_swap it runs on y = x - |a_i|^2 (one FMA per
+// entry, threshold X* - |a_i|^2 per row).  Wave-uniform "edge" tiles (the diagonal, ragged
+// rows / columns) take a checked path.  Column minima (anchor_swap, Losses.py:106-108) are
+// reduced over the workgroup's 4 waves in LDS, then one atomicMin per column per workgroup.
+// pos (the diagonal) is recomputed in exact fp32 by k_pos.  One workgroup = 128 anchors (4
+// waves x 32, A fragments resident in registers) sweeping the positives in double-buffered
+// LDS tiles of 64 (rows padded to 272 B: conflict-free ds_read_b128).
 // ---------------------------------------------------------------------------------------
-constexpr float kDm8Thr = (0.008f - 1e-8f);  // dm < 0.008  <=>  sqrt(x+1e-6) < 0.008 - 1e-8
-
-__device__ __forceinline__ float dm_of(float x) { return sqrtf(x + 1e-6f) + 1e-8f; }
+__device__ __forceinline__ float dm_of(float x) { return sqrtf(fmaxf(x + 1e-6f, 0.f)) + 1e-8f; }
 
 __global__ __launch_bounds__(256) void k_sq(const float* __restrict__ v, int B, float* __restrict__ sq) {
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -144,30 +152,34 @@ __global__ __launch_bounds__(256) void k_sq(const float* __restrict__ v, int B, 
   if (lane == 0) sq[i] = s;
 }
 
+// pos[i] = dm(a_i, p_{row0 + i}) for the NA local anchors
 __global__ __launch_bounds__(256) void k_pos(const float* __restrict__ a, const float* __restrict__ p,
                                              const float* __restrict__ asq, const float* __restrict__ psq,
-                                             int B, float* __restrict__ pos) {
+                                             int NA, int row0, float* __restrict__ pos) {
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (i >= B) return;
-  const float d = wave_sum(a[(size_t)i * 128 + lane] * p[(size_t)i * 128 + lane] +
-                           a[(size_t)i * 128 + 64 + lane] * p[(size_t)i * 128 + 64 + lane]);
-  if (lane == 0) pos[i] = dm_of((asq[i] + psq[i]) - 2.0f * d);
+  if (i >= NA) return;
+  const size_t pj = (size_t)(row0 + i) * 128;
+  const float d = wave_sum(a[(size_t)i * 128 + lane] * p[pj + lane] +
+                           a[(size_t)i * 128 + 64 + lane] * p[pj + 64 + lane]);
+  if (lane == 0) pos[i] = dm_of((asq[i] + psq[row0 + i]) - 2.0f * d);
 }
 
-__global__ __launch_bounds__(256) void k_pairdist_mfma(const float* __restrict__ a, const float* __restrict__ p,
-                                                       const float* __restrict__ asq,
-                                                       const float* __restrict__ psq, int B, int swap,
-                                                       float* __restrict__ rowmin,
-                                                       unsigned* __restrict__ colmin) {
+template <bool SWAP>
+__global__ __launch_bounds__(256, 2) void k_pairdist_rows(
+    const float* __restrict__ a, int NA, int row0, const float* __restrict__ p, int B,
+    const float* __restrict__ asq, const float* __restrict__ psq, float xthr,
+    float* __restrict__ rowmin, unsigned* __restrict__ colmin) {
   constexpr int TN = 64, ROWB = 272, PLANE = TN * ROWB, BUF = 2 * PLANE + TN * 4;
   __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+  __shared__ float cred[2][4][TN];  // per-wave column minima of a tile (SWAP), by tile parity
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
-  const int i0 = blockIdx.x * 128 + wave * 32;  // this wave's anchors
+  const int i0 = blockIdx.x * 128 + wave * 32;  // this wave's first local anchor
+  const int g0 = row0 + i0;                     // ... and its global row
   // A fragments: lane (r, h) holds anchor i0+r, k = 16 ks + 8 h + j
   bf16x8 ah[8], al[8];
   {
-    const int ia = min(i0 + r, B - 1);
+    const int ia = min(i0 + r, NA - 1);
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks) {
       const float4 x0 = *reinterpret_cast<const float4*>(a + (size_t)ia * 128 + ks * 16 + h * 8);
@@ -178,12 +190,18 @@ __global__ __launch_bounds__(256) void k_pairdist_mfma(const float* __restrict__
       al[ks] = as_bf16x8(lo);
     }
   }
-  float arow[16];  // |a|^2 of the rows this lane's accumulator registers hold
+  // per accumulator row (C row (i&3) + 8(i>>2) + 4h): SWAP |a_i|^2, else the y-space mask
+  // threshold X* - |a_i|^2 (|a_i|^2 is reloaded for the final y -> x)
+  float rowc[16];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) arow[i] = asq[min(i0 + (i & 3) + 8 * (i >> 2) + 4 * h, B - 1)];
-  float xu[16], xm[16];
+  for (int i = 0; i < 16; ++i) {
+    const float aq = asq[min(i0 + (i & 3) + 8 * (i >> 2) + 4 * h, NA - 1)];
+    rowc[i] = SWAP ? aq : xthr - aq;
+  }
+  float xu[16], xm[16];  // SWAP: x space; else y = x - |a_i|^2
 #pragma unroll
   for (int i = 0; i < 16; ++i) { xu[i] = INFINITY; xm[i] = INFINITY; }
+  const bool rows_ragged = i0 + 32 > NA;
 
   // P tile staging: 64 rows x 128 fp32 = 2048 float4 -> 8 per thread
   const int srow = tid >> 2, scol = (tid & 3) * 32;  // each thread: 32 consecutive floats of one row
@@ -212,6 +230,13 @@ __global__ __launch_bounds__(256) void k_pairdist_mfma(const float* __restrict__
     const char* cur = smem + (t & 1) * BUF;
     const int j0 = t * TN;
     if (t + 1 < ntile) load_tile(j0 + TN);
+    if (SWAP && t > 0 && wave == ((t - 1) & 3) && lane < TN) {
+      // the previous tile's column minima, combined over the 4 waves: one atomic per column
+      const int j = j0 - TN + lane;
+      const float* c = cred[(t - 1) & 1][0];
+      const float ce = fminf(fminf(c[lane], c[TN + lane]), fminf(c[2 * TN + lane], c[3 * TN + lane]));
+      if (j < B && ce < INFINITY) atomicMin(colmin + j, __float_as_uint(ce));
+    }
     const float* ps = reinterpret_cast<const float*>(cur + 2 * PLANE);
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt) {
@@ -223,31 +248,67 @@ __global__ __launch_bounds__(256) void k_pairdist_mfma(const float* __restrict__
         const bf16x8 bl = as_bf16x8(*reinterpret_cast<const uint4*>(cur + PLANE + off));
         acc = mfma3(ah[ks], al[ks], bh, bl, acc);
       }
-      const int j = j0 + nt * 32 + r;  // this lane's column
+      const int jb = j0 + nt * 32, j = jb + r;  // this lane's column
       const float pj = ps[nt * 32 + r];
       float cu = INFINITY, cm = INFINITY;
+      const bool edge = rows_ragged || jb + 32 > B || (g0 < jb + 32 && jb < g0 + 32);
+      if (!edge) {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int row = i0 + (i & 3) + 8 * (i >> 2) + 4 * h;
-        const float x = (arow[i] + pj) - 2.0f * acc[i];
-        const bool valid = j < B && row < B;
-        const bool plus10 = row == j || sqrtf(fmaxf(x + 1e-6f, 0.f)) < kDm8Thr;
-        const float xv = valid ? x : INFINITY;
-        if (plus10) { xm[i] = fminf(xm[i], xv); cm = fminf(cm, xv); }
-        else { xu[i] = fminf(xu[i], xv); cu = fminf(cu, xv); }
+        for (int i = 0; i < 16; ++i) {
+          if constexpr (SWAP) {
+            const float x = fmaf(-2.0f, acc[i], rowc[i] + pj);
+            const bool m = x < xthr;
+            const float tu = m ? INFINITY : x, tm = m ? x : INFINITY;
+            xu[i] = fminf(xu[i], tu);
+            xm[i] = fminf(xm[i], tm);
+            cu = fminf(cu, tu);
+            cm = fminf(cm, tm);
+          } else {
+            const float y = fmaf(-2.0f, acc[i], pj);
+            const bool m = y < rowc[i];
+            xu[i] = fminf(xu[i], m ? INFINITY : y);
+            xm[i] = fminf(xm[i], m ? y : INFINITY);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int row = i0 + (i & 3) + 8 * (i >> 2) + 4 * h;
+          const bool valid = j < B && row < NA;
+          float v;
+          bool m;
+          if constexpr (SWAP) {
+            v = fmaf(-2.0f, acc[i], rowc[i] + pj);
+            m = v < xthr;
+          } else {
+            v = fmaf(-2.0f, acc[i], pj);
+            m = v < rowc[i];
+          }
+          m = m || row0 + row == j;
+          v = valid ? v : INFINITY;
+          const float tu = m ? INFINITY : v, tm = m ? v : INFINITY;
+          xu[i] = fminf(xu[i], tu);
+          xm[i] = fminf(xm[i], tm);
+          if constexpr (SWAP) {
+            cu = fminf(cu, tu);
+            cm = fminf(cm, tm);
+          }
+        }
       }
-      if (swap) {
+      if constexpr (SWAP) {
         cu = fminf(cu, __shfl_xor(cu, 32, 64));
         cm = fminf(cm, __shfl_xor(cm, 32, 64));
-        if (h == 0 && j < B) {
-          const float ce = fminf(cu < INFINITY ? dm_of(cu) : INFINITY,
-                                 cm < INFINITY ? dm_of(cm) + 10.f : INFINITY);
-          if (ce < INFINITY) atomicMin(colmin + j, __float_as_uint(ce));
-        }
+        if (h == 0) cred[t & 1][wave][nt * 32 + r] = fminf(dm_of(cu), dm_of(cm) + 10.f);
       }
     }
     if (t + 1 < ntile) store_tile(smem + ((t + 1) & 1) * BUF, j0 + TN);
     __syncthreads();
+  }
+  if (SWAP && wave == ((ntile - 1) & 3) && lane < TN) {  // the last tile's column minima
+    const int j = (ntile - 1) * TN + lane;
+    const float* c = cred[(ntile - 1) & 1][0];
+    const float ce = fminf(fminf(c[lane], c[TN + lane]), fminf(c[2 * TN + lane], c[3 * TN + lane]));
+    if (j < B && ce < INFINITY) atomicMin(colmin + j, __float_as_uint(ce));
   }
   // row minima: reduce over the 32 lanes of each half-wave (the columns)
 #pragma unroll
@@ -259,11 +320,87 @@ __global__ __launch_bounds__(256) void k_pairdist_mfma(const float* __restrict__
       m = fminf(m, __shfl_xor(m, o, 64));
     }
     const int row = i0 + (i & 3) + 8 * (i >> 2) + 4 * h;
-    if (r == 0 && row < B) rowmin[row] = u < INFINITY ? dm_of(u) : dm_of(m) + 10.f;
+    if (!SWAP) {
+      const float aq = asq[min(row, NA - 1)];
+      u += aq;
+      m += aq;
+    }
+    if (r == 0 && row < NA) rowmin[row] = fminf(dm_of(u), dm_of(m) + 10.f);
   }
 }
 
+// The margin losses of loss_HardNet (Losses.py:142-153) over the 'min' reduce, one workgroup
+// (fixed summation order: deterministic); min_neg = min(row_min, col_min) when col_min is given.
+__global__ __launch_bounds__(1024) void k_loss(const float* __restrict__ pos, const float* __restrict__ rmin,
+                                               const float* __restrict__ cmin, int n, float margin,
+                                               int type, float scale, float* __restrict__ min_neg,
+                                               float* __restrict__ loss) {
+  __shared__ float part[16];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += 1024) {
+    const float mn = cmin ? fminf(rmin[i], cmin[i]) : rmin[i];
+    if (min_neg) min_neg[i] = mn;
+    const float ps = pos[i];
+    float l;
+    if (type == 0) {
+      l = fmaxf(margin + ps - mn, 0.f);
+    } else if (type == 1) {
+      const float ep = expf(2.0f - ps);
+      l = -logf(ep / (ep + expf(2.0f - mn) + 1e-8f));
+    } else {
+      l = fmaxf(margin - mn, 0.f) + ps;
+    }
+    s += l;
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int w = 0; w < 16; ++w) t += part[w];
+    loss[0] = t * scale;
+  }
+}
+
+// X*: the smallest fp32 x with sqrt(x + 1e-6) + 1e-8 >= 0.008 in fp32, so that the
+// reference's mask test (dm < 0.008, Losses.py:101) is exactly x < X* (dm is monotone in x).
+float mask_threshold_x() {
+  auto masked = [](float x) {
+    const float u = x + 1e-6f;
+    return !(u >= 0.f) || std::sqrt(u) + 1e-8f < 0.008f;
+  };
+  uint32_t lo = 0, hi = 0x3f800000u;  // x = 0 is masked, x = 1 is not
+  while (hi - lo > 1) {
+    const uint32_t mid = lo + (hi - lo) / 2;
+    float x;
+    std::memcpy(&x, &mid, 4);
+    (masked(x) ? lo : hi) = mid;
+  }
+  float x;
+  std::memcpy(&x, &hi, 4);
+  return x;
+}
+
 }  // namespace
+
+hipError_t hn_launch_pairdist_rows(const float* a, int NA, int row0, const float* p, int B, float* pos,
+                                   float* rowmin, float* colmin, void* ws, hipStream_t st) {
+  float* asq = static_cast<float*>(ws);
+  float* psq = asq + ((NA + 63) / 64) * 64;
+  static const float xthr = mask_threshold_x();
+  if (colmin) hipLaunchKernelGGL(k_colmin_init, dim3((B + 255) / 256), dim3(256), 0, st,
+                                 reinterpret_cast<unsigned*>(colmin), B);
+  hipLaunchKernelGGL(k_sq, dim3((NA + 3) / 4), dim3(256), 0, st, a, NA, asq);
+  hipLaunchKernelGGL(k_sq, dim3((B + 3) / 4), dim3(256), 0, st, p, B, psq);
+  hipLaunchKernelGGL(k_pos, dim3((NA + 3) / 4), dim3(256), 0, st, a, p, asq, psq, NA, row0, pos);
+  if (colmin)
+    hipLaunchKernelGGL(k_pairdist_rows<true>, dim3((NA + 127) / 128), dim3(256), 0, st, a, NA, row0, p, B,
+                       asq, psq, xthr, rowmin, reinterpret_cast<unsigned*>(colmin));
+  else
+    hipLaunchKernelGGL(k_pairdist_rows<false>, dim3((NA + 127) / 128), dim3(256), 0, st, a, NA, row0, p, B,
+                       asq, psq, xthr, rowmin, nullptr);
+  return hipGetLastError();
+}
 
 hipError_t hn_launch_pairdist(const float* a, const float* p, int B, int D_, int swap,
                               float* pos, float* minneg, void* ws, hipStream_t st) {
@@ -272,14 +409,9 @@ hipError_t hn_launch_pairdist(const float* a, const float* p, int B, int D_, int
   const unsigned g = (B + 255) / 256;
   const bool valu = hn_knobs().pairdist_valu;  // HN_PAIRDIST_VALU (A/B), read once per process
   if (!valu) {
-    float* asq = reinterpret_cast<float*>(cm + ((B + 63) / 64) * 64);
-    float* psq = asq + ((B + 63) / 64) * 64;
-    if (swap) hipLaunchKernelGGL(k_colmin_init, dim3(g), dim3(256), 0, st, cm, B);
-    hipLaunchKernelGGL(k_sq, dim3((B + 3) / 4), dim3(256), 0, st, a, B, asq);
-    hipLaunchKernelGGL(k_sq, dim3((B + 3) / 4), dim3(256), 0, st, p, B, psq);
-    hipLaunchKernelGGL(k_pos, dim3((B + 3) / 4), dim3(256), 0, st, a, p, asq, psq, B, pos);
-    hipLaunchKernelGGL(k_pairdist_mfma, dim3((B + 127) / 128), dim3(256), 0, st, a, p, asq, psq,
-                       B, swap, minneg, cm);
+    float* colmin = swap ? reinterpret_cast<float*>(cm) : nullptr;
+    hipError_t e = hn_launch_pairdist_rows(a, B, 0, p, B, pos, minneg, colmin, cm + ((B + 63) / 64) * 64, st);
+    if (e != hipSuccess) return e;
     if (swap) hipLaunchKernelGGL(k_combine, dim3(g), dim3(256), 0, st, minneg, cm, B);
     return hipGetLastError();
   }
@@ -287,5 +419,12 @@ hipError_t hn_launch_pairdist(const float* a, const float* p, int B, int D_, int
   hipLaunchKernelGGL(k_pairdist, dim3((B + TM - 1) / TM), dim3(256), 0, st, a, p, B, swap, pos,
                      minneg, cm);
   if (swap) hipLaunchKernelGGL(k_combine, dim3(g), dim3(256), 0, st, minneg, cm, B);
+  return hipGetLastError();
+}
+
+hipError_t hn_launch_loss(const float* pos, const float* rmin, const float* cmin, int n, float margin,
+                          int type, float scale, float* min_neg, float* loss, hipStream_t st) {
+  hipLaunchKernelGGL(k_loss, dim3(1), dim3(1024), 0, st, pos, rmin, cmin, n, margin, type, scale, min_neg,
+                     loss);
   return hipGetLastError();
 }

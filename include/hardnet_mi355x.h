@@ -106,6 +106,29 @@ int hn_pairdist_hardneg(const float* d_anchor, const float* d_positive, int64_t 
                         int32_t anchor_swap, float* d_pos, float* d_min_neg,
                         void* d_workspace, size_t workspace_bytes, void* hip_stream);
 
+/* Row block of the same computation, for a batch sharded over ranks: rows
+ * [row0, row0 + n_rows) of the batch x batch distance matrix between this rank's anchors
+ * d_anchor_rows [n_rows, dim] and ALL positives d_positive [batch, dim] (all-gathered).
+ * Outputs for the local rows: d_pos[i] = dist(a_i, p_{row0+i}) + 1e-8, d_row_min[i] = masked
+ * row minimum; if d_col_min is not NULL it receives, for every column j of the batch, the
+ * masked minimum over these rows (reduce it across ranks with an all-reduce(MIN), then
+ * min_neg = min(row_min, col_min[row0 + i]) for anchor_swap; hn_hardnet_loss does that).
+ * The single-GPU hn_pairdist_hardneg is this call with row0 = 0, n_rows = batch. */
+int hn_pairdist_rows_workspace_bytes(int64_t n_rows, int64_t batch, size_t* bytes_out);
+int hn_pairdist_rows(const float* d_anchor_rows, int64_t n_rows, int64_t row0, const float* d_positive,
+                     int64_t batch, int32_t dim, float* d_pos, float* d_row_min, float* d_col_min,
+                     void* d_workspace, size_t workspace_bytes, void* hip_stream);
+
+/* loss_HardNet's margin loss over the 'min' reduce (hardnet/Losses.py:142-153) for n rows:
+ * min_neg = d_col_min ? min(d_row_min, d_col_min) : d_row_min (written to d_min_neg if not
+ * NULL); *d_loss = scale * sum_i loss_i (scale = 1/B for torch.mean; with a sharded batch
+ * every rank passes 1/B_total and the partial sums are all-reduced).  One workgroup, fixed
+ * summation order (deterministic). */
+enum hn_loss_type { HN_LOSS_TRIPLET_MARGIN = 0, HN_LOSS_SOFTMAX = 1, HN_LOSS_CONTRASTIVE = 2 };
+int hn_hardnet_loss(const float* d_pos, const float* d_row_min, const float* d_col_min, int64_t n,
+                    float margin, int32_t loss_type, float scale, float* d_min_neg, float* d_loss,
+                    void* hip_stream);
+
 /* FPR at 95 % recall of an evaluation batch of descriptor pairs (hardnet/HardNet.py:450-472
  * + hardnet/EvalMetrics.py:6-19): per-pair L2 distance, scores -> distances transform, sort,
  * first index reaching 95 % recall, FP / (FP + TN).

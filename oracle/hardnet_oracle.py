@@ -220,6 +220,30 @@ def hardest_negative(anchor, positive, anchor_swap=False):
     return pos1, min_neg
 
 
+def hardest_negative_rows(anchor, positive, rows, anchor_swap=False):
+    """(pos, min_neg) of hardest_negative for the given row indices only (the full matrix is
+    never formed: row i needs row i and, with anchor_swap, column i of dm; Losses.py:95-108)."""
+    eps = 1e-8
+    rows = torch.as_tensor(rows)
+    a, p = anchor, positive
+    a_sq = torch.sum(a * a, dim=1)
+    p_sq = torch.sum(p * p, dim=1)
+
+    def masked(dm, diag_col):
+        d = dm.clone()
+        idx = torch.arange(d.shape[0])
+        d[idx, diag_col] += 10
+        return d + (d.ge(0.008).to(d.dtype) - 1.0) * (-1) * 10
+
+    dm_r = torch.sqrt(a_sq[rows, None] + p_sq[None, :] - 2.0 * a[rows] @ p.t() + 1e-6) + eps
+    pos = dm_r[torch.arange(len(rows)), rows]
+    min_neg = masked(dm_r, rows).min(dim=1)[0]
+    if anchor_swap:
+        dm_c = torch.sqrt(p_sq[rows, None] + a_sq[None, :] - 2.0 * p[rows] @ a.t() + 1e-6) + eps
+        min_neg = torch.minimum(min_neg, masked(dm_c, rows).min(dim=1)[0])
+    return pos, min_neg
+
+
 def loss_hardnet(anchor, positive, anchor_swap=False, margin=1.0, loss_type="triplet_margin"):
     """loss_HardNet with batch_reduce='min', hardnet/Losses.py:87-154."""
     eps = 1e-8

@@ -69,3 +69,49 @@ def test_sharded_forward_equals_single_process(name, n):
     assert np.abs(y - ref).max() <= 1e-6
     assert np.abs(y - fx["y"][:n]).max() <= 1e-5
     assert g[:, 0].tolist() == [0, 0, 0, 1, 1]
+
+
+def _loss_worker(rank, world, port, n, swap, loss_type, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from hardnetnas_amd.distributed import sharded_hardnet_loss
+        g = torch.Generator().manual_seed(5)
+        a = torch.nn.functional.normalize(torch.randn(n, 128, generator=g), dim=1)
+        p = torch.nn.functional.normalize(a + 0.4 * torch.randn(n, 128, generator=g), dim=1)
+        p[3] = a[7]  # a near-duplicate off the diagonal: exercises the < 0.008 mask
+        s, e = shard_range(n, world, rank)
+        loss, pos, mn = sharded_hardnet_loss(a[s:e], p[s:e], n, anchor_swap=swap, loss_type=loss_type)
+        parts = [None] * world
+        dist.all_gather_object(parts, (pos, mn))
+        if rank == 0:
+            q.put((float(loss), torch.cat([x[0] for x in parts]).numpy(),
+                   torch.cat([x[1] for x in parts]).numpy(), a.numpy(), p.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n,swap,loss_type", [(2, 64, True, "triplet_margin"),
+                                                    (2, 37, False, "softmax"),
+                                                    (3, 50, True, "contrastive")])
+def test_sharded_hardnet_loss_equals_reference(world, n, swap, loss_type):
+    """Config 5 at scale on gloo: row blocks + all-reduce(MIN) of the column minima + summed
+    partial losses == loss_HardNet on the whole batch (oracle restatement of Losses.py:87-154)."""
+    from oracle import hardnet_oracle as O
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_loss_worker, args=(r, world, port, n, swap, loss_type, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    loss, pos, mn, a, pp = q.get(timeout=300)
+    pos, mn, a, pp = (torch.from_numpy(v) for v in (pos, mn, a, pp))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    rpos, rmn = O.hardest_negative(a.double(), pp.double(), swap)
+    ref = O.loss_hardnet(a.double(), pp.double(), swap, loss_type=loss_type).item()
+    assert (pos.double() - rpos).abs().max().item() < 1e-5
+    assert (mn.double() - rmn).abs().max().item() < 1e-5
+    assert abs(loss - ref) < 1e-5

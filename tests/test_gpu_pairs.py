@@ -1,0 +1,85 @@
+"""The triplet-mining step on MI355X (BASELINE config 5): the fused
+masked distance + hardest negative (hardnet/Losses.py:5-13, 87-154) against the fp64 oracle --
+row blocks of a sharded batch, descriptors that are not unit-norm (dm > 10, where the +10 mask
+must not win), the full 65,536-pair batch on a row sample, and the three margin losses."""
+import pytest
+import torch
+
+from oracle import hardnet_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _pairs(b, seed, scale=1.0, dup=()):
+    g = torch.Generator().manual_seed(seed)
+    a = torch.nn.functional.normalize(torch.randn(b, 128, generator=g), dim=1)
+    p = torch.nn.functional.normalize(a + 0.3 * torch.randn(b, 128, generator=g), dim=1)
+    for i, j in dup:  # positive i is (almost) anchor j: dm < 0.008 off the diagonal
+        p[i] = a[j] + 1e-4 * torch.randn(128, generator=g)
+    return a * scale, p * scale
+
+
+@pytest.mark.parametrize("swap", [False, True])
+@pytest.mark.parametrize("scale", [1.0, 9.0])
+def test_pairdist_unnormalised_and_duplicates(swap, scale, cuda_device):
+    from hardnetnas_amd._native import pairdist_hardneg
+    # near-duplicates only at unit norm: at |a| = 9 the fp32 form |a|^2 + |p|^2 - 2 a.p loses
+    # ~1e-5 absolute to cancellation, which a distance of ~0.008 cannot absorb (the reference's
+    # fp32 arithmetic has the same conditioning)
+    a, p = _pairs(1000, 3, scale, dup=[(5, 9), (700, 12), (13, 13)] if scale == 1.0 else [])
+    pos, mn = pairdist_hardneg(a.to(cuda_device), p.to(cuda_device), swap)
+    rpos, rmn = O.hardest_negative(a.double(), p.double(), swap)
+    tol = 1e-4 * scale
+    assert (pos.cpu().double() - rpos).abs().max().item() < tol
+    assert (mn.cpu().double() - rmn).abs().max().item() < tol
+
+
+@pytest.mark.parametrize("swap", [False, True])
+def test_row_shards_reassemble_the_full_result(swap, cuda_device):
+    """Three uneven row blocks (hn_pairdist_rows) + min over their column minima == the
+    single-call result, bit for bit (same kernel, same per-element arithmetic)."""
+    from hardnetnas_amd._native import hardnet_loss, pairdist_hardneg, pairdist_rows
+    a, p = _pairs(3001, 4, dup=[(100, 2000)])
+    a, p = a.to(cuda_device), p.to(cuda_device)
+    pos_f, mn_f = pairdist_hardneg(a, p, swap)
+    cuts = [0, 1000, 2200, 3001]
+    parts, cmins = [], []
+    for s, e in zip(cuts, cuts[1:]):
+        pos, rmin, cmin = pairdist_rows(a[s:e], s, p, col_min=swap)
+        parts.append((pos, rmin))
+        cmins.append(cmin)
+    pos = torch.cat([x[0] for x in parts])
+    if swap:
+        cm = torch.stack(cmins).min(dim=0)[0]
+        mn = torch.cat([hardnet_loss(x[0], x[1], cm[s:e])[1] for x, s, e in zip(parts, cuts, cuts[1:])])
+    else:
+        mn = torch.cat([x[1] for x in parts])
+    assert torch.equal(pos, pos_f)
+    assert torch.equal(mn, mn_f)
+
+
+def test_full_config5_batch_on_a_row_sample(cuda_device):
+    """65,536 pairs with anchor_swap (BASELINE config 5's distance step): 256 sampled rows of
+    pos / min_neg against the fp64 oracle restricted to those rows and columns."""
+    from hardnetnas_amd._native import pairdist_hardneg
+    b = 65536
+    a, p = _pairs(b, 6, dup=[(17, 40000)])
+    pos, mn = pairdist_hardneg(a.to(cuda_device), p.to(cuda_device), True)
+    rows = torch.cat([torch.arange(0, b, b // 254)[:254], torch.tensor([17, b - 1])])
+    rpos, rmn = O.hardest_negative_rows(a.double(), p.double(), rows, True)
+    assert (pos.cpu()[rows].double() - rpos).abs().max().item() < 1e-4
+    assert (mn.cpu()[rows].double() - rmn).abs().max().item() < 1e-4
+
+
+@pytest.mark.parametrize("loss_type", ["triplet_margin", "softmax", "contrastive"])
+@pytest.mark.parametrize("swap", [False, True])
+def test_hardnet_loss_matches_reference(loss_type, swap, cuda_device):
+    from hardnetnas_amd._native import hardnet_loss, pairdist_rows
+    a, p = _pairs(777, 8, dup=[(1, 2)])
+    ad, pd = a.to(cuda_device), p.to(cuda_device)
+    pos, rmin, cmin = pairdist_rows(ad, 0, pd, col_min=swap)
+    loss, mn = hardnet_loss(pos, rmin, cmin, margin=1.0, loss_type=loss_type)
+    ref = O.loss_hardnet(a.double(), p.double(), swap, loss_type=loss_type).item()
+    assert abs(loss.item() - ref) < 1e-5
+    _, rmn = O.hardest_negative(a.double(), p.double(), swap)
+    assert (mn.cpu().double() - rmn).abs().max().item() < 1e-4
