@@ -148,36 +148,96 @@ def flop_per_patch(name: str) -> int:
     return 2 * (A.hardnet_macs() if name == "hardnet" else A.nas_macs(name))
 
 
-def cpu_baseline(name: str, model, seconds: float = 12.0):
-    """Time the oracle (torch fp32 CPU restatement of the reference forward) on host cores."""
+def _cpu_model_string() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def _cpu_quota() -> float:
+    """CPUs this cgroup may use (cpu.max quota / period), or 0 if unlimited / unknown."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        return 0.0 if q == "max" else int(q) / int(per)
+    except (OSError, ValueError):
+        return 0.0
+
+
+def cpu_baseline(name: str, model, seconds: float = 12.0, x_timed=None, y_timed=None, check_rows=1024):
+    """The oracle (torch fp32 CPU restatement of the reference forward) timed on
+    the host's cores: torch.set_num_threads(nproc), plus a 1-thread figure and -- when the
+    cgroup grants fewer CPUs than nproc shows -- the quota's thread count; ``value`` is the best
+    of them (the strongest CPU number this host gives).  With the timed GPU input/output it
+    also checks the GPU run at its own size: a strided ``check_rows``-row sample of the timed
+    batch through the same oracle (the sample *is* the timed CPU workload)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from oracle import hardnet_oracle as O
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-    torch.set_num_threads(threads)
     p = {k: v.detach().cpu() for k, v in model.state_dict().items()}
     b = 1024
-    x = torch.from_numpy(synth.synth_patches(b, seed=11))
+    if x_timed is not None:
+        idx = torch.arange(0, x_timed.shape[0], max(1, x_timed.shape[0] // check_rows))[:check_rows]
+        idx = idx + min(255, x_timed.shape[0] - 1 - int(idx[-1]))  # also rows away from chunk starts
+        x = x_timed[idx.to(x_timed.device)].cpu()
+        b = x.shape[0]
+    else:
+        idx, x = None, torch.from_numpy(synth.synth_patches(b, seed=11))
 
     def run():
         with torch.no_grad():
             if name == "hardnet":
-                O.hardnet_forward(p, x)
-            elif name in FDL_MODELS:
-                O.fdl_forward(p, FDL_MODELS[name], x)
-            else:
-                O.nas_forward(p, model.arch_ops, x)
+                return O.hardnet_forward(p, x)
+            if name in FDL_MODELS:
+                return O.fdl_forward(p, FDL_MODELS[name], x)
+            return O.nas_forward(p, model.arch_ops, x)
 
-    run()
-    run()
-    rates, t_start = [], time.perf_counter()
-    while time.perf_counter() - t_start < seconds or len(rates) < 3:
-        t0 = time.perf_counter()
+    def timed(threads, secs, min_runs=3):
+        torch.set_num_threads(threads)
         run()
-        rates.append(b / (time.perf_counter() - t0))
-    return {"value": round(statistics.median(rates), 1), "unit": "patches/s", "cores": threads,
-            "kind": "port",
-            "sample": f"oracle/hardnet_oracle.py {name} fp32 torch-CPU forward, batch {b} x "
-                      f"{len(rates)} batches (~{seconds:.0f} s), {threads} threads, median"}
+        rates, t_start = [], time.perf_counter()
+        while time.perf_counter() - t_start < secs or len(rates) < min_runs:
+            t0 = time.perf_counter()
+            run()
+            rates.append(b / (time.perf_counter() - t0))
+        return statistics.median(rates), len(rates)
+
+    nproc = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = _cpu_quota()
+    legs = {nproc: None}
+    if 0 < quota < nproc:
+        legs[max(1, int(quota))] = None
+    legs[1] = None
+    share = seconds / (len(legs) + 1)
+    for t in sorted(legs, reverse=True):
+        # nproc threads under a much smaller CPU quota are throttled: keep that leg short
+        legs[t] = timed(t, 2 * share if t == nproc else share,
+                        1 if (t == nproc and 0 < quota < nproc / 2) else 3)
+    torch.set_num_threads(best_threads := max(legs, key=lambda t: legs[t][0]))
+    best = best_threads
+    out = {"value": round(legs[best][0], 1), "unit": "patches/s", "cores": best, "kind": "port",
+           "nproc": nproc, "cgroup_cpu_quota": quota or None, "model": _cpu_model_string(),
+           "value_nproc": round(legs[nproc][0], 1), "value_1t": round(legs[1][0], 1),
+           "sample": f"oracle/hardnet_oracle.py {name} fp32 torch-CPU forward, batch {b} "
+                     + ("(a strided sample of the timed GPU batch)" if idx is not None else "")
+                     + f", ~{seconds:.0f} s over thread counts "
+                     + ", ".join(f"{t}: {legs[t][0]:.0f}/s x{legs[t][1]}" for t in sorted(legs))
+                     + f"; value = best ({best} threads), median per leg"}
+    if 0 < quota < nproc:
+        out["value_quota"] = round(legs[max(1, int(quota))][0], 1)
+    if idx is not None and y_timed is not None:
+        ref = run()
+        got = y_timed[idx.to(y_timed.device)].cpu()
+        tol = 1e-4 if name == "hardnet" else 2e-5
+        err = float((got - ref).abs().max())
+        dev_norm = float((y_timed.norm(dim=1) - 1).abs().max())
+        out_check = {"rows": int(b), "of": int(x_timed.shape[0]), "max_abs_err_vs_oracle": err, "tol": tol,
+                     "unit_norm_max_dev_all_rows": dev_norm, "ok": bool(err <= tol and dev_norm < 1e-5)}
+        return out, out_check
+    return out, None
 
 
 def read_traffic(name: str, stage: str, patches_per_launch: float):
@@ -193,129 +253,284 @@ def read_traffic(name: str, stage: str, patches_per_launch: float):
         return None
 
 
+def nas_stage_flop(name: str) -> dict:
+    """Algorithmic FLOP per patch of each NAS / FDL stage class (summed over its launches in one
+    forward), mirroring hn_api.hip::forward_nas (fused front = stem + layer 0; "irf" = every
+    fused IRF block; "skip" = the fused maxpool + 1x1 ConvBNRelu; head = 4x4 conv)."""
+    if name in FDL_MODELS:
+        v = FDL_MODELS[name]
+        front = 9 * 32 * 32 * 32 + (32 * 32 * 16 * 16 + 32 * 64 * 64 if v == "NASNet" else 32 * 64 * 64)
+        irf, hw = 0, 8
+        for (ci, co, st), op in zip(A.FDL_LAYERS, A.FDL_OPS):
+            irf += A.layer_macs(ci, co, st, op, hw)
+            hw //= st
+        return {"front": 2 * front, "irf": 2 * irf, "head": 2 * 128 * 128 * 16}
+    ops = A.arch_ops(name)
+    out = {"front": 0, "irf": 0, "skip": 0, "head": 2 * A.SEARCH_SPACE2[-1][1] * 128 * 16}
+    hw = 32
+    for i, (op, (ci, co, st)) in enumerate(zip(ops, A.SEARCH_SPACE2)):
+        macs = A.layer_macs(ci, co, st, op, hw)
+        if i == 0:
+            out["front"] += 2 * (9 * 32 * 32 * 32 + macs)
+        elif A.OP_SPECS[op].kind == "skip":
+            out["skip"] += 2 * macs
+        else:
+            out["irf"] += 2 * macs
+        hw //= st
+    return out
+
+
+# PMC evidence of what binds the NAS kernels (profiles/r01_pmc_mfma_wang2.json: VALU vs MFMA
+# instructions per dispatch; MFMA busy 10-25 %): their roof is VALU issue, not HBM or MFMA
+NAS_BINDING = ("VALU issue (PMC, profiles/r01_pmc_mfma_wang2.json: k_front 209 M VALU vs 11 M MFMA "
+               "instructions per dispatch, MFMA busy 17.5 %; HBM traffic = algorithmic bytes)")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--model", default="hardnet")
+    ap.add_argument("--config", type=int, default=None, choices=[2, 3, 4, 5],
+                    help="BASELINE config: 2/3/4 = descriptor forward (the default), 5 = HardNet forward "
+                         "of 65,536 anchor/positive pairs + the fused distance / hardest-negative / "
+                         "margin loss (Losses.py:87-154)")
     ap.add_argument("--batch", type=int, default=None,
                     help="patches per GPU per step (default: 262,144 = BASELINE config 2 at N=1; "
-                         "2,097,152 per rank = config 4's 16.7M patches over 8 GPUs when N > 1)")
+                         "2,097,152 per rank = config 4's 16.7M patches over 8 GPUs when N > 1); "
+                         "config 5: pairs per step (default 65,536, split over the ranks)")
+    ap.add_argument("--backend", default=None, choices=["nccl", "gloo"],
+                    help="process-group backend for N > 1 (default nccl = RCCL on GPUs, gloo on CPU)")
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                    help="cpu = plumbing dry run of the same step (module torch layers, gloo): no GPU")
     ap.add_argument("--no-allgather", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     args = ap.parse_args()
+    cfg5 = args.config == 5
+    if cfg5 and args.model != "hardnet":
+        ap.error("config 5 is the stock HardNet pair step")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    on_gpu = args.device == "cuda"
+    if on_gpu:
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+    else:
+        dev = torch.device("cpu")
+        torch.set_num_threads(max(1, min(4, (os.cpu_count() or 2) // max(world, 1))))
+    backend = args.backend or ("nccl" if on_gpu else "gloo")
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     model = build_model(args.model)
-    nm = NativeModel.from_module(model, dev)
-    b = args.batch
-    if b is None:
-        b = CONFIG4_PER_RANK if (world > 1 and args.model == "hardnet") else 262144
+    nm = NativeModel.from_module(model, dev) if on_gpu else None
+    if cfg5:
+        pairs = args.batch or 65536
+        from hardnetnas_amd.distributed import shard_range, sharded_hardnet_loss
+        s0, e0 = shard_range(pairs, world, rank) if world > 1 else (0, pairs)
+        b = 2 * (e0 - s0)  # this rank's anchors and positives, one forward
+    else:
+        b = args.batch
+        if b is None:
+            b = (CONFIG4_PER_RANK if (world > 1 and args.model == "hardnet") else 262144) if on_gpu else 256
     x = synth_input_on_device(b, dev, seed=1000 + rank)
+    if cfg5:  # positives = anchors + noise (the same patch seen twice), as a real pair batch
+        x[b // 2:] = x[: b // 2] + 0.3 * torch.randn(b // 2, 1, 32, 32, device=dev,
+                                                     generator=torch.Generator(device=dev).manual_seed(7 + rank))
     out = torch.empty((b, 128), device=dev)
-    ws = torch.empty(nm.workspace_bytes(b), device=dev, dtype=torch.uint8)
-    gathered = torch.empty((b * world, 128), device=dev) if world > 1 else None
+    ws = torch.empty(nm.workspace_bytes(b), device=dev, dtype=torch.uint8) if on_gpu else None
+    gathered = torch.empty((b * world, 128), device=dev) if (world > 1 and not cfg5) else None
+    loss = None
 
-    def step():
-        nm.forward(x, out=out, workspace=ws)
-        if world > 1 and not args.no_allgather:
-            dist.all_gather_into_tensor(gathered, out)
+    def forward():
+        if on_gpu:
+            nm.forward(x, out=out, workspace=ws)
+        else:
+            with torch.no_grad():
+                out.copy_(model(x))
+
+    def collective_or_pairs():
+        nonlocal loss
+        if cfg5:
+            n = b // 2
+            if world > 1:
+                loss, _, _ = sharded_hardnet_loss(out[:n], out[n:], pairs, anchor_swap=True)
+            else:
+                from hardnetnas_amd._native import hardnet_loss, pairdist_rows
+                pos, rmin, cmin = pairdist_rows(out[:n], 0, out[n:], col_min=True)
+                loss, _ = hardnet_loss(pos, rmin, cmin)
+        elif world > 1 and not args.no_allgather:
+            if backend == "gloo":
+                dist.all_gather(list(gathered.chunk(world)), out)
+            else:
+                dist.all_gather_into_tensor(gathered, out)
+
+    if on_gpu:
+        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    cpu_phase = [0.0, 0.0]
+
+    def step(k=None):
+        if on_gpu and k is not None:
+            evs[k][0].record()
+        t0 = time.perf_counter()
+        forward()
+        if on_gpu and k is not None:
+            evs[k][1].record()
+        t1 = time.perf_counter()
+        collective_or_pairs()
+        if on_gpu and k is not None:
+            evs[k][2].record()
+        if not on_gpu and k is not None:
+            cpu_phase[0] += t1 - t0
+            cpu_phase[1] += time.perf_counter() - t1
 
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
-    nm.stage_times()  # clear
-    nm.set_profiling(True)
+    if on_gpu:
+        torch.cuda.synchronize()
+        nm.stage_times()  # clear
+        nm.set_profiling(True)
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    if on_gpu:
+        torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
+    for k in range(args.steps):
+        step(k)
+    if on_gpu:
+        torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    nm.set_profiling(False)
-    stages = nm.stage_times()
+    if on_gpu:
+        nm.set_profiling(False)
+        stages = nm.stage_times()
+        phase = [sum(e[0].elapsed_time(e[1]) for e in evs), sum(e[1].elapsed_time(e[2]) for e in evs)]
+    else:
+        stages = {}
+        phase = [1e3 * cpu_phase[0], 1e3 * cpu_phase[1]]
+    ranks_seen = world
     if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed, phase[0], phase[1]], device=dev if backend == "nccl" else "cpu",
+                         dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
+        elapsed, phase = t[0].item(), [t[1].item(), t[2].item()]
+        cnt = torch.ones(1, device=dev if backend == "nccl" else "cpu")
+        dist.all_reduce(cnt)
+        ranks_seen = int(cnt.item())
 
-    total = b * world * args.steps
+    total = (pairs * 2 if cfg5 else b * world) * args.steps
     value = total / elapsed / 1e6
     result = None
     if rank == 0:
-        # dominant kernel = stage with the largest summed device time
-        dom = max(stages, key=lambda k: stages[k][0])
-        dom_ms, dom_n = stages[dom]
-        avg_ms = dom_ms / max(dom_n, 1)
-        launches_per_step = dom_n / args.steps
-        patches_per_launch = b / launches_per_step
-        if args.model == "hardnet":
-            flop = 2 * HARDNET_STAGE_MAC[dom] * patches_per_launch
-            bound, peak = "mfma", PEAK_BF16X3
-            achieved = flop / (avg_ms * 1e-3) / 1e12
-            unit = "TFLOP/s"
-            alg = HARDNET_STAGE_BYTES[dom] * patches_per_launch
+        roof = None
+        if on_gpu:
+            if cfg5:
+                # the pair step's own roofline: distance FLOP (2 B^2 D, SURVEY 8(d)) over its time
+                pair_ms = phase[1] / args.steps
+                flop = 2.0 * pairs * pairs * 128 / world
+                achieved = flop / (pair_ms * 1e-3) / 1e12
+                roof = {"bound": "mfma", "kernel": "pair step (k_pairdist_rows + k_sq/k_pos/k_loss)",
+                        "achieved": round(achieved, 2), "peak": round(PEAK_BF16X3, 1), "unit": "TFLOP/s",
+                        "frac": round(achieved / PEAK_BF16X3, 4), "traffic": None,
+                        "avg_launch_ms": round(pair_ms, 4), "launches": args.steps,
+                        "pairs_per_launch": int(pairs),
+                        "peak_basis": "bf16 MFMA dense 2.5 PFLOP/s / 3 (bf16x3 split-precision distance "
+                                      "dots); algorithmic FLOP = 2 * B^2 * 128 per step",
+                        "stages_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in stages.items()}}
+            else:
+                # dominant kernel = stage with the largest summed device time
+                dom = max(stages, key=lambda k: stages[k][0])
+                dom_ms, dom_n = stages[dom]
+                avg_ms = dom_ms / max(dom_n, 1)
+                launches_per_step = dom_n / args.steps
+                patches_per_launch = b / launches_per_step
+                if args.model == "hardnet":
+                    flop = 2 * HARDNET_STAGE_MAC[dom] * patches_per_launch
+                    achieved = flop / (avg_ms * 1e-3) / 1e12
+                    alg = HARDNET_STAGE_BYTES[dom] * patches_per_launch
+                    binding = "MFMA (PMC: k_c12 58 % MFMA busy, profiles/r01_pmc_mfma_hardnet.json)"
+                else:
+                    # a NAS stage class aggregates different layers' launches: its summed
+                    # algorithmic FLOP / summed device time, against the fp16x3 MFMA roof
+                    per_patch = nas_stage_flop(args.model).get(dom, 0)
+                    achieved = per_patch * b * args.steps / (dom_ms * 1e-3) / 1e12
+                    alg = (fdl_stage_bytes(args.model) if args.model in FDL_MODELS
+                           else nas_stage_bytes(args.model)).get(dom, 0) * b / launches_per_step
+                    binding = NAS_BINDING
+                roof = {"bound": "mfma", "kernel": dom,
+                        "achieved": round(achieved, 2), "peak": round(PEAK_BF16X3, 1), "unit": "TFLOP/s",
+                        "frac": round(achieved / PEAK_BF16X3, 4),
+                        "traffic": read_traffic(args.model, dom, b / launches_per_step),
+                        "avg_launch_ms": round(avg_ms, 4), "launches": dom_n,
+                        "patches_per_launch": int(patches_per_launch),
+                        "algorithmic_bytes_per_launch": int(alg) if alg else None,
+                        "hbm_gbps_algorithmic": round(alg / (avg_ms * 1e-3) / 1e9, 1) if alg else None,
+                        "binding_counter": binding,
+                        "peak_basis": ("bf16 MFMA dense 2.5 PFLOP/s / 3 (bf16x3 split-precision fp32 "
+                                       "products)" if args.model == "hardnet" else
+                                       "fp16 MFMA dense 2.5 PFLOP/s / 3 (fp16x3 split-precision 1x1 "
+                                       "convs; depthwise on the VALU)") + "; algorithmic FLOP = 2*MAC",
+                        "stages_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in stages.items()}}
+        if cfg5:
+            workload = (f"Stock HardNet forward of {pairs} anchor/positive pairs ({2 * pairs} patches) + "
+                        "fused masked distance / hardest negative (anchor_swap) / triplet margin loss")
+            if world > 1:
+                workload += f", pairs sharded over {world} ranks (RCCL all-gather of positives, all-reduce MIN/SUM)"
         else:
-            # NAS: HBM-bound fp32 kernels; a stage class aggregates its launches (e.g. every
-            # pw of the 6 blocks), so use its summed algorithmic bytes / summed device time
-            per_patch = (fdl_stage_bytes(args.model) if args.model in FDL_MODELS
-                         else nas_stage_bytes(args.model)).get(dom, 0)
-            alg = per_patch * b / launches_per_step
-            bound, peak, unit = "hbm", PEAK_HBM, "GB/s"
-            achieved = per_patch * b * args.steps / (dom_ms * 1e-3) / 1e9
-        traffic = read_traffic(args.model, dom, b / launches_per_step)
-        roof = {"bound": bound, "kernel": dom,
-                "achieved": round(achieved, 2) if achieved is not None else None,
-                "peak": round(peak, 1), "unit": unit,
-                "frac": round(achieved / peak, 4) if achieved is not None else None,
-                "traffic": traffic,
-                "avg_launch_ms": round(avg_ms, 4), "launches": dom_n,
-                "patches_per_launch": int(patches_per_launch),
-                "algorithmic_bytes_per_launch": int(alg) if alg else None,
-                "peak_basis": ("bf16 MFMA dense 2.5 PFLOP/s / 3 (bf16x3 split-precision fp32 "
-                               "products); algorithmic fp32 FLOP = 2*MAC") if bound == "mfma"
-                else "HBM3E 8 TB/s",
-                "stages_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in stages.items()}}
+            workload = (("Stock HardNet forward" if args.model == "hardnet"
+                         else f"FDLNet HardNetNeiMask {FDL_MODELS[args.model]} forward"
+                         if args.model in FDL_MODELS else f"hardnetNAS {args.model} forward")
+                        + f", {b} synthetic 32x32 patches per GPU"
+                        + (" (BASELINE config 4 per-rank shard)" if world > 1 and b == CONFIG4_PER_RANK else "")
+                        + (", RCCL all-gather of descriptors" if world > 1 and not args.no_allgather else ""))
+        if not on_gpu:
+            workload += " [CPU plumbing dry run: module torch layers, gloo; not a throughput figure]"
         result = {
-            "metric": METRIC, "value": round(value, 4), "unit": "Mpatches/s", "n_gpus": world,
+            "metric": METRIC, "value": round(value, 4 if on_gpu else 6), "unit": "Mpatches/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": ("Stock HardNet forward" if args.model == "hardnet"
-                                    else f"FDLNet HardNetNeiMask {FDL_MODELS[args.model]} forward"
-                                    if args.model in FDL_MODELS
-                                    else f"hardnetNAS {args.model} forward")
-                       + f", {b} synthetic 32x32 patches per GPU"
-                       + (" (BASELINE config 4 per-rank shard)" if world > 1 and b == CONFIG4_PER_RANK else "")
-                       + (", RCCL all-gather of descriptors" if world > 1 and not args.no_allgather else ""),
-                       "model": args.model, "global_batch": b * world, "per_gpu_batch": b,
+            "scaling": "strong" if (cfg5 and world > 1) else "weak", "vs_baseline": None,
+            "dtype": ("bf16x3" if args.model == "hardnet" else "fp16x3") if on_gpu else "f32",
+            "data": "synthetic",
+            "config": {"workload": workload, "model": args.model,
+                       "baseline_config": 5 if cfg5 else (4 if world > 1 and b == CONFIG4_PER_RANK
+                                                          else (2 if args.model == "hardnet" else 3)),
+                       "global_batch": pairs * 2 if cfg5 else b * world, "per_gpu_batch": b,
                        "parallelism": f"dp{world}",
-                       "precision": "bf16x3 split-precision MFMA, fp32 accumulate" if args.model == "hardnet"
-                       else "fp16x3 split-precision MFMA for 1x1 convs and head, fp32 VALU depthwise"
-                       + (" and front" if args.model in FDL_MODELS else ""),
+                       "precision": "fp32 torch CPU layers (dry run)" if not on_gpu else
+                                    ("bf16x3 split-precision MFMA (fp32-accurate: hi/lo bf16 operands, "
+                                     "3 products, fp32 accumulate)" if args.model == "hardnet"
+                                     else "fp16x3 split-precision MFMA for 1x1 convs and head, fp32 VALU depthwise"
+                                     + (" and front" if args.model in FDL_MODELS else "")),
                        "flop_per_patch": flop_per_patch(args.model)},
+            "ranks_seen": ranks_seen,
+            "compute_ms": round(phase[0] / args.steps, 3),
+            ("pair_step_ms" if cfg5 else "allgather_ms"): round(phase[1] / args.steps, 3),
             "roofline": roof,
             "cpu_baseline": None,
         }
-        if world == 1 and not args.no_cpu_baseline:
-            result["cpu_baseline"] = cpu_baseline(args.model, model, args.cpu_seconds)
-            cb = result["cpu_baseline"]["value"]
-            result["gpu_vs_cpu"] = round(value * 1e6 / cb, 1)
+        if cfg5:
+            result["pairs_per_s"] = round(pairs * args.steps / elapsed, 1)
+            result["loss"] = float(loss.item()) if loss is not None else None
+        if world == 1 and on_gpu and not args.no_cpu_baseline:
+            if cfg5:
+                cb, check = cpu_baseline(args.model, model, args.cpu_seconds)
+            else:
+                cb, check = cpu_baseline(args.model, model, args.cpu_seconds, x_timed=x, y_timed=out)
+            result["cpu_baseline"] = cb
+            result["gpu_vs_cpu"] = round(value * 1e6 / cb["value"], 1)
+            if check is not None:
+                result["check"] = check
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.barrier()
