@@ -14,6 +14,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 
 namespace {
 constexpr int TM = 64, TN = 64, D = 128, LDP = D + 4;
@@ -164,19 +165,24 @@ __global__ __launch_bounds__(256) void k_pos(const float* __restrict__ a, const 
   if (lane == 0) pos[i] = dm_of((asq[i] + psq[row0 + i]) - 2.0f * d);
 }
 
-template <bool SWAP>
-__global__ __launch_bounds__(256, 2) void k_pairdist_rows(
+// NW waves per workgroup (32 anchors each): every workgroup streams all B positives through LDS,
+// so the positives' L2/MALL traffic is B * 512 bytes per 32 * NW anchors -- 8 waves (one
+// workgroup per CU, still two waves per SIMD) halve it against 4.
+constexpr int kPdWaves = 8;
+template <bool SWAP, int NW>
+__global__ __launch_bounds__(NW * 64) void k_pairdist_rows(
     const float* __restrict__ a, int NA, int row0, const float* __restrict__ p, int B,
     const float* __restrict__ asq, const float* __restrict__ psq, float xthr,
     float* __restrict__ rowmin, unsigned* __restrict__ colmin) {
   constexpr int TN = 64, ROWB = 272, PLANE = TN * ROWB, BUF = 2 * PLANE + TN * 4;
   __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
-  __shared__ float cred[2][4][TN];  // per-wave column minima of a tile (SWAP), by tile parity
+  __shared__ float cred[3][NW][TN];  // per-wave column minima of a tile (SWAP), tile % 3
+  __shared__ __attribute__((aligned(16))) float ainit[NW][32];  // -|a_i|^2 / 2 per wave row
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
-  const int i0 = blockIdx.x * 128 + wave * 32;  // this wave's first local anchor
+  const int i0 = blockIdx.x * (32 * NW) + wave * 32;  // this wave's first local anchor
   const int g0 = row0 + i0;                     // ... and its global row
-  // A fragments: lane (r, h) holds anchor i0+r, k = 16 ks + 8 h + j
+  // A fragments: lane (r, h) holds anchor i0+r (clamped), k = 16 ks + 8 h + j
   bf16x8 ah[8], al[8];
   {
     const int ia = min(i0 + r, NA - 1);
@@ -190,125 +196,152 @@ __global__ __launch_bounds__(256, 2) void k_pairdist_rows(
       al[ks] = as_bf16x8(lo);
     }
   }
-  // per accumulator row (C row (i&3) + 8(i>>2) + 4h): SWAP |a_i|^2, else the y-space mask
-  // threshold X* - |a_i|^2 (|a_i|^2 is reloaded for the final y -> x)
-  float rowc[16];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const float aq = asq[min(i0 + (i & 3) + 8 * (i >> 2) + 4 * h, NA - 1)];
-    rowc[i] = SWAP ? aq : xthr - aq;
-  }
-  float xu[16], xm[16];  // SWAP: x space; else y = x - |a_i|^2
+  // every MFMA chain starts from -|a_i|^2 / 2 in the row of anchor i, so that
+  // x = |p_j|^2 - 2 acc = |a_i|^2 + |p_j|^2 - 2 a_i.p_j is one FMA per entry and no per-row
+  // value occupies registers; rows past NA start at -inf (x = +inf: they reach no minimum)
+  if (lane < 32) ainit[wave][lane] = i0 + lane < NA ? -0.5f * asq[i0 + lane] : -INFINITY;
+  float xu[16], xm[16];  // minima of x over unmasked / +10-masked entries
 #pragma unroll
   for (int i = 0; i < 16; ++i) { xu[i] = INFINITY; xm[i] = INFINITY; }
-  const bool rows_ragged = i0 + 32 > NA;
 
-  // P tile staging: 64 rows x 128 fp32 = 2048 float4 -> 8 per thread
-  const int srow = tid >> 2, scol = (tid & 3) * 32;  // each thread: 32 consecutive floats of one row
-  float4 pr[8];
-  auto load_tile = [&](int j0) {
-    const int jr = min(j0 + srow, B - 1);
+  // P tile staging, in two halves of 32 rows (one per sub-tile, so few loads are in flight per
+  // thread): thread -> row of the half, PQ consecutive float4; rows past B repeat row B - 1
+  // (with its diagonal test done on the clamped column, a repeated column changes no minimum)
+  constexpr int PQ = 1024 / (NW * 64);  // float4 per thread per half
+  constexpr int TPR = 32 / PQ;          // threads per row
+  const int srow = tid / TPR, scol = (tid % TPR) * PQ * 4;
+  float4 pr[PQ];
+  auto load_half = [&](int j0, int half) {
+    const int jr = min(j0 + half * 32 + srow, B - 1);
 #pragma unroll
-    for (int q = 0; q < 8; ++q) pr[q] = *reinterpret_cast<const float4*>(p + (size_t)jr * 128 + scol + q * 4);
+    for (int q = 0; q < PQ; ++q) pr[q] = *reinterpret_cast<const float4*>(p + (size_t)jr * 128 + scol + q * 4);
   };
-  auto store_tile = [&](char* buf, int j0) {
+  auto store_half = [&](char* buf, int j0, int half) {
+    const int row = half * 32 + srow;
 #pragma unroll
-    for (int q = 0; q < 8; q += 2) {
+    for (int q = 0; q < PQ; q += 2) {
       uint4 hi, lo;
       split8(pr[q], pr[q + 1], hi, lo);
-      *reinterpret_cast<uint4*>(buf + srow * ROWB + (scol + q * 4) * 2) = hi;
-      *reinterpret_cast<uint4*>(buf + PLANE + srow * ROWB + (scol + q * 4) * 2) = lo;
+      *reinterpret_cast<uint4*>(buf + row * ROWB + (scol + q * 4) * 2) = hi;
+      *reinterpret_cast<uint4*>(buf + PLANE + row * ROWB + (scol + q * 4) * 2) = lo;
     }
-    if (tid < TN) reinterpret_cast<float*>(buf + 2 * PLANE)[tid] = psq[min(j0 + tid, B - 1)];
+    if (tid < 32) reinterpret_cast<float*>(buf + 2 * PLANE)[half * 32 + tid] = psq[min(j0 + half * 32 + tid, B - 1)];
   };
+  // One 32-column sub-tile's MFMA chain (bf16x3, K = 128) with the epilogue of the previous
+  // sub-tile woven into its gaps: two of that sub-tile's 16 accumulator entries per K-step
+  // (branch-free; pj = |p_j|^2 of this lane's column, dsel = column - g0: accumulator row rr(i)
+  // is on the diagonal iff rr(i) == dsel, -1000 when the sub-tile has no diagonal).  B
+  // fragments are read one K-step ahead.
+  float cu, cm;
+  auto epi_entry = [&](const f32x16& acc, int i, float pj, int dsel) {
+    const int rr = (i & 3) + 8 * (i >> 2) + 4 * h;
+    const float v = fmaf(-2.0f, acc[i], pj);
+    const bool m = v < xthr || rr == dsel;
+    const float tu = m ? INFINITY : v, tm = m ? v : INFINITY;
+    xu[i] = fminf(xu[i], tu);
+    xm[i] = fminf(xm[i], tm);
+    if constexpr (SWAP) {
+      cu = fminf(cu, tu);
+      cm = fminf(cm, tm);
+    }
+  };
+  auto epi_close = [&](int cslot) {
+    if constexpr (SWAP) {
+      cu = fminf(cu, __shfl_xor(cu, 32, 64));
+      cm = fminf(cm, __shfl_xor(cm, 32, 64));
+      if (h == 0) (&cred[0][0][0])[cslot + r] = fminf(dm_of(cu), dm_of(cm) + 10.f);
+    }
+  };
+  auto chain_epi = [&](const char* cur, int nt, const f32x16& accp, float pj, int dsel, int cslot) {
+    f32x16 acc;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {  // accumulator rows 8q + 4h + {0..3}
+      const float4 v = *reinterpret_cast<const float4*>(&ainit[wave][8 * q + 4 * h]);
+      acc[4 * q] = v.x;
+      acc[4 * q + 1] = v.y;
+      acc[4 * q + 2] = v.z;
+      acc[4 * q + 3] = v.w;
+    }
+    cu = INFINITY;
+    cm = INFINITY;
+    const char* base = cur + (nt * 32 + r) * ROWB + h * 16;
+    uint4 bh = *reinterpret_cast<const uint4*>(base);
+    uint4 bl = *reinterpret_cast<const uint4*>(base + PLANE);
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      uint4 nh, nl;
+      if (ks + 1 < 8) {
+        nh = *reinterpret_cast<const uint4*>(base + (ks + 1) * 32);
+        nl = *reinterpret_cast<const uint4*>(base + PLANE + (ks + 1) * 32);
+      }
+      acc = mfma3(ah[ks], al[ks], as_bf16x8(bh), as_bf16x8(bl), acc);
+      epi_entry(accp, 2 * ks, pj, dsel);
+      epi_entry(accp, 2 * ks + 1, pj, dsel);
+      if (ks + 1 < 8) {
+        bh = nh;
+        bl = nl;
+      }
+    }
+    epi_close(cslot);
+    return acc;
+  };
+  auto epilogue = [&](const f32x16& accp, float pj, int dsel, int cslot) {
+    cu = INFINITY;
+    cm = INFINITY;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) epi_entry(accp, i, pj, dsel);
+    epi_close(cslot);
+  };
+  auto reduce_cols = [&](int t) {  // tile t's column minima over the 4 waves: one atomic per column
+    const int j = t * TN + lane;
+    const float* c = cred[t % 3][0];
+    float ce = c[lane];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) ce = fminf(ce, c[w * TN + lane]);
+    if (j < B && ce < INFINITY) atomicMin(colmin + j, __float_as_uint(ce));
+  };
+  auto sub_meta = [&](const float* ps, int j0, int nt, float& pj, int& dsel, int& cslot, int t) {
+    const int jb = j0 + nt * 32;
+    pj = ps[nt * 32 + r];
+    // overlap of the wave's rows with the sub-tile's (clamped) columns
+    const int jlo = min(jb, B - 1), jhi = min(jb + 31, B - 1);
+    dsel = (jlo < g0 + 32 && jhi >= g0) ? min(jb + r, B - 1) - g0 : -1000;
+    cslot = ((t % 3) * NW + wave) * TN + nt * 32;
+  };
+
   const int ntile = (B + TN - 1) / TN;
-  load_tile(0);
-  store_tile(smem, 0);
+  load_half(0, 0);
+  store_half(smem, 0, 0);
+  load_half(0, 1);
+  store_half(smem, 0, 1);
   __syncthreads();
+  // software pipeline over 32-column sub-tiles: the chain of sub-tile k runs beside the epilogue
+  // of sub-tile k - 1 (a harmless empty one before the first)
+  f32x16 accp{};
+  float pjp = INFINITY;
+  int dselp = -1000, cslotp = wave * TN + 32;  // (tile 0's slot: overwritten by the real sub-tile)
 #pragma unroll 1
   for (int t = 0; t < ntile; ++t) {
     const char* cur = smem + (t & 1) * BUF;
     const int j0 = t * TN;
-    if (t + 1 < ntile) load_tile(j0 + TN);
-    if (SWAP && t > 0 && wave == ((t - 1) & 3) && lane < TN) {
-      // the previous tile's column minima, combined over the 4 waves: one atomic per column
-      const int j = j0 - TN + lane;
-      const float* c = cred[(t - 1) & 1][0];
-      const float ce = fminf(fminf(c[lane], c[TN + lane]), fminf(c[2 * TN + lane], c[3 * TN + lane]));
-      if (j < B && ce < INFINITY) atomicMin(colmin + j, __float_as_uint(ce));
-    }
+    const bool more = t + 1 < ntile;
+    char* nxt = smem + ((t + 1) & 1) * BUF;
+    if (SWAP && t >= 2 && wave == (t - 2) % NW) reduce_cols(t - 2);
     const float* ps = reinterpret_cast<const float*>(cur + 2 * PLANE);
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt) {
-      f32x16 acc{};
-#pragma unroll
-      for (int ks = 0; ks < 8; ++ks) {
-        const int off = (nt * 32 + r) * ROWB + (ks * 16 + h * 8) * 2;
-        const bf16x8 bh = as_bf16x8(*reinterpret_cast<const uint4*>(cur + off));
-        const bf16x8 bl = as_bf16x8(*reinterpret_cast<const uint4*>(cur + PLANE + off));
-        acc = mfma3(ah[ks], al[ks], bh, bl, acc);
-      }
-      const int jb = j0 + nt * 32, j = jb + r;  // this lane's column
-      const float pj = ps[nt * 32 + r];
-      float cu = INFINITY, cm = INFINITY;
-      const bool edge = rows_ragged || jb + 32 > B || (g0 < jb + 32 && jb < g0 + 32);
-      if (!edge) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          if constexpr (SWAP) {
-            const float x = fmaf(-2.0f, acc[i], rowc[i] + pj);
-            const bool m = x < xthr;
-            const float tu = m ? INFINITY : x, tm = m ? x : INFINITY;
-            xu[i] = fminf(xu[i], tu);
-            xm[i] = fminf(xm[i], tm);
-            cu = fminf(cu, tu);
-            cm = fminf(cm, tm);
-          } else {
-            const float y = fmaf(-2.0f, acc[i], pj);
-            const bool m = y < rowc[i];
-            xu[i] = fminf(xu[i], m ? INFINITY : y);
-            xm[i] = fminf(xm[i], m ? y : INFINITY);
-          }
-        }
-      } else {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int row = i0 + (i & 3) + 8 * (i >> 2) + 4 * h;
-          const bool valid = j < B && row < NA;
-          float v;
-          bool m;
-          if constexpr (SWAP) {
-            v = fmaf(-2.0f, acc[i], rowc[i] + pj);
-            m = v < xthr;
-          } else {
-            v = fmaf(-2.0f, acc[i], pj);
-            m = v < rowc[i];
-          }
-          m = m || row0 + row == j;
-          v = valid ? v : INFINITY;
-          const float tu = m ? INFINITY : v, tm = m ? v : INFINITY;
-          xu[i] = fminf(xu[i], tu);
-          xm[i] = fminf(xm[i], tm);
-          if constexpr (SWAP) {
-            cu = fminf(cu, tu);
-            cm = fminf(cm, tm);
-          }
-        }
-      }
-      if constexpr (SWAP) {
-        cu = fminf(cu, __shfl_xor(cu, 32, 64));
-        cm = fminf(cm, __shfl_xor(cm, 32, 64));
-        if (h == 0) cred[t & 1][wave][nt * 32 + r] = fminf(dm_of(cu), dm_of(cm) + 10.f);
-      }
+      if (more) load_half(j0 + TN, nt);
+      accp = chain_epi(cur, nt, accp, pjp, dselp, cslotp);
+      sub_meta(ps, j0, nt, pjp, dselp, cslotp, t);
+      if (more) store_half(nxt, j0 + TN, nt);
     }
-    if (t + 1 < ntile) store_tile(smem + ((t + 1) & 1) * BUF, j0 + TN);
     __syncthreads();
   }
-  if (SWAP && wave == ((ntile - 1) & 3) && lane < TN) {  // the last tile's column minima
-    const int j = (ntile - 1) * TN + lane;
-    const float* c = cred[(ntile - 1) & 1][0];
-    const float ce = fminf(fminf(c[lane], c[TN + lane]), fminf(c[2 * TN + lane], c[3 * TN + lane]));
-    if (j < B && ce < INFINITY) atomicMin(colmin + j, __float_as_uint(ce));
+  epilogue(accp, pjp, dselp, cslotp);
+  if (SWAP) {
+    __syncthreads();
+    if (ntile >= 2 && wave == (ntile - 2) % NW) reduce_cols(ntile - 2);
+    if (wave == (ntile - 1) % NW) reduce_cols(ntile - 1);
   }
   // row minima: reduce over the 32 lanes of each half-wave (the columns)
 #pragma unroll
@@ -320,11 +353,6 @@ __global__ __launch_bounds__(256, 2) void k_pairdist_rows(
       m = fminf(m, __shfl_xor(m, o, 64));
     }
     const int row = i0 + (i & 3) + 8 * (i >> 2) + 4 * h;
-    if (!SWAP) {
-      const float aq = asq[min(row, NA - 1)];
-      u += aq;
-      m += aq;
-    }
     if (r == 0 && row < NA) rowmin[row] = fminf(dm_of(u), dm_of(m) + 10.f);
   }
 }
@@ -393,12 +421,22 @@ hipError_t hn_launch_pairdist_rows(const float* a, int NA, int row0, const float
   hipLaunchKernelGGL(k_sq, dim3((NA + 3) / 4), dim3(256), 0, st, a, NA, asq);
   hipLaunchKernelGGL(k_sq, dim3((B + 3) / 4), dim3(256), 0, st, p, B, psq);
   hipLaunchKernelGGL(k_pos, dim3((NA + 3) / 4), dim3(256), 0, st, a, p, asq, psq, NA, row0, pos);
-  if (colmin)
-    hipLaunchKernelGGL(k_pairdist_rows<true>, dim3((NA + 127) / 128), dim3(256), 0, st, a, NA, row0, p, B,
-                       asq, psq, xthr, rowmin, reinterpret_cast<unsigned*>(colmin));
+  // 8-wave workgroups when they still give every CU one (NA >= 65,536 anchors), else 4-wave
+  // ones (twice the workgroups: a row shard of a sharded batch)
+  auto go = [&](auto nw) {
+    constexpr int NW = decltype(nw)::value;
+    const dim3 grid((NA + 32 * NW - 1) / (32 * NW)), block(64 * NW);
+    if (colmin)
+      hipLaunchKernelGGL((k_pairdist_rows<true, NW>), grid, block, 0, st, a, NA, row0, p, B, asq, psq, xthr,
+                         rowmin, reinterpret_cast<unsigned*>(colmin));
+    else
+      hipLaunchKernelGGL((k_pairdist_rows<false, NW>), grid, block, 0, st, a, NA, row0, p, B, asq, psq, xthr,
+                         rowmin, nullptr);
+  };
+  if (NA >= 256 * 32 * kPdWaves)
+    go(std::integral_constant<int, kPdWaves>{});
   else
-    hipLaunchKernelGGL(k_pairdist_rows<false>, dim3((NA + 127) / 128), dim3(256), 0, st, a, NA, row0, p, B,
-                       asq, psq, xthr, rowmin, nullptr);
+    go(std::integral_constant<int, 4>{});
   return hipGetLastError();
 }
 
