@@ -48,7 +48,8 @@ class HnArchDesc(ctypes.Structure):
 
 EXPORTED = ["hn_param_count", "hn_create", "hn_workspace_bytes", "hn_forward",
             "hn_pairdist_workspace_bytes", "hn_pairdist_hardneg", "hn_pairdist_rows_workspace_bytes",
-            "hn_pairdist_rows", "hn_hardnet_loss", "hn_fpr95_workspace_bytes",
+            "hn_pairdist_rows", "hn_hardnet_loss", "hn_workspace_bytes_u8", "hn_forward_u8",
+            "hn_fpr95_workspace_bytes",
             "hn_fpr95", "hn_preprocess", "hn_set_profiling",
             "hn_stage_times", "hn_destroy", "hn_last_error", "hn_abi_version"]
 
@@ -77,6 +78,8 @@ def load_library():
         lib.hn_create.argtypes = [ctypes.POINTER(HnArchDesc), P, S, ctypes.POINTER(P)]
         lib.hn_workspace_bytes.argtypes = [P, I64, ctypes.POINTER(S)]
         lib.hn_forward.argtypes = [P, P, I64, P, P, S, P]
+        lib.hn_workspace_bytes_u8.argtypes = [P, I64, ctypes.POINTER(S)]
+        lib.hn_forward_u8.argtypes = [P, P, I64, I32, I32, I32, ctypes.c_float, ctypes.c_float, P, P, S, P]
         lib.hn_pairdist_workspace_bytes.argtypes = [I64, ctypes.POINTER(S)]
         lib.hn_pairdist_hardneg.argtypes = [P, P, I64, I32, I32, P, P, P, S, P]
         lib.hn_pairdist_rows_workspace_bytes.argtypes = [I64, I64, ctypes.POINTER(S)]
@@ -95,7 +98,7 @@ def load_library():
                      "hn_pairdist_workspace_bytes", "hn_pairdist_hardneg", "hn_abi_version",
                      "hn_set_profiling", "hn_stage_times", "hn_fpr95_workspace_bytes",
                      "hn_fpr95", "hn_pairdist_rows_workspace_bytes", "hn_pairdist_rows",
-                     "hn_hardnet_loss"):
+                     "hn_hardnet_loss", "hn_workspace_bytes_u8", "hn_forward_u8"):
             getattr(lib, name).restype = ctypes.c_int
         _lib = lib
         return lib
@@ -227,6 +230,45 @@ class NativeModel:
         return out
 
     __call__ = forward
+
+    def forward_u8(self, u8: torch.Tensor, resize: str = "cv2", normalize: bool = True,
+                   mean: float = 0.443728476019, std: float = 0.20197947209,
+                   out: Optional[torch.Tensor] = None, workspace: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Descriptors straight from uint8 patches ([n,64,64] / [n,1,64,64]; [n,32,32] for
+        resize='none'): the loader transforms (hardnet/HardNet.py:333-337, 345-349) fused into the
+        forward -- equal to ``forward(preprocess(u8, ...))`` bit for bit."""
+        if resize not in RESIZE_MODES:
+            raise ValueError(f"resize must be one of {sorted(RESIZE_MODES)}")
+        if u8.dtype != torch.uint8 or u8.device != self.device:
+            raise ValueError(f"expected a uint8 tensor on {self.device}")
+        hw = 32 if resize == "none" else 64
+        b = u8.shape[0]
+        if u8.numel() != b * hw * hw:
+            raise ValueError(f"expected {hw}x{hw} patches, got shape {tuple(u8.shape)}")
+        x = u8.contiguous()
+        if out is None:
+            out = torch.empty((b, 128), device=self.device, dtype=torch.float32)
+        elif (tuple(out.shape) != (b, 128) or out.dtype != torch.float32 or out.device != self.device
+              or not out.is_contiguous()):
+            raise ValueError(f"out must be a contiguous fp32 [{b},128] tensor on {self.device}")
+        n = ctypes.c_size_t()
+        _check(self.lib.hn_workspace_bytes_u8(self._h, b, ctypes.byref(n)), "hn_workspace_bytes_u8")
+        if workspace is not None and (workspace.dtype != torch.uint8 or workspace.device != self.device
+                                      or not workspace.is_contiguous()):
+            raise ValueError(f"workspace must be a contiguous uint8 tensor on {self.device}")
+        if workspace is None or workspace.numel() < n.value:
+            workspace = torch.empty(max(n.value, 16), device=self.device, dtype=torch.uint8)
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        with torch.cuda.device(self.device):
+            _check(self.lib.hn_forward_u8(self._h, x.data_ptr(), b, hw, RESIZE_MODES[resize], int(normalize),
+                                          mean, std, out.data_ptr(), workspace.data_ptr(), workspace.numel(),
+                                          stream), "hn_forward_u8")
+        return out
+
+    def workspace_bytes_u8(self, batch: int) -> int:
+        n = ctypes.c_size_t()
+        _check(self.lib.hn_workspace_bytes_u8(self._h, batch, ctypes.byref(n)), "hn_workspace_bytes_u8")
+        return n.value
 
     def set_profiling(self, on: bool):
         _check(self.lib.hn_set_profiling(self._h, int(on)), "hn_set_profiling")

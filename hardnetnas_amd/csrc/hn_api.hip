@@ -762,7 +762,7 @@ extern "C" int hn_workspace_bytes(const hn_model* m, int64_t batch, size_t* byte
 
 // pmax: the largest chunk of this call; the buffers keep the same offsets for every chunk
 static int forward_hardnet(hn_model* m, const float* in, int P, int pmax, float* out, float* ws,
-                           hipStream_t st) {
+                           hipStream_t st, const HnU8In* u8 = nullptr) {
   const size_t per = m->ws_floats_per_patch * (size_t)pmax;
   float* a0 = ws;
   float* a1 = ws + per;
@@ -777,7 +777,13 @@ static int forward_hardnet(hn_model* m, const float* in, int P, int pmax, float*
     for (int s0 = 0; s0 < P; s0 += sub) {
       const int n = std::min(sub, P - s0);
       float* a5 = a1 + (size_t)s0 * 8192;
-      STAGE("stem+conv1+conv2", hn_launch_c12(in + (size_t)s0 * 1024, a2, m->hd, n, ineps, st));
+      if (u8) {
+        HnU8In sub = *u8;
+        sub.in += (size_t)s0 * (u8->resize == HN_RESIZE_NONE ? 1024 : 4096);
+        STAGE("stem+conv1+conv2", hn_launch_c12(nullptr, a2, m->hd, n, ineps, st, &sub));
+      } else {
+        STAGE("stem+conv1+conv2", hn_launch_c12(in + (size_t)s0 * 1024, a2, m->hd, n, ineps, st));
+      }
       STAGE("conv3", hn_launch_hardnet_conv(3, m->variant[3], m->hd, a2, a0, n, 0.f, st));
       STAGE("conv4", hn_launch_hardnet_conv(4, m->variant[4], m->hd, a0, a2, n, 0.f, st));
       STAGE("conv5", hn_launch_hardnet_conv(5, m->variant[5], m->hd, a2, a5, n, 0.f, st));
@@ -901,6 +907,68 @@ extern "C" int hn_forward(hn_model* m, const float* d_in, int64_t batch, float* 
     const int pmax = (int)std::min<int64_t>(m->chunk, batch);
     const int rc = m->desc.kind == HN_KIND_HARDNET ? forward_hardnet(m, in, P, pmax, out, ws, st)
                                                    : forward_nas(m, in, P, pmax, out, ws, st);
+    if (rc) return rc;
+  }
+  return HN_OK;
+}
+
+// uint8 input: the stock HardNet's fused k_c12 preprocesses in its patch
+// load; every other model / configuration runs hn_preprocess into the workspace tail first.
+static bool u8_fused(const hn_model* m) {
+  return m->desc.kind == HN_KIND_HARDNET && m->c12 && !m->unfused_stem && m->knobs.c12_cfg == 12 &&
+         !m->knobs.c12_abl;
+}
+
+extern "C" int hn_workspace_bytes_u8(const hn_model* m, int64_t batch, size_t* bytes_out) {
+  int rc = hn_workspace_bytes(m, batch, bytes_out);
+  if (rc) return rc;
+  if (!u8_fused(m)) *bytes_out += (size_t)std::min<int64_t>(batch, m->chunk) * 1024 * sizeof(float);
+  return HN_OK;
+}
+
+extern "C" int hn_forward_u8(hn_model* m, const uint8_t* d_in, int64_t batch, int32_t in_hw, int32_t resize,
+                             int32_t normalize, float mean, float stdv, float* d_out, void* d_workspace,
+                             size_t workspace_bytes, void* hip_stream) {
+  if (!m) return fail(HN_ERR_ARG, "model is NULL");
+  if (batch < 0) return fail(HN_ERR_ARG, "negative batch");
+  if (resize != HN_RESIZE_NONE && resize != HN_RESIZE_CV2_LINEAR && resize != HN_RESIZE_PIL_BILINEAR)
+    return fail(HN_ERR_ARG, "unknown resize mode " + std::to_string(resize));
+  const int want = resize == HN_RESIZE_NONE ? 32 : 64;
+  if (in_hw != want)
+    return fail(HN_ERR_ARG, "in_hw must be " + std::to_string(want) + " for this resize mode, got " +
+                                std::to_string(in_hw));
+  if (normalize && !(stdv != 0.0f)) return fail(HN_ERR_ARG, "std must be nonzero");
+  if (batch == 0) return HN_OK;
+  if (!d_in || !d_out || !d_workspace) return fail(HN_ERR_ARG, "NULL device pointer");
+  if ((reinterpret_cast<uintptr_t>(d_in) | reinterpret_cast<uintptr_t>(d_out) |
+       reinterpret_cast<uintptr_t>(d_workspace)) & 15)
+    return fail(HN_ERR_ARG, "device pointers must be 16-byte aligned");
+  size_t need = 0;
+  hn_workspace_bytes_u8(m, batch, &need);
+  if (workspace_bytes < need)
+    return fail(HN_ERR_WORKSPACE, "workspace too small: need " + std::to_string(need) + " bytes");
+  hipStream_t st = static_cast<hipStream_t>(hip_stream);
+  KnobScope knobs(&m->knobs);
+  const bool fused = u8_fused(m);
+  const size_t inb = (size_t)in_hw * in_hw;
+  float* ws = static_cast<float*>(d_workspace);
+  size_t base = 0;
+  hn_workspace_bytes(m, batch, &base);
+  float* pre = reinterpret_cast<float*>(static_cast<char*>(d_workspace) + base);  // unfused: fp32 patches
+  const int pmax = (int)std::min<int64_t>(m->chunk, batch);
+  for (int64_t off = 0; off < batch; off += m->chunk) {
+    const int P = (int)std::min<int64_t>(m->chunk, batch - off);
+    const uint8_t* in = d_in + off * inb;
+    float* out = d_out + off * 128;
+    int rc;
+    if (fused) {
+      const HnU8In u8{in, resize, normalize, mean, stdv};
+      rc = forward_hardnet(m, nullptr, P, pmax, out, ws, st, &u8);
+    } else {
+      STAGE("preprocess", hn_launch_preprocess(in, P, resize, normalize, mean, stdv, pre, st));
+      rc = m->desc.kind == HN_KIND_HARDNET ? forward_hardnet(m, pre, P, pmax, out, ws, st)
+                                           : forward_nas(m, pre, P, pmax, out, ws, st);
+    }
     if (rc) return rc;
   }
   return HN_OK;

@@ -20,6 +20,7 @@
 // permlane swaps.  Two barriers per band: P3 of band b overlaps P1 of band b+1 across waves.
 #include "hn_common.h"
 #include "hn_internal.h"
+#include "hn_preproc.h"
 
 #include <algorithm>
 #include <cstdlib>
@@ -79,11 +80,17 @@ HN_DEV int w1_slot(int x) { return ((x + 1) & 1) ? 17 + (x >> 1) : (x + 1) >> 1;
 // P3's steps (+5-10 %: the register file then holds conv2 fragments only one tap ahead); the
 // 29 split-stem products K-packed into two independent MFMAs instead of the dependent mfma3
 // chain (+1 %: P1 is not bound by its MFMA latency).
-template <int ABL, int NW, int RB2, int WPE, bool P3I = false, int WA = 2, bool P2I = false, int PRIO = 0>
+// U8 (preprocessing fused into the patch load): -1 = fp32 [P,1,32,32] input;
+// HN_RESIZE_NONE / _CV2_LINEAR / _PIL_BILINEAR = uint8 patches (32x32 / 64x64) resized,
+// /255'd and Normalize'd in the load (hn_preproc.h, the same arithmetic as hn_preprocess), so
+// the input costs 1 / 4 KiB of HBM per patch and no intermediate fp32 tensor exists.
+template <int ABL, int NW, int RB2, int WPE, bool P3I = false, int WA = 2, bool P2I = false, int PRIO = 0,
+          int U8 = -1>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void k_c12(
-    const float* __restrict__ in, float* __restrict__ out, const float* __restrict__ stem_w,
+    const void* __restrict__ in_, float* __restrict__ out, const float* __restrict__ stem_w,
     const float* __restrict__ stem_b, const uint4* __restrict__ w1p, const float* __restrict__ b1,
-    const uint4* __restrict__ w2p, const float* __restrict__ b2, int P, float eps) {
+    const uint4* __restrict__ w2p, const float* __restrict__ b2, int P, float eps, float pmean,
+    float pstd, int pnorm) {
   constexpr int NA0 = C12Ring<RB2>::NA0, NA1 = C12Ring<RB2>::NA1;
   constexpr int W0B = C12Ring<RB2>::W0B, W1B = C12Ring<RB2>::W1B;
   __shared__ __attribute__((aligned(16))) char s_w0[W0B];
@@ -206,16 +213,34 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, WP
   if constexpr ((ABL & 128) != 0) {                                                         \
     if (patch == patch_ts && lane == 0) dbg[48 + band * 4 + (K)] = (long long)__builtin_amdgcn_s_memtime(); \
   }
-  // the next patch's pixels are fetched one patch ahead
+  // the next patch's pixels are fetched one patch ahead (U8: its raw bytes; resized at use)
   constexpr int PPT = 1024 / (NW * 64);  // patch pixels per thread (2 or 4)
   typedef float pxv __attribute__((ext_vector_type(PPT)));
-  pxv vnext = reinterpret_cast<const pxv*>(in + pb * 1024)[t];
+  const float* in = static_cast<const float*>(in_);
+  const uint8_t* in8 = static_cast<const uint8_t*>(in_);
+  constexpr int INB = U8 == HN_RESIZE_NONE ? 1024 : 4096;  // bytes per uint8 patch
+  const int py = (PPT * t) >> 5, px = (PPT * t) & 31;      // this thread's pixels (py, px ..)
+  pxv vnext;
+  hnpre::U8Px<U8 < 0 ? HN_RESIZE_NONE : U8, PPT> rnext;
+  if constexpr (U8 < 0)
+    vnext = reinterpret_cast<const pxv*>(in + pb * 1024)[t];
+  else
+    rnext.load(in8 + pb * INB, py, px);
 #pragma unroll 1
   for (long patch = pb; patch < pe; ++patch) {
     if constexpr ((ABL & 192) != 0) patch_ts = pb + 2;
     {
-      const pxv v = vnext;
-      if (patch + 1 < pe) vnext = reinterpret_cast<const pxv*>(in + (patch + 1) * 1024)[t];
+      pxv v;
+      if constexpr (U8 < 0) {
+        v = vnext;
+        if (patch + 1 < pe) vnext = reinterpret_cast<const pxv*>(in + (patch + 1) * 1024)[t];
+      } else {
+        int q[PPT];
+        rnext.resized(py, px, q);
+#pragma unroll
+        for (int j = 0; j < PPT; ++j) v[j] = hnpre::to_input(q[j], pmean, pstd, pnorm);
+        if (patch + 1 < pe) rnext.load(in8 + (patch + 1) * INB, py, px);
+      }
       float mean = 0.f, sd = 1.f;
       if (eps >= 0.f) {  // input_norm: (x - mean) / (std_unbiased + eps), HardNet.py:306-310
         float a = 0.f;
@@ -562,12 +587,13 @@ bool hn_c12_cfg_ok(int cfg, int abl) {
 }
 
 hipError_t hn_launch_c12(const float* in, float* out, const HardnetDev& d, int P, float eps,
-                         hipStream_t st) {
+                         hipStream_t st, const HnU8In* u8) {
   if (P <= 0) return hipSuccess;
   // the calling model's HN_C12_CFG (and, in the HN_EXPERIMENTS library, HN_C12_ABL), hn_create
   const int cfg = hn_knobs().c12_cfg;  // same-box A/Bs: 12 2-4 % < 7 1.5 % < 2 4.5 % < 0
   const int abl = hn_knobs().c12_abl;
   if (!hn_c12_cfg_ok(cfg, abl)) return hipErrorInvalidValue;
+  if (u8 && (cfg != 12 || abl)) return hipErrorInvalidValue;  // the uint8 loads: production build only
   static const void* const fns[kC12Cfgs] = {
 #define HN_C12_FN(C, W, R, E, I, A, Q, PR) reinterpret_cast<const void*>(&k_c12<0, W, R, E, I, A, Q, PR>),
       HN_C12_CFGS(HN_C12_FN)
@@ -583,11 +609,21 @@ hipError_t hn_launch_c12(const float* in, float* out, const HardnetDev& d, int P
   const hipError_t e = hn_resident_blocks(fns[cfg], nw * 64, 0, &resident);
   if (e != hipSuccess) return e;
   const int grid = (int)std::min<long>((long)P, resident);
-#define HN_C12_GO(A, W, R, E, I, WA, Q, PR)                                                      \
-  hipLaunchKernelGGL((k_c12<A, W, R, E, I, WA, Q, PR>), dim3(grid), dim3(W * 64), 0, st, in, out,      \
-                     d.stem_w, d.stem_b, static_cast<const uint4*>(d.c12_w1), d.bias[1],        \
-                     static_cast<const uint4*>(d.c12_w2), d.bias[2], P, eps)
-  if (abl) {
+  const void* src = u8 ? u8->in : static_cast<const void*>(in);
+  const float pm = u8 ? u8->mean : 0.f, ps = u8 ? u8->stdv : 1.f;
+  const int pn = u8 ? u8->normalize : 0;
+#define HN_C12_GO(A, W, R, E, I, WA, Q, PR, ...)                                                 \
+  hipLaunchKernelGGL((k_c12<A, W, R, E, I, WA, Q, PR, ##__VA_ARGS__>), dim3(grid), dim3(W * 64), 0, st, src, \
+                     out, d.stem_w, d.stem_b, static_cast<const uint4*>(d.c12_w1), d.bias[1],   \
+                     static_cast<const uint4*>(d.c12_w2), d.bias[2], P, eps, pm, ps, pn)
+  if (u8) {
+    switch (u8->resize) {
+      case HN_RESIZE_NONE: HN_C12_GO(0, 4, 2, 2, false, 2, true, 5, HN_RESIZE_NONE); break;
+      case HN_RESIZE_CV2_LINEAR: HN_C12_GO(0, 4, 2, 2, false, 2, true, 5, HN_RESIZE_CV2_LINEAR); break;
+      case HN_RESIZE_PIL_BILINEAR: HN_C12_GO(0, 4, 2, 2, false, 2, true, 5, HN_RESIZE_PIL_BILINEAR); break;
+      default: return hipErrorInvalidValue;
+    }
+  } else if (abl) {
 #ifdef HN_EXPERIMENTS
     if (cfg == 0) {
       switch (abl) {

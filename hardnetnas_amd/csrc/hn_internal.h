@@ -35,9 +35,17 @@ struct HardnetDev {
   void* c12_w1 = nullptr;    // conv1 / conv2 as 16x16x32 A operands for the fused k_c12
   void* c12_w2 = nullptr;
 };
-// fused input_norm + conv0 + conv1 + conv2 (hn_c12.hip): [P,1,32,32] -> a2 [P,16,16,64]
+// uint8 patches for the fused preprocessing load (hn_forward_u8)
+struct HnU8In {
+  const uint8_t* in;  // this chunk's patches
+  int resize;         // enum hn_resize
+  int normalize;
+  float mean, stdv;
+};
+// fused input_norm + conv0 + conv1 + conv2 (hn_c12.hip): [P,1,32,32] -> a2 [P,16,16,64]; with
+// u8 the patches are uint8 and preprocessed in the load (production configuration only)
 hipError_t hn_launch_c12(const float* in, float* out, const HardnetDev& d, int P, float eps,
-                         hipStream_t st);
+                         hipStream_t st, const HnU8In* u8 = nullptr);
 
 hipError_t hn_launch_stem(const float* in, float* out, const float* w, const float* b, int P,
                           bool norm, float eps, hipStream_t st);

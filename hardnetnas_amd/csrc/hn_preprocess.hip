@@ -19,25 +19,17 @@
 
 #include "hardnet_mi355x.h"
 #include "hn_internal.h"
+#include "hn_preproc.h"
 
 namespace {
 
-// Pillow coefficients for 64 -> 32 (precompute_coeffs + normalize_coeffs_8bpc):
-// interior taps at 2c-1..2c+2 = 0.125, 0.375, 0.375, 0.125; the border outputs have three
-// taps 0.75/1.75, 0.75/1.75, 0.25/1.75 quantised to 22 bits.
-constexpr int kPB = 22;
-constexpr int kK0 = 524288, kK1 = 1572864, kE1 = 1797559, kE0 = 599186;
-
-__device__ __forceinline__ int clip8(int ss) {
-  ss >>= kPB;
-  return ss < 0 ? 0 : (ss > 255 ? 255 : ss);
-}
-
-__device__ __forceinline__ float to_input(int v, float mean, float stdv, int norm) {
-  float f = (float)v / 255.0f;
-  if (norm) f = (f - mean) / stdv;
-  return f;
-}
+using hnpre::clip8;
+using hnpre::kE0;
+using hnpre::kE1;
+using hnpre::kK0;
+using hnpre::kK1;
+using hnpre::kPB;
+using hnpre::to_input;
 
 __device__ __forceinline__ int byte_of(const uint4& q, int k) {  // k is a compile-time constant
   const unsigned w = k < 4 ? q.x : k < 8 ? q.y : k < 12 ? q.z : q.w;

@@ -152,6 +152,18 @@ enum hn_resize { HN_RESIZE_NONE = 0, HN_RESIZE_CV2_LINEAR = 1, HN_RESIZE_PIL_BIL
 int hn_preprocess(const uint8_t* d_in, int64_t n, int32_t in_hw, int32_t resize, int32_t normalize,
                   float mean, float std, float* d_out, void* hip_stream);
 
+/* Descriptor forward from uint8 patches (the loader transforms of
+ * hardnet/HardNet.py:333-337 / 345-349 + Utils.py:10-11 fused into the network's patch load):
+ * d_in [B, in_hw, in_hw] uint8; resize / normalize / mean / std as hn_preprocess.  Equals
+ * hn_preprocess followed by hn_forward bit for bit.  For the stock HardNet the preprocessing
+ * runs inside the first fused kernel (4 / 1 KiB of input HBM per patch and no fp32 copy); the
+ * other models preprocess each chunk into the workspace tail first.  Workspace:
+ * hn_workspace_bytes_u8. */
+int hn_workspace_bytes_u8(const hn_model* m, int64_t batch, size_t* bytes_out);
+int hn_forward_u8(hn_model* m, const uint8_t* d_in, int64_t batch, int32_t in_hw, int32_t resize,
+                  int32_t normalize, float mean, float std, float* d_out, void* d_workspace,
+                  size_t workspace_bytes, void* hip_stream);
+
 /* Per-stage timing (profiling aid used by bench.py): when enabled, hn_forward records a
  * hipEvent pair around every kernel launch on the caller's stream.  hn_stage_times
  * waits for the recorded events, accumulates their durations per stage name and returns

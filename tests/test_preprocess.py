@@ -122,3 +122,64 @@ def test_preprocess_rejects_wrong_shapes(cuda_device):
         N.preprocess(torch.zeros((2, 32, 32), dtype=torch.uint8, device=cuda_device), resize="cv2")
     with pytest.raises(ValueError):
         N.preprocess(torch.zeros((2, 64, 64), dtype=torch.float32, device=cuda_device))
+
+
+# ------------------------------------------------- fused preprocessing (hn_forward_u8) ----
+def _u8_batch(n, seed, hw=64):
+    """The Pillow fixture patches, tiled and perturbed to n patches (edges: 0 / 255 blocks)."""
+    fx = _fx()
+    base = fx["u8_64"] if hw == 64 else fx["pil_u8_32"]
+    g = np.random.default_rng(seed)
+    reps = -(-n // base.shape[0])
+    u = np.concatenate([base] * reps)[:n].astype(np.int32)
+    u = (u + g.integers(-3, 4, size=u.shape)).clip(0, 255).astype(np.uint8)
+    u[0] = 0
+    if n > 1:
+        u[1] = 255
+    return u
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["hardnet", "wang2"])
+@pytest.mark.parametrize("resize,normalize", [("pil", False), ("pil", True), ("cv2", True), ("none", True)])
+@pytest.mark.parametrize("n", [1, 37, 3001])
+def test_forward_u8_equals_preprocess_then_forward(name, resize, normalize, n, cuda_device):
+    """hn_forward_u8 == hn_preprocess followed by hn_forward, bit for bit (HardNet: fused into
+    k_c12's patch load; NAS: preprocessed into the workspace); 3,001 patches run every
+    persistent k_c12 workgroup over several patches and end on a ragged one."""
+    m, _, _ = build_module(name)
+    nm = N.NativeModel.from_module(m, cuda_device)
+    hw = 32 if resize == "none" else 64
+    u = torch.from_numpy(_u8_batch(n, 7, hw)).to(cuda_device)
+    ref = nm.forward(N.preprocess(u, resize=resize, normalize=normalize))
+    nm.set_profiling(True)
+    got = nm.forward_u8(u, resize=resize, normalize=normalize)
+    st = nm.stage_times()
+    assert ("preprocess" in st) == (name != "hardnet")
+    assert torch.equal(got, ref)
+
+
+@pytest.mark.gpu
+def test_forward_u8_matches_the_reference_chain(cuda_device):
+    """PIL fixtures -> (Pillow resize, ToTensor, Normalize) -> the fp32 oracle forward, against
+    the fused uint8 forward: the whole reference data path at the descriptor tolerance."""
+    fx = _fx()
+    m, _, p = build_module("hardnet")
+    nm = N.NativeModel.from_module(m, cuda_device)
+    got = nm.forward_u8(torch.from_numpy(fx["u8_64"]).to(cuda_device), resize="pil").cpu()
+    t = {k: torch.from_numpy(v) for k, v in p.items()}
+    x = torch.from_numpy(fx["pil_norm_f32"])
+    ref = O.hardnet_forward(t, x)
+    # constant patches (fixture rows 0 / 1, all 0 / all 255) are excluded: after Normalize their
+    # pixels are one fp32 value whose mean rounds differently per summation order, and
+    # input_norm's 1 / (0 + 1e-7) turns that rounding into the descriptor (ill-posed in fp32 for
+    # the reference itself); the same patches through hn_forward agree bit for bit above
+    keep = x.flatten(1).std(dim=1) > 1e-3
+    assert int(keep.sum()) >= x.shape[0] - 2
+    assert (got[keep] - ref[keep]).abs().max().item() <= 1e-4
+
+
+def test_abi_rejects_bad_forward_u8_args_without_gpu():
+    lib = N.load_library()
+    assert lib.hn_forward_u8(None, None, 4, 64, 1, 1, 0.0, 1.0, None, None, 0, None) == 1
+    assert b"model" in lib.hn_last_error()
