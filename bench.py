@@ -304,6 +304,10 @@ def main():
                     help="process-group backend for N > 1 (default nccl = RCCL on GPUs, gloo on CPU)")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu = plumbing dry run of the same step (module torch layers, gloo): no GPU")
+    ap.add_argument("--input", default="f32", choices=["f32", "u8-cv2", "u8-pil", "u8-none"],
+                    help="f32: normalised fp32 [B,1,32,32] patches (the reference's model input); u8-*: "
+                         "raw uint8 patches (64x64, or 32x32 for u8-none) with the loader's resize / "
+                         "ToTensor / Normalize fused into the forward (hn_forward_u8, SURVEY 8(f) row 3)")
     ap.add_argument("--no-allgather", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -342,17 +346,27 @@ def main():
         b = args.batch
         if b is None:
             b = (CONFIG4_PER_RANK if (world > 1 and args.model == "hardnet") else 262144) if on_gpu else 256
+    u8_mode = args.input[3:] if args.input.startswith("u8-") else None
+    if u8_mode and (not on_gpu or cfg5):
+        ap.error("--input u8-* is a GPU descriptor-forward mode")
     x = synth_input_on_device(b, dev, seed=1000 + rank)
+    if u8_mode:
+        hw = 32 if u8_mode == "none" else 64
+        x8 = torch.randint(0, 256, (b, hw, hw), device=dev, dtype=torch.uint8,
+                           generator=torch.Generator(device=dev).manual_seed(1000 + rank))
     if cfg5:  # positives = anchors + noise (the same patch seen twice), as a real pair batch
         x[b // 2:] = x[: b // 2] + 0.3 * torch.randn(b // 2, 1, 32, 32, device=dev,
                                                      generator=torch.Generator(device=dev).manual_seed(7 + rank))
     out = torch.empty((b, 128), device=dev)
-    ws = torch.empty(nm.workspace_bytes(b), device=dev, dtype=torch.uint8) if on_gpu else None
+    ws = torch.empty(nm.workspace_bytes_u8(b) if u8_mode else nm.workspace_bytes(b), device=dev,
+                     dtype=torch.uint8) if on_gpu else None
     gathered = torch.empty((b * world, 128), device=dev) if (world > 1 and not cfg5) else None
     loss = None
 
     def forward():
-        if on_gpu:
+        if u8_mode:
+            nm.forward_u8(x8, resize=u8_mode, out=out, workspace=ws)
+        elif on_gpu:
             nm.forward(x, out=out, workspace=ws)
         else:
             with torch.no_grad():
@@ -495,6 +509,9 @@ def main():
                         + (", RCCL all-gather of descriptors" if world > 1 and not args.no_allgather else ""))
         if not on_gpu:
             workload += " [CPU plumbing dry run: module torch layers, gloo; not a throughput figure]"
+        if u8_mode:
+            workload += (f" from uint8 {'32x32' if u8_mode == 'none' else '64x64'} patches, loader "
+                         f"preprocessing ({u8_mode}) fused into the forward")
         result = {
             "metric": METRIC, "value": round(value, 4 if on_gpu else 6), "unit": "Mpatches/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
@@ -523,7 +540,7 @@ def main():
             result["pairs_per_s"] = round(pairs * args.steps / elapsed, 1)
             result["loss"] = float(loss.item()) if loss is not None else None
         if world == 1 and on_gpu and not args.no_cpu_baseline:
-            if cfg5:
+            if cfg5 or u8_mode:
                 cb, check = cpu_baseline(args.model, model, args.cpu_seconds)
             else:
                 cb, check = cpu_baseline(args.model, model, args.cpu_seconds, x_timed=x, y_timed=out)

