@@ -49,6 +49,7 @@ class HnArchDesc(ctypes.Structure):
 EXPORTED = ["hn_param_count", "hn_create", "hn_workspace_bytes", "hn_forward",
             "hn_pairdist_workspace_bytes", "hn_pairdist_hardneg", "hn_pairdist_rows_workspace_bytes",
             "hn_pairdist_rows", "hn_hardnet_loss", "hn_workspace_bytes_u8", "hn_forward_u8",
+            "hn_hardnet_train_workspace_bytes", "hn_hardnet_train_forward", "hn_hardnet_train_backward",
             "hn_fpr95_workspace_bytes",
             "hn_fpr95", "hn_preprocess", "hn_set_profiling",
             "hn_stage_times", "hn_destroy", "hn_last_error", "hn_abi_version"]
@@ -79,6 +80,11 @@ def load_library():
         lib.hn_workspace_bytes.argtypes = [P, I64, ctypes.POINTER(S)]
         lib.hn_forward.argtypes = [P, P, I64, P, P, S, P]
         lib.hn_workspace_bytes_u8.argtypes = [P, I64, ctypes.POINTER(S)]
+        PP = ctypes.POINTER(P)
+        lib.hn_hardnet_train_workspace_bytes.argtypes = [I64, ctypes.POINTER(S)]
+        lib.hn_hardnet_train_forward.argtypes = [P, I64, PP, PP, PP, ctypes.c_float, ctypes.c_float,
+                                                 ctypes.c_uint64, P, P, S, P]
+        lib.hn_hardnet_train_backward.argtypes = [P, I64, PP, PP, P, ctypes.c_float, ctypes.c_uint64, P, S, P]
         lib.hn_forward_u8.argtypes = [P, P, I64, I32, I32, I32, ctypes.c_float, ctypes.c_float, P, P, S, P]
         lib.hn_pairdist_workspace_bytes.argtypes = [I64, ctypes.POINTER(S)]
         lib.hn_pairdist_hardneg.argtypes = [P, P, I64, I32, I32, P, P, P, S, P]
@@ -98,7 +104,9 @@ def load_library():
                      "hn_pairdist_workspace_bytes", "hn_pairdist_hardneg", "hn_abi_version",
                      "hn_set_profiling", "hn_stage_times", "hn_fpr95_workspace_bytes",
                      "hn_fpr95", "hn_pairdist_rows_workspace_bytes", "hn_pairdist_rows",
-                     "hn_hardnet_loss", "hn_workspace_bytes_u8", "hn_forward_u8"):
+                     "hn_hardnet_loss", "hn_workspace_bytes_u8", "hn_forward_u8",
+                     "hn_hardnet_train_workspace_bytes", "hn_hardnet_train_forward",
+                     "hn_hardnet_train_backward"):
             getattr(lib, name).restype = ctypes.c_int
         _lib = lib
         return lib
@@ -442,3 +450,60 @@ def _forward_fake(x, handle):
     if x.dim() != 4 or tuple(x.shape[1:]) != (1, 32, 32):
         raise ValueError(f"expected [B,1,32,32], got {tuple(x.shape)}")
     return x.new_empty((x.shape[0], 128))
+
+
+# ----------------------------------------------------------------------------------
+# train-mode stock HardNet (hn_hardnet_train_*): an autograd.Function over the C ABI
+# ----------------------------------------------------------------------------------
+HARDNET_CONV_IDX = (0, 3, 6, 9, 12, 15, 19)   # features.{i}.weight (HardNet.py:280-301)
+HARDNET_BN_IDX = (1, 4, 7, 10, 13, 16, 20)
+
+
+def _ptr_array(ts):
+    return (ctypes.c_void_p * len(ts))(*[t.data_ptr() for t in ts])
+
+
+class HardNetTrainFunction(torch.autograd.Function):
+    """model.train() forward of the stock HardNet on the GPU kernels (BatchNorm batch
+    statistics + running-statistics update, Dropout, L2Norm) and its backward to the 7 conv
+    weights and the input -- what autograd does over the reference module in the training loop
+    (hardnet/HardNet.py:379-441).  ``bn`` is a list of the 7 BatchNorm2d modules (their running
+    buffers are updated in place, num_batches_tracked incremented)."""
+
+    @staticmethod
+    def forward(ctx, x, drop_p, seed, bn, *weights):
+        lib = load_library()
+        b = x.shape[0]
+        n = ctypes.c_size_t()
+        _check(lib.hn_hardnet_train_workspace_bytes(b, ctypes.byref(n)), "hn_hardnet_train_workspace_bytes")
+        ws = torch.empty(n.value, device=x.device, dtype=torch.uint8)
+        out = torch.empty((b, 128), device=x.device, dtype=torch.float32)
+        ws_w = [w.detach().contiguous() for w in weights]
+        rm = [m.running_mean for m in bn]
+        rv = [m.running_var for m in bn]
+        stream = torch.cuda.current_stream(x.device).cuda_stream
+        with torch.cuda.device(x.device):
+            _check(lib.hn_hardnet_train_forward(x.data_ptr(), b, _ptr_array(ws_w), _ptr_array(rm), _ptr_array(rv),
+                                                float(bn[0].momentum), float(drop_p), int(seed), out.data_ptr(),
+                                                ws.data_ptr(), ws.numel(), stream), "hn_hardnet_train_forward")
+        for m in bn:
+            m.num_batches_tracked.add_(1)
+        ctx.ws, ctx.drop_p, ctx.seed, ctx.b = ws, float(drop_p), int(seed), b
+        ctx.save_for_backward(*ws_w)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        lib = load_library()
+        ws_w = ctx.saved_tensors
+        dws = [torch.empty_like(w) for w in ws_w]
+        need_x = ctx.needs_input_grad[0]
+        din = torch.empty((ctx.b, 1, 32, 32), device=dout.device, dtype=torch.float32) if need_x else None
+        stream = torch.cuda.current_stream(dout.device).cuda_stream
+        with torch.cuda.device(dout.device):
+            _check(lib.hn_hardnet_train_backward(dout.contiguous().data_ptr(), ctx.b, _ptr_array(ws_w),
+                                                 _ptr_array(dws), din.data_ptr() if din is not None else None,
+                                                 ctx.drop_p, ctx.seed, ctx.ws.data_ptr(), ctx.ws.numel(), stream),
+                   "hn_hardnet_train_backward")
+        ctx.ws = None
+        return (din, None, None, None, *dws)

@@ -36,6 +36,7 @@ void hn_read_knobs(HnKnobs* k) {
   k->naive_dw = std::getenv("HN_NAIVE_DW") != nullptr;
   k->no_skipfuse = std::getenv("HN_NO_SKIPFUSE") != nullptr;
   k->pairdist_valu = std::getenv("HN_PAIRDIST_VALU") != nullptr;
+  k->train_splitk = std::max(16, env_int("HN_TRAIN_SPLITK", 4096)) / 16 * 16;
 #ifdef HN_EXPERIMENTS
   k->c12_abl = env_int("HN_C12_ABL", 0) & 255;
   k->dbg = env_int("HN_DEBUG", 0);
@@ -971,6 +972,59 @@ extern "C" int hn_forward_u8(hn_model* m, const uint8_t* d_in, int64_t batch, in
     }
     if (rc) return rc;
   }
+  return HN_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+// train-mode stock HardNet (hn_train.hip)
+// ---------------------------------------------------------------------------------------
+extern "C" int hn_hardnet_train_workspace_bytes(int64_t batch, size_t* bytes_out) {
+  if (!bytes_out || batch < 2 || batch > (1 << 24)) return fail(HN_ERR_ARG, "batch must be 2 .. 2^24");
+  *bytes_out = hn_train_layout((long)batch).total;
+  return HN_OK;
+}
+
+static int train_args(int64_t batch, const void* const* ptrs, int n, void* ws, size_t ws_bytes) {
+  size_t need = 0;
+  int rc = hn_hardnet_train_workspace_bytes(batch, &need);
+  if (rc) return rc;
+  if (!ws) return fail(HN_ERR_ARG, "NULL workspace");
+  if (ws_bytes < need) return fail(HN_ERR_WORKSPACE, "workspace too small: need " + std::to_string(need) + " bytes");
+  if (!ptrs) return fail(HN_ERR_ARG, "NULL weight pointer array");
+  for (int i = 0; i < n; ++i)
+    if (!ptrs[i]) return fail(HN_ERR_ARG, "NULL weight pointer " + std::to_string(i));
+  return HN_OK;
+}
+
+extern "C" int hn_hardnet_train_forward(const float* d_in, int64_t batch, const float* const* d_weights,
+                                        float* const* d_running_mean, float* const* d_running_var, float momentum,
+                                        float dropout_p, uint64_t seed, float* d_out, void* d_workspace,
+                                        size_t workspace_bytes, void* hip_stream) {
+  int rc = train_args(batch, reinterpret_cast<const void* const*>(d_weights), 7, d_workspace, workspace_bytes);
+  if (rc) return rc;
+  if (!d_in || !d_out) return fail(HN_ERR_ARG, "NULL device pointer");
+  if ((d_running_mean == nullptr) != (d_running_var == nullptr))
+    return fail(HN_ERR_ARG, "running_mean and running_var must both be given or both NULL");
+  if (!(dropout_p >= 0.f && dropout_p < 1.f)) return fail(HN_ERR_ARG, "dropout_p must be in [0, 1)");
+  HIPCHK(hn_train_forward(d_in, (long)batch, d_weights, d_running_mean, d_running_var, momentum, 1e-5f, 1e-7f,
+                          1e-10f, dropout_p, (unsigned long long)seed, d_out, static_cast<char*>(d_workspace),
+                          static_cast<hipStream_t>(hip_stream)));
+  return HN_OK;
+}
+
+extern "C" int hn_hardnet_train_backward(const float* d_dout, int64_t batch, const float* const* d_weights,
+                                         float* const* d_dweights, float* d_din, float dropout_p, uint64_t seed,
+                                         void* d_workspace, size_t workspace_bytes, void* hip_stream) {
+  int rc = train_args(batch, reinterpret_cast<const void* const*>(d_weights), 7, d_workspace, workspace_bytes);
+  if (rc) return rc;
+  if (!d_dout) return fail(HN_ERR_ARG, "NULL device pointer");
+  if (!d_dweights) return fail(HN_ERR_ARG, "NULL gradient pointer array");
+  for (int i = 0; i < 7; ++i)
+    if (!d_dweights[i]) return fail(HN_ERR_ARG, "NULL gradient pointer " + std::to_string(i));
+  if (!(dropout_p >= 0.f && dropout_p < 1.f)) return fail(HN_ERR_ARG, "dropout_p must be in [0, 1)");
+  HIPCHK(hn_train_backward(d_dout, (long)batch, d_weights, d_dweights, d_din, 1e-10f, dropout_p,
+                           (unsigned long long)seed, static_cast<char*>(d_workspace),
+                           static_cast<hipStream_t>(hip_stream)));
   return HN_OK;
 }
 

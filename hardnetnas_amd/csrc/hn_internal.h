@@ -15,6 +15,7 @@ struct HnKnobs {
   bool naive_dw = false;       // HN_NAIVE_DW: untiled depthwise kernel
   bool no_skipfuse = false;    // HN_NO_SKIPFUSE: maxpool + pw instead of k_skip_s2
   bool pairdist_valu = false;  // HN_PAIRDIST_VALU: fp32 VALU pair-distance kernel
+  int train_splitk = 4096;     // HN_TRAIN_SPLITK: K per split-K slice of the train GEMMs
   int c12_abl = 0;             // HN_C12_ABL (HN_EXPERIMENTS only)
   int dbg = 0;                 // HN_DEBUG (HN_EXPERIMENTS only)
 };
@@ -125,3 +126,18 @@ hipError_t hn_launch_preprocess(const uint8_t* in, int64_t n, int resize, int no
                                 float stdv, float* out, hipStream_t st);
 hipError_t hn_launch_fpr95(const float* a, const float* p, const int* labels, int64_t n, int dim,
                            float* dists, double* fpr, void* ws, size_t ws_bytes, hipStream_t st);
+
+// train-mode stock HardNet (hn_train.hip): conv shapes and workspace layout
+struct HnTrainLayer {
+  int cin, cout, hin, ks, s, pad;
+};
+extern const HnTrainLayer kHardnetTrainLayers[7];
+struct HnTrainWs {  // byte offsets into the train workspace
+  size_t xn, inv_sd, z[7], rstd[7], g0, g1, col, part, total;
+};
+HnTrainWs hn_train_layout(long B);
+hipError_t hn_train_forward(const float* in, long B, const float* const* W, float* const* rmean, float* const* rvar,
+                            float mom, float bn_eps, float in_eps, float l2_eps, float drop_p,
+                            unsigned long long seed, float* out, char* ws, hipStream_t st);
+hipError_t hn_train_backward(const float* dout, long B, const float* const* W, float* const* dW, float* din,
+                             float l2_eps, float drop_p, unsigned long long seed, char* ws, hipStream_t st);

@@ -1,0 +1,465 @@
+// Train-mode stock HardNet on the GPU: the forward with BatchNorm batch
+// statistics (and running-statistics update), Dropout(0.3), and the backward to every conv
+// weight (and optionally the input), as the reference's training step runs it through autograd
+// (hardnet/HardNet.py:379-441 over the module of :275-315).
+//
+// Layout: activations are kept channel-major across the whole batch, CNHW ([C][B][H][W]), so
+//   * each conv is ONE plain GEMM per chunk of patches over an im2col matrix col [K][n*Ho*Wo]
+//     (K = Cin*k*k):  forward  Y  [Cout][nHW] = W [Cout][K] . col,
+//                     wgrad    dW [Cout][K]  += dY [Cout][nHW] . col^T,
+//                     dgrad    dcol [K][nHW]  = W^T . dY, then col2im (gather, no atomics);
+//   * BatchNorm's per-channel batch statistics are reductions over one contiguous row.
+// GEMMs run on the f32 MFMA (exact fp32 products, fp64 sums across split-K slices).
+// Saved for the backward (the workspace the caller keeps between the calls): the normalised
+// pre-ReLU output z of every BN layer, its 1/sqrt(var + eps), the normalised input and the
+// per-patch input std.  The next layer's input relu(z) (x mask / (1 - p) after the dropout) is
+// formed on the fly in im2col; the dropout mask is a counter hash of (seed, element), so the
+// backward recomputes it instead of storing it.
+#include "hn_common.h"
+#include "hn_internal.h"
+
+#include <algorithm>
+#include <cstring>
+
+namespace {
+
+// ------------------------------------------------------------------------------------------
+// generic fp32 GEMM: C(i,j) = alpha * sum_k A(i,k) B(k,j) + beta * C(i,j), element strides
+// A(i,k) = A[i*sai + k*sak], B(k,j) = B[k*sbk + j*sbj], C(i,j) = C[i*sci + j*scj].  64x64
+// workgroup tiles (4 waves of 32x32, v_mfma_f32_32x32x2_f32), K steps of 16 staged through LDS
+// as fp32 (bounds-checked, zero-filled).
+// ------------------------------------------------------------------------------------------
+struct GemmArgs {
+  const float* A;
+  const float* B;
+  float* C;
+  long M, N, K;
+  long sai, sak, sbk, sbj, sci, scj;
+  float alpha, beta;
+};
+
+// split-K: workgroup z of gridDim.z covers K range [z * kslice, (z + 1) * kslice) and writes
+// its partial tile to part[z] (M x N, row-major); k_splitk_sum adds the slices in fp64, so a
+// weight gradient's reduction over all B*H*W positions never runs as one fp32 chain
+__global__ __launch_bounds__(256) void k_gemm(GemmArgs g, long kslice, float* __restrict__ part) {
+  __shared__ float sA[64][17];
+  __shared__ float sB[16][65];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int wm = w >> 1, wn = w & 1, r = lane & 31, h = lane >> 5;
+  const long i0 = (long)blockIdx.y * 64, j0 = (long)blockIdx.x * 64;
+  const long kb = (long)blockIdx.z * kslice, ke = min(g.K, kb + kslice);
+  f32x16 acc{};
+  for (long k0 = kb; k0 < ke; k0 += 16) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {  // A tile 64 x 16, B tile 16 x 64
+      const int idx = t + 256 * e;
+      {
+        const int ii = g.sak == 1 ? idx >> 4 : idx & 63, kk = g.sak == 1 ? idx & 15 : idx >> 6;
+        const long gi = i0 + ii, gk = k0 + kk;
+        sA[ii][kk] = (gi < g.M && gk < ke) ? g.A[gi * g.sai + gk * g.sak] : 0.f;
+      }
+      {
+        const int kk = g.sbj == 1 ? idx >> 6 : idx & 15, jj = g.sbj == 1 ? idx & 63 : idx >> 4;
+        const long gk = k0 + kk, gj = j0 + jj;
+        sB[kk][jj] = (gk < ke && gj < g.N) ? g.B[gk * g.sbk + gj * g.sbj] : 0.f;
+      }
+    }
+    __syncthreads();
+    // v_mfma_f32_32x32x2_f32: exact fp32 products (an fmaf chain per output, bitwise), so the
+    // backward through train-mode BatchNorm -- whose 1/sigma amplifies rounding -- carries fp32
+    // accuracy, as the reference's fp32 autograd does (bf16x3's 2^-16 products measured 3-10x
+    // further from the fp64 gradients than torch-CPU fp32)
+#pragma unroll
+    for (int kk = 0; kk < 16; kk += 2)
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(sA[wm * 32 + r][kk + h], sB[kk + h][wn * 32 + r], acc, 0, 0, 0);
+    __syncthreads();
+  }
+  // acc[4q + e]: row 8q + 4h + e, column r of the wave's 32 x 32 tile
+  const long j = j0 + wn * 32 + r;
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const long i = i0 + wm * 32 + 8 * q + 4 * h + e;
+      if (i < g.M && j < g.N) {
+        if (part) {
+          part[((long)blockIdx.z * g.M + i) * g.N + j] = acc[4 * q + e];
+        } else {
+          float* c = g.C + i * g.sci + j * g.scj;
+          *c = g.beta == 0.f ? g.alpha * acc[4 * q + e] : g.alpha * acc[4 * q + e] + g.beta * *c;
+        }
+      }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_splitk_sum(GemmArgs g, int S, const float* __restrict__ part) {
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= g.M * g.N) return;
+  double s = 0.0;
+  for (int z = 0; z < S; ++z) s += part[(long)z * g.M * g.N + e];
+  const long i = e / g.N, j = e % g.N;
+  float* c = g.C + i * g.sci + j * g.scj;
+  *c = g.beta == 0.f ? (float)(g.alpha * s) : (float)(g.alpha * s + g.beta * (double)*c);
+}
+
+constexpr long kSplitK = 16;  // the smallest K per split-K slice (the workspace is sized for it)
+
+// part: scratch for M x N x ceil(K / kSplitK) floats when K > kSplitK (nullptr: one slice)
+hipError_t gemm(const GemmArgs& g, hipStream_t st, float* part = nullptr) {
+  if (g.M <= 0 || g.N <= 0) return hipSuccess;
+  const long ks = hn_knobs().train_splitk;  // K per slice (HN_TRAIN_SPLITK, default 4096)
+  const int S = part && g.K > ks ? (int)((g.K + ks - 1) / ks) : 1;
+  const dim3 grid((unsigned)((g.N + 63) / 64), (unsigned)((g.M + 63) / 64), (unsigned)S);
+  hipLaunchKernelGGL(k_gemm, grid, dim3(256), 0, st, g, S > 1 ? ks : g.K, S > 1 ? part : nullptr);
+  if (S > 1) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_splitk_sum, dim3((unsigned)((g.M * g.N + 255) / 256)), dim3(256), 0, st, g, S, part);
+  }
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+// counter-hash dropout mask (keep with probability 1 - p), recomputed in the backward
+// ------------------------------------------------------------------------------------------
+HN_DEV float drop_scale(unsigned long long seed, unsigned long long e, float p) {
+  unsigned long long x = seed ^ (e * 0x9E3779B97F4A7C15ull);
+  x ^= x >> 30;
+  x *= 0xBF58476D1CE4E5B9ull;
+  x ^= x >> 27;
+  x *= 0x94D049BB133111EBull;
+  x ^= x >> 31;
+  const float u = (float)(x >> 40) * (1.0f / 16777216.0f);  // [0, 1)
+  return u < p ? 0.f : 1.f / (1.f - p);
+}
+
+// the input of the next layer from a saved BN output: relu(z) [x dropout]
+struct ActIn {
+  const float* z;  // CNHW
+  int relu;
+  float drop_p;    // 0: no dropout
+  unsigned long long seed;
+};
+HN_DEV float act_at(const ActIn& a, long idx) {
+  float v = a.z[idx];
+  if (a.relu) v = fmaxf(v, 0.f);
+  if (a.drop_p > 0.f) v *= drop_scale(a.seed, (unsigned long long)idx, a.drop_p);
+  return v;
+}
+
+// im2col for patches [n0, n0 + n) of a CNHW activation [C][B][H][W]: col [C*KS*KS][n*Ho*Wo]
+__global__ __launch_bounds__(256) void k_im2col(ActIn a, int C, long B, int H, int W, int KS, int S, int PAD,
+                                                int Ho, int Wo, long n0, long n, float* __restrict__ col) {
+  const long cols = n * Ho * Wo;
+  const long total = (long)C * KS * KS * cols;
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
+    const long k = e / cols, q = e % cols;
+    const int c = (int)(k / (KS * KS)), tap = (int)(k % (KS * KS)), dy = tap / KS, dx = tap % KS;
+    const long p = q / (Ho * Wo);
+    const int o = (int)(q % (Ho * Wo)), oy = o / Wo, ox = o % Wo;
+    const int y = oy * S - PAD + dy, x = ox * S - PAD + dx;
+    col[e] = (y >= 0 && y < H && x >= 0 && x < W) ? act_at(a, (((long)c * B + n0 + p) * H + y) * W + x) : 0.f;
+  }
+}
+
+// col2im (gather): d_in [C][B][H][W] patches [n0, n0 + n) = sum of the dcol entries that read them
+__global__ __launch_bounds__(256) void k_col2im(const float* __restrict__ dcol, int C, long B, int H, int W, int KS,
+                                                int S, int PAD, int Ho, int Wo, long n0, long n,
+                                                float* __restrict__ din) {
+  const long cols = n * Ho * Wo;
+  const long total = (long)C * n * H * W;
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
+    const int x = (int)(e % W), y = (int)((e / W) % H);
+    const long p = (e / ((long)W * H)) % n;
+    const int c = (int)(e / ((long)W * H * n));
+    float s = 0.f;
+    for (int dy = 0; dy < KS; ++dy) {
+      const int ty = y + PAD - dy;
+      if (ty < 0 || ty % S) continue;
+      const int oy = ty / S;
+      if (oy >= Ho) continue;
+      for (int dx = 0; dx < KS; ++dx) {
+        const int tx = x + PAD - dx;
+        if (tx < 0 || tx % S) continue;
+        const int ox = tx / S;
+        if (ox >= Wo) continue;
+        s += dcol[((long)c * KS * KS + dy * KS + dx) * cols + p * Ho * Wo + oy * Wo + ox];
+      }
+    }
+    din[(((long)c * B + n0 + p) * H + y) * W + x] = s;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// BatchNorm2d(affine=False) in train mode, one workgroup per channel over its row of L values
+// ------------------------------------------------------------------------------------------
+HN_DEV double block_sum(double v, double* sh) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) sh[w] = v;
+  __syncthreads();
+  double s = 0.0;
+  for (int i = 0; i < (int)(blockDim.x >> 6); ++i) s += sh[i];
+  return s;
+}
+
+// y (in place) -> z = (y - mean) * rstd; running stats: (1 - m) r + m stat (var unbiased)
+__global__ __launch_bounds__(256) void k_bn_train(float* __restrict__ y, long L, float eps, float mom,
+                                                  float* __restrict__ rmean, float* __restrict__ rvar,
+                                                  float* __restrict__ rstd_out) {
+  __shared__ double sh[4];
+  const int c = blockIdx.x;
+  float* row = y + (long)c * L;
+  double s = 0.0;
+  for (long i = threadIdx.x; i < L; i += 256) s += row[i];
+  const double mean = block_sum(s, sh) / (double)L;
+  double q = 0.0;
+  for (long i = threadIdx.x; i < L; i += 256) {
+    const double d = row[i] - mean;
+    q += d * d;
+  }
+  const double var = block_sum(q, sh) / (double)L;
+  const float m = (float)mean, rs = (float)(1.0 / std::sqrt(var + (double)eps));
+  for (long i = threadIdx.x; i < L; i += 256) row[i] = (row[i] - m) * rs;
+  if (threadIdx.x == 0) {
+    rstd_out[c] = rs;
+    if (rmean) {
+      rmean[c] = (1.f - mom) * rmean[c] + mom * m;
+      rvar[c] = (1.f - mom) * rvar[c] + mom * (float)(L > 1 ? var * (double)L / (double)(L - 1) : var);
+    }
+  }
+}
+
+// backward through [dropout o] ReLU o BN(train): g = da * relu'(z) [* mask]; dy = rstd * (g -
+// mean(g) - z mean(g z)), in place in da (which becomes dY of the conv)
+__global__ __launch_bounds__(256) void k_bn_train_bwd(float* __restrict__ da, const float* __restrict__ z, long L,
+                                                      const float* __restrict__ rstd, int relu, float drop_p,
+                                                      unsigned long long seed) {
+  __shared__ double sh[4];
+  const int c = blockIdx.x;
+  float* g = da + (long)c * L;
+  const float* zr = z + (long)c * L;
+  const long base = (long)c * L;
+  double s1 = 0.0, s2 = 0.0;
+  for (long i = threadIdx.x; i < L; i += 256) {
+    float v = g[i];
+    if (relu && zr[i] <= 0.f) v = 0.f;
+    if (drop_p > 0.f) v *= drop_scale(seed, (unsigned long long)(base + i), drop_p);
+    g[i] = v;
+    s1 += v;
+    s2 += (double)v * zr[i];
+  }
+  const float m1 = (float)(block_sum(s1, sh) / (double)L);
+  const float m2 = (float)(block_sum(s2, sh) / (double)L);
+  const float rs = rstd[c];
+  for (long i = threadIdx.x; i < L; i += 256) g[i] = rs * (g[i] - m1 - zr[i] * m2);
+}
+
+// input_norm (HardNet.py:306-310, mean / std detached): one wave per patch; saves 1 / (std + eps)
+__global__ __launch_bounds__(256) void k_input_norm(const float* __restrict__ in, long B, float eps,
+                                                    float* __restrict__ xn, float* __restrict__ inv_sd) {
+  const long p = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (p >= B) return;
+  float v[16];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    v[j] = in[p * 1024 + j * 64 + lane];
+    s += v[j];
+  }
+  const float mean = wave_sum(s) * (1.f / 1024.f);
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) q += (v[j] - mean) * (v[j] - mean);
+  const float sd = sqrtf(wave_sum(q) * (1.f / 1023.f)) + eps;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) xn[p * 1024 + j * 64 + lane] = (v[j] - mean) / sd;
+  if (lane == 0) inv_sd[p] = 1.f / sd;
+}
+
+__global__ __launch_bounds__(256) void k_scale_rows(float* __restrict__ g, long B, const float* __restrict__ s) {
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  if (e < B * 1024) g[e] *= s[e >> 10];
+}
+
+// L2Norm (Utils.py:15-22) of z6 [128][B] -> out [B][128]; one wave per patch
+__global__ __launch_bounds__(256) void k_l2_fwd(const float* __restrict__ z, long B, float eps, float* __restrict__ out) {
+  const long p = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (p >= B) return;
+  const float a = z[(long)lane * B + p], b = z[(long)(lane + 64) * B + p];
+  const float n = sqrtf(wave_sum(a * a + b * b) + eps);
+  out[p * 128 + lane] = a / n;
+  out[p * 128 + 64 + lane] = b / n;
+}
+
+// dz6 [128][B] from dout [B][128]: y = z / n, dz = (dy - y (y . dy)) / n
+__global__ __launch_bounds__(256) void k_l2_bwd(const float* __restrict__ z, const float* __restrict__ dout, long B,
+                                                float eps, float* __restrict__ dz) {
+  const long p = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (p >= B) return;
+  const float a = z[(long)lane * B + p], b = z[(long)(lane + 64) * B + p];
+  const float n = sqrtf(wave_sum(a * a + b * b) + eps);
+  const float ya = a / n, yb = b / n, da = dout[p * 128 + lane], db = dout[p * 128 + 64 + lane];
+  const float dot = wave_sum(ya * da + yb * db);
+  dz[(long)lane * B + p] = (da - ya * dot) / n;
+  dz[(long)(lane + 64) * B + p] = (db - yb * dot) / n;
+}
+
+unsigned grid_for(long n) { return (unsigned)std::min<long>((n + 255) / 256, 65536); }
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------
+// host side
+// ------------------------------------------------------------------------------------------
+const HnTrainLayer kHardnetTrainLayers[7] = {
+    // cin, cout, hin, ks, s, pad
+    {1, 32, 32, 3, 1, 1},   {32, 32, 32, 3, 1, 1}, {32, 64, 32, 3, 2, 1}, {64, 64, 16, 3, 1, 1},
+    {64, 128, 16, 3, 2, 1}, {128, 128, 8, 3, 1, 1}, {128, 128, 8, 8, 1, 0}};
+
+static long hout_of(const HnTrainLayer& l) { return (l.hin + 2 * l.pad - l.ks) / l.s + 1; }
+
+// patches per im2col chunk: col = K x (n Ho Wo) floats within kColBudget
+static constexpr size_t kColBudget = (size_t)256 << 20;
+static long chunk_of(const HnTrainLayer& l, long B) {
+  const long ho = hout_of(l);
+  const size_t per = (size_t)l.cin * l.ks * l.ks * ho * ho * sizeof(float);
+  return std::max<long>(1, std::min<long>(B, (long)(kColBudget / per)));
+}
+
+HnTrainWs hn_train_layout(long B) {
+  HnTrainWs w{};
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    const size_t o = off;
+    off += (bytes + 255) / 256 * 256;
+    return o;
+  };
+  w.xn = take((size_t)B * 1024 * 4);
+  w.inv_sd = take((size_t)B * 4);
+  size_t maxact = (size_t)B * 1024;
+  for (int l = 0; l < 7; ++l) {
+    const long ho = hout_of(kHardnetTrainLayers[l]);
+    w.z[l] = take((size_t)kHardnetTrainLayers[l].cout * B * ho * ho * 4);
+    w.rstd[l] = take((size_t)kHardnetTrainLayers[l].cout * 4);
+    maxact = std::max(maxact, (size_t)kHardnetTrainLayers[l].cout * B * ho * ho);
+  }
+  w.g0 = take(maxact * 4);
+  w.g1 = take(maxact * 4);
+  size_t col = 0;
+  for (int l = 0; l < 7; ++l) {
+    const HnTrainLayer& L = kHardnetTrainLayers[l];
+    const long ho = hout_of(L);
+    col = std::max(col, (size_t)L.cin * L.ks * L.ks * chunk_of(L, B) * ho * ho * 4);
+  }
+  w.col = take(col);
+  size_t part = 0;  // split-K partials of the weight gradients
+  for (int l = 0; l < 7; ++l) {
+    const HnTrainLayer& L = kHardnetTrainLayers[l];
+    const long ho = hout_of(L), kk = chunk_of(L, B) * ho * ho;
+    part = std::max(part, (size_t)L.cout * L.cin * L.ks * L.ks * ((kk + hn_knobs().train_splitk - 1) / hn_knobs().train_splitk) * 4);
+  }
+  w.part = take(part);
+  w.total = off;
+  return w;
+}
+
+#define HCK(x)                        \
+  do {                                \
+    hipError_t e_ = (x);              \
+    if (e_ != hipSuccess) return e_;  \
+  } while (0)
+
+hipError_t hn_train_forward(const float* in, long B, const float* const* W, float* const* rmean, float* const* rvar,
+                            float mom, float bn_eps, float in_eps, float l2_eps, float drop_p,
+                            unsigned long long seed, float* out, char* ws, hipStream_t st) {
+  const HnTrainWs L = hn_train_layout(B);
+  float* xn = reinterpret_cast<float*>(ws + L.xn);
+  float* col = reinterpret_cast<float*>(ws + L.col);
+  hipLaunchKernelGGL(k_input_norm, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, in, B, in_eps, xn,
+                     reinterpret_cast<float*>(ws + L.inv_sd));
+  HCK(hipGetLastError());
+  for (int l = 0; l < 7; ++l) {
+    const HnTrainLayer& S = kHardnetTrainLayers[l];
+    const long ho = hout_of(S), hw = ho * ho, K = (long)S.cin * S.ks * S.ks;
+    // this layer's input: the normalised patch, or relu(z) of the previous layer (x the dropout
+    // mask before conv6, HardNet.py:299)
+    const ActIn a{l == 0 ? xn : reinterpret_cast<const float*>(ws + L.z[l - 1]), l > 0 ? 1 : 0,
+                  l == 6 ? drop_p : 0.f, seed};
+    float* z = reinterpret_cast<float*>(ws + L.z[l]);
+    const long nc = chunk_of(S, B);
+    for (long n0 = 0; n0 < B; n0 += nc) {
+      const long n = std::min(nc, B - n0);
+      hipLaunchKernelGGL(k_im2col, dim3(grid_for(K * n * hw)), dim3(256), 0, st, a, S.cin, B, S.hin, S.hin,
+                         S.ks, S.s, S.pad, (int)ho, (int)ho, n0, n, col);
+      HCK(hipGetLastError());
+      // Y[Cout][n0 .. n0 + n) = W [Cout][K] . col [K][n hw]
+      GemmArgs g{W[l], col, z + n0 * hw, S.cout, n * hw, K, K, 1, n * hw, 1, B * hw, 1, 1.f, 0.f};
+      HCK(gemm(g, st));
+    }
+    hipLaunchKernelGGL(k_bn_train, dim3(S.cout), dim3(256), 0, st, z, B * hw, bn_eps, mom, rmean ? rmean[l] : nullptr,
+                       rvar ? rvar[l] : nullptr, reinterpret_cast<float*>(ws + L.rstd[l]));
+    HCK(hipGetLastError());
+  }
+  hipLaunchKernelGGL(k_l2_fwd, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st,
+                     reinterpret_cast<const float*>(ws + L.z[6]), B, l2_eps, out);
+  return hipGetLastError();
+}
+
+hipError_t hn_train_backward(const float* dout, long B, const float* const* W, float* const* dW, float* din,
+                             float l2_eps, float drop_p, unsigned long long seed, char* ws, hipStream_t st) {
+  const HnTrainWs L = hn_train_layout(B);
+  const float* xn = reinterpret_cast<const float*>(ws + L.xn);
+  float* col = reinterpret_cast<float*>(ws + L.col);
+  float* gbuf[2] = {reinterpret_cast<float*>(ws + L.g0), reinterpret_cast<float*>(ws + L.g1)};
+  // g: gradient w.r.t. layer l's output activation a_l (a_6 = z_6 into the L2 norm; a_5 =
+  // dropout(relu(z_5)); a_l = relu(z_l) below), then in place w.r.t. its conv output
+  float* g = gbuf[0];
+  hipLaunchKernelGGL(k_l2_bwd, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st,
+                     reinterpret_cast<const float*>(ws + L.z[6]), dout, B, l2_eps, g);
+  HCK(hipGetLastError());
+  for (int l = 6; l >= 0; --l) {
+    const HnTrainLayer& S = kHardnetTrainLayers[l];
+    const long ho = hout_of(S), hw = ho * ho, K = (long)S.cin * S.ks * S.ks;
+    hipLaunchKernelGGL(k_bn_train_bwd, dim3(S.cout), dim3(256), 0, st, g, reinterpret_cast<const float*>(ws + L.z[l]),
+                       B * hw, reinterpret_cast<const float*>(ws + L.rstd[l]), l < 6 ? 1 : 0,
+                       l == 5 ? drop_p : 0.f, seed);
+    HCK(hipGetLastError());
+    const ActIn a{l == 0 ? xn : reinterpret_cast<const float*>(ws + L.z[l - 1]), l > 0 ? 1 : 0,
+                  l == 6 ? drop_p : 0.f, seed};
+    float* gin = gbuf[(7 - l) & 1];  // gradient w.r.t. this layer's input activation
+    const bool want_in = l > 0 || din;
+    const long nc = chunk_of(S, B);
+    for (long n0 = 0; n0 < B; n0 += nc) {
+      const long n = std::min(nc, B - n0);
+      hipLaunchKernelGGL(k_im2col, dim3(grid_for(K * n * hw)), dim3(256), 0, st, a, S.cin, B, S.hin, S.hin,
+                         S.ks, S.s, S.pad, (int)ho, (int)ho, n0, n, col);
+      HCK(hipGetLastError());
+      // dW [Cout][K] (+)= dY [Cout][n hw] . col^T
+      GemmArgs gw{g + n0 * hw, col, dW[l], S.cout, K, n * hw, B * hw, 1, 1, n * hw, K, 1, 1.f, n0 == 0 ? 0.f : 1.f};
+      HCK(gemm(gw, st, reinterpret_cast<float*>(ws + L.part)));
+      if (want_in) {
+        // dcol [K][n hw] = W^T [K][Cout] . dY [Cout][n hw]  (into col: its im2col is consumed)
+        GemmArgs gd{W[l], g + n0 * hw, col, K, n * hw, S.cout, 1, K, B * hw, 1, n * hw, 1, 1.f, 0.f};
+        HCK(gemm(gd, st));
+        hipLaunchKernelGGL(k_col2im, dim3(grid_for((long)S.cin * n * S.hin * S.hin)), dim3(256), 0, st, col,
+                           S.cin, B, S.hin, S.hin, S.ks, S.s, S.pad, (int)ho, (int)ho, n0, n, gin);
+        HCK(hipGetLastError());
+      }
+    }
+    g = gin;
+  }
+  if (din) {
+    // input_norm with detached mean / std (HardNet.py:309-310): d input = d xn / (std + eps)
+    hipLaunchKernelGGL(k_scale_rows, dim3(grid_for(B * 1024)), dim3(256), 0, st, g, B,
+                       reinterpret_cast<const float*>(ws + L.inv_sd));
+    HCK(hipGetLastError());
+    HCK(hipMemcpyAsync(din, g, (size_t)B * 1024 * 4, hipMemcpyDeviceToDevice, st));
+  }
+  return hipSuccess;
+}

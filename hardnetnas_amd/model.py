@@ -156,10 +156,33 @@ class HardNet(_NativeMixin, nn.Module):
         sp = torch.std(flat, dim=1) + self.input_norm_eps
         return (x - mp.detach().view(-1, 1, 1, 1)) / sp.detach().view(-1, 1, 1, 1)
 
+    def _train_native_eligible(self, x) -> bool:
+        """model.train() on a HIP fp32 [B>=2,1,32,32] batch with the reference's BatchNorm setup
+        (momentum given, running statistics tracked) runs hn_hardnet_train_* (SURVEY 8(f) row 4)."""
+        if not (getattr(self, "native_train", True) and self.training and x.is_cuda
+                and x.dtype == torch.float32 and x.dim() == 4
+                and tuple(x.shape[1:]) == (1, 32, 32) and x.shape[0] >= 2):
+            return False
+        bns = [self.features[i] for i in (1, 4, 7, 10, 13, 16, 20)]
+        return (self.input_norm_eps == 1e-7 and self.l2_eps == 1e-10
+                and all(b.momentum is not None and b.track_running_stats and b.eps == 1e-5 for b in bns)
+                and all(self.features[i].weight.is_cuda for i in (0, 3, 6, 9, 12, 15, 19)))
+
+    def _train_native_forward(self, x):
+        from . import _native as N
+        bns = [self.features[i] for i in N.HARDNET_BN_IDX]
+        ws = [self.features[i].weight for i in N.HARDNET_CONV_IDX]
+        drop = self.features[18]
+        p = drop.p if drop.training else 0.0
+        seed = int(torch.randint(0, 2 ** 62, (1,), device="cpu").item()) if p > 0 else 0
+        return N.HardNetTrainFunction.apply(x.contiguous(), p, seed, bns, *ws)
+
     def forward(self, input):
         y = self._dispatch_native(input)
         if y is not None:
             return y
+        if self._train_native_eligible(input):
+            return self._train_native_forward(input)
         x_features = self.features(self.input_norm(input))
         x = x_features.view(x_features.size(0), -1)
         norm = torch.sqrt(torch.sum(x * x, dim=1) + self.l2_eps)

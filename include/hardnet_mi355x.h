@@ -164,6 +164,27 @@ int hn_forward_u8(hn_model* m, const uint8_t* d_in, int64_t batch, int32_t in_hw
                   int32_t normalize, float mean, float std, float* d_out, void* d_workspace,
                   size_t workspace_bytes, void* hip_stream);
 
+/* Train-mode stock HardNet (the module of hardnet/HardNet.py:275-315 in
+ * model.train() as the training loop :379-441 runs it through autograd).
+ *  forward : input_norm (mean / std detached), 7 x [conv -> BatchNorm2d(affine=False) with the
+ *            batch's statistics (running_mean / running_var updated in place with `momentum`,
+ *            unbiased variance) -> ReLU], Dropout(dropout_p) before conv6, L2Norm.
+ *  backward: d_dout [B,128] -> d_dweights[l] (each [Cout,Cin,k,k] like the module's weights,
+ *            overwritten), and d_din [B,1,32,32] if not NULL.
+ * d_weights / d_running_* / d_dweights are host arrays of 7 device pointers (features.{0,3,6,9,
+ * 12,15,19}.weight and the matching BN buffers, fp32 contiguous).  The workspace holds what the
+ * backward needs: keep it (unchanged) between a forward and its backward, with the same batch,
+ * dropout_p and seed (the dropout mask is a counter hash of (seed, element), recomputed).
+ * Batch >= 2 (train-mode BatchNorm of the 1x1 conv6 output needs more than one value). */
+int hn_hardnet_train_workspace_bytes(int64_t batch, size_t* bytes_out);
+int hn_hardnet_train_forward(const float* d_in, int64_t batch, const float* const* d_weights,
+                             float* const* d_running_mean, float* const* d_running_var, float momentum,
+                             float dropout_p, uint64_t seed, float* d_out, void* d_workspace,
+                             size_t workspace_bytes, void* hip_stream);
+int hn_hardnet_train_backward(const float* d_dout, int64_t batch, const float* const* d_weights,
+                              float* const* d_dweights, float* d_din, float dropout_p, uint64_t seed,
+                              void* d_workspace, size_t workspace_bytes, void* hip_stream);
+
 /* Per-stage timing (profiling aid used by bench.py): when enabled, hn_forward records a
  * hipEvent pair around every kernel launch on the caller's stream.  hn_stage_times
  * waits for the recorded events, accumulates their durations per stage name and returns

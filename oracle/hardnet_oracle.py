@@ -209,7 +209,7 @@ def hardest_negative(anchor, positive, anchor_swap=False):
     (pos, min_neg) per row."""
     eps = 1e-8
     dm = distance_matrix_vector(anchor, positive) + eps
-    eye = torch.eye(dm.size(1), dtype=dm.dtype)
+    eye = torch.eye(dm.size(1), dtype=dm.dtype, device=dm.device)
     pos1 = torch.diag(dm)
     d = dm + eye * 10
     mask = (d.ge(0.008).to(d.dtype) - 1.0) * (-1)

@@ -1,0 +1,202 @@
+"""Train-mode stock HardNet on MI355X: the HIP forward with BatchNorm batch
+statistics + running-statistics update and the backward of loss_HardNet, against the
+reference module's own layers run by autograd on the CPU (hardnet/HardNet.py:379-441; the
+module is hardnetnas_amd.model.HardNet, whose torch path is the reference's Sequential).
+Dropout is off (p = 0) wherever results are compared: the reference draws its mask from
+torch's RNG, the HIP kernels from a counter hash.
+
+Gradient tolerance.  The forward is compared at 1e-4 max abs (north_star).  Gradients are
+compared with the fp64 run of the same module by relative L2 error: a max-abs bar cannot hold
+for ANY fp32 implementation, because a BN output within rounding of a ReLU kink can land on
+either side, zeroing (or not) one large gradient entry that then propagates to every earlier
+layer.  Measured on CPU (/tmp-free restatement in DESIGN.md 10): the same algorithm in fp32
+with torch's own conv-gradient kernels is 2.3e-2 max-abs-relative from fp64 at conv5 from a
+single flipped element, while torch-autograd fp32 happens to flip none (1e-6).  The L2 bar
+below (5e-3) is what fp32 implementations meet with or without such a flip (MIOpen through the
+reference layers on the same GPU: up to 1.1e-3 at conv0, torch-CPU fp32 1.3e-3)."""
+import numpy as np
+import pytest
+import torch
+
+from fixtures import build_module, golden_inputs
+from oracle import hardnet_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _fresh(seed=0):
+    """The reference training run's starting point: HardNet() with its own weights_init
+    (orthogonal, gain 0.6, HardNet.py:317-324) and fresh BatchNorm buffers."""
+    from hardnetnas_amd.model import HardNet
+    torch.manual_seed(seed)
+    return HardNet()
+
+
+def _pair(dev, dropout=0.0, fresh=False):
+    if fresh:
+        mg, fx = _fresh(), build_module("hardnet")[1]
+        mc = _fresh()
+    else:
+        mg, fx, _ = build_module("hardnet")
+        mc, _, _ = build_module("hardnet")
+    mg = mg.to(dev).train()
+    mc = mc.train()
+    mg.features[18].p = dropout
+    mc.features[18].p = dropout
+    return mg, mc, fx
+
+
+def _model64(fresh):
+    md = _fresh() if fresh else build_module("hardnet")[0]
+    md = md.double().train()
+    md.features[18].p = 0.0
+    return md
+
+
+def _rel(a, b):
+    return (a.detach().cpu().double() - b.detach().double()).abs().max().item() / max(1e-12, b.abs().max().item())
+
+
+def _rel2(a, b):
+    a, b = a.detach().cpu().double(), b.detach().double()
+    return ((a - b).norm() / max(1e-30, b.norm())).item()
+
+
+L2_BAR = 5e-3
+
+
+def test_train_forward_and_running_stats(cuda_device):
+    mg, mc, fx = _pair(cuda_device)
+    x = torch.from_numpy(golden_inputs(fx))
+    yg = mg(x.to(cuda_device))
+    yc = mc(x)
+    assert yg.grad_fn is not None and "HardNetTrainFunction" in type(yg.grad_fn).__name__
+    assert (yg.detach().cpu() - yc.detach()).abs().max().item() <= 1e-4
+    for i in (1, 4, 7, 10, 13, 16, 20):
+        bg, bc = mg.features[i], mc.features[i]
+        assert _rel(bg.running_mean, bc.running_mean) <= 1e-5, i
+        assert _rel(bg.running_var, bc.running_var) <= 1e-5, i
+        assert int(bg.num_batches_tracked) == int(bc.num_batches_tracked) == 1
+
+
+@pytest.mark.parametrize("fresh", [True, False])
+def test_smooth_loss_gradients_vs_fp64(fresh, cuda_device):
+    """A smooth objective (a fixed projection of the descriptors) isolates the kernels'
+    arithmetic from the hardest-negative argmin: every weight gradient and the input gradient
+    against the module run in fp64, next to the torch-CPU fp32 error of the same module."""
+    mg, mc, fx = _pair(cuda_device, fresh=fresh)
+    md = _model64(fresh)
+    x = torch.from_numpy(golden_inputs(fx))
+    c = torch.randn(x.shape[0], 128, generator=torch.Generator().manual_seed(3))
+    xs = {"gpu": x.to(cuda_device).requires_grad_(True), "cpu32": x.clone().requires_grad_(True),
+          "cpu64": x.double().requires_grad_(True)}
+    mm = _fresh() if fresh else build_module("hardnet")[0]  # the torch layers on the GPU (MIOpen)
+    mm = mm.to(cuda_device).train()
+    mm.features[18].p = 0.0
+    mm.native_train = False
+    xs["miopen"] = x.to(cuda_device).requires_grad_(True)
+    torch.backends.cudnn.allow_tf32 = False
+    for key, m in (("gpu", mg), ("cpu32", mc), ("cpu64", md), ("miopen", mm)):
+        y = m(xs[key])
+        (y * c.to(y)).sum().backward()
+    for i in (0, 3, 6, 9, 12, 15, 19):
+        print(f"smooth fresh={fresh}: features.{i}.weight MIOpen fp32 rel err vs fp64 "
+              f"{_rel(mm.features[i].weight.grad, md.features[i].weight.grad):.2e}")
+    worst = 0.0
+    for i in (0, 3, 6, 9, 12, 15, 19):
+        gd = md.features[i].weight.grad
+        eg, ec = _rel(mg.features[i].weight.grad, gd), _rel(mc.features[i].weight.grad, gd)
+        print(f"smooth fresh={fresh}: features.{i}.weight grad rel err vs fp64: HIP {eg:.2e}, torch-CPU fp32 {ec:.2e}")
+        worst = max(worst, eg)
+    print(f"smooth: input grad rel err vs fp64: HIP {_rel(xs['gpu'].grad, xs['cpu64'].grad):.2e}, "
+          f"torch-CPU fp32 {_rel(xs['cpu32'].grad, xs['cpu64'].grad):.2e}")
+    for i in (0, 3, 6, 9, 12, 15, 19):
+        gd = md.features[i].weight.grad
+        e2 = _rel2(mg.features[i].weight.grad, gd)
+        print(f"smooth fresh={fresh}: features.{i}.weight grad L2-rel err vs fp64: HIP {e2:.2e}, "
+              f"torch-CPU fp32 {_rel2(mc.features[i].weight.grad, gd):.2e}, MIOpen {_rel2(mm.features[i].weight.grad, gd):.2e}")
+        assert e2 <= L2_BAR, i
+    assert _rel2(xs["gpu"].grad, xs["cpu64"].grad) <= L2_BAR
+
+
+@pytest.mark.parametrize("fresh", [True, False])
+@pytest.mark.parametrize("swap", [False, True])
+def test_loss_hardnet_gradients(swap, fresh, cuda_device):
+    """loss_HardNet (batch_reduce 'min', triplet margin, Losses.py:87-154) over anchor /
+    positive descriptors of 128 + 128 golden patches: weight and input gradients."""
+    mg, mc, fx = _pair(cuda_device, fresh=fresh)
+    md = _model64(fresh)
+    x = torch.from_numpy(golden_inputs(fx))
+    xg = x.to(cuda_device).requires_grad_(True)
+    xc = x.clone().requires_grad_(True)
+    xd = x.double().requires_grad_(True)
+    res = {}
+    for key, m, xx in (("gpu", mg, xg), ("cpu32", mc, xc), ("cpu64", md, xd)):
+        y = m(xx)
+        loss = O.loss_hardnet(y[:128], y[128:], anchor_swap=swap)
+        loss.backward()
+        res[key] = loss.item()
+    assert abs(res["gpu"] - res["cpu64"]) <= 1e-5
+    for i in (0, 3, 6, 9, 12, 15, 19):
+        gd = md.features[i].weight.grad
+        eg, ec = _rel(mg.features[i].weight.grad, gd), _rel(mc.features[i].weight.grad, gd)
+        print(f"loss swap={swap} fresh={fresh}: features.{i}.weight grad rel err vs fp64: HIP {eg:.2e}, "
+              f"torch-CPU fp32 {ec:.2e}")
+    for i in (0, 3, 6, 9, 12, 15, 19):  # the same bar as the smooth objective
+        gd = md.features[i].weight.grad
+        e2 = _rel2(mg.features[i].weight.grad, gd)
+        print(f"loss swap={swap} fresh={fresh}: features.{i}.weight grad L2-rel err vs fp64: HIP {e2:.2e}, "
+              f"torch-CPU fp32 {_rel2(mc.features[i].weight.grad, gd):.2e}")
+        assert e2 <= L2_BAR, i
+    assert _rel2(xg.grad, xd.grad) <= L2_BAR
+
+
+def test_sgd_steps_track_the_reference(cuda_device):
+    """Three optimizer steps of the reference training loop's shape (SGD with weight decay,
+    HardNet.py:507-513, 421-423) from the reference's own init on the HIP train path stay with
+    the CPU module (weights: L2-relative 1e-3)."""
+    mg, mc, fx = _pair(cuda_device, fresh=True)
+    og = torch.optim.SGD(mg.features.parameters(), lr=0.1, momentum=0.9, dampening=0.9, weight_decay=1e-4)
+    oc = torch.optim.SGD(mc.features.parameters(), lr=0.1, momentum=0.9, dampening=0.9, weight_decay=1e-4)
+    x = torch.from_numpy(golden_inputs(fx))
+    for step in range(3):
+        xs = x.roll(37 * step, 0)
+        for m, o, xx in ((mg, og, xs.to(cuda_device)), (mc, oc, xs)):
+            y = m(xx)
+            loss = O.loss_hardnet(y[:128], y[128:], anchor_swap=True)
+            o.zero_grad()
+            loss.backward()
+            o.step()
+    # the steps move the weights by lr x gradients that carry fp32's ~1e-3 (conv0) error
+    for i in (0, 3, 6, 9, 12, 15, 19):
+        assert _rel2(mg.features[i].weight, mc.features[i].weight) <= 1e-3, i
+    for i in (1, 4, 7, 10, 13, 16, 20):
+        assert _rel2(mg.features[i].running_var, mc.features[i].running_var) <= 1e-3, i
+
+
+def test_dropout_is_seeded_and_active(cuda_device):
+    mg, _, fx = _pair(cuda_device, dropout=0.3)
+    x = torch.from_numpy(golden_inputs(fx)).to(cuda_device)
+    torch.manual_seed(1)
+    y1 = mg(x)
+    torch.manual_seed(1)
+    y2 = mg(x)
+    torch.manual_seed(2)
+    y3 = mg(x)
+    assert torch.equal(y1, y2)
+    assert not torch.allclose(y1, y3)
+    assert torch.isfinite(y1).all() and ((y1.norm(dim=1) - 1).abs().max().item() < 1e-5)
+    y1.sum().backward()
+    assert all(torch.isfinite(mg.features[i].weight.grad).all() for i in (0, 3, 6, 9, 12, 15, 19))
+
+
+def test_train_step_at_reference_batch(cuda_device):
+    """batch 1024 (HardNet.py --batch-size default) forward + backward: finite, unit norm."""
+    from hardnetnas_amd import synth
+    mg, _, _ = _pair(cuda_device, dropout=0.3)
+    x = torch.from_numpy(synth.synth_patches(1024, seed=4)).to(cuda_device)
+    y = mg(x)
+    loss = O.loss_hardnet(y[:512], y[512:], anchor_swap=True)
+    loss.backward()
+    assert torch.isfinite(loss) and (y.norm(dim=1) - 1).abs().max().item() < 1e-5
+    assert all(torch.isfinite(mg.features[i].weight.grad).all() for i in (0, 3, 6, 9, 12, 15, 19))
