@@ -40,56 +40,95 @@ struct GemmArgs {
 
 // split-K: workgroup z of gridDim.z covers K range [z * kslice, (z + 1) * kslice) and writes
 // its partial tile to part[z] (M x N, row-major); k_splitk_sum adds the slices in fp64, so a
-// weight gradient's reduction over all B*H*W positions never runs as one fp32 chain
+// weight gradient's reduction over all B*H*W positions never runs as one fp32 chain.
+// Tiles: 64 (M) x 128 (N) per workgroup, 4 waves of 32 x 64 (two 32 x 32 f32 accumulators),
+// K stages of 32 double-buffered in LDS with the next stage's global loads in registers while
+// the current stage's MFMAs run (each operand is loaded along whichever index is contiguous).
+constexpr int GBM = 64, GBN = 128, GBK = 32;
 __global__ __launch_bounds__(256) void k_gemm(GemmArgs g, long kslice, float* __restrict__ part) {
-  __shared__ float sA[64][17];
-  __shared__ float sB[16][65];
+  __shared__ float sA[2][GBK][GBM + 4];   // [k][m]
+  __shared__ float sB[2][GBK][GBN + 4];   // [k][n]
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int wm = w >> 1, wn = w & 1, r = lane & 31, h = lane >> 5;
-  const long i0 = (long)blockIdx.y * 64, j0 = (long)blockIdx.x * 64;
+  const long i0 = (long)blockIdx.y * GBM, j0 = (long)blockIdx.x * GBN;
   const long kb = (long)blockIdx.z * kslice, ke = min(g.K, kb + kslice);
-  f32x16 acc{};
-  for (long k0 = kb; k0 < ke; k0 += 16) {
+  const bool a_k = g.sak == 1, b_n = g.sbj == 1;  // contiguous index of each operand
+  constexpr int AN = GBM * GBK / 256, BNN = GBK * GBN / 256;  // 8 / 16 elements per thread
+  float ra[AN], rb[BNN];
+  auto load = [&](long k0) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {  // A tile 64 x 16, B tile 16 x 64
+    for (int e = 0; e < AN; ++e) {
       const int idx = t + 256 * e;
-      {
-        const int ii = g.sak == 1 ? idx >> 4 : idx & 63, kk = g.sak == 1 ? idx & 15 : idx >> 6;
-        const long gi = i0 + ii, gk = k0 + kk;
-        sA[ii][kk] = (gi < g.M && gk < ke) ? g.A[gi * g.sai + gk * g.sak] : 0.f;
-      }
-      {
-        const int kk = g.sbj == 1 ? idx >> 6 : idx & 15, jj = g.sbj == 1 ? idx & 63 : idx >> 4;
-        const long gk = k0 + kk, gj = j0 + jj;
-        sB[kk][jj] = (gk < ke && gj < g.N) ? g.B[gk * g.sbk + gj * g.sbj] : 0.f;
-      }
+      const int mm = a_k ? idx / GBK : idx % GBM, kk = a_k ? idx % GBK : idx / GBM;
+      const long gi = i0 + mm, gk = k0 + kk;
+      ra[e] = (gi < g.M && gk < ke) ? g.A[gi * g.sai + gk * g.sak] : 0.f;
     }
-    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < BNN; ++e) {
+      const int idx = t + 256 * e;
+      const int kk = b_n ? idx / GBN : idx % GBK, nn = b_n ? idx % GBN : idx / GBK;
+      const long gk = k0 + kk, gj = j0 + nn;
+      rb[e] = (gk < ke && gj < g.N) ? g.B[gk * g.sbk + gj * g.sbj] : 0.f;
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int e = 0; e < AN; ++e) {
+      const int idx = t + 256 * e;
+      const int mm = a_k ? idx / GBK : idx % GBM, kk = a_k ? idx % GBK : idx / GBM;
+      sA[buf][kk][mm] = ra[e];
+    }
+#pragma unroll
+    for (int e = 0; e < BNN; ++e) {
+      const int idx = t + 256 * e;
+      const int kk = b_n ? idx / GBN : idx % GBK, nn = b_n ? idx % GBN : idx / GBK;
+      sB[buf][kk][nn] = rb[e];
+    }
+  };
+  f32x16 acc0{}, acc1{};
+  load(kb);
+  store(0);
+  __syncthreads();
+  int buf = 0;
+  for (long k0 = kb; k0 < ke; k0 += GBK) {
+    const bool more = k0 + GBK < ke;
+    if (more) load(k0 + GBK);
     // v_mfma_f32_32x32x2_f32: exact fp32 products (an fmaf chain per output, bitwise), so the
     // backward through train-mode BatchNorm -- whose 1/sigma amplifies rounding -- carries fp32
     // accuracy, as the reference's fp32 autograd does (bf16x3's 2^-16 products measured 3-10x
     // further from the fp64 gradients than torch-CPU fp32)
 #pragma unroll
-    for (int kk = 0; kk < 16; kk += 2)
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(sA[wm * 32 + r][kk + h], sB[kk + h][wn * 32 + r], acc, 0, 0, 0);
-    __syncthreads();
+    for (int kk = 0; kk < GBK; kk += 2) {
+      const float av = sA[buf][kk + h][wm * 32 + r];
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(av, sB[buf][kk + h][wn * 64 + r], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(av, sB[buf][kk + h][wn * 64 + 32 + r], acc1, 0, 0, 0);
+    }
+    if (more) {
+      store(buf ^ 1);
+      __syncthreads();
+      buf ^= 1;
+    }
   }
-  // acc[4q + e]: row 8q + 4h + e, column r of the wave's 32 x 32 tile
-  const long j = j0 + wn * 32 + r;
+  // acc[4q + e]: row 8q + 4h + e, column r of each 32 x 32 sub-tile
 #pragma unroll
-  for (int q = 0; q < 4; ++q)
+  for (int nt = 0; nt < 2; ++nt) {
+    const long j = j0 + wn * 64 + nt * 32 + r;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const long i = i0 + wm * 32 + 8 * q + 4 * h + e;
-      if (i < g.M && j < g.N) {
-        if (part) {
-          part[((long)blockIdx.z * g.M + i) * g.N + j] = acc[4 * q + e];
-        } else {
-          float* c = g.C + i * g.sci + j * g.scj;
-          *c = g.beta == 0.f ? g.alpha * acc[4 * q + e] : g.alpha * acc[4 * q + e] + g.beta * *c;
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const long i = i0 + wm * 32 + 8 * q + 4 * h + e;
+        const float v = nt ? acc1[4 * q + e] : acc0[4 * q + e];
+        if (i < g.M && j < g.N) {
+          if (part) {
+            part[((long)blockIdx.z * g.M + i) * g.N + j] = v;
+          } else {
+            float* c = g.C + i * g.sci + j * g.scj;
+            *c = g.beta == 0.f ? g.alpha * v : g.alpha * v + g.beta * *c;
+          }
         }
       }
-    }
+  }
 }
 
 __global__ __launch_bounds__(256) void k_splitk_sum(GemmArgs g, int S, const float* __restrict__ part) {
@@ -102,14 +141,14 @@ __global__ __launch_bounds__(256) void k_splitk_sum(GemmArgs g, int S, const flo
   *c = g.beta == 0.f ? (float)(g.alpha * s) : (float)(g.alpha * s + g.beta * (double)*c);
 }
 
-constexpr long kSplitK = 16;  // the smallest K per split-K slice (the workspace is sized for it)
+constexpr long kSplitK = 32;  // the smallest K per split-K slice (the workspace is sized for it)
 
 // part: scratch for M x N x ceil(K / kSplitK) floats when K > kSplitK (nullptr: one slice)
 hipError_t gemm(const GemmArgs& g, hipStream_t st, float* part = nullptr) {
   if (g.M <= 0 || g.N <= 0) return hipSuccess;
   const long ks = hn_knobs().train_splitk;  // K per slice (HN_TRAIN_SPLITK, default 4096)
   const int S = part && g.K > ks ? (int)((g.K + ks - 1) / ks) : 1;
-  const dim3 grid((unsigned)((g.N + 63) / 64), (unsigned)((g.M + 63) / 64), (unsigned)S);
+  const dim3 grid((unsigned)((g.N + GBN - 1) / GBN), (unsigned)((g.M + GBM - 1) / GBM), (unsigned)S);
   hipLaunchKernelGGL(k_gemm, grid, dim3(256), 0, st, g, S > 1 ? ks : g.K, S > 1 ? part : nullptr);
   if (S > 1) {
     hipError_t e = hipGetLastError();
@@ -191,70 +230,130 @@ __global__ __launch_bounds__(256) void k_col2im(const float* __restrict__ dcol, 
 }
 
 // ------------------------------------------------------------------------------------------
-// BatchNorm2d(affine=False) in train mode, one workgroup per channel over its row of L values
+// BatchNorm2d(affine=False) in train mode over CNHW rows of L values.  Statistics in two
+// stages so the whole GPU works on them: grid (C, NS) workgroups each reduce a slice of a
+// channel's row in fp64 (sum y, sum y^2 -- fp64 keeps E[y^2] - E[y]^2 exact enough), then one
+// thread per channel combines its NS partials in a fixed order (deterministic).
 // ------------------------------------------------------------------------------------------
-HN_DEV double block_sum(double v, double* sh) {
+HN_DEV void block_sum2(double& a, double& b, double* sh) {
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  for (int o = 32; o > 0; o >>= 1) {
+    a += __shfl_xor(a, o, 64);
+    b += __shfl_xor(b, o, 64);
+  }
   const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    sh[2 * w] = a;
+    sh[2 * w + 1] = b;
+  }
   __syncthreads();
-  if ((threadIdx.x & 63) == 0) sh[w] = v;
-  __syncthreads();
-  double s = 0.0;
-  for (int i = 0; i < (int)(blockDim.x >> 6); ++i) s += sh[i];
-  return s;
+  a = sh[0] + sh[2] + sh[4] + sh[6];
+  b = sh[1] + sh[3] + sh[5] + sh[7];
 }
 
-// y (in place) -> z = (y - mean) * rstd; running stats: (1 - m) r + m stat (var unbiased)
-__global__ __launch_bounds__(256) void k_bn_train(float* __restrict__ y, long L, float eps, float mom,
-                                                  float* __restrict__ rmean, float* __restrict__ rvar,
-                                                  float* __restrict__ rstd_out) {
-  __shared__ double sh[4];
-  const int c = blockIdx.x;
-  float* row = y + (long)c * L;
-  double s = 0.0;
-  for (long i = threadIdx.x; i < L; i += 256) s += row[i];
-  const double mean = block_sum(s, sh) / (double)L;
-  double q = 0.0;
-  for (long i = threadIdx.x; i < L; i += 256) {
-    const double d = row[i] - mean;
-    q += d * d;
+constexpr int kBnSlices = 64;  // partial-sum workgroups per channel (at most)
+int bn_slices(long C, long L) {
+  return (int)std::max<long>(1, std::min<long>(kBnSlices, std::min<long>((2048 + C - 1) / C, (L + 4095) / 4096)));
+}
+
+// forward stats: part[(c * NS + s) * 2 + {0, 1}] = sum y, sum y^2 over slice s of row c
+__global__ __launch_bounds__(256) void k_bn_part(const float* __restrict__ y, long L, int NS, double* __restrict__ part) {
+  __shared__ double sh[8];
+  const int c = blockIdx.x, sl = blockIdx.y;
+  const long per = (L + NS - 1) / NS, b = sl * per, e = min(L, b + per);
+  const float* row = y + (long)c * L;
+  double s1 = 0.0, s2 = 0.0;
+  for (long i = b + threadIdx.x; i < e; i += 256) {
+    const double v = row[i];
+    s1 += v;
+    s2 += v * v;
   }
-  const double var = block_sum(q, sh) / (double)L;
-  const float m = (float)mean, rs = (float)(1.0 / std::sqrt(var + (double)eps));
-  for (long i = threadIdx.x; i < L; i += 256) row[i] = (row[i] - m) * rs;
+  block_sum2(s1, s2, sh);
   if (threadIdx.x == 0) {
-    rstd_out[c] = rs;
-    if (rmean) {
-      rmean[c] = (1.f - mom) * rmean[c] + mom * m;
-      rvar[c] = (1.f - mom) * rvar[c] + mom * (float)(L > 1 ? var * (double)L / (double)(L - 1) : var);
-    }
+    part[((long)c * NS + sl) * 2] = s1;
+    part[((long)c * NS + sl) * 2 + 1] = s2;
   }
 }
 
-// backward through [dropout o] ReLU o BN(train): g = da * relu'(z) [* mask]; dy = rstd * (g -
-// mean(g) - z mean(g z)), in place in da (which becomes dY of the conv)
-__global__ __launch_bounds__(256) void k_bn_train_bwd(float* __restrict__ da, const float* __restrict__ z, long L,
-                                                      const float* __restrict__ rstd, int relu, float drop_p,
-                                                      unsigned long long seed) {
-  __shared__ double sh[4];
-  const int c = blockIdx.x;
-  float* g = da + (long)c * L;
-  const float* zr = z + (long)c * L;
+// one thread per channel: mean, 1/sqrt(var + eps), running statistics (var unbiased)
+__global__ __launch_bounds__(256) void k_bn_final(const double* __restrict__ part, int C, int NS, long L, float eps,
+                                                  float mom, float* __restrict__ rmean, float* __restrict__ rvar,
+                                                  float* __restrict__ mean_out, float* __restrict__ rstd_out) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  double s1 = 0.0, s2 = 0.0;
+  for (int sl = 0; sl < NS; ++sl) {
+    s1 += part[((long)c * NS + sl) * 2];
+    s2 += part[((long)c * NS + sl) * 2 + 1];
+  }
+  const double mean = s1 / (double)L;
+  const double var = fmax(s2 / (double)L - mean * mean, 0.0);
+  mean_out[c] = (float)mean;
+  rstd_out[c] = (float)(1.0 / sqrt(var + (double)eps));
+  if (rmean) {
+    rmean[c] = (1.f - mom) * rmean[c] + mom * (float)mean;
+    rvar[c] = (1.f - mom) * rvar[c] + mom * (float)(L > 1 ? var * (double)L / (double)(L - 1) : var);
+  }
+}
+
+// y (in place) -> z = (y - mean) * rstd over [C][L]
+__global__ __launch_bounds__(256) void k_bn_apply(float* __restrict__ y, long C, long L,
+                                                  const float* __restrict__ mean, const float* __restrict__ rstd) {
+  const long n = C * L;
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
+    const long c = e / L;
+    y[e] = (y[e] - mean[c]) * rstd[c];
+  }
+}
+
+// backward through [dropout o] ReLU o BN(train): g = da * relu'(z) [* mask] (written back), and
+// the slice sums of g and g z
+__global__ __launch_bounds__(256) void k_bn_bwd_part(float* __restrict__ da, const float* __restrict__ z, long L,
+                                                     int NS, int relu, float drop_p, unsigned long long seed,
+                                                     double* __restrict__ part) {
+  __shared__ double sh[8];
+  const int c = blockIdx.x, sl = blockIdx.y;
+  const long per = (L + NS - 1) / NS, b = sl * per, e = min(L, b + per);
   const long base = (long)c * L;
   double s1 = 0.0, s2 = 0.0;
-  for (long i = threadIdx.x; i < L; i += 256) {
-    float v = g[i];
-    if (relu && zr[i] <= 0.f) v = 0.f;
+  for (long i = b + threadIdx.x; i < e; i += 256) {
+    const float zv = z[base + i];
+    float v = da[base + i];
+    if (relu && zv <= 0.f) v = 0.f;
     if (drop_p > 0.f) v *= drop_scale(seed, (unsigned long long)(base + i), drop_p);
-    g[i] = v;
+    da[base + i] = v;
     s1 += v;
-    s2 += (double)v * zr[i];
+    s2 += (double)v * zv;
   }
-  const float m1 = (float)(block_sum(s1, sh) / (double)L);
-  const float m2 = (float)(block_sum(s2, sh) / (double)L);
-  const float rs = rstd[c];
-  for (long i = threadIdx.x; i < L; i += 256) g[i] = rs * (g[i] - m1 - zr[i] * m2);
+  block_sum2(s1, s2, sh);
+  if (threadIdx.x == 0) {
+    part[((long)c * NS + sl) * 2] = s1;
+    part[((long)c * NS + sl) * 2 + 1] = s2;
+  }
+}
+
+// one thread per channel: m1 = mean(g), m2 = mean(g z)
+__global__ __launch_bounds__(256) void k_bn_bwd_final(const double* __restrict__ part, int C, int NS, long L,
+                                                      float* __restrict__ m12) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  double s1 = 0.0, s2 = 0.0;
+  for (int sl = 0; sl < NS; ++sl) {
+    s1 += part[((long)c * NS + sl) * 2];
+    s2 += part[((long)c * NS + sl) * 2 + 1];
+  }
+  m12[2 * c] = (float)(s1 / (double)L);
+  m12[2 * c + 1] = (float)(s2 / (double)L);
+}
+
+// dy = rstd * (g - m1 - z m2), in place
+__global__ __launch_bounds__(256) void k_bn_bwd_apply(float* __restrict__ g, const float* __restrict__ z, long C, long L,
+                                                      const float* __restrict__ m12, const float* __restrict__ rstd) {
+  const long n = C * L;
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
+    const long c = e / L;
+    g[e] = rstd[c] * (g[e] - m12[2 * c] - z[e] * m12[2 * c + 1]);
+  }
 }
 
 // input_norm (HardNet.py:306-310, mean / std detached): one wave per patch; saves 1 / (std + eps)
@@ -365,6 +464,8 @@ HnTrainWs hn_train_layout(long B) {
     part = std::max(part, (size_t)L.cout * L.cin * L.ks * L.ks * ((kk + hn_knobs().train_splitk - 1) / hn_knobs().train_splitk) * 4);
   }
   w.part = take(part);
+  w.bnpart = take((size_t)128 * kBnSlices * 2 * sizeof(double));
+  w.bnmean = take((size_t)2 * 128 * sizeof(float));
   w.total = off;
   return w;
 }
@@ -402,9 +503,18 @@ hipError_t hn_train_forward(const float* in, long B, const float* const* W, floa
       GemmArgs g{W[l], col, z + n0 * hw, S.cout, n * hw, K, K, 1, n * hw, 1, B * hw, 1, 1.f, 0.f};
       HCK(gemm(g, st));
     }
-    hipLaunchKernelGGL(k_bn_train, dim3(S.cout), dim3(256), 0, st, z, B * hw, bn_eps, mom, rmean ? rmean[l] : nullptr,
-                       rvar ? rvar[l] : nullptr, reinterpret_cast<float*>(ws + L.rstd[l]));
-    HCK(hipGetLastError());
+    {
+      const int NS = bn_slices(S.cout, B * hw);
+      double* part = reinterpret_cast<double*>(ws + L.bnpart);
+      float* mean = reinterpret_cast<float*>(ws + L.bnmean);
+      float* rstd = reinterpret_cast<float*>(ws + L.rstd[l]);
+      hipLaunchKernelGGL(k_bn_part, dim3(S.cout, NS), dim3(256), 0, st, z, B * hw, NS, part);
+      hipLaunchKernelGGL(k_bn_final, dim3((S.cout + 255) / 256), dim3(256), 0, st, part, S.cout, NS, B * hw, bn_eps,
+                         mom, rmean ? rmean[l] : nullptr, rvar ? rvar[l] : nullptr, mean, rstd);
+      hipLaunchKernelGGL(k_bn_apply, dim3(grid_for(S.cout * B * hw)), dim3(256), 0, st, z, (long)S.cout, B * hw,
+                         mean, rstd);
+      HCK(hipGetLastError());
+    }
   }
   hipLaunchKernelGGL(k_l2_fwd, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st,
                      reinterpret_cast<const float*>(ws + L.z[6]), B, l2_eps, out);
@@ -426,10 +536,18 @@ hipError_t hn_train_backward(const float* dout, long B, const float* const* W, f
   for (int l = 6; l >= 0; --l) {
     const HnTrainLayer& S = kHardnetTrainLayers[l];
     const long ho = hout_of(S), hw = ho * ho, K = (long)S.cin * S.ks * S.ks;
-    hipLaunchKernelGGL(k_bn_train_bwd, dim3(S.cout), dim3(256), 0, st, g, reinterpret_cast<const float*>(ws + L.z[l]),
-                       B * hw, reinterpret_cast<const float*>(ws + L.rstd[l]), l < 6 ? 1 : 0,
-                       l == 5 ? drop_p : 0.f, seed);
-    HCK(hipGetLastError());
+    {
+      const int NS = bn_slices(S.cout, B * hw);
+      double* part = reinterpret_cast<double*>(ws + L.bnpart);
+      float* m12 = reinterpret_cast<float*>(ws + L.bnmean);
+      const float* zl = reinterpret_cast<const float*>(ws + L.z[l]);
+      hipLaunchKernelGGL(k_bn_bwd_part, dim3(S.cout, NS), dim3(256), 0, st, g, zl, B * hw, NS, l < 6 ? 1 : 0,
+                         l == 5 ? drop_p : 0.f, seed, part);
+      hipLaunchKernelGGL(k_bn_bwd_final, dim3((S.cout + 255) / 256), dim3(256), 0, st, part, S.cout, NS, B * hw, m12);
+      hipLaunchKernelGGL(k_bn_bwd_apply, dim3(grid_for(S.cout * B * hw)), dim3(256), 0, st, g, zl, (long)S.cout,
+                         B * hw, m12, reinterpret_cast<const float*>(ws + L.rstd[l]));
+      HCK(hipGetLastError());
+    }
     const ActIn a{l == 0 ? xn : reinterpret_cast<const float*>(ws + L.z[l - 1]), l > 0 ? 1 : 0,
                   l == 6 ? drop_p : 0.f, seed};
     float* gin = gbuf[(7 - l) & 1];  // gradient w.r.t. this layer's input activation
