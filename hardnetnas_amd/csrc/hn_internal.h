@@ -133,7 +133,7 @@ struct HnTrainLayer {
 };
 extern const HnTrainLayer kHardnetTrainLayers[7];
 struct HnTrainWs {  // byte offsets into the train workspace
-  size_t xn, inv_sd, z[7], rstd[7], g0, g1, col, part, bnpart, bnmean, total;
+  size_t xn, inv_sd, z[7], rstd[7], g0, g1, col, part, bnpart, bnmean, wt, total;
 };
 HnTrainWs hn_train_layout(long B);
 hipError_t hn_train_forward(const float* in, long B, const float* const* W, float* const* rmean, float* const* rvar,

@@ -4,17 +4,18 @@
 // (hardnet/HardNet.py:379-441 over the module of :275-315).
 //
 // Layout: activations are kept channel-major across the whole batch, CNHW ([C][B][H][W]), so
-//   * each conv is ONE plain GEMM per chunk of patches over an im2col matrix col [K][n*Ho*Wo]
-//     (K = Cin*k*k):  forward  Y  [Cout][nHW] = W [Cout][K] . col,
-//                     wgrad    dW [Cout][K]  += dY [Cout][nHW] . col^T,
-//                     dgrad    dcol [K][nHW]  = W^T . dY, then col2im (gather, no atomics);
+//   * each conv is ONE implicit GEMM over the whole batch, its column matrix never stored (the
+//     B-operand loader computes the im2col / col2im addresses; K = Cin*k*k):
+//                     forward  Y  [Cout][BHW]  = W [Cout][K] . col,
+//                     wgrad    dW [Cout][K]    = dY [Cout][BHW] . col^T  (split-K, fp64 sums),
+//                     dgrad    dX [Cin][BHinWin] = Wt [Cin][Cout k k] . gather(dY);
 //   * BatchNorm's per-channel batch statistics are reductions over one contiguous row.
 // GEMMs run on the f32 MFMA (exact fp32 products, fp64 sums across split-K slices).
 // Saved for the backward (the workspace the caller keeps between the calls): the normalised
 // pre-ReLU output z of every BN layer, its 1/sqrt(var + eps), the normalised input and the
 // per-patch input std.  The next layer's input relu(z) (x mask / (1 - p) after the dropout) is
-// formed on the fly in im2col; the dropout mask is a counter hash of (seed, element), so the
-// backward recomputes it instead of storing it.
+// formed on the fly in the im2col loader; the dropout mask is a counter hash of (seed, element),
+// so the backward recomputes it instead of storing it.
 #include "hn_common.h"
 #include "hn_internal.h"
 
@@ -29,6 +30,34 @@ namespace {
 // workgroup tiles (4 waves of 32x32, v_mfma_f32_32x32x2_f32), K steps of 16 staged through LDS
 // as fp32 (bounds-checked, zero-filled).
 // ------------------------------------------------------------------------------------------
+// ------------------------------------------------------------------------------------------
+// counter-hash dropout mask (keep with probability 1 - p), recomputed in the backward
+// ------------------------------------------------------------------------------------------
+HN_DEV float drop_scale(unsigned long long seed, unsigned long long e, float p) {
+  unsigned long long x = seed ^ (e * 0x9E3779B97F4A7C15ull);
+  x ^= x >> 30;
+  x *= 0xBF58476D1CE4E5B9ull;
+  x ^= x >> 27;
+  x *= 0x94D049BB133111EBull;
+  x ^= x >> 31;
+  const float u = (float)(x >> 40) * (1.0f / 16777216.0f);  // [0, 1)
+  return u < p ? 0.f : 1.f / (1.f - p);
+}
+
+// the input of the next layer from a saved BN output: relu(z) [x dropout]
+struct ActIn {
+  const float* z;  // CNHW
+  int relu;
+  float drop_p;    // 0: no dropout
+  unsigned long long seed;
+};
+HN_DEV float act_at(const ActIn& a, long idx) {
+  float v = a.z[idx];
+  if (a.relu) v = fmaxf(v, 0.f);
+  if (a.drop_p > 0.f) v *= drop_scale(a.seed, (unsigned long long)idx, a.drop_p);
+  return v;
+}
+
 struct GemmArgs {
   const float* A;
   const float* B;
@@ -44,12 +73,66 @@ struct GemmArgs {
 // Tiles: 64 (M) x 128 (N) per workgroup, 4 waves of 32 x 64 (two 32 x 32 f32 accumulators),
 // K stages of 32 double-buffered in LDS with the next stage's global loads in registers while
 // the current stage's MFMAs run (each operand is loaded along whichever index is contiguous).
-constexpr int GBM = 64, GBN = 128, GBK = 32;
-__global__ __launch_bounds__(256) void k_gemm(GemmArgs g, long kslice, float* __restrict__ part) {
+constexpr int GBM = 64, GBN = 128, GBK = 32;  // (GBM: the largest M tile)
+
+// B operand loaders: plain strided memory, or an implicit im2col of a saved BN output
+// (relu(z) [x dropout]) for a 3x3 / 8x8 conv layer with compile-time geometry, so the forward
+// and the weight gradient never materialise the column matrix:
+//   Im2col<..., false>: B(k, j) = col(kconv = k, pos = j)   (forward, N = B Ho Wo)
+//   Im2col<..., true> : B(k, j) = col(kconv = j, pos = k)   (wgrad,  K = B Ho Wo)
+struct StridedB {
+  HN_DEV float at(const GemmArgs& g, long k, long j) const { return g.B[k * g.sbk + j * g.sbj]; }
+};
+template <int C, int H, int KS, int S, int PAD, bool T>
+struct Im2colB {
+  static constexpr int HO = (H + 2 * PAD - KS) / S + 1, HWO = HO * HO, KK = KS * KS;
+  ActIn a;
+  long B;  // batch (CNHW channel stride = B * H * H)
+  HN_DEV float at(const GemmArgs&, long k, long j) const {
+    const long kc = T ? j : k, pos = T ? k : j;
+    const int c = (int)(kc / KK), tap = (int)(kc % KK), dy = tap / KS, dx = tap % KS;
+    const long p = pos / HWO;
+    const int o = (int)(pos % HWO), oy = o / HO, ox = o % HO;
+    const int y = oy * S - PAD + dy, x = ox * S - PAD + dx;
+    return (y >= 0 && y < H && x >= 0 && x < H) ? act_at(a, ((long)c * B + p) * (H * H) + y * H + x) : 0.f;
+  }
+};
+
+// dgrad as an implicit GEMM (no column matrix, no col2im): dX[c][pos_in] = sum over (co, tap) of
+// Wt[c][co][tap] . dY[co][pos_out(pos_in, tap)], the entry zero where the tap does not land on a
+// stride-S output; B(k = co * KS^2 + tap, j = pos_in), contiguous along j
+template <int COUT, int H, int KS, int S, int PAD>
+struct Col2imB {
+  static constexpr int HO = (H + 2 * PAD - KS) / S + 1, HWO = HO * HO, KK = KS * KS;
+  const float* dY;  // [COUT][B][HO][HO]
+  long B;
+  HN_DEV float at(const GemmArgs&, long k, long j) const {
+    const int co = (int)(k / KK), tap = (int)(k % KK), dy = tap / KS, dx = tap % KS;
+    const long p = j / (H * H);
+    const int q = (int)(j % (H * H)), y = q / H, x = q % H;
+    const int ty = y + PAD - dy, tx = x + PAD - dx;
+    if (ty < 0 || tx < 0 || ty % S || tx % S) return 0.f;
+    const int oy = ty / S, ox = tx / S;
+    return (oy < HO && ox < HO) ? dY[((long)co * B + p) * HWO + oy * HO + ox] : 0.f;
+  }
+};
+
+// Wt[c][co][tap] = W[co][c][tap]
+__global__ __launch_bounds__(256) void k_wt(const float* __restrict__ w, int cout, int cin, int kk, float* __restrict__ wt) {
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (long)cout * cin * kk) return;
+  const int tap = (int)(e % kk), c = (int)((e / kk) % cin), co = (int)(e / ((long)kk * cin));
+  wt[((long)c * cout + co) * kk + tap] = w[e];
+}
+
+// BM = 64: 2 x 2 waves of 32 x 64; BM = 32 (the 32-output-channel layers): 1 x 4 waves of 32 x 32
+template <int BM, class BL>
+__global__ __launch_bounds__(256) void k_gemm(GemmArgs g, BL bl, long kslice, float* __restrict__ part) {
+  constexpr int GBM = BM, WN = BM == 64 ? 64 : 32;  // M rows per workgroup, N columns per wave
   __shared__ float sA[2][GBK][GBM + 4];   // [k][m]
   __shared__ float sB[2][GBK][GBN + 4];   // [k][n]
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int wm = w >> 1, wn = w & 1, r = lane & 31, h = lane >> 5;
+  const int wm = BM == 64 ? w >> 1 : 0, wn = BM == 64 ? w & 1 : w, r = lane & 31, h = lane >> 5;
   const long i0 = (long)blockIdx.y * GBM, j0 = (long)blockIdx.x * GBN;
   const long kb = (long)blockIdx.z * kslice, ke = min(g.K, kb + kslice);
   const bool a_k = g.sak == 1, b_n = g.sbj == 1;  // contiguous index of each operand
@@ -68,7 +151,7 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g, long kslice, float* __
       const int idx = t + 256 * e;
       const int kk = b_n ? idx / GBN : idx % GBK, nn = b_n ? idx % GBN : idx / GBK;
       const long gk = k0 + kk, gj = j0 + nn;
-      rb[e] = (gk < ke && gj < g.N) ? g.B[gk * g.sbk + gj * g.sbj] : 0.f;
+      rb[e] = (gk < ke && gj < g.N) ? bl.at(g, gk, gj) : 0.f;
     }
   };
   auto store = [&](int buf) {
@@ -100,8 +183,9 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g, long kslice, float* __
 #pragma unroll
     for (int kk = 0; kk < GBK; kk += 2) {
       const float av = sA[buf][kk + h][wm * 32 + r];
-      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(av, sB[buf][kk + h][wn * 64 + r], acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(av, sB[buf][kk + h][wn * 64 + 32 + r], acc1, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(av, sB[buf][kk + h][wn * WN + r], acc0, 0, 0, 0);
+      if constexpr (BM == 64)
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(av, sB[buf][kk + h][wn * WN + 32 + r], acc1, 0, 0, 0);
     }
     if (more) {
       store(buf ^ 1);
@@ -111,8 +195,8 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g, long kslice, float* __
   }
   // acc[4q + e]: row 8q + 4h + e, column r of each 32 x 32 sub-tile
 #pragma unroll
-  for (int nt = 0; nt < 2; ++nt) {
-    const long j = j0 + wn * 64 + nt * 32 + r;
+  for (int nt = 0; nt < (BM == 64 ? 2 : 1); ++nt) {
+    const long j = j0 + wn * WN + nt * 32 + r;
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
@@ -141,15 +225,26 @@ __global__ __launch_bounds__(256) void k_splitk_sum(GemmArgs g, int S, const flo
   *c = g.beta == 0.f ? (float)(g.alpha * s) : (float)(g.alpha * s + g.beta * (double)*c);
 }
 
-constexpr long kSplitK = 32;  // the smallest K per split-K slice (the workspace is sized for it)
 
-// part: scratch for M x N x ceil(K / kSplitK) floats when K > kSplitK (nullptr: one slice)
-hipError_t gemm(const GemmArgs& g, hipStream_t st, float* part = nullptr) {
+// part: scratch for the split-K partials, M x N x slices floats (nullptr: one slice).
+// The B loader's contiguous index: StridedB reads g.sbj to decide; Im2colB<.., T> is
+// contiguous along pos (N for the forward, K for the wgrad) -- set in g.sbj / g.sbk.
+template <class BL = StridedB>
+hipError_t gemm(const GemmArgs& g, hipStream_t st, float* part = nullptr, BL bl = BL{}) {
   if (g.M <= 0 || g.N <= 0) return hipSuccess;
-  const long ks = hn_knobs().train_splitk;  // K per slice (HN_TRAIN_SPLITK, default 4096)
+  const int bm = g.M <= 32 ? 32 : 64;
+  const long tiles = ((g.N + GBN - 1) / GBN) * ((g.M + bm - 1) / bm);
+  long ks = hn_knobs().train_splitk;  // K per slice (HN_TRAIN_SPLITK, default 4096)
+  if (part && tiles < 256 && g.K > 64) {  // a small grid: split K until every CU has a workgroup
+    const long want = std::min<long>((256 + tiles - 1) / tiles, (g.K + 63) / 64);
+    ks = std::min(ks, ((g.K + want - 1) / want + GBK - 1) / GBK * GBK);
+  }
   const int S = part && g.K > ks ? (int)((g.K + ks - 1) / ks) : 1;
-  const dim3 grid((unsigned)((g.N + GBN - 1) / GBN), (unsigned)((g.M + GBM - 1) / GBM), (unsigned)S);
-  hipLaunchKernelGGL(k_gemm, grid, dim3(256), 0, st, g, S > 1 ? ks : g.K, S > 1 ? part : nullptr);
+  const dim3 grid((unsigned)((g.N + GBN - 1) / GBN), (unsigned)((g.M + bm - 1) / bm), (unsigned)S);
+  if (bm == 32)
+    hipLaunchKernelGGL((k_gemm<32, BL>), grid, dim3(256), 0, st, g, bl, S > 1 ? ks : g.K, S > 1 ? part : nullptr);
+  else
+    hipLaunchKernelGGL((k_gemm<64, BL>), grid, dim3(256), 0, st, g, bl, S > 1 ? ks : g.K, S > 1 ? part : nullptr);
   if (S > 1) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
@@ -158,50 +253,8 @@ hipError_t gemm(const GemmArgs& g, hipStream_t st, float* part = nullptr) {
   return hipGetLastError();
 }
 
-// ------------------------------------------------------------------------------------------
-// counter-hash dropout mask (keep with probability 1 - p), recomputed in the backward
-// ------------------------------------------------------------------------------------------
-HN_DEV float drop_scale(unsigned long long seed, unsigned long long e, float p) {
-  unsigned long long x = seed ^ (e * 0x9E3779B97F4A7C15ull);
-  x ^= x >> 30;
-  x *= 0xBF58476D1CE4E5B9ull;
-  x ^= x >> 27;
-  x *= 0x94D049BB133111EBull;
-  x ^= x >> 31;
-  const float u = (float)(x >> 40) * (1.0f / 16777216.0f);  // [0, 1)
-  return u < p ? 0.f : 1.f / (1.f - p);
-}
-
-// the input of the next layer from a saved BN output: relu(z) [x dropout]
-struct ActIn {
-  const float* z;  // CNHW
-  int relu;
-  float drop_p;    // 0: no dropout
-  unsigned long long seed;
-};
-HN_DEV float act_at(const ActIn& a, long idx) {
-  float v = a.z[idx];
-  if (a.relu) v = fmaxf(v, 0.f);
-  if (a.drop_p > 0.f) v *= drop_scale(a.seed, (unsigned long long)idx, a.drop_p);
-  return v;
-}
-
-// im2col for patches [n0, n0 + n) of a CNHW activation [C][B][H][W]: col [C*KS*KS][n*Ho*Wo]
-__global__ __launch_bounds__(256) void k_im2col(ActIn a, int C, long B, int H, int W, int KS, int S, int PAD,
-                                                int Ho, int Wo, long n0, long n, float* __restrict__ col) {
-  const long cols = n * Ho * Wo;
-  const long total = (long)C * KS * KS * cols;
-  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
-    const long k = e / cols, q = e % cols;
-    const int c = (int)(k / (KS * KS)), tap = (int)(k % (KS * KS)), dy = tap / KS, dx = tap % KS;
-    const long p = q / (Ho * Wo);
-    const int o = (int)(q % (Ho * Wo)), oy = o / Wo, ox = o % Wo;
-    const int y = oy * S - PAD + dy, x = ox * S - PAD + dx;
-    col[e] = (y >= 0 && y < H && x >= 0 && x < W) ? act_at(a, (((long)c * B + n0 + p) * H + y) * W + x) : 0.f;
-  }
-}
-
-// col2im (gather): d_in [C][B][H][W] patches [n0, n0 + n) = sum of the dcol entries that read them
+// col2im (gather) for the strided / 8x8 dgrads: d_in [C][B][H][W] patches [n0, n0 + n) = sum of the
+// dcol [C*KS*KS][n*Ho*Wo] entries that read them
 __global__ __launch_bounds__(256) void k_col2im(const float* __restrict__ dcol, int C, long B, int H, int W, int KS,
                                                 int S, int PAD, int Ho, int Wo, long n0, long n,
                                                 float* __restrict__ din) {
@@ -411,6 +464,66 @@ __global__ __launch_bounds__(256) void k_l2_bwd(const float* __restrict__ z, con
 
 unsigned grid_for(long n) { return (unsigned)std::min<long>((n + 255) / 256, 65536); }
 
+// implicit-im2col convs of one layer (compile-time geometry): the forward Y = W . col and the
+// weight gradient dW = dY . col^T over the whole batch, with no column matrix in memory
+template <int C, int H, int KS, int S, int PAD>
+hipError_t conv_fwd(const ActIn& a, long B, const float* W, int cout, float* z, float* part, hipStream_t st) {
+  using L = Im2colB<C, H, KS, S, PAD, false>;
+  const long n = B * L::HWO, K = (long)C * KS * KS;
+  GemmArgs g{W, nullptr, z, cout, n, K, K, 1, 2, 1, n, 1, 1.f, 0.f};  // B contiguous along N
+  return gemm(g, st, part, L{a, B});
+}
+// dX [C][B H H] = Wt [C][COUT KK] . col2im-gather(dY), Wt transposed into `wt` first
+template <int C, int H, int KS, int S, int PAD>
+hipError_t conv_dgrad(const float* dY, long B, const float* W, int cout, float* wt, float* dX, hipStream_t st) {
+  constexpr int KK = KS * KS;
+  const long nw = (long)cout * C * KK;
+  hipLaunchKernelGGL(k_wt, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, st, W, cout, C, KK, wt);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const long n = B * H * H, K = (long)cout * KK;
+  GemmArgs g{wt, nullptr, dX, C, n, K, K, 1, 2, 1, n, 1, 1.f, 0.f};
+  if (cout == 32)
+    return gemm(g, st, nullptr, Col2imB<32, H, KS, S, PAD>{dY, B});
+  if (cout == 64)
+    return gemm(g, st, nullptr, Col2imB<64, H, KS, S, PAD>{dY, B});
+  return gemm(g, st, nullptr, Col2imB<128, H, KS, S, PAD>{dY, B});
+}
+template <int C, int H, int KS, int S, int PAD>
+hipError_t conv_wgrad(const ActIn& a, long B, const float* dY, int cout, float* dW, float* part, hipStream_t st) {
+  using L = Im2colB<C, H, KS, S, PAD, true>;
+  const long n = B * L::HWO, K = (long)C * KS * KS;
+  GemmArgs g{dY, nullptr, dW, cout, K, n, n, 1, 1, 2, K, 1, 1.f, 0.f};  // B contiguous along K (= pos)
+  return gemm(g, st, part, L{a, B});
+}
+#define HN_TRAIN_LAYERS(X) \
+  X(0, 1, 32, 3, 1, 1) X(1, 32, 32, 3, 1, 1) X(2, 32, 32, 3, 2, 1) X(3, 64, 16, 3, 1, 1) X(4, 64, 16, 3, 2, 1) \
+  X(5, 128, 8, 3, 1, 1) X(6, 128, 8, 8, 1, 0)
+hipError_t conv_fwd_l(int l, const ActIn& a, long B, const float* W, int cout, float* z, float* part,
+                      hipStream_t st) {
+#define HN_F(L_, C, H, KS, S, PAD) \
+  if (l == L_) return conv_fwd<C, H, KS, S, PAD>(a, B, W, cout, z, part, st);
+  HN_TRAIN_LAYERS(HN_F)
+#undef HN_F
+  return hipErrorInvalidValue;
+}
+hipError_t conv_wgrad_l(int l, const ActIn& a, long B, const float* dY, int cout, float* dW, float* part,
+                        hipStream_t st) {
+#define HN_W(L_, C, H, KS, S, PAD) \
+  if (l == L_) return conv_wgrad<C, H, KS, S, PAD>(a, B, dY, cout, dW, part, st);
+  HN_TRAIN_LAYERS(HN_W)
+#undef HN_W
+  return hipErrorInvalidValue;
+}
+hipError_t conv_dgrad_l(int l, const float* dY, long B, const float* W, int cout, float* wt, float* dX,
+                        hipStream_t st) {
+#define HN_D(L_, C, H, KS, S, PAD) \
+  if (l == L_) return conv_dgrad<C, H, KS, S, PAD>(dY, B, W, cout, wt, dX, st);
+  HN_TRAIN_LAYERS(HN_D)
+#undef HN_D
+  return hipErrorInvalidValue;
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------------------------------
@@ -423,7 +536,7 @@ const HnTrainLayer kHardnetTrainLayers[7] = {
 
 static long hout_of(const HnTrainLayer& l) { return (l.hin + 2 * l.pad - l.ks) / l.s + 1; }
 
-// patches per im2col chunk: col = K x (n Ho Wo) floats within kColBudget
+// patches per dgrad column chunk: col = K x (n Ho Wo) floats within kColBudget
 static constexpr size_t kColBudget = (size_t)256 << 20;
 static long chunk_of(const HnTrainLayer& l, long B) {
   const long ho = hout_of(l);
@@ -450,21 +563,24 @@ HnTrainWs hn_train_layout(long B) {
   }
   w.g0 = take(maxact * 4);
   w.g1 = take(maxact * 4);
-  size_t col = 0;
+  size_t col = 0;  // the strided / 8x8 dgrads' column chunk
   for (int l = 0; l < 7; ++l) {
     const HnTrainLayer& L = kHardnetTrainLayers[l];
+    if (L.s == 1 && L.ks == 3) continue;
     const long ho = hout_of(L);
     col = std::max(col, (size_t)L.cin * L.ks * L.ks * chunk_of(L, B) * ho * ho * 4);
   }
   w.col = take(col);
-  size_t part = 0;  // split-K partials of the weight gradients
+  size_t part = 0;  // split-K partials of the weight gradients (one GEMM over the whole batch)
   for (int l = 0; l < 7; ++l) {
     const HnTrainLayer& L = kHardnetTrainLayers[l];
-    const long ho = hout_of(L), kk = chunk_of(L, B) * ho * ho;
+    const long ho = hout_of(L), kk = B * ho * ho;
     part = std::max(part, (size_t)L.cout * L.cin * L.ks * L.ks * ((kk + hn_knobs().train_splitk - 1) / hn_knobs().train_splitk) * 4);
   }
+  part = std::max(part, (size_t)512 * GBM * GBN * 4);  // small-grid forward splits (S <= ceil(256 / tiles))
   w.part = take(part);
   w.bnpart = take((size_t)128 * kBnSlices * 2 * sizeof(double));
+  w.wt = take((size_t)128 * 128 * 64 * sizeof(float));  // a transposed weight (conv6 is the largest)
   w.bnmean = take((size_t)2 * 128 * sizeof(float));
   w.total = off;
   return w;
@@ -481,28 +597,18 @@ hipError_t hn_train_forward(const float* in, long B, const float* const* W, floa
                             unsigned long long seed, float* out, char* ws, hipStream_t st) {
   const HnTrainWs L = hn_train_layout(B);
   float* xn = reinterpret_cast<float*>(ws + L.xn);
-  float* col = reinterpret_cast<float*>(ws + L.col);
   hipLaunchKernelGGL(k_input_norm, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, in, B, in_eps, xn,
                      reinterpret_cast<float*>(ws + L.inv_sd));
   HCK(hipGetLastError());
   for (int l = 0; l < 7; ++l) {
     const HnTrainLayer& S = kHardnetTrainLayers[l];
-    const long ho = hout_of(S), hw = ho * ho, K = (long)S.cin * S.ks * S.ks;
+    const long ho = hout_of(S), hw = ho * ho;
     // this layer's input: the normalised patch, or relu(z) of the previous layer (x the dropout
     // mask before conv6, HardNet.py:299)
     const ActIn a{l == 0 ? xn : reinterpret_cast<const float*>(ws + L.z[l - 1]), l > 0 ? 1 : 0,
                   l == 6 ? drop_p : 0.f, seed};
     float* z = reinterpret_cast<float*>(ws + L.z[l]);
-    const long nc = chunk_of(S, B);
-    for (long n0 = 0; n0 < B; n0 += nc) {
-      const long n = std::min(nc, B - n0);
-      hipLaunchKernelGGL(k_im2col, dim3(grid_for(K * n * hw)), dim3(256), 0, st, a, S.cin, B, S.hin, S.hin,
-                         S.ks, S.s, S.pad, (int)ho, (int)ho, n0, n, col);
-      HCK(hipGetLastError());
-      // Y[Cout][n0 .. n0 + n) = W [Cout][K] . col [K][n hw]
-      GemmArgs g{W[l], col, z + n0 * hw, S.cout, n * hw, K, K, 1, n * hw, 1, B * hw, 1, 1.f, 0.f};
-      HCK(gemm(g, st));
-    }
+    HCK(conv_fwd_l(l, a, B, W[l], S.cout, z, reinterpret_cast<float*>(ws + L.part), st));  // Y = W . im2col(a)
     {
       const int NS = bn_slices(S.cout, B * hw);
       double* part = reinterpret_cast<double*>(ws + L.bnpart);
@@ -525,7 +631,6 @@ hipError_t hn_train_backward(const float* dout, long B, const float* const* W, f
                              float l2_eps, float drop_p, unsigned long long seed, char* ws, hipStream_t st) {
   const HnTrainWs L = hn_train_layout(B);
   const float* xn = reinterpret_cast<const float*>(ws + L.xn);
-  float* col = reinterpret_cast<float*>(ws + L.col);
   float* gbuf[2] = {reinterpret_cast<float*>(ws + L.g0), reinterpret_cast<float*>(ws + L.g1)};
   // g: gradient w.r.t. layer l's output activation a_l (a_6 = z_6 into the L2 norm; a_5 =
   // dropout(relu(z_5)); a_l = relu(z_l) below), then in place w.r.t. its conv output
@@ -552,17 +657,18 @@ hipError_t hn_train_backward(const float* dout, long B, const float* const* W, f
                   l == 6 ? drop_p : 0.f, seed};
     float* gin = gbuf[(7 - l) & 1];  // gradient w.r.t. this layer's input activation
     const bool want_in = l > 0 || din;
-    const long nc = chunk_of(S, B);
-    for (long n0 = 0; n0 < B; n0 += nc) {
-      const long n = std::min(nc, B - n0);
-      hipLaunchKernelGGL(k_im2col, dim3(grid_for(K * n * hw)), dim3(256), 0, st, a, S.cin, B, S.hin, S.hin,
-                         S.ks, S.s, S.pad, (int)ho, (int)ho, n0, n, col);
-      HCK(hipGetLastError());
-      // dW [Cout][K] (+)= dY [Cout][n hw] . col^T
-      GemmArgs gw{g + n0 * hw, col, dW[l], S.cout, K, n * hw, B * hw, 1, 1, n * hw, K, 1, 1.f, n0 == 0 ? 0.f : 1.f};
-      HCK(gemm(gw, st, reinterpret_cast<float*>(ws + L.part)));
-      if (want_in) {
-        // dcol [K][n hw] = W^T [K][Cout] . dY [Cout][n hw]  (into col: its im2col is consumed)
+    // dW [Cout][K] = dY [Cout][B hw] . im2col(a)^T (split-K slices summed in fp64)
+    HCK(conv_wgrad_l(l, a, B, g, S.cout, dW[l], reinterpret_cast<float*>(ws + L.part), st));
+    if (want_in && S.s == 1 && S.ks == 3) {
+      // stride-1 3x3: d a_{l-1} [Cin][B H H] = implicit col2im-gather GEMM Wt . dY (every tap lands)
+      HCK(conv_dgrad_l(l, g, B, W[l], S.cout, reinterpret_cast<float*>(ws + L.wt), gin, st));
+    } else if (want_in) {
+      // stride 2 (3 of 4 taps miss a given input pixel) and the 8x8 conv6 (one tap per pixel):
+      // dcol [K][n hw] = W^T [K][Cout] . dY, then the gather col2im, in chunks of patches
+      float* col = reinterpret_cast<float*>(ws + L.col);
+      const long nc = chunk_of(S, B);
+      for (long n0 = 0; n0 < B; n0 += nc) {
+        const long n = std::min(nc, B - n0);
         GemmArgs gd{W[l], g + n0 * hw, col, K, n * hw, S.cout, 1, K, B * hw, 1, n * hw, 1, 1.f, 0.f};
         HCK(gemm(gd, st));
         hipLaunchKernelGGL(k_col2im, dim3(grid_for((long)S.cin * n * S.hin * S.hin)), dim3(256), 0, st, col,
