@@ -466,6 +466,33 @@ static std::vector<uint16_t> pack_c12(const std::vector<float>& w, int cout) {
   return a;
 }
 
+// stride-1 3x3 conv (BN folded) as Winograd F(2x2,3x3) U = G g G^T (fp64, then bf16 hi/lo),
+// packed as the B operand of hn_wino.hip's 32x32x16 MFMAs: [cout/32][cin/16][xi 16][plane][lane
+// 64][8], lane (column l & 31 -> output channel, k-group l >> 5 -> input channels 8 (l >> 5) + j)
+static std::vector<uint16_t> pack_wino(const std::vector<float>& w, int cin, int cout) {
+  static const double G[4][3] = {{1, 0, 0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0, 0, 1}};
+  const int ncb = cout / 32, nks = cin / 16;
+  std::vector<uint16_t> a((size_t)ncb * nks * 16 * 2 * 64 * 8);
+  for (int cb = 0; cb < ncb; ++cb)
+    for (int ks = 0; ks < nks; ++ks)
+      for (int xi = 0; xi < 16; ++xi)
+        for (int lane = 0; lane < 64; ++lane)
+          for (int j = 0; j < 8; ++j) {
+            const int co = 32 * cb + (lane & 31), ci = 16 * ks + 8 * (lane >> 5) + j;
+            const float* g = &w[((size_t)co * cin + ci) * 9];
+            const int i0 = xi >> 2, j0 = xi & 3;
+            double u = 0;
+            for (int r = 0; r < 3; ++r)
+              for (int c = 0; c < 3; ++c) u += G[i0][r] * (double)g[r * 3 + c] * G[j0][c];
+            const float v = (float)u;
+            const uint16_t hv = f2bf(v);
+            const size_t o = ((((size_t)(cb * nks + ks) * 16 + xi) * 2) * 64 + lane) * 8 + j;
+            a[o] = hv;
+            a[o + 64 * 8] = f2bf(v - bf2f(hv));
+          }
+  return a;
+}
+
 static int build_hardnet(hn_model* m, Cursor& cur) {
   static const int cin[7] = {1, 32, 32, 64, 64, 128, 128};
   static const int cout[7] = {32, 32, 64, 64, 128, 128, 128};
@@ -492,6 +519,11 @@ static int build_hardnet(hn_model* m, Cursor& cur) {
     if ((rc = m->upload(pk, &d))) return rc;
     m->hd.wpack[l] = d;
     if ((rc = m->upload(f.b, &m->hd.bias[l]))) return rc;
+    if (l == 3 || l == 5) {
+      uint16_t* c = nullptr;
+      if ((rc = m->upload(pack_wino(f.w, cin[l], cout[l]), &c))) return rc;
+      m->hd.wino[l] = c;
+    }
     if (l == 1 || l == 2) {
       uint16_t* c = nullptr;
       if ((rc = m->upload(pack_c12(f.w, cout[l]), &c))) return rc;

@@ -1433,6 +1433,7 @@ bool hn_hardnet_variant_ok(int layer, int v) {
 #endif
   }
   if (v >= 13 && v <= 15) return layer == 4;
+  if (v == 17) return layer == 3 || layer == 5;  // Winograd F(2x2,3x3), hn_wino.hip
   if (v == 16) return layer == 3 || layer == 5;
   if (v == 7) return layer >= 3;
   if (v == 0 || v == 1) return true;
@@ -1461,6 +1462,7 @@ hipError_t hn_launch_hardnet_conv(int layer, int variant, const HardnetDev& d, c
     return (variant == 13 ? ws4_np2s : variant == 14 ? ws4_s : ws4_np2s22)(in, out, d.wpack[4], d.bias[4], P,
                                                                           nullptr, nullptr, 0.f, st);
   }
+  if (variant == 17) return hn_launch_wino(layer, d, in, out, P, st);
   if (variant == 16) {  // coalesced epilogue stores
     switch (layer) {
       case 3: return ws3_cst(in, out, d.wpack[3], d.bias[3], P, nullptr, nullptr, 0.f, st);

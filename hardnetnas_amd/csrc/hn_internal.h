@@ -35,6 +35,7 @@ struct HardnetDev {
   float* bias[7] = {};       // folded BN bias per conv
   void* c12_w1 = nullptr;    // conv1 / conv2 as 16x16x32 A operands for the fused k_c12
   void* c12_w2 = nullptr;
+  void* wino[7] = {};        // conv3 / conv5: Winograd F(2x2,3x3) U fragments (hn_wino.hip)
 };
 // uint8 patches for the fused preprocessing load (hn_forward_u8)
 struct HnU8In {
@@ -57,6 +58,8 @@ hipError_t hn_launch_hardnet_conv(int layer, int variant, const HardnetDev& d, c
 hipError_t hn_launch_head(const float* a, float* out, const void* wp, const float* bias, int P,
                           int K, float l2eps, hipStream_t st, bool f16 = false);
 int hn_conv_lds_bytes(int layer);
+// Winograd F(2x2,3x3) conv3 / conv5 (hn_wino.hip; HN_VARIANT digit h)
+hipError_t hn_launch_wino(int layer, const HardnetDev& d, const float* in, float* out, int P, hipStream_t st);
 
 hipError_t hn_launch_pw(const float* in, float* out, const float* wt, const float* bias,
                         const float* res, long npix, int cin, int cout, int groups, bool relu,

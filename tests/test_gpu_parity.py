@@ -79,7 +79,7 @@ def test_chunked_forward_equals_unchunked(name, cuda_device, monkeypatch):
     assert torch.equal(full, chunked)
 
 
-@pytest.mark.parametrize("variant", ["111111", "010101", "101010", "202222", "303333", "202323", "005555", "006666", "505663", "605663", "6056d3", "6056e3", "6056f3", "605gf3", "605gfg"])
+@pytest.mark.parametrize("variant", ["111111", "010101", "101010", "202222", "303333", "202323", "005555", "006666", "505663", "605663", "6056d3", "6056e3", "6056f3", "605gf3", "605gfg", "605hfh", "605gfh", "605hfg"])
 def test_tiling_variants_match_reference(variant, cuda_device, monkeypatch):
     from hardnetnas_amd._native import NativeModel
     m, fx, _ = build_module("hardnet")

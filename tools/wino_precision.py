@@ -26,9 +26,12 @@ G = torch.tensor([[1, 0, 0], [.5, .5, .5], [.5, -.5, .5], [0, 0, 1]], dtype=torc
 AT = torch.tensor([[1, 1, 1, 0], [0, 1, -1, -1]], dtype=torch.float64)
 
 
-def split(x):
-    h = x.to(torch.bfloat16).to(torch.float64)
-    lo = (x.to(torch.float64) - h).to(torch.bfloat16).to(torch.float64)
+MODE = os.environ.get("WINO_MODE", "bf16x3")  # bf16x3 | f16u1: V fp16 hi/lo, U one fp16
+
+
+def split(x, dt=torch.bfloat16):
+    h = x.to(dt).to(torch.float64)
+    lo = (x.to(torch.float64) - h).to(dt).to(torch.float64)
     return h, lo
 
 
@@ -49,10 +52,15 @@ def conv_wino_x3(y, w, b):
     # V = BT d B in fp32
     V = torch.einsum("ab,pcijbd,ed->pcijae", BT.float(), d, BT.float())
     U = torch.einsum("ab,kcbd,ed->kcae", G, w, G)  # fp64
-    Vh, Vl = split(V)
-    Uh, Ul = split(U)
-    M = (torch.einsum("kcae,pcijae->pkijae", Uh, Vh) + torch.einsum("kcae,pcijae->pkijae", Uh, Vl)
-         + torch.einsum("kcae,pcijae->pkijae", Ul, Vh))
+    if MODE == "f16u1":
+        Vh, Vl = split(V, torch.float16)
+        Uh = U.to(torch.float16).to(torch.float64)
+        M = torch.einsum("kcae,pcijae->pkijae", Uh, Vh) + torch.einsum("kcae,pcijae->pkijae", Uh, Vl)
+    else:
+        Vh, Vl = split(V)
+        Uh, Ul = split(U)
+        M = (torch.einsum("kcae,pcijae->pkijae", Uh, Vh) + torch.einsum("kcae,pcijae->pkijae", Uh, Vl)
+             + torch.einsum("kcae,pcijae->pkijae", Ul, Vh))
     M = M.to(torch.float32)
     Yt = torch.einsum("ra,pkijae,se->pkijrs", AT.float(), M, AT.float())  # [P,K,T,T,2,2]
     Yt = Yt.permute(0, 1, 2, 4, 3, 5).reshape(P, -1, H, H)
