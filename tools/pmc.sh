@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 rm -rf gpurun_out/pmc; mkdir -p gpurun_out/pmc
 MODEL=${MODEL:-hardnet}
-ARGS="--no-cpu-baseline --steps 1 --warmup 1 --batch ${PMC_BATCH:-32768} --model $MODEL"
+ARGS="--no-cpu-baseline --steps 1 --warmup 1 --batch ${PMC_BATCH:-32768} --model $MODEL ${PMC_EXTRA:-}"
 timeout -k 10 120 rocprofv3 -L > gpurun_out/pmc/counters.txt 2>&1 || true
 i=0
 while IFS= read -r group; do
