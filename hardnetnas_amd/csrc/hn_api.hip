@@ -36,7 +36,8 @@ void hn_read_knobs(HnKnobs* k) {
   k->naive_dw = std::getenv("HN_NAIVE_DW") != nullptr;
   k->no_skipfuse = std::getenv("HN_NO_SKIPFUSE") != nullptr;
   k->pairdist_valu = std::getenv("HN_PAIRDIST_VALU") != nullptr;
-  k->train_splitk = std::max(32, env_int("HN_TRAIN_SPLITK", 4096)) / 32 * 32;
+  k->train_splitk = std::max(32, env_int("HN_TRAIN_SPLITK", 1024)) / 32 * 32;
+  k->train_f32 = env_int("HN_TRAIN_F32", 1) & 3;
 #ifdef HN_EXPERIMENTS
   k->c12_abl = env_int("HN_C12_ABL", 0) & 255;
   k->dbg = env_int("HN_DEBUG", 0);

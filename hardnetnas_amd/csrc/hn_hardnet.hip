@@ -140,7 +140,7 @@ __global__ __launch_bounds__(256) void k_conv3x3(const float* __restrict__ in, f
                                                  const float* __restrict__ bias, int P,
                                                  const float* __restrict__ stem_w,
                                                  const float* __restrict__ stem_b, float eps,
-                                                 int dbg) {
+                                                 int dbg, float relu_lo) {
   using C = ConvCfg<CIN, COUT, HIN, S, NP, TR, WM, WN>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -355,10 +355,10 @@ __global__ __launch_bounds__(256) void k_conv3x3(const float* __restrict__ in, f
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         float4 v;
-        v.x = fmaxf(acc[mt][nt][4 * q + 0] + bv[q].x, 0.f);
-        v.y = fmaxf(acc[mt][nt][4 * q + 1] + bv[q].y, 0.f);
-        v.z = fmaxf(acc[mt][nt][4 * q + 2] + bv[q].z, 0.f);
-        v.w = fmaxf(acc[mt][nt][4 * q + 3] + bv[q].w, 0.f);
+        v.x = fmaxf(acc[mt][nt][4 * q + 0] + bv[q].x, relu_lo);
+        v.y = fmaxf(acc[mt][nt][4 * q + 1] + bv[q].y, relu_lo);
+        v.z = fmaxf(acc[mt][nt][4 * q + 2] + bv[q].z, relu_lo);
+        v.w = fmaxf(acc[mt][nt][4 * q + 3] + bv[q].w, relu_lo);
         *reinterpret_cast<float4*>(obase + (size_t)mt * 32 * COUT + nt * 32 + 8 * q) = v;
       }
     }
@@ -402,7 +402,7 @@ template <int CIN, int COUT, int HIN, int S, int NP, int TR, int WM, int WN, boo
 __global__ __launch_bounds__(WM * WN * 64, 2) void k_conv_pipe(
     const float* __restrict__ in, float* __restrict__ out, const uint4* __restrict__ wp,
     const float* __restrict__ bias, int P, const float* __restrict__ stem_w,
-    const float* __restrict__ stem_b, float eps) {
+    const float* __restrict__ stem_b, float eps, float relu_lo) {
   using C = PipeCfg<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM, CST>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -681,10 +681,10 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void k_conv_pipe(
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
               float4 v;
-              v.x = fmaxf(acc[mt][nt][4 * q + 0] + bv[q].x, 0.f);
-              v.y = fmaxf(acc[mt][nt][4 * q + 1] + bv[q].y, 0.f);
-              v.z = fmaxf(acc[mt][nt][4 * q + 2] + bv[q].z, 0.f);
-              v.w = fmaxf(acc[mt][nt][4 * q + 3] + bv[q].w, 0.f);
+              v.x = fmaxf(acc[mt][nt][4 * q + 0] + bv[q].x, relu_lo);
+              v.y = fmaxf(acc[mt][nt][4 * q + 1] + bv[q].y, relu_lo);
+              v.z = fmaxf(acc[mt][nt][4 * q + 2] + bv[q].z, relu_lo);
+              v.w = fmaxf(acc[mt][nt][4 * q + 3] + bv[q].w, relu_lo);
               if constexpr (CST) {
                 *reinterpret_cast<float4*>(scr + r * C::SROW + 8 * (q & 1) + 4 * h) = v;
                 if (q & 1) {  // channels 16 (q / 2) .. + 15 of the tile: 16 rows of 64 bytes per store
@@ -760,7 +760,7 @@ template <int CIN, int COUT, int HIN, int S, int NP, int TR, int WM, int WN, boo
 __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_ws(
     const float* __restrict__ in, float* __restrict__ out, const uint4* __restrict__ wp,
     const float* __restrict__ bias, int P, const float* __restrict__ stem_w,
-    const float* __restrict__ stem_b, float eps) {
+    const float* __restrict__ stem_b, float eps, float relu_lo) {
   using C = WsCfg<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM, PX, CST>;
   static_assert(PX == 80 || !STEM, "the stem producer writes the 80-byte layout");
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1070,10 +1070,10 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_ws(
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
               float4 v;
-              v.x = fmaxf(acc[mt][nt][4 * q + 0] + bv[q].x, 0.f);
-              v.y = fmaxf(acc[mt][nt][4 * q + 1] + bv[q].y, 0.f);
-              v.z = fmaxf(acc[mt][nt][4 * q + 2] + bv[q].z, 0.f);
-              v.w = fmaxf(acc[mt][nt][4 * q + 3] + bv[q].w, 0.f);
+              v.x = fmaxf(acc[mt][nt][4 * q + 0] + bv[q].x, relu_lo);
+              v.y = fmaxf(acc[mt][nt][4 * q + 1] + bv[q].y, relu_lo);
+              v.z = fmaxf(acc[mt][nt][4 * q + 2] + bv[q].z, relu_lo);
+              v.w = fmaxf(acc[mt][nt][4 * q + 3] + bv[q].w, relu_lo);
               if constexpr (CST) {
                 float* scr = reinterpret_cast<float*>(smem + 2 * C::BUF) + wave * (C::SCR / 4);
                 *reinterpret_cast<float4*>(scr + r * C::SROW + 8 * q + 4 * h) = v;
@@ -1287,9 +1287,9 @@ constexpr int conv_lds() { return CFG::LDS + (STEM ? (34 * 34 + 8) * 4 : 0); }
 
 #define HN_CONV(NAME, STEM, CIN, COUT, HIN, S, NP, TR, WM, WN)                             \
   using NAME##_cfg = ConvCfg<CIN, COUT, HIN, S, NP, TR, WM, WN>;                           \
-  static hipError_t NAME(const float* in, float* out, const void* wp, const float* bias,   \
+  static hipError_t NAME##_lo(const float* in, float* out, const void* wp, const float* bias,\
                          int P, const float* sw, const float* sb, float eps,               \
-                         hipStream_t st) {                                                 \
+                         hipStream_t st, float lo) {                                       \
     constexpr int lds = conv_lds<NAME##_cfg, STEM>();                                      \
     int resident = 0; /* sets the dynamic-LDS limit on this device */                     \
     hipError_t e = hn_resident_blocks(                                                     \
@@ -1299,8 +1299,12 @@ constexpr int conv_lds() { return CFG::LDS + (STEM ? (34 * 34 + 8) * 4 : 0); }
     const int grid = (P + NP - 1) / NP * NAME##_cfg::RT;                                   \
     hipLaunchKernelGGL((k_conv3x3<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM>), dim3(grid),   \
                        dim3(256), lds, st, in, out, static_cast<const uint4*>(wp), bias, P, \
-                       sw, sb, eps, hn_knobs().dbg);                                       \
+                       sw, sb, eps, hn_knobs().dbg, lo);                                   \
     return hipGetLastError();                                                              \
+  }                                                                                        \
+  static hipError_t NAME(const float* in, float* out, const void* wp, const float* bias,   \
+                         int P, const float* sw, const float* sb, float eps, hipStream_t st) { \
+    return NAME##_lo(in, out, wp, bias, P, sw, sb, eps, st, 0.f);                          \
   }
 
 // variant 0 = default tiling; variant 1 = smaller LDS footprint / more workgroups per CU
@@ -1321,9 +1325,9 @@ HN_CONV(conv5_v1, false, 128, 128, 8, 1, 1, 8, 1, 4)
 #define HN_PIPE_A(NAME, STEM, CIN, COUT, HIN, S, NP, TR, WM, WN, ABL) HN_PIPE_C(NAME, STEM, CIN, COUT, HIN, S, NP, TR, WM, WN, ABL, false)
 #define HN_PIPE_C(NAME, STEM, CIN, COUT, HIN, S, NP, TR, WM, WN, ABL, CST)                 \
   using NAME##_cfg = PipeCfg<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM, CST>;                \
-  static hipError_t NAME(const float* in, float* out, const void* wp, const float* bias,   \
+  static hipError_t NAME##_lo(const float* in, float* out, const void* wp, const float* bias,\
                          int P, const float* sw, const float* sb, float eps,               \
-                         hipStream_t st) {                                                 \
+                         hipStream_t st, float lo) {                                       \
     constexpr int lds = NAME##_cfg::SMEM;                                                  \
     const void* fn = reinterpret_cast<const void*>(                                        \
         &k_conv_pipe<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM, ABL, CST>);                       \
@@ -1334,8 +1338,12 @@ HN_CONV(conv5_v1, false, 128, 128, 8, 1, 1, 8, 1, 4)
     const int grid = std::min(tiles, resident);                                            \
     hipLaunchKernelGGL((k_conv_pipe<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM, ABL, CST>), dim3(grid), \
                        dim3(NAME##_cfg::NTHR), lds, st, in, out,                           \
-                       static_cast<const uint4*>(wp), bias, P, sw, sb, eps);               \
+                       static_cast<const uint4*>(wp), bias, P, sw, sb, eps, lo);               \
     return hipGetLastError();                                                              \
+  }                                                                                        \
+  static hipError_t NAME(const float* in, float* out, const void* wp, const float* bias,   \
+                         int P, const float* sw, const float* sb, float eps, hipStream_t st) { \
+    return NAME##_lo(in, out, wp, bias, P, sw, sb, eps, st, 0.f);                          \
   }
 
 HN_PIPE(pipe1s, true, 32, 32, 32, 1, 1, 4, 4, 1)
@@ -1356,8 +1364,9 @@ HN_PIPE_C(pipe5_cst, false, 128, 128, 8, 1, 2, 8, 1, 4, 0, true)  // HN_VARIANT 
 #define HN_WS_X(NAME, STEM, CIN, COUT, HIN, S, NP, TR, WM, WN, ABL, PX) HN_WS_C(NAME, STEM, CIN, COUT, HIN, S, NP, TR, WM, WN, ABL, PX, false)
 #define HN_WS_C(NAME, STEM, CIN, COUT, HIN, S, NP, TR, WM, WN, ABL, PX, CST)             \
   using NAME##_cfg = WsCfg<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM, PX, CST>;                   \
-  static hipError_t NAME(const float* in, float* out, const void* wp, const float* bias,   \
-                         int P, const float* sw, const float* sb, float eps, hipStream_t st) { \
+  static hipError_t NAME##_lo(const float* in, float* out, const void* wp, const float* bias,\
+                         int P, const float* sw, const float* sb, float eps, hipStream_t st, \
+                         float lo) {                                                       \
     constexpr int lds = NAME##_cfg::SMEM;                                                  \
     const void* fn =                                                                       \
         reinterpret_cast<const void*>(&k_conv_ws<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM, ABL, PX, CST>); \
@@ -1368,8 +1377,12 @@ HN_PIPE_C(pipe5_cst, false, 128, 128, 8, 1, 2, 8, 1, 4, 0, true)  // HN_VARIANT 
     const int grid = std::min(tiles, resident);                                            \
     hipLaunchKernelGGL((k_conv_ws<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM, ABL, PX, CST>), dim3(grid), \
                        dim3(NAME##_cfg::NTHR), lds, st, in, out,                           \
-                       static_cast<const uint4*>(wp), bias, P, sw, sb, eps);               \
+                       static_cast<const uint4*>(wp), bias, P, sw, sb, eps, lo);               \
     return hipGetLastError();                                                              \
+  }                                                                                        \
+  static hipError_t NAME(const float* in, float* out, const void* wp, const float* bias,   \
+                         int P, const float* sw, const float* sb, float eps, hipStream_t st) { \
+    return NAME##_lo(in, out, wp, bias, P, sw, sb, eps, st, 0.f);                          \
   }
 
 HN_WS_S(ws1s, true, 32, 32, 32, 1, 1, 4, 4, 1)
@@ -1515,6 +1528,23 @@ hipError_t hn_launch_hardnet_conv(int layer, int variant, const HardnetDev& d, c
       return (v1 ? conv4_v1 : conv4_launch)(in, out, d.wpack[4], d.bias[4], P, nullptr, nullptr, 0.f, st);
     case 5:
       return (v1 ? conv5_v1 : conv5_launch)(in, out, d.wpack[5], d.bias[5], P, nullptr, nullptr, 0.f, st);
+  }
+  return hipErrorInvalidValue;
+}
+
+// Train mode (hn_train.hip): layer `layer`'s production tiling as a plain convolution over NHWC
+// fp32 -- zero bias, no ReLU floor -- with bf16x3 fragments packed on the GPU (k_pack3x3).  The
+// stride-1 layers also run the data gradient (weights flipped and transposed: same shapes).
+hipError_t hn_launch_conv_raw(int layer, const void* wp, const float* zero_bias, const float* in, float* out,
+                              int P, hipStream_t st) {
+  if (P <= 0) return hipSuccess;
+  const float lo = -INFINITY;
+  switch (layer) {
+    case 1: return conv1_launch_lo(in, out, wp, zero_bias, P, nullptr, nullptr, 0.f, st, lo);
+    case 2: return ws2_lo(in, out, wp, zero_bias, P, nullptr, nullptr, 0.f, st, lo);
+    case 3: return ws3_cst_lo(in, out, wp, zero_bias, P, nullptr, nullptr, 0.f, st, lo);
+    case 4: return ws4_np2s22_lo(in, out, wp, zero_bias, P, nullptr, nullptr, 0.f, st, lo);
+    case 5: return pipe5_cst_lo(in, out, wp, zero_bias, P, nullptr, nullptr, 0.f, st, lo);
   }
   return hipErrorInvalidValue;
 }

@@ -15,7 +15,9 @@ struct HnKnobs {
   bool naive_dw = false;       // HN_NAIVE_DW: untiled depthwise kernel
   bool no_skipfuse = false;    // HN_NO_SKIPFUSE: maxpool + pw instead of k_skip_s2
   bool pairdist_valu = false;  // HN_PAIRDIST_VALU: fp32 VALU pair-distance kernel
-  int train_splitk = 4096;     // HN_TRAIN_SPLITK: K per split-K slice of the train GEMMs
+  int train_splitk = 1024;     // HN_TRAIN_SPLITK: K per split-K slice of the train GEMMs
+  int train_f32 = 1;           // HN_TRAIN_F32: bit 0 train forward convs, bit 1 stride-1 dgrads as f32-MFMA
+                               // GEMMs (else the bf16x3 conv kernels); default 1 = bf16x3 dgrads only
   int c12_abl = 0;             // HN_C12_ABL (HN_EXPERIMENTS only)
   int dbg = 0;                 // HN_DEBUG (HN_EXPERIMENTS only)
 };
@@ -58,6 +60,10 @@ hipError_t hn_launch_hardnet_conv(int layer, int variant, const HardnetDev& d, c
 hipError_t hn_launch_head(const float* a, float* out, const void* wp, const float* bias, int P,
                           int K, float l2eps, hipStream_t st, bool f16 = false);
 int hn_conv_lds_bytes(int layer);
+// train mode: conv layer 1..5 as a plain NHWC convolution (no bias, no ReLU), bf16x3 fragments
+// in the pack_conv3x3 layout
+hipError_t hn_launch_conv_raw(int layer, const void* wp, const float* zero_bias, const float* in, float* out,
+                              int P, hipStream_t st);
 // Winograd F(2x2,3x3) conv3 / conv5 (hn_wino.hip; HN_VARIANT digit h)
 hipError_t hn_launch_wino(int layer, const HardnetDev& d, const float* in, float* out, int P, hipStream_t st);
 
@@ -136,7 +142,7 @@ struct HnTrainLayer {
 };
 extern const HnTrainLayer kHardnetTrainLayers[7];
 struct HnTrainWs {  // byte offsets into the train workspace
-  size_t xn, inv_sd, z[7], rstd[7], g0, g1, col, part, bnpart, bnmean, wt, total;
+  size_t xn, inv_sd, z[7], rstd[7], g0, g1, col, part, bnpart, bnmean, wt, nhwc0, nhwc1, wpack, zero, total;
 };
 HnTrainWs hn_train_layout(long B);
 hipError_t hn_train_forward(const float* in, long B, const float* const* W, float* const* rmean, float* const* rvar,

@@ -215,16 +215,26 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g, BL bl, long kslice, fl
   }
 }
 
-__global__ __launch_bounds__(256) void k_splitk_sum(GemmArgs g, int S, const float* __restrict__ part) {
-  const long e = (long)blockIdx.x * 256 + threadIdx.x;
-  if (e >= g.M * g.N) return;
+// 64 consecutive outputs x 16 slice groups per workgroup: lane x of group y sums slices y, y + 16,
+// ... (coalesced 256-byte rows per slice), then the 16 group sums are added in a fixed order
+// (deterministic; fp64 throughout)
+__global__ __launch_bounds__(1024) void k_splitk_sum(GemmArgs g, int S, const float* __restrict__ part) {
+  __shared__ double red[16][64];
+  const int x = threadIdx.x & 63, y = threadIdx.x >> 6;
+  const long e = (long)blockIdx.x * 64 + x, mn = g.M * g.N;
   double s = 0.0;
-  for (int z = 0; z < S; ++z) s += part[(long)z * g.M * g.N + e];
+  if (e < mn)
+    for (int z = y; z < S; z += 16) s += part[(long)z * mn + e];
+  red[y][x] = s;
+  __syncthreads();
+  if (y != 0 || e >= mn) return;
+  double t = 0.0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) t += red[k][x];
   const long i = e / g.N, j = e % g.N;
   float* c = g.C + i * g.sci + j * g.scj;
-  *c = g.beta == 0.f ? (float)(g.alpha * s) : (float)(g.alpha * s + g.beta * (double)*c);
+  *c = g.beta == 0.f ? (float)(g.alpha * t) : (float)(g.alpha * t + g.beta * (double)*c);
 }
-
 
 // part: scratch for the split-K partials, M x N x slices floats (nullptr: one slice).
 // The B loader's contiguous index: StridedB reads g.sbj to decide; Im2colB<.., T> is
@@ -234,7 +244,7 @@ hipError_t gemm(const GemmArgs& g, hipStream_t st, float* part = nullptr, BL bl 
   if (g.M <= 0 || g.N <= 0) return hipSuccess;
   const int bm = g.M <= 32 ? 32 : 64;
   const long tiles = ((g.N + GBN - 1) / GBN) * ((g.M + bm - 1) / bm);
-  long ks = hn_knobs().train_splitk;  // K per slice (HN_TRAIN_SPLITK, default 4096)
+  long ks = hn_knobs().train_splitk;  // K per slice (HN_TRAIN_SPLITK, default 1024)
   if (part && tiles < 256 && g.K > 64) {  // a small grid: split K until every CU has a workgroup
     const long want = std::min<long>((256 + tiles - 1) / tiles, (g.K + 63) / 64);
     ks = std::min(ks, ((g.K + want - 1) / want + GBK - 1) / GBK * GBK);
@@ -248,7 +258,7 @@ hipError_t gemm(const GemmArgs& g, hipStream_t st, float* part = nullptr, BL bl 
   if (S > 1) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_splitk_sum, dim3((unsigned)((g.M * g.N + 255) / 256)), dim3(256), 0, st, g, S, part);
+    hipLaunchKernelGGL(k_splitk_sum, dim3((unsigned)((g.M * g.N + 63) / 64)), dim3(1024), 0, st, g, S, part);
   }
   return hipGetLastError();
 }
@@ -462,6 +472,64 @@ __global__ __launch_bounds__(256) void k_l2_bwd(const float* __restrict__ z, con
   dz[(long)(lane + 64) * B + p] = (db - yb * dot) / n;
 }
 
+// conv weights W [cout][cin][3][3] (raw, or flipped and transposed for the data gradient:
+// W'[ci][co][tap] = W[co][ci][8 - tap]) -> the bf16x3 MFMA fragments of the inference conv kernels
+// (hn_api.hip pack_conv3x3 layout [cin/32][tap][ks][cout/32][plane][lane][8]), on the GPU since
+// the weights change every step
+__global__ __launch_bounds__(256) void k_pack3x3(const float* __restrict__ w, int cin_w, int cout_w, int flip,
+                                                 unsigned short* __restrict__ out) {
+  const int cin = flip ? cout_w : cin_w, cout = flip ? cin_w : cout_w, ntot = cout / 32;
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;  // one (hi, lo) pair per thread
+  if (e >= (long)cin * cout * 9) return;
+  const int j = (int)(e & 7), lane = (int)((e >> 3) & 63);
+  long r = e >> 9;
+  const int nt = (int)(r % ntot);
+  r /= ntot;
+  const int ks = (int)(r & 1);
+  r >>= 1;
+  const int tap = (int)(r % 9), cc = (int)(r / 9);
+  const int n = nt * 32 + (lane & 31), c = cc * 32 + ks * 16 + (lane >> 5) * 8 + j;
+  const float v = flip ? w[((long)c * cin_w + n) * 9 + 8 - tap] : w[((long)n * cin_w + c) * 9 + tap];
+  const __bf16 hv = (__bf16)v, lv = (__bf16)(v - (float)hv);
+  const long o = ((((long)(cc * 9 + tap) * 2 + ks) * ntot + nt) * 2 * 64 + lane) * 8 + j;
+  out[o] = __builtin_bit_cast(unsigned short, hv);
+  out[o + 64 * 8] = __builtin_bit_cast(unsigned short, lv);
+}
+
+// CNHW [C][B][HW] (relu optional) <-> NHWC [B][HW][C] through a 64-pixel x C LDS tile: both sides
+// coalesced.  grid (HW / 64, B)
+__global__ __launch_bounds__(256) void k_cnhw_to_nhwc(const float* __restrict__ z, int C, long B, int HW, int relu,
+                                                      float* __restrict__ out) {
+  __shared__ float tile[128][65];
+  const long b = blockIdx.y;
+  const int p0 = blockIdx.x * 64, t = threadIdx.x;
+  for (int i = t; i < C * 64; i += 256) {
+    const int c = i >> 6, p = i & 63;
+    float v = z[((long)c * B + b) * HW + p0 + p];
+    tile[c][p] = relu ? fmaxf(v, 0.f) : v;
+  }
+  __syncthreads();
+  for (int i = t; i < C * 64; i += 256) {
+    const int p = i / C, c = i % C;
+    out[(b * HW + p0 + p) * C + c] = tile[c][p];
+  }
+}
+__global__ __launch_bounds__(256) void k_nhwc_to_cnhw(const float* __restrict__ in, int C, long B, int HW,
+                                                      float* __restrict__ z) {
+  __shared__ float tile[128][65];
+  const long b = blockIdx.y;
+  const int p0 = blockIdx.x * 64, t = threadIdx.x;
+  for (int i = t; i < C * 64; i += 256) {
+    const int p = i / C, c = i % C;
+    tile[c][p] = in[(b * HW + p0 + p) * C + c];
+  }
+  __syncthreads();
+  for (int i = t; i < C * 64; i += 256) {
+    const int c = i >> 6, p = i & 63;
+    z[((long)c * B + b) * HW + p0 + p] = tile[c][p];
+  }
+}
+
 unsigned grid_for(long n) { return (unsigned)std::min<long>((n + 255) / 256, 65536); }
 
 // implicit-im2col convs of one layer (compile-time geometry): the forward Y = W . col and the
@@ -582,6 +650,12 @@ HnTrainWs hn_train_layout(long B) {
   w.bnpart = take((size_t)128 * kBnSlices * 2 * sizeof(double));
   w.wt = take((size_t)128 * 128 * 64 * sizeof(float));  // a transposed weight (conv6 is the largest)
   w.bnmean = take((size_t)2 * 128 * sizeof(float));
+  // the bf16x3 conv path: NHWC in / out (the largest activation: 32 x 32 x 32 per patch), one
+  // packed layer (conv5: 128 x 128 x 9 x 2 bf16 pairs) and a zero bias
+  w.nhwc0 = take((size_t)B * 32 * 1024 * 4);
+  w.nhwc1 = take((size_t)B * 32 * 1024 * 4);
+  w.wpack = take((size_t)128 * 128 * 9 * 2 * 2 * 2);
+  w.zero = take(128 * sizeof(float));
   w.total = off;
   return w;
 }
@@ -592,10 +666,33 @@ HnTrainWs hn_train_layout(long B) {
     if (e_ != hipSuccess) return e_;  \
   } while (0)
 
+// conv layer l (1..5) as the inference kernels' bf16x3 MFMA conv over NHWC: CNHW `x` (relu'd if
+// asked) -> NHWC -> conv (flip: the data gradient, input = the conv's output space) -> CNHW `y`
+static hipError_t conv_bf16x3(int l, bool flip, const float* x, bool relu, long B, const float* W, float* y,
+                              char* ws, const HnTrainWs& L, hipStream_t st) {
+  const HnTrainLayer& S = kHardnetTrainLayers[l];
+  const long ho = hout_of(S);
+  const int cin = flip ? S.cout : S.cin, cout = flip ? S.cin : S.cout;
+  const int hin = flip ? (int)ho : S.hin, hout = flip ? S.hin : (int)ho;
+  float* a = reinterpret_cast<float*>(ws + L.nhwc0);
+  float* o = reinterpret_cast<float*>(ws + L.nhwc1);
+  unsigned short* wp = reinterpret_cast<unsigned short*>(ws + L.wpack);
+  hipLaunchKernelGGL(k_cnhw_to_nhwc, dim3(hin * hin / 64, (unsigned)B), dim3(256), 0, st, x, cin, B, hin * hin,
+                     relu ? 1 : 0, a);
+  hipLaunchKernelGGL(k_pack3x3, dim3((S.cin * S.cout * 9 + 255) / 256), dim3(256), 0, st, W, S.cin, S.cout,
+                     flip ? 1 : 0, wp);
+  HCK(hipGetLastError());
+  HCK(hn_launch_conv_raw(l, wp, reinterpret_cast<const float*>(ws + L.zero), a, o, (int)B, st));
+  hipLaunchKernelGGL(k_nhwc_to_cnhw, dim3(hout * hout / 64, (unsigned)B), dim3(256), 0, st, o, cout, B,
+                     hout * hout, y);
+  return hipGetLastError();
+}
+
 hipError_t hn_train_forward(const float* in, long B, const float* const* W, float* const* rmean, float* const* rvar,
                             float mom, float bn_eps, float in_eps, float l2_eps, float drop_p,
                             unsigned long long seed, float* out, char* ws, hipStream_t st) {
   const HnTrainWs L = hn_train_layout(B);
+  HCK(hipMemsetAsync(ws + L.zero, 0, 128 * sizeof(float), st));  // the bf16x3 convs' zero bias
   float* xn = reinterpret_cast<float*>(ws + L.xn);
   hipLaunchKernelGGL(k_input_norm, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, in, B, in_eps, xn,
                      reinterpret_cast<float*>(ws + L.inv_sd));
@@ -608,7 +705,10 @@ hipError_t hn_train_forward(const float* in, long B, const float* const* W, floa
     const ActIn a{l == 0 ? xn : reinterpret_cast<const float*>(ws + L.z[l - 1]), l > 0 ? 1 : 0,
                   l == 6 ? drop_p : 0.f, seed};
     float* z = reinterpret_cast<float*>(ws + L.z[l]);
-    HCK(conv_fwd_l(l, a, B, W[l], S.cout, z, reinterpret_cast<float*>(ws + L.part), st));  // Y = W . im2col(a)
+    if (l >= 1 && l <= 5 && !(hn_knobs().train_f32 & 1))  // conv1..5: the bf16x3 MFMA conv kernels
+      HCK(conv_bf16x3(l, false, a.z, true, B, W[l], z, ws, L, st));
+    else
+      HCK(conv_fwd_l(l, a, B, W[l], S.cout, z, reinterpret_cast<float*>(ws + L.part), st));  // Y = W . im2col(a)
     {
       const int NS = bn_slices(S.cout, B * hw);
       double* part = reinterpret_cast<double*>(ws + L.bnpart);
@@ -630,6 +730,7 @@ hipError_t hn_train_forward(const float* in, long B, const float* const* W, floa
 hipError_t hn_train_backward(const float* dout, long B, const float* const* W, float* const* dW, float* din,
                              float l2_eps, float drop_p, unsigned long long seed, char* ws, hipStream_t st) {
   const HnTrainWs L = hn_train_layout(B);
+  HCK(hipMemsetAsync(ws + L.zero, 0, 128 * sizeof(float), st));
   const float* xn = reinterpret_cast<const float*>(ws + L.xn);
   float* gbuf[2] = {reinterpret_cast<float*>(ws + L.g0), reinterpret_cast<float*>(ws + L.g1)};
   // g: gradient w.r.t. layer l's output activation a_l (a_6 = z_6 into the L2 norm; a_5 =
@@ -659,7 +760,11 @@ hipError_t hn_train_backward(const float* dout, long B, const float* const* W, f
     const bool want_in = l > 0 || din;
     // dW [Cout][K] = dY [Cout][B hw] . im2col(a)^T (split-K slices summed in fp64)
     HCK(conv_wgrad_l(l, a, B, g, S.cout, dW[l], reinterpret_cast<float*>(ws + L.part), st));
-    if (want_in && S.s == 1 && S.ks == 3) {
+    if (want_in && S.s == 1 && S.ks == 3 && l >= 1 && !(hn_knobs().train_f32 & 2)) {
+      // stride-1 3x3 (conv1 / conv3 / conv5: Cin = Cout): the data gradient is the same conv with
+      // the weights flipped and transposed, on the bf16x3 MFMA conv kernels
+      HCK(conv_bf16x3(l, true, g, false, B, W[l], gin, ws, L, st));
+    } else if (want_in && S.s == 1 && S.ks == 3) {
       // stride-1 3x3: d a_{l-1} [Cin][B H H] = implicit col2im-gather GEMM Wt . dY (every tap lands)
       HCK(conv_dgrad_l(l, g, B, W[l], S.cout, reinterpret_cast<float*>(ws + L.wt), gin, st));
     } else if (want_in) {

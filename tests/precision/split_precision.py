@@ -8,7 +8,7 @@ Modes (products accumulated in fp64; the kernels accumulate in fp32, far below t
     fp16x2x  (x_hi + x_lo)*w_hi: activation split, weight rounded once to fp16
     bf16x2w  x_hi*(w_hi + w_lo) with bf16 halves
 Usage:
-    python tools/split_precision.py [mode] [layers, e.g. 12345] [n_patches]
+    python tests/precision/split_precision.py [mode] [layers, e.g. 12345] [n_patches]
 """
 from __future__ import annotations
 
@@ -18,7 +18,7 @@ import sys
 import torch
 import torch.nn.functional as F
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 from fixtures import build_module, golden_inputs  # noqa: E402

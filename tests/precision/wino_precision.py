@@ -4,7 +4,7 @@ Winograd F(2x2,3x3) on bf16x3 split operands, against the fp64 oracle.
 Emulation: transforms in fp32 (input / output) and fp64 -> bf16 hi/lo (filter, done once on
 the host); products hi*hi + hi*lo + lo*hi accumulated in fp64 (the kernel accumulates in
 fp32; that rounding is far below the split error).  Usage:
-    python tools/wino_precision.py [layers, e.g. 135] [n_patches]
+    python tests/precision/wino_precision.py [layers, e.g. 135] [n_patches]
 """
 from __future__ import annotations
 
@@ -15,7 +15,7 @@ import numpy as np
 import torch
 import torch.nn.functional as F
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 from fixtures import build_module, golden_inputs  # noqa: E402

@@ -11,8 +11,8 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+from hardnetnas_amd.losses import loss_HardNet  # noqa: E402
 from hardnetnas_amd.model import HardNet  # noqa: E402
-from oracle import hardnet_oracle as O  # noqa: E402  (the loss, as the training loop computes it)
 
 dev = torch.device("cuda:0")
 pairs = int(os.environ.get("PAIRS", "1024"))
@@ -27,7 +27,7 @@ for name, native in (("hip", True), ("torch_miopen", False)):
 
     def step():
         y = m(x)
-        loss = O.loss_hardnet(y[:pairs], y[pairs:], anchor_swap=True)
+        loss = loss_HardNet(y[:pairs], y[pairs:], anchor_swap=True)
         opt.zero_grad()
         loss.backward()
         opt.step()
