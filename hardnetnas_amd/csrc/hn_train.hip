@@ -532,6 +532,141 @@ __global__ __launch_bounds__(256) void k_nhwc_to_cnhw(const float* __restrict__ 
 
 unsigned grid_for(long n) { return (unsigned)std::min<long>((n + 255) / 256, 65536); }
 
+// ------------------------------------------------------------------------------------------
+// weight gradient of a stride-1 3x3 layer (conv1 / conv3 / conv5):
+//   dW[co][ci][tap] = sum over (b, y, x) of dY[co][b][y][x] . X[ci][b][y + dy - 1][x + dx - 1]
+// with X = relu(z of the previous layer) (CNHW).  One wave per (32 co x 32 ci) block and run of
+// patches, all 9 taps in registers (9 f32 MFMA accumulators, v_mfma_f32_32x32x2_f32: exact fp32
+// products); the wave streams its patches row by row through its own LDS: the dY row and a ring
+// of three X rows with zero halo columns (rows -1 and H are zero rows), so the 9 shifted operands
+// are plain ds_read_b32 at padded (odd) row strides -- no im2col index arithmetic.  Each wave
+// writes its partial sums as one split-K slice (slice = chunk * 4 + wave; k_splitk_sum adds the
+// slices in fp64).  Chunk = 4096 / (H * H) patches, 1,024 positions per wave.
+// ------------------------------------------------------------------------------------------
+template <int CIN, int COUT, int H>
+struct Wg3Cfg {
+  static constexpr int NPC = 4096 / (H * H);   // patches per workgroup chunk (4 waves)
+  static constexpr int NPW = NPC / 4;          // patches per wave
+  static constexpr int RSY = H + 1;            // dY row stride (floats): odd -> conflict-free
+  static constexpr int XW = H + 2;             // X row with halo
+  static constexpr int RSX = (3 * XW) | 1;     // per-channel ring stride (odd)
+  static constexpr int WAVE_F = 32 * RSY + 32 * RSX;  // floats of LDS per wave
+  static constexpr int NCO = COUT / 32, NCI = CIN / 32;
+  static_assert(NPW >= 1 && NPC % 4 == 0, "chunking");
+};
+
+template <int CIN, int COUT, int H>
+__global__ __launch_bounds__(256) void k_wgrad3(const float* __restrict__ zx, const float* __restrict__ dY, long B,
+                                                float* __restrict__ part) {
+  using C = Wg3Cfg<CIN, COUT, H>;
+  __shared__ float smem[4 * C::WAVE_F];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
+  const int blk = blockIdx.x, co0 = (blk / C::NCI) * 32, ci0 = (blk % C::NCI) * 32;
+  const long chunk = blockIdx.y;
+  float* sy = smem + w * C::WAVE_F;  // [32 co][RSY]
+  float* sx = sy + 32 * C::RSY;      // [32 ci][3 slots][XW] (+pad)
+  // halo columns and unused pad stay zero for the kernel's lifetime
+  for (int i = lane; i < 32 * C::RSX; i += 64) sx[i] = 0.f;
+  __builtin_amdgcn_wave_barrier();
+  f32x16 acc[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) acc[t] = f32x16{};
+  constexpr int HH = H * H, NPR = 32 * H / 64;  // floats per lane of one 32-channel row
+  static_assert(NPR >= 1 && (32 * H) % 64 == 0, "row split");
+  // one 32-channel row (channels c0.., patch b, row y) of src: lane -> NPR consecutive floats
+  auto load_row = [&](const float* src, int c0, long b, int y, float (&v)[NPR], bool relu) {
+#pragma unroll
+    for (int i = 0; i < NPR; ++i) {
+      const int e = lane * NPR + i, c = e / H, x = e % H;
+      float t = 0.f;
+      if (y >= 0 && y < H) t = src[((long)(c0 + c) * B + b) * HH + y * H + x];
+      v[i] = relu ? fmaxf(t, 0.f) : t;
+    }
+  };
+  auto put_y = [&](const float (&v)[NPR]) {
+#pragma unroll
+    for (int i = 0; i < NPR; ++i) {
+      const int e = lane * NPR + i, c = e / H, x = e % H;
+      sy[c * C::RSY + x] = v[i];
+    }
+  };
+  auto put_x = [&](const float (&v)[NPR], int y) {  // row y (-1 .. H) into its ring slot
+    const int slot = (y + 1) % 3;
+#pragma unroll
+    for (int i = 0; i < NPR; ++i) {
+      const int e = lane * NPR + i, c = e / H, x = e % H;
+      sx[c * C::RSX + slot * C::XW + 1 + x] = v[i];
+    }
+  };
+#pragma unroll 1
+  for (int pi = 0; pi < C::NPW; ++pi) {
+    const long b = chunk * C::NPC + w + 4 * pi;
+    if (b >= B) break;  // wave-uniform
+    float vy[NPR], vx[NPR];
+    // prologue: X rows -1, 0, 1 and dY row 0
+    load_row(zx, ci0, b, -1, vx, true); put_x(vx, -1);
+    load_row(zx, ci0, b, 0, vx, true);  put_x(vx, 0);
+    load_row(zx, ci0, b, 1, vx, true);  put_x(vx, 1);
+    load_row(dY, co0, b, 0, vy, false); put_y(vy);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll 1
+    for (int y = 0; y < H; ++y) {
+      // prefetch dY row y + 1 and X row y + 2 while row y's MFMAs run
+      if (y + 1 < H) load_row(dY, co0, b, y + 1, vy, false);
+      load_row(zx, ci0, b, y + 2, vx, true);
+      const float* xr[3];
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy) xr[dy] = sx + r * C::RSX + ((y + dy) % 3) * C::XW;  // row y + dy - 1
+#pragma unroll
+      for (int m = 0; m < H / 2; ++m) {  // positions x = 2m + h
+        const int x = 2 * m + h;
+        const float av = sy[r * C::RSY + x];
+#pragma unroll
+        for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+          for (int dx = 0; dx < 3; ++dx)
+            acc[dy * 3 + dx] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, xr[dy][x + dx], acc[dy * 3 + dx], 0, 0, 0);
+      }
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+      if (y + 1 < H) put_y(vy);
+      put_x(vx, y + 2);
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+    }
+  }
+  // slice write: acc[t][4q + e] = dW row co0 + 8q + 4h + e, column (ci0 + r) * 9 + t
+  const long slice = chunk * 4 + w;
+  float* dst = part + slice * (long)COUT * CIN * 9;
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        dst[(long)(co0 + 8 * q + 4 * h + e) * (CIN * 9) + (ci0 + r) * 9 + t] = acc[t][4 * q + e];
+}
+
+template <int CIN, int COUT, int H>
+hipError_t wgrad3(const float* zx, const float* dY, long B, float* dW, float* part, hipStream_t st) {
+  using C = Wg3Cfg<CIN, COUT, H>;
+  const long chunks = (B + C::NPC - 1) / C::NPC;
+  hipLaunchKernelGGL((k_wgrad3<CIN, COUT, H>), dim3(C::NCO * C::NCI, (unsigned)chunks), dim3(256), 0, st, zx, dY,
+                     B, part);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  GemmArgs g{nullptr, nullptr, dW, COUT, (long)CIN * 9, 0, 0, 0, 0, 0, (long)CIN * 9, 1, 1.f, 0.f};
+  hipLaunchKernelGGL(k_splitk_sum, dim3((unsigned)((g.M * g.N + 63) / 64)), dim3(1024), 0, st, g,
+                     (int)(chunks * 4), part);
+  return hipGetLastError();
+}
+
+// slices k_wgrad3 writes for layer l (0 if it does not take that layer)
+static long wgrad3_slices(int l, long B) {
+  const int npc = l == 1 ? Wg3Cfg<32, 32, 32>::NPC : l == 3 ? Wg3Cfg<64, 64, 16>::NPC : l == 5 ? Wg3Cfg<128, 128, 8>::NPC : 0;
+  return npc ? 4 * ((B + npc - 1) / npc) : 0;
+}
+
 // implicit-im2col convs of one layer (compile-time geometry): the forward Y = W . col and the
 // weight gradient dW = dY . col^T over the whole batch, with no column matrix in memory
 template <int C, int H, int KS, int S, int PAD>
@@ -646,6 +781,10 @@ HnTrainWs hn_train_layout(long B) {
     part = std::max(part, (size_t)L.cout * L.cin * L.ks * L.ks * ((kk + hn_knobs().train_splitk - 1) / hn_knobs().train_splitk) * 4);
   }
   part = std::max(part, (size_t)512 * GBM * GBN * 4);  // small-grid forward splits (S <= ceil(256 / tiles))
+  for (int l = 1; l <= 5; l += 2) {  // k_wgrad3's slices
+    const HnTrainLayer& L = kHardnetTrainLayers[l];
+    part = std::max(part, (size_t)L.cout * L.cin * 9 * wgrad3_slices(l, B) * 4);
+  }
   w.part = take(part);
   w.bnpart = take((size_t)128 * kBnSlices * 2 * sizeof(double));
   w.wt = take((size_t)128 * 128 * 64 * sizeof(float));  // a transposed weight (conv6 is the largest)
@@ -759,7 +898,15 @@ hipError_t hn_train_backward(const float* dout, long B, const float* const* W, f
     float* gin = gbuf[(7 - l) & 1];  // gradient w.r.t. this layer's input activation
     const bool want_in = l > 0 || din;
     // dW [Cout][K] = dY [Cout][B hw] . im2col(a)^T (split-K slices summed in fp64)
-    HCK(conv_wgrad_l(l, a, B, g, S.cout, dW[l], reinterpret_cast<float*>(ws + L.part), st));
+    float* part = reinterpret_cast<float*>(ws + L.part);
+    if ((l == 1 || l == 3 || l == 5) && !(hn_knobs().train_f32 & 4)) {  // stride-1 3x3: k_wgrad3
+      const float* zx = reinterpret_cast<const float*>(ws + L.z[l - 1]);
+      if (l == 1) HCK((wgrad3<32, 32, 32>(zx, g, B, dW[l], part, st)));
+      if (l == 3) HCK((wgrad3<64, 64, 16>(zx, g, B, dW[l], part, st)));
+      if (l == 5) HCK((wgrad3<128, 128, 8>(zx, g, B, dW[l], part, st)));
+    } else {
+      HCK(conv_wgrad_l(l, a, B, g, S.cout, dW[l], part, st));
+    }
     if (want_in && S.s == 1 && S.ks == 3 && l >= 1 && !(hn_knobs().train_f32 & 2)) {
       // stride-1 3x3 (conv1 / conv3 / conv5: Cin = Cout): the data gradient is the same conv with
       // the weights flipped and transposed, on the bf16x3 MFMA conv kernels

@@ -200,3 +200,20 @@ def test_train_step_at_reference_batch(cuda_device):
     loss.backward()
     assert torch.isfinite(loss) and (y.norm(dim=1) - 1).abs().max().item() < 1e-5
     assert all(torch.isfinite(mg.features[i].weight.grad).all() for i in (0, 3, 6, 9, 12, 15, 19))
+
+
+@pytest.mark.parametrize("b", [3, 37])
+def test_odd_batch_gradients(b, cuda_device):
+    """Odd batches: the stride-1 data gradients run on the eval conv kernels, whose conv5 tiling
+    stages two patches at a time (a ragged last pair); the smooth-objective gradients still meet
+    the fp64 bar."""
+    mg, _, fx = _pair(cuda_device, fresh=True)
+    md = _model64(True)
+    x = torch.from_numpy(golden_inputs(fx)[:b])
+    c = torch.randn(b, 128, generator=torch.Generator().manual_seed(5))
+    xg, xd = x.to(cuda_device).requires_grad_(True), x.double().requires_grad_(True)
+    for m, xx in ((mg, xg), (md, xd)):
+        (m(xx) * c.to(device=xx.device, dtype=xx.dtype)).sum().backward()
+    for i in (0, 3, 6, 9, 12, 15, 19):
+        assert _rel2(mg.features[i].weight.grad, md.features[i].weight.grad) <= L2_BAR, i
+    assert _rel2(xg.grad, xd.grad) <= L2_BAR
