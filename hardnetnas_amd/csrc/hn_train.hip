@@ -667,6 +667,129 @@ static long wgrad3_slices(int l, long B) {
   return npc ? 4 * ((B + npc - 1) / npc) : 0;
 }
 
+// ------------------------------------------------------------------------------------------
+// forward of a stride-1 3x3 layer (conv1 / conv3 / conv5) on the f32 MFMA, the same streaming as
+// k_wgrad3: z[co][b][p] = sum over (ci, tap) of W[co][ci][tap] . X[ci][b][p shifted by tap].  A wave
+// owns whole patches; per group of G = 32 / H output rows (32 positions = the MFMA's N) it holds
+// all COUT / 32 accumulator blocks, reads the shifted X operand from its LDS ring of G + 2 zero-
+// haloed input rows (all CIN channels) and the weights W[co][ci][0..8] straight from L2 (9 taps
+// contiguous: three loads per lane per input-channel pair, prefetched one pair ahead).
+// ------------------------------------------------------------------------------------------
+template <int CIN, int COUT, int H>
+struct Fw3Cfg {
+  static constexpr int G = 32 / H, R = G + 2;  // output rows per step, ring slots
+  static constexpr int XW = H + 2;
+  static constexpr int RSX = (R * XW) | 1;     // per-channel ring stride (odd)
+  static constexpr int WAVE_F = CIN * RSX;
+  static constexpr int NCO = COUT / 32;
+  static constexpr int NLD = G * CIN * H / 64;  // floats per lane of one step's new rows
+  static_assert(32 % H == 0 && (G * CIN * H) % 64 == 0, "geometry");
+};
+
+template <int CIN, int COUT, int H>
+__global__ __launch_bounds__(256) void k_fwd3(const float* __restrict__ zx, int relu, const float* __restrict__ W,
+                                              long B, float* __restrict__ z) {
+  using C = Fw3Cfg<CIN, COUT, H>;
+  constexpr int G = C::G;
+  __shared__ float smem[4 * C::WAVE_F];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
+  float* sx = smem + w * C::WAVE_F;  // [CIN][R slots][XW] (+pad)
+  for (int i = lane; i < C::WAVE_F; i += 64) sx[i] = 0.f;
+  __builtin_amdgcn_wave_barrier();
+  constexpr int HH = H * H;
+  const long b = (long)blockIdx.x * 4 + w;  // one patch per wave
+  if (b >= B) return;
+  // input rows y0 .. y0 + G - 1 of all CIN channels (zero outside the patch): lane -> NLD floats
+  auto load_rows = [&](int y0, float (&v)[C::NLD]) {
+#pragma unroll
+    for (int i = 0; i < C::NLD; ++i) {
+      const int e = lane * C::NLD + i, c = e / (G * H), rr = (e / H) % G, x = e % H, y = y0 + rr;
+      float t = 0.f;
+      if (y >= 0 && y < H) t = zx[((long)c * B + b) * HH + y * H + x];
+      v[i] = relu ? fmaxf(t, 0.f) : t;
+    }
+  };
+  auto put_rows = [&](int y0, const float (&v)[C::NLD], int ymax) {  // rows y0 .. min(y0 + G - 1, ymax)
+#pragma unroll
+    for (int i = 0; i < C::NLD; ++i) {
+      const int e = lane * C::NLD + i, c = e / (G * H), rr = (e / H) % G, x = e % H, y = y0 + rr;
+      if (y <= ymax) sx[c * C::RSX + ((y + 1 + C::R) % C::R) * C::XW + 1 + x] = v[i];
+    }
+  };
+  {  // prologue: rows -1 .. G into the ring
+    float v[C::NLD];
+    load_rows(-1, v);
+    put_rows(-1, v, G);
+#pragma unroll 1
+    for (int y0 = G - 1; y0 <= G; y0 += G) {
+      load_rows(y0, v);
+      put_rows(y0, v, G);
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  // this lane's output position within the step: row rr0 = r / H, column x0 = r % H
+  const int rr0 = r / H, x0 = r % H;
+  const float* wl = W + (long)r * CIN * 9 + h * 9;  // W[co = cb * 32 + r][ci = 2 j + h][0..8]
+#pragma unroll 1
+  for (int y = 0; y < H; y += G) {
+    float nv[C::NLD];
+    if (y + G < H) load_rows(y + G + 1, nv);  // rows y + G + 1 .. y + 2G (zero past the patch)
+    f32x16 acc[C::NCO];
+#pragma unroll
+    for (int cb = 0; cb < C::NCO; ++cb) acc[cb] = f32x16{};
+    float wc[C::NCO][9], wn[C::NCO][9];
+    auto ldw = [&](int j, float (&wv)[C::NCO][9]) {
+#pragma unroll
+      for (int cb = 0; cb < C::NCO; ++cb)
+#pragma unroll
+        for (int t = 0; t < 9; ++t) wv[cb][t] = wl[(long)cb * 32 * CIN * 9 + j * 18 + t];
+    };
+    ldw(0, wc);
+#pragma unroll 1
+    for (int j = 0; j < CIN / 2; ++j) {
+      if (j + 1 < CIN / 2) ldw(j + 1, wn);
+      const float* xc = sx + (2 * j + h) * C::RSX;
+      float bv[9];
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx)
+          bv[dy * 3 + dx] = xc[((y + rr0 + dy - 1 + 1 + C::R) % C::R) * C::XW + x0 + dx];
+#pragma unroll
+      for (int cb = 0; cb < C::NCO; ++cb)
+#pragma unroll
+        for (int t = 0; t < 9; ++t) acc[cb] = __builtin_amdgcn_mfma_f32_32x32x2f32(wc[cb][t], bv[t], acc[cb], 0, 0, 0);
+      if (j + 1 < CIN / 2) {
+#pragma unroll
+        for (int cb = 0; cb < C::NCO; ++cb)
+#pragma unroll
+          for (int t = 0; t < 9; ++t) wc[cb][t] = wn[cb][t];
+      }
+    }
+    // acc[cb][4q + e]: co = 32 cb + 8q + 4h + e, position r of the step -> CNHW
+#pragma unroll
+    for (int cb = 0; cb < C::NCO; ++cb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int co = 32 * cb + 8 * q + 4 * h + e;
+          z[((long)co * B + b) * HH + (y + rr0) * H + x0] = acc[cb][4 * q + e];
+        }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    if (y + G < H) put_rows(y + G + 1, nv, 1 << 30);
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+  }
+}
+
+template <int CIN, int COUT, int H>
+hipError_t fwd3(const float* zx, bool relu, const float* W, long B, float* z, hipStream_t st) {
+  hipLaunchKernelGGL((k_fwd3<CIN, COUT, H>), dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, zx, relu ? 1 : 0, W, B, z);
+  return hipGetLastError();
+}
+
 // implicit-im2col convs of one layer (compile-time geometry): the forward Y = W . col and the
 // weight gradient dW = dY . col^T over the whole batch, with no column matrix in memory
 template <int C, int H, int KS, int S, int PAD>
@@ -844,9 +967,14 @@ hipError_t hn_train_forward(const float* in, long B, const float* const* W, floa
     const ActIn a{l == 0 ? xn : reinterpret_cast<const float*>(ws + L.z[l - 1]), l > 0 ? 1 : 0,
                   l == 6 ? drop_p : 0.f, seed};
     float* z = reinterpret_cast<float*>(ws + L.z[l]);
-    if (l >= 1 && l <= 5 && !(hn_knobs().train_f32 & 1))  // conv1..5: the bf16x3 MFMA conv kernels
+    const int tf = hn_knobs().train_f32;
+    if (l >= 1 && l <= 5 && !(tf & 1))  // conv1..5: the bf16x3 MFMA conv kernels
       HCK(conv_bf16x3(l, false, a.z, true, B, W[l], z, ws, L, st));
-    else
+    else if ((l == 1 || l == 3 || l == 5) && !(tf & 8)) {  // stride-1 3x3: k_fwd3 (f32 MFMA)
+      if (l == 1) HCK((fwd3<32, 32, 32>(a.z, true, W[l], B, z, st)));
+      if (l == 3) HCK((fwd3<64, 64, 16>(a.z, true, W[l], B, z, st)));
+      if (l == 5) HCK((fwd3<128, 128, 8>(a.z, true, W[l], B, z, st)));
+    } else
       HCK(conv_fwd_l(l, a, B, W[l], S.cout, z, reinterpret_cast<float*>(ws + L.part), st));  // Y = W . im2col(a)
     {
       const int NS = bn_slices(S.cout, B * hw);
