@@ -784,6 +784,15 @@ __global__ __launch_bounds__(256) void k_fwd3(const float* __restrict__ zx, int 
   }
 }
 
+// W'[ci][co][tap] = W[co][ci][8 - tap]: the data gradient of a stride-1 3x3 conv is the same conv
+// of dY with these weights
+__global__ __launch_bounds__(256) void k_wflip(const float* __restrict__ w, int cout, int cin, float* __restrict__ wf) {
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (long)cout * cin * 9) return;
+  const int t = (int)(e % 9), ci = (int)((e / 9) % cin), co = (int)(e / (9L * cin));
+  wf[((long)ci * cout + co) * 9 + 8 - t] = w[e];
+}
+
 template <int CIN, int COUT, int H>
 hipError_t fwd3(const float* zx, bool relu, const float* W, long B, float* z, hipStream_t st) {
   hipLaunchKernelGGL((k_fwd3<CIN, COUT, H>), dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, zx, relu ? 1 : 0, W, B, z);
@@ -1035,7 +1044,16 @@ hipError_t hn_train_backward(const float* dout, long B, const float* const* W, f
     } else {
       HCK(conv_wgrad_l(l, a, B, g, S.cout, dW[l], part, st));
     }
-    if (want_in && S.s == 1 && S.ks == 3 && l >= 1 && !(hn_knobs().train_f32 & 2)) {
+    if (want_in && S.s == 1 && S.ks == 3 && l >= 1 && !(hn_knobs().train_f32 & 16)) {
+      // stride-1 3x3 (Cin = Cout): the data gradient is k_fwd3 over dY with the flipped weights
+      float* wf = reinterpret_cast<float*>(ws + L.wt);
+      hipLaunchKernelGGL(k_wflip, dim3((unsigned)((S.cout * S.cin * 9 + 255) / 256)), dim3(256), 0, st, W[l], S.cout,
+                         S.cin, wf);
+      HCK(hipGetLastError());
+      if (l == 1) HCK((fwd3<32, 32, 32>(g, false, wf, B, gin, st)));
+      if (l == 3) HCK((fwd3<64, 64, 16>(g, false, wf, B, gin, st)));
+      if (l == 5) HCK((fwd3<128, 128, 8>(g, false, wf, B, gin, st)));
+    } else if (want_in && S.s == 1 && S.ks == 3 && l >= 1 && !(hn_knobs().train_f32 & 2)) {
       // stride-1 3x3 (conv1 / conv3 / conv5: Cin = Cout): the data gradient is the same conv with
       // the weights flipped and transposed, on the bf16x3 MFMA conv kernels
       HCK(conv_bf16x3(l, true, g, false, B, W[l], gin, ws, L, st));
