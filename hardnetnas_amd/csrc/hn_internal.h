@@ -17,10 +17,12 @@ struct HnKnobs {
   bool pairdist_valu = false;  // HN_PAIRDIST_VALU: fp32 VALU pair-distance kernel
   int train_splitk = 1024;     // HN_TRAIN_SPLITK: K per split-K slice of the train GEMMs
   int train_f32 = 1;           // HN_TRAIN_F32: bit 0 train forward convs, bit 1 stride-1 dgrads as f32-MFMA
-                               // GEMMs (else the bf16x3 conv kernels); default 1 = bf16x3 dgrads only;
+                               // GEMMs (else the bf16x3 conv kernels); default 1 = every product f32;
                                // bit 2: stride-1 weight gradients as the generic GEMM (else k_wgrad3);
                                // bit 3: stride-1 f32 forwards as the generic GEMM (else k_fwd3);
-                               // bit 4: stride-1 dgrads not as k_fwd3 over dY (then bit 1 decides)
+                               // bit 4: stride-1 dgrads not as k_fwd3 over dY (then bit 1 decides);
+                               // bit 5: stride-2 layers as the generic GEMM + col2im (else k_fwd2 /
+                               // k_wgrad2 / k_dgrad2)
   int c12_abl = 0;             // HN_C12_ABL (HN_EXPERIMENTS only)
   int dbg = 0;                 // HN_DEBUG (HN_EXPERIMENTS only)
 };

@@ -799,6 +799,377 @@ hipError_t fwd3(const float* zx, bool relu, const float* W, long B, float* z, hi
   return hipGetLastError();
 }
 
+// ------------------------------------------------------------------------------------------
+// the stride-2 3x3 pad-1 layers (conv2: 32 -> 64 at 32 -> 16, conv4: 64 -> 128 at 16 -> 8), the same
+// per-wave LDS streaming on the f32 MFMA as the stride-1 kernels above.
+//
+// k_fwd2: forward.  Output rows y .. y + G - 1 (G = 32 / HO: 32 positions = the MFMA's N) read
+// input rows 2y - 1 .. 2y + 2G - 1 from a ring of R = 2G + 1 rows of all CIN channels (column 0 is
+// the zero pad at x = -1, the ring starts zeroed, so row -1 is the zero pad too); each step loads
+// the next 2G rows while its MFMAs run.
+// ------------------------------------------------------------------------------------------
+template <int CIN, int COUT, int HI>
+struct Fw2Cfg {
+  static constexpr int HO = HI / 2, G = 32 / HO, R = 2 * G + 1;
+  static constexpr int XW = HI + 1;
+  static constexpr int RSX = (R * XW) | 1;
+  static constexpr int WAVE_F = CIN * RSX;
+  static constexpr int NCO = COUT / 32;
+  static constexpr int NLD = 2 * G * CIN * HI / 64;  // floats per lane of one step's 2G new rows
+  static_assert(32 % HO == 0 && (2 * G * CIN * HI) % 64 == 0 && HO >= G, "geometry");
+};
+
+template <int CIN, int COUT, int HI>
+__global__ __launch_bounds__(256) void k_fwd2(const float* __restrict__ zx, int relu, const float* __restrict__ W,
+                                              long B, float* __restrict__ z) {
+  using C = Fw2Cfg<CIN, COUT, HI>;
+  constexpr int G = C::G, HO = C::HO, HHI = HI * HI;
+  __shared__ float smem[4 * C::WAVE_F];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
+  float* sx = smem + w * C::WAVE_F;  // [CIN][R slots][XW] (+pad); input row k in slot (k + 1) % R
+  for (int i = lane; i < C::WAVE_F; i += 64) sx[i] = 0.f;
+  __builtin_amdgcn_wave_barrier();
+  const long b = (long)blockIdx.x * 4 + w;
+  if (b >= B) return;
+  auto load_rows = [&](int y0, float (&v)[C::NLD]) {  // input rows y0 .. y0 + 2G - 1 (all in the patch)
+#pragma unroll
+    for (int i = 0; i < C::NLD; ++i) {
+      const int e = lane * C::NLD + i, c = e / (2 * G * HI), rr = (e / HI) % (2 * G), x = e % HI;
+      const float t = zx[((long)c * B + b) * HHI + (y0 + rr) * HI + x];
+      v[i] = relu ? fmaxf(t, 0.f) : t;
+    }
+  };
+  auto put_rows = [&](int y0, const float (&v)[C::NLD]) {
+#pragma unroll
+    for (int i = 0; i < C::NLD; ++i) {
+      const int e = lane * C::NLD + i, c = e / (2 * G * HI), rr = (e / HI) % (2 * G), x = e % HI;
+      sx[c * C::RSX + ((y0 + rr + 1) % C::R) * C::XW + 1 + x] = v[i];
+    }
+  };
+  {
+    float v[C::NLD];
+    load_rows(0, v);
+    put_rows(0, v);
+  }
+  __builtin_amdgcn_wave_barrier();
+  const int rr0 = r / HO, x0 = r % HO;
+  const float* wl = W + (long)r * CIN * 9 + h * 9;  // W[co = cb * 32 + r][ci = 2 j + h][0..8]
+#pragma unroll 1
+  for (int y = 0; y < HO; y += G) {
+    float nv[C::NLD];
+    if (y + G < HO) load_rows(2 * (y + G), nv);
+    f32x16 acc[C::NCO];
+#pragma unroll
+    for (int cb = 0; cb < C::NCO; ++cb) acc[cb] = f32x16{};
+    float wc[C::NCO][9], wn[C::NCO][9];
+    auto ldw = [&](int j, float (&wv)[C::NCO][9]) {
+#pragma unroll
+      for (int cb = 0; cb < C::NCO; ++cb)
+#pragma unroll
+        for (int t = 0; t < 9; ++t) wv[cb][t] = wl[(long)cb * 32 * CIN * 9 + j * 18 + t];
+    };
+    ldw(0, wc);
+#pragma unroll 1
+    for (int j = 0; j < CIN / 2; ++j) {
+      if (j + 1 < CIN / 2) ldw(j + 1, wn);
+      const float* xc = sx + (2 * j + h) * C::RSX;
+      float bv[9];
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy)  // input row 2 (y + rr0) + dy - 1 -> slot (2 (y + rr0) + dy) % R
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx) bv[dy * 3 + dx] = xc[((2 * (y + rr0) + dy) % C::R) * C::XW + 2 * x0 + dx];
+#pragma unroll
+      for (int cb = 0; cb < C::NCO; ++cb)
+#pragma unroll
+        for (int t = 0; t < 9; ++t) acc[cb] = __builtin_amdgcn_mfma_f32_32x32x2f32(wc[cb][t], bv[t], acc[cb], 0, 0, 0);
+      if (j + 1 < CIN / 2) {
+#pragma unroll
+        for (int cb = 0; cb < C::NCO; ++cb)
+#pragma unroll
+          for (int t = 0; t < 9; ++t) wc[cb][t] = wn[cb][t];
+      }
+    }
+#pragma unroll
+    for (int cb = 0; cb < C::NCO; ++cb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int co = 32 * cb + 8 * q + 4 * h + e;
+          z[((long)co * B + b) * (HO * HO) + (y + rr0) * HO + x0] = acc[cb][4 * q + e];
+        }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    if (y + G < HO) put_rows(2 * (y + G), nv);
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+  }
+}
+
+template <int CIN, int COUT, int HI>
+hipError_t fwd2(const float* zx, bool relu, const float* W, long B, float* z, hipStream_t st) {
+  hipLaunchKernelGGL((k_fwd2<CIN, COUT, HI>), dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, zx, relu ? 1 : 0, W, B, z);
+  return hipGetLastError();
+}
+
+// k_dgrad2: data gradient, without the 3 of 4 zero taps of the transposed conv.  Input pixel
+// (2m + py, 2n + px) of channel ci collects W[co][ci][ky][kx] . dY[co][m + (ky == 0)][n + (kx == 0)]
+// over its parity class's taps (py = 0: ky = 1; py = 1: ky = 2 at m and ky = 0 at m + 1; the same
+// in x): 1 + 2 + 2 + 4 = 9 MFMAs per output-channel pair for the four pixels of a 2x2 cell.  A wave
+// owns whole patches; per step of G = 32 / HO cell rows it reads dY rows m .. m + G of all CO
+// channels from its LDS ring (row HO and column HO are zero) and W[co][ci][0..8] from L2 (no flip),
+// and stores each cell row pair (px = 0, 1) as one float2.
+template <int CO, int CI, int HO>
+struct Dg2Cfg {
+  static constexpr int G = 32 / HO, R = G + 1, XW = HO + 1;
+  static constexpr int RSX = (R * XW) | 1;
+  static constexpr int WAVE_F = CO * RSX;
+  static constexpr int NCI = CI / 32;
+  static constexpr int NLD = G * CO * HO / 64;
+  static_assert(32 % HO == 0 && (G * CO * HO) % 64 == 0 && HO >= G, "geometry");
+};
+
+template <int CO, int CI, int HO>
+__global__ __launch_bounds__(256) void k_dgrad2(const float* __restrict__ dY, const float* __restrict__ W, long B,
+                                                float* __restrict__ din) {
+  using C = Dg2Cfg<CO, CI, HO>;
+  constexpr int G = C::G, HI = 2 * HO, HH = HO * HO;
+  __shared__ float smem[4 * C::WAVE_F];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
+  float* sx = smem + w * C::WAVE_F;  // [CO][R slots][XW]; dY row k in slot k % R
+  for (int i = lane; i < C::WAVE_F; i += 64) sx[i] = 0.f;
+  __builtin_amdgcn_wave_barrier();
+  const long b = (long)blockIdx.x * 4 + w;
+  if (b >= B) return;
+  auto load_rows = [&](int y0, float (&v)[C::NLD]) {  // dY rows y0 .. y0 + G - 1 (zero past the patch)
+#pragma unroll
+    for (int i = 0; i < C::NLD; ++i) {
+      const int e = lane * C::NLD + i, c = e / (G * HO), rr = (e / HO) % G, x = e % HO, y = y0 + rr;
+      v[i] = y < HO ? dY[((long)c * B + b) * HH + y * HO + x] : 0.f;
+    }
+  };
+  auto put_rows = [&](int y0, const float (&v)[C::NLD], int ymax) {
+#pragma unroll
+    for (int i = 0; i < C::NLD; ++i) {
+      const int e = lane * C::NLD + i, c = e / (G * HO), rr = (e / HO) % G, x = e % HO, y = y0 + rr;
+      if (y <= ymax) sx[c * C::RSX + (y % C::R) * C::XW + x] = v[i];
+    }
+  };
+  {  // prologue: rows 0 .. G
+    float v[C::NLD];
+    load_rows(0, v);
+    put_rows(0, v, G);
+    load_rows(G, v);
+    put_rows(G, v, G);
+  }
+  __builtin_amdgcn_wave_barrier();
+  const int rr0 = r / HO, n0 = r % HO;
+  const float* wl = W + ((long)h * CI + r) * 9;  // W[co = 2 j + h][ci = cb * 32 + r][0..8]
+#pragma unroll 1
+  for (int y = 0; y < HO; y += G) {
+    float nv[C::NLD];
+    if (y + G < HO) load_rows(y + G + 1, nv);
+    f32x16 acc[4][C::NCI];  // [2 py + px][ci block]
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int cb = 0; cb < C::NCI; ++cb) acc[k][cb] = f32x16{};
+    float wc[C::NCI][9], wn[C::NCI][9];
+    auto ldw = [&](int j, float (&wv)[C::NCI][9]) {
+#pragma unroll
+      for (int cb = 0; cb < C::NCI; ++cb)
+#pragma unroll
+        for (int t = 0; t < 9; ++t) wv[cb][t] = wl[(long)j * 2 * CI * 9 + cb * 32 * 9 + t];
+    };
+    ldw(0, wc);
+#pragma unroll 1
+    for (int j = 0; j < CO / 2; ++j) {
+      if (j + 1 < CO / 2) ldw(j + 1, wn);
+      const float* xc = sx + (2 * j + h) * C::RSX;
+      const int s0 = ((y + rr0) % C::R) * C::XW + n0, s1 = ((y + rr0 + 1) % C::R) * C::XW + n0;
+      const float b00 = xc[s0], b01 = xc[s0 + 1], b10 = xc[s1], b11 = xc[s1 + 1];
+#pragma unroll
+      for (int cb = 0; cb < C::NCI; ++cb) {
+        acc[0][cb] = __builtin_amdgcn_mfma_f32_32x32x2f32(wc[cb][4], b00, acc[0][cb], 0, 0, 0);
+        acc[1][cb] = __builtin_amdgcn_mfma_f32_32x32x2f32(wc[cb][5], b00, acc[1][cb], 0, 0, 0);
+        acc[2][cb] = __builtin_amdgcn_mfma_f32_32x32x2f32(wc[cb][7], b00, acc[2][cb], 0, 0, 0);
+        acc[3][cb] = __builtin_amdgcn_mfma_f32_32x32x2f32(wc[cb][8], b00, acc[3][cb], 0, 0, 0);
+        acc[1][cb] = __builtin_amdgcn_mfma_f32_32x32x2f32(wc[cb][3], b01, acc[1][cb], 0, 0, 0);
+        acc[3][cb] = __builtin_amdgcn_mfma_f32_32x32x2f32(wc[cb][6], b01, acc[3][cb], 0, 0, 0);
+        acc[2][cb] = __builtin_amdgcn_mfma_f32_32x32x2f32(wc[cb][1], b10, acc[2][cb], 0, 0, 0);
+        acc[3][cb] = __builtin_amdgcn_mfma_f32_32x32x2f32(wc[cb][2], b10, acc[3][cb], 0, 0, 0);
+        acc[3][cb] = __builtin_amdgcn_mfma_f32_32x32x2f32(wc[cb][0], b11, acc[3][cb], 0, 0, 0);
+      }
+      if (j + 1 < CO / 2) {
+#pragma unroll
+        for (int cb = 0; cb < C::NCI; ++cb)
+#pragma unroll
+          for (int t = 0; t < 9; ++t) wc[cb][t] = wn[cb][t];
+      }
+    }
+    // acc[2 py + px][cb][4q + e]: ci = 32 cb + 8q + 4h + e, input pixel (2 (y + rr0) + py, 2 n0 + px)
+#pragma unroll
+    for (int cb = 0; cb < C::NCI; ++cb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int ci = 32 * cb + 8 * q + 4 * h + e;
+          float* o = din + ((long)ci * B + b) * (HI * HI) + 2 * (y + rr0) * HI + 2 * n0;
+#pragma unroll
+          for (int py = 0; py < 2; ++py)
+            *reinterpret_cast<float2*>(o + py * HI) = make_float2(acc[2 * py][cb][4 * q + e], acc[2 * py + 1][cb][4 * q + e]);
+        }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    if (y + G < HO) put_rows(y + G + 1, nv, 1 << 30);
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+  }
+}
+
+template <int CO, int CI, int HO>
+hipError_t dgrad2(const float* dY, const float* W, long B, float* din, hipStream_t st) {
+  hipLaunchKernelGGL((k_dgrad2<CO, CI, HO>), dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, dY, W, B, din);
+  return hipGetLastError();
+}
+
+// k_wgrad2: weight gradient, k_wgrad3's streaming with the stride: per output row y the wave holds
+// the dY row and X rows 2y - 1, 2y, 2y + 1 (ring of 3, column 0 = the zero pad at x = -1), so tap
+// (dy, dx) of position x is the ds_read at column 2x + dx.  Chunk = 2048 / HO^2 patches (>= 4).
+template <int CIN, int COUT, int HO>
+struct Wg2Cfg {
+  static constexpr int HI = 2 * HO;
+  static constexpr int NPC = 2048 / (HO * HO) >= 4 ? 2048 / (HO * HO) : 4;
+  static constexpr int NPW = NPC / 4;
+  static constexpr int RSY = HO + 1;
+  static constexpr int XW = HI + 1;
+  static constexpr int RSX = (3 * XW) | 1;
+  static constexpr int WAVE_F = 32 * RSY + 32 * RSX;
+  static constexpr int NCO = COUT / 32, NCI = CIN / 32;
+  static constexpr int NPY = 32 * HO / 64, NPX = 32 * HI / 64;  // floats per lane of a dY / X row
+  static_assert(NPY >= 1 && NPC % 4 == 0 && HO % 2 == 0, "geometry");
+};
+
+template <int CIN, int COUT, int HO>
+__global__ __launch_bounds__(256) void k_wgrad2(const float* __restrict__ zx, const float* __restrict__ dY, long B,
+                                                float* __restrict__ part) {
+  using C = Wg2Cfg<CIN, COUT, HO>;
+  constexpr int HI = C::HI;
+  __shared__ float smem[4 * C::WAVE_F];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
+  const int blk = blockIdx.x, co0 = (blk / C::NCI) * 32, ci0 = (blk % C::NCI) * 32;
+  const long chunk = blockIdx.y;
+  float* sy = smem + w * C::WAVE_F;  // [32 co][RSY]
+  float* sx = sy + 32 * C::RSY;      // [32 ci][3 slots][XW]; X row k in slot (k + 1) % 3
+  for (int i = lane; i < 32 * C::RSX; i += 64) sx[i] = 0.f;
+  __builtin_amdgcn_wave_barrier();
+  f32x16 acc[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) acc[t] = f32x16{};
+  auto load_y = [&](long b, int y, float (&v)[C::NPY]) {
+#pragma unroll
+    for (int i = 0; i < C::NPY; ++i) {
+      const int e = lane * C::NPY + i, c = e / HO, x = e % HO;
+      v[i] = dY[((long)(co0 + c) * B + b) * (HO * HO) + y * HO + x];
+    }
+  };
+  auto put_y = [&](const float (&v)[C::NPY]) {
+#pragma unroll
+    for (int i = 0; i < C::NPY; ++i) {
+      const int e = lane * C::NPY + i, c = e / HO, x = e % HO;
+      sy[c * C::RSY + x] = v[i];
+    }
+  };
+  auto load_x = [&](long b, int y, float (&v)[C::NPX]) {  // relu(X) row y (0 .. HI - 1)
+#pragma unroll
+    for (int i = 0; i < C::NPX; ++i) {
+      const int e = lane * C::NPX + i, c = e / HI, x = e % HI;
+      v[i] = fmaxf(zx[((long)(ci0 + c) * B + b) * (HI * HI) + y * HI + x], 0.f);
+    }
+  };
+  auto put_x = [&](const float (&v)[C::NPX], int y) {
+    const int slot = (y + 1) % 3;
+#pragma unroll
+    for (int i = 0; i < C::NPX; ++i) {
+      const int e = lane * C::NPX + i, c = e / HI, x = e % HI;
+      sx[c * C::RSX + slot * C::XW + 1 + x] = v[i];
+    }
+  };
+#pragma unroll 1
+  for (int pi = 0; pi < C::NPW; ++pi) {
+    const long b = chunk * C::NPC + w + 4 * pi;
+    if (b >= B) break;  // wave-uniform
+    float vy[C::NPY], va[C::NPX], vb[C::NPX];
+    // prologue: X row -1 = zeros (slot 0), rows 0 and 1, dY row 0
+    for (int i = 0; i < C::NPX; ++i) va[i] = 0.f;
+    put_x(va, -1);
+    load_x(b, 0, va); put_x(va, 0);
+    load_x(b, 1, va); put_x(va, 1);
+    load_y(b, 0, vy); put_y(vy);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll 1
+    for (int y = 0; y < HO; ++y) {
+      const bool more = y + 1 < HO;  // prefetch dY row y + 1 and X rows 2y + 2, 2y + 3
+      if (more) {
+        load_y(b, y + 1, vy);
+        load_x(b, 2 * y + 2, va);
+        load_x(b, 2 * y + 3, vb);
+      }
+      const float* xr[3];
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy) xr[dy] = sx + r * C::RSX + ((2 * y + dy) % 3) * C::XW;  // X row 2y + dy - 1
+#pragma unroll
+      for (int m = 0; m < HO / 2; ++m) {  // positions x = 2m + h
+        const int x = 2 * m + h;
+        const float av = sy[r * C::RSY + x];
+#pragma unroll
+        for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+          for (int dx = 0; dx < 3; ++dx)
+            acc[dy * 3 + dx] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, xr[dy][2 * x + dx], acc[dy * 3 + dx], 0, 0, 0);
+      }
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+      if (more) {
+        put_y(vy);
+        put_x(va, 2 * y + 2);
+        put_x(vb, 2 * y + 3);
+      }
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+    }
+  }
+  const long slice = chunk * 4 + w;
+  float* dst = part + slice * (long)COUT * CIN * 9;
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        dst[(long)(co0 + 8 * q + 4 * h + e) * (CIN * 9) + (ci0 + r) * 9 + t] = acc[t][4 * q + e];
+}
+
+template <int CIN, int COUT, int HO>
+hipError_t wgrad2(const float* zx, const float* dY, long B, float* dW, float* part, hipStream_t st) {
+  using C = Wg2Cfg<CIN, COUT, HO>;
+  const long chunks = (B + C::NPC - 1) / C::NPC;
+  hipLaunchKernelGGL((k_wgrad2<CIN, COUT, HO>), dim3(C::NCO * C::NCI, (unsigned)chunks), dim3(256), 0, st, zx, dY,
+                     B, part);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  GemmArgs g{nullptr, nullptr, dW, COUT, (long)CIN * 9, 0, 0, 0, 0, 0, (long)CIN * 9, 1, 1.f, 0.f};
+  hipLaunchKernelGGL(k_splitk_sum, dim3((unsigned)((g.M * g.N + 63) / 64)), dim3(1024), 0, st, g,
+                     (int)(chunks * 4), part);
+  return hipGetLastError();
+}
+
+static long wgrad2_slices(int l, long B) {
+  const int npc = l == 2 ? Wg2Cfg<32, 64, 16>::NPC : l == 4 ? Wg2Cfg<64, 128, 8>::NPC : 0;
+  return npc ? 4 * ((B + npc - 1) / npc) : 0;
+}
+
 // implicit-im2col convs of one layer (compile-time geometry): the forward Y = W . col and the
 // weight gradient dW = dY . col^T over the whole batch, with no column matrix in memory
 template <int C, int H, int KS, int S, int PAD>
@@ -913,9 +1284,9 @@ HnTrainWs hn_train_layout(long B) {
     part = std::max(part, (size_t)L.cout * L.cin * L.ks * L.ks * ((kk + hn_knobs().train_splitk - 1) / hn_knobs().train_splitk) * 4);
   }
   part = std::max(part, (size_t)512 * GBM * GBN * 4);  // small-grid forward splits (S <= ceil(256 / tiles))
-  for (int l = 1; l <= 5; l += 2) {  // k_wgrad3's slices
+  for (int l = 1; l <= 5; ++l) {  // k_wgrad3's / k_wgrad2's slices
     const HnTrainLayer& L = kHardnetTrainLayers[l];
-    part = std::max(part, (size_t)L.cout * L.cin * 9 * wgrad3_slices(l, B) * 4);
+    part = std::max(part, (size_t)L.cout * L.cin * 9 * (wgrad3_slices(l, B) + wgrad2_slices(l, B)) * 4);
   }
   w.part = take(part);
   w.bnpart = take((size_t)128 * kBnSlices * 2 * sizeof(double));
@@ -983,6 +1354,9 @@ hipError_t hn_train_forward(const float* in, long B, const float* const* W, floa
       if (l == 1) HCK((fwd3<32, 32, 32>(a.z, true, W[l], B, z, st)));
       if (l == 3) HCK((fwd3<64, 64, 16>(a.z, true, W[l], B, z, st)));
       if (l == 5) HCK((fwd3<128, 128, 8>(a.z, true, W[l], B, z, st)));
+    } else if ((l == 2 || l == 4) && !(tf & 32)) {  // stride-2 3x3: k_fwd2 (f32 MFMA)
+      if (l == 2) HCK((fwd2<32, 64, 32>(a.z, true, W[l], B, z, st)));
+      if (l == 4) HCK((fwd2<64, 128, 16>(a.z, true, W[l], B, z, st)));
     } else
       HCK(conv_fwd_l(l, a, B, W[l], S.cout, z, reinterpret_cast<float*>(ws + L.part), st));  // Y = W . im2col(a)
     {
@@ -1041,6 +1415,10 @@ hipError_t hn_train_backward(const float* dout, long B, const float* const* W, f
       if (l == 1) HCK((wgrad3<32, 32, 32>(zx, g, B, dW[l], part, st)));
       if (l == 3) HCK((wgrad3<64, 64, 16>(zx, g, B, dW[l], part, st)));
       if (l == 5) HCK((wgrad3<128, 128, 8>(zx, g, B, dW[l], part, st)));
+    } else if ((l == 2 || l == 4) && !(hn_knobs().train_f32 & 32)) {  // stride-2 3x3: k_wgrad2
+      const float* zx = reinterpret_cast<const float*>(ws + L.z[l - 1]);
+      if (l == 2) HCK((wgrad2<32, 64, 16>(zx, g, B, dW[l], part, st)));
+      if (l == 4) HCK((wgrad2<64, 128, 8>(zx, g, B, dW[l], part, st)));
     } else {
       HCK(conv_wgrad_l(l, a, B, g, S.cout, dW[l], part, st));
     }
@@ -1060,6 +1438,10 @@ hipError_t hn_train_backward(const float* dout, long B, const float* const* W, f
     } else if (want_in && S.s == 1 && S.ks == 3) {
       // stride-1 3x3: d a_{l-1} [Cin][B H H] = implicit col2im-gather GEMM Wt . dY (every tap lands)
       HCK(conv_dgrad_l(l, g, B, W[l], S.cout, reinterpret_cast<float*>(ws + L.wt), gin, st));
+    } else if (want_in && (l == 2 || l == 4) && !(hn_knobs().train_f32 & 32)) {
+      // stride-2 3x3: k_dgrad2 (the parity classes' taps only, f32 MFMA)
+      if (l == 2) HCK((dgrad2<64, 32, 16>(g, W[l], B, gin, st)));
+      if (l == 4) HCK((dgrad2<128, 64, 8>(g, W[l], B, gin, st)));
     } else if (want_in) {
       // stride 2 (3 of 4 taps miss a given input pixel) and the 8x8 conv6 (one tap per pixel):
       // dcol [K][n hw] = W^T [K][Cout] . dY, then the gather col2im, in chunks of patches
