@@ -22,7 +22,8 @@ struct HnKnobs {
                                // bit 3: stride-1 f32 forwards as the generic GEMM (else k_fwd3);
                                // bit 4: stride-1 dgrads not as k_fwd3 over dY (then bit 1 decides);
                                // bit 5: stride-2 layers as the generic GEMM + col2im (else k_fwd2 /
-                               // k_wgrad2 / k_dgrad2)
+                               // k_wgrad2 / k_dgrad2); bit 6: conv0 as the generic GEMM (else
+                               // k_fwd0 / k_wgrad0)
   int c12_abl = 0;             // HN_C12_ABL (HN_EXPERIMENTS only)
   int dbg = 0;                 // HN_DEBUG (HN_EXPERIMENTS only)
 };

@@ -532,6 +532,25 @@ __global__ __launch_bounds__(256) void k_nhwc_to_cnhw(const float* __restrict__ 
 
 unsigned grid_for(long n) { return (unsigned)std::min<long>((n + 255) / 256, 65536); }
 
+// conv6's data gradient (8x8 kernel over an 8x8 input, one output position): the column matrix
+// dcol [(ci, p)][b] = W^T . dY is the gradient itself, in [ci][p][b] order -- transpose each ci's
+// 64 x n block to [ci][b][p] through an LDS tile (coalesced on both sides)
+__global__ __launch_bounds__(256) void k_col6_to_cnhw(const float* __restrict__ dcol, long B, long n0, long n,
+                                                      float* __restrict__ din) {
+  __shared__ float tile[64][65];
+  const int ci = blockIdx.x, t = threadIdx.x;
+  const long b0 = (long)blockIdx.y * 64;
+  for (int i = t; i < 64 * 64; i += 256) {
+    const int p = i >> 6, bb = i & 63;
+    tile[p][bb] = b0 + bb < n ? dcol[((long)ci * 64 + p) * n + b0 + bb] : 0.f;
+  }
+  __syncthreads();
+  for (int i = t; i < 64 * 64; i += 256) {
+    const int bb = i >> 6, p = i & 63;
+    if (b0 + bb < n) din[((long)ci * B + n0 + b0 + bb) * 64 + p] = tile[p][bb];
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // weight gradient of a stride-1 3x3 layer (conv1 / conv3 / conv5):
 //   dW[co][ci][tap] = sum over (b, y, x) of dY[co][b][y][x] . X[ci][b][y + dy - 1][x + dx - 1]
@@ -1165,6 +1184,117 @@ hipError_t wgrad2(const float* zx, const float* dY, long B, float* dW, float* pa
   return hipGetLastError();
 }
 
+// ------------------------------------------------------------------------------------------
+// conv0 (1 -> 32, 3x3, pad 1, on the normalised patch xn [B][32][32]): the 9 taps are the MFMA's
+// K (forward: 5 K-pairs, tap 9 zero) or its N (weight gradient: columns 0..8 of the 32).
+// k_fwd0: one wave per patch, the patch in LDS with a zero frame; output row y = one 32-position
+// tile: z[co][b][y][x] = sum_t W[co][t] . xn[y + t / 3 - 1][x + t % 3 - 1].
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_fwd0(const float* __restrict__ xn, const float* __restrict__ W, long B,
+                                              float* __restrict__ z) {
+  __shared__ float smem[4][34 * 34 + 2];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
+  float* s = smem[w];
+  for (int i = lane; i < 34 * 34; i += 64) s[i] = 0.f;
+  __builtin_amdgcn_wave_barrier();
+  const long b = (long)blockIdx.x * 4 + w;
+  if (b >= B) return;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int e = lane + 64 * i;
+    s[(e / 32 + 1) * 34 + e % 32 + 1] = xn[b * 1024 + e];
+  }
+  __builtin_amdgcn_wave_barrier();
+  float a[5];  // A[m = co r][k = tap 2 j + h]
+#pragma unroll
+  for (int j = 0; j < 5; ++j) a[j] = 2 * j + h < 9 ? W[r * 9 + 2 * j + h] : 0.f;
+#pragma unroll 2
+  for (int y = 0; y < 32; ++y) {
+    f32x16 acc = f32x16{};
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      const int t = 2 * j + h;
+      const float bv = t < 9 ? s[(y + t / 3) * 34 + r + t % 3] : 0.f;
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[j], bv, acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) z[((long)(8 * q + 4 * h + e) * B + b) * 1024 + y * 32 + r] = acc[4 * q + e];
+  }
+}
+
+// k_wgrad0: dW[co][t] = sum over (b, y, x) of dY[co][b][y][x] . xn[b][y + t / 3 - 1][x + t % 3 - 1]:
+// A[m = co][k = position pair] from the wave's LDS dY row, B[k][n = tap] from the patch in LDS
+// (taps 9..31 zero), one MFMA per position pair; NPC patches per workgroup chunk, one split-K slice
+// per wave.
+constexpr int kWg0Npc = 8;
+__global__ __launch_bounds__(256) void k_wgrad0(const float* __restrict__ xn, const float* __restrict__ dY, long B,
+                                                float* __restrict__ part) {
+  __shared__ float smem[4][34 * 34 + 32 * 33 + 2];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
+  float* sx = smem[w];
+  float* sy = sx + 34 * 34;  // [32 co][33]
+  for (int i = lane; i < 34 * 34; i += 64) sx[i] = 0.f;
+  __builtin_amdgcn_wave_barrier();
+  const int tdy = r < 9 ? r / 3 : 0, tdx = r < 9 ? r % 3 : 0;
+  f32x16 acc = f32x16{};
+#pragma unroll 1
+  for (int pi = 0; pi < kWg0Npc / 4; ++pi) {
+    const long b = (long)blockIdx.x * kWg0Npc + w + 4 * pi;
+    if (b >= B) break;  // wave-uniform
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int e = lane + 64 * i;
+      sx[(e / 32 + 1) * 34 + e % 32 + 1] = xn[b * 1024 + e];
+    }
+    float vy[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {  // dY row 0: lane -> channel (lane * 16 + i) / 32
+      const int e = lane * 16 + i;
+      vy[i] = dY[((long)(e / 32) * B + b) * 1024 + e % 32];
+    }
+#pragma unroll 1
+    for (int y = 0; y < 32; ++y) {
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int e = lane * 16 + i;
+        sy[(e / 32) * 33 + e % 32] = vy[i];
+      }
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+      if (y + 1 < 32) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int e = lane * 16 + i;
+          vy[i] = dY[((long)(e / 32) * B + b) * 1024 + (y + 1) * 32 + e % 32];
+        }
+      }
+      const float* xr = sx + (y + tdy) * 34 + tdx;
+#pragma unroll
+      for (int m = 0; m < 16; ++m) {
+        const int x = 2 * m + h;
+        const float bv = r < 9 ? xr[x] : 0.f;
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(sy[r * 33 + x], bv, acc, 0, 0, 0);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+  }
+  // acc[4q + e] = dW[co = 8q + 4h + e][tap r] (r < 9)
+  float* dst = part + ((long)blockIdx.x * 4 + w) * 288;
+  if (r < 9)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) dst[(8 * q + 4 * h + e) * 9 + r] = acc[4 * q + e];
+}
+
+static long wgrad0_slices(long B) { return 4 * ((B + kWg0Npc - 1) / kWg0Npc); }
+
 static long wgrad2_slices(int l, long B) {
   const int npc = l == 2 ? Wg2Cfg<32, 64, 16>::NPC : l == 4 ? Wg2Cfg<64, 128, 8>::NPC : 0;
   return npc ? 4 * ((B + npc - 1) / npc) : 0;
@@ -1284,6 +1414,7 @@ HnTrainWs hn_train_layout(long B) {
     part = std::max(part, (size_t)L.cout * L.cin * L.ks * L.ks * ((kk + hn_knobs().train_splitk - 1) / hn_knobs().train_splitk) * 4);
   }
   part = std::max(part, (size_t)512 * GBM * GBN * 4);  // small-grid forward splits (S <= ceil(256 / tiles))
+  part = std::max(part, (size_t)32 * 9 * wgrad0_slices(B) * 4);  // k_wgrad0's slices
   for (int l = 1; l <= 5; ++l) {  // k_wgrad3's / k_wgrad2's slices
     const HnTrainLayer& L = kHardnetTrainLayers[l];
     part = std::max(part, (size_t)L.cout * L.cin * 9 * (wgrad3_slices(l, B) + wgrad2_slices(l, B)) * 4);
@@ -1348,7 +1479,10 @@ hipError_t hn_train_forward(const float* in, long B, const float* const* W, floa
                   l == 6 ? drop_p : 0.f, seed};
     float* z = reinterpret_cast<float*>(ws + L.z[l]);
     const int tf = hn_knobs().train_f32;
-    if (l >= 1 && l <= 5 && !(tf & 1))  // conv1..5: the bf16x3 MFMA conv kernels
+    if (l == 0 && !(tf & 64)) {  // conv0: k_fwd0 (taps as the MFMA's K)
+      hipLaunchKernelGGL(k_fwd0, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, xn, W[0], B, z);
+      HCK(hipGetLastError());
+    } else if (l >= 1 && l <= 5 && !(tf & 1))  // conv1..5: the bf16x3 MFMA conv kernels
       HCK(conv_bf16x3(l, false, a.z, true, B, W[l], z, ws, L, st));
     else if ((l == 1 || l == 3 || l == 5) && !(tf & 8)) {  // stride-1 3x3: k_fwd3 (f32 MFMA)
       if (l == 1) HCK((fwd3<32, 32, 32>(a.z, true, W[l], B, z, st)));
@@ -1410,7 +1544,14 @@ hipError_t hn_train_backward(const float* dout, long B, const float* const* W, f
     const bool want_in = l > 0 || din;
     // dW [Cout][K] = dY [Cout][B hw] . im2col(a)^T (split-K slices summed in fp64)
     float* part = reinterpret_cast<float*>(ws + L.part);
-    if ((l == 1 || l == 3 || l == 5) && !(hn_knobs().train_f32 & 4)) {  // stride-1 3x3: k_wgrad3
+    if (l == 0 && !(hn_knobs().train_f32 & 64)) {  // conv0: k_wgrad0 (taps as the MFMA's N)
+      const long ns = wgrad0_slices(B);
+      hipLaunchKernelGGL(k_wgrad0, dim3((unsigned)(ns / 4)), dim3(256), 0, st, xn, g, B, part);
+      HCK(hipGetLastError());
+      GemmArgs gs{nullptr, nullptr, dW[0], 32, 9, 0, 0, 0, 0, 0, 9, 1, 1.f, 0.f};
+      hipLaunchKernelGGL(k_splitk_sum, dim3((unsigned)((32 * 9 + 63) / 64)), dim3(1024), 0, st, gs, (int)ns, part);
+      HCK(hipGetLastError());
+    } else if ((l == 1 || l == 3 || l == 5) && !(hn_knobs().train_f32 & 4)) {  // stride-1 3x3: k_wgrad3
       const float* zx = reinterpret_cast<const float*>(ws + L.z[l - 1]);
       if (l == 1) HCK((wgrad3<32, 32, 32>(zx, g, B, dW[l], part, st)));
       if (l == 3) HCK((wgrad3<64, 64, 16>(zx, g, B, dW[l], part, st)));
@@ -1451,8 +1592,12 @@ hipError_t hn_train_backward(const float* dout, long B, const float* const* W, f
         const long n = std::min(nc, B - n0);
         GemmArgs gd{W[l], g + n0 * hw, col, K, n * hw, S.cout, 1, K, B * hw, 1, n * hw, 1, 1.f, 0.f};
         HCK(gemm(gd, st));
-        hipLaunchKernelGGL(k_col2im, dim3(grid_for((long)S.cin * n * S.hin * S.hin)), dim3(256), 0, st, col,
-                           S.cin, B, S.hin, S.hin, S.ks, S.s, S.pad, (int)ho, (int)ho, n0, n, gin);
+        if (S.ks == 8 && ho == 1)  // conv6: the column matrix is the gradient, transposed
+          hipLaunchKernelGGL(k_col6_to_cnhw, dim3(S.cin, (unsigned)((n + 63) / 64)), dim3(256), 0, st, col, B, n0,
+                             n, gin);
+        else
+          hipLaunchKernelGGL(k_col2im, dim3(grid_for((long)S.cin * n * S.hin * S.hin)), dim3(256), 0, st, col,
+                             S.cin, B, S.hin, S.hin, S.ks, S.s, S.pad, (int)ho, (int)ho, n0, n, gin);
         HCK(hipGetLastError());
       }
     }

@@ -17,8 +17,11 @@ from hardnetnas_amd.model import HardNet  # noqa: E402
 dev = torch.device("cuda:0")
 pairs = int(os.environ.get("PAIRS", "1024"))
 steps = int(os.environ.get("STEPS", "10"))
+legs = os.environ.get("LEGS", "hip,torch_miopen").split(",")  # LEGS=hip: profile the HIP leg alone
 res = {"config": f"HardNet train step, {pairs} pairs ({2 * pairs} patches), loss_HardNet + SGD"}
 for name, native in (("hip", True), ("torch_miopen", False)):
+    if name not in legs:
+        continue
     torch.manual_seed(0)
     m = HardNet().to(dev).train()
     m.native_train = native
