@@ -37,7 +37,7 @@ void hn_read_knobs(HnKnobs* k) {
   k->no_skipfuse = std::getenv("HN_NO_SKIPFUSE") != nullptr;
   k->pairdist_valu = std::getenv("HN_PAIRDIST_VALU") != nullptr;
   k->train_splitk = std::max(32, env_int("HN_TRAIN_SPLITK", 1024)) / 32 * 32;
-  k->train_f32 = env_int("HN_TRAIN_F32", 1) & 127;
+  k->train_f32 = env_int("HN_TRAIN_F32", 1) & 255;
 #ifdef HN_EXPERIMENTS
   k->c12_abl = env_int("HN_C12_ABL", 0) & 255;
   k->dbg = env_int("HN_DEBUG", 0);

@@ -803,6 +803,98 @@ __global__ __launch_bounds__(256) void k_fwd3(const float* __restrict__ zx, int 
   }
 }
 
+// k_fwd3s: k_fwd3 with the ring shared by NWP waves of a workgroup that split the output channels
+// (one 32-channel block each) -- 4 / NWP patches per workgroup.  Per patch one ring instead of NWP,
+// so conv3 (NWP 2, 37 KB per workgroup) and conv5 (NWP 4, 31 KB) run 4-5 waves per SIMD instead
+// of one and the MFMA chains of different waves hide each other's ring and weight loads.
+template <int CIN, int COUT, int H, int NWP>
+__global__ __launch_bounds__(256) void k_fwd3s(const float* __restrict__ zx, int relu, const float* __restrict__ W,
+                                               long B, float* __restrict__ z) {
+  using C = Fw3Cfg<CIN, COUT, H>;
+  constexpr int G = C::G, PPB = 4 / NWP, NLDT = C::NLD / NWP, HH = H * H;
+  static_assert(C::NCO == NWP && C::NLD % NWP == 0, "one 32-channel block per wave");
+  __shared__ float smem[PPB * C::WAVE_F];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
+  const int lp = w / NWP, cb = w % NWP;  // local patch, output-channel block
+  float* sx = smem + lp * C::WAVE_F;
+  for (int i = threadIdx.x; i < PPB * C::WAVE_F; i += 256) smem[i] = 0.f;
+  __syncthreads();
+  const long b = (long)blockIdx.x * PPB + lp;
+  const bool valid = b < B;  // no early return: the waves of a workgroup meet at barriers
+  auto load_rows = [&](int y0, float (&v)[NLDT]) {  // this wave's share of rows y0 .. y0 + G - 1
+#pragma unroll
+    for (int i = 0; i < NLDT; ++i) {
+      const int e = (cb * 64 + lane) * NLDT + i, c = e / (G * H), rr = (e / H) % G, x = e % H, y = y0 + rr;
+      float t = 0.f;
+      if (valid && y >= 0 && y < H) t = zx[((long)c * B + b) * HH + y * H + x];
+      v[i] = relu ? fmaxf(t, 0.f) : t;
+    }
+  };
+  auto put_rows = [&](int y0, const float (&v)[NLDT], int ymax) {
+#pragma unroll
+    for (int i = 0; i < NLDT; ++i) {
+      const int e = (cb * 64 + lane) * NLDT + i, c = e / (G * H), rr = (e / H) % G, x = e % H, y = y0 + rr;
+      if (y <= ymax) sx[c * C::RSX + ((y + 1 + C::R) % C::R) * C::XW + 1 + x] = v[i];
+    }
+  };
+  {
+    float v[NLDT];
+    load_rows(-1, v);
+    put_rows(-1, v, G);
+#pragma unroll 1
+    for (int y0 = G - 1; y0 <= G; y0 += G) {
+      load_rows(y0, v);
+      put_rows(y0, v, G);
+    }
+  }
+  __syncthreads();
+  const int rr0 = r / H, x0 = r % H;
+  const float* wl = W + (long)(cb * 32 + r) * CIN * 9 + h * 9;  // W[co][ci = 2 j + h][0..8]
+#pragma unroll 1
+  for (int y = 0; y < H; y += G) {
+    float nv[NLDT];
+    if (y + G < H) load_rows(y + G + 1, nv);
+    f32x16 acc = f32x16{};
+    float wc[9], wn[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) wc[t] = wl[t];
+#pragma unroll 2
+    for (int j = 0; j < CIN / 2; ++j) {
+      if (j + 1 < CIN / 2)
+#pragma unroll
+        for (int t = 0; t < 9; ++t) wn[t] = wl[(j + 1) * 18 + t];
+      const float* xc = sx + (2 * j + h) * C::RSX;
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx)
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(
+              wc[dy * 3 + dx], xc[((y + rr0 + dy - 1 + 1 + C::R) % C::R) * C::XW + x0 + dx], acc, 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) wc[t] = wn[t];
+    }
+    if (valid)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int co = 32 * cb + 8 * q + 4 * h + e;
+          z[((long)co * B + b) * HH + (y + rr0) * H + x0] = acc[4 * q + e];
+        }
+    __syncthreads();
+    if (y + G < H) put_rows(y + G + 1, nv, 1 << 30);
+    __syncthreads();
+  }
+}
+
+template <int CIN, int COUT, int H>
+hipError_t fwd3s(const float* zx, bool relu, const float* W, long B, float* z, hipStream_t st) {
+  constexpr int NWP = COUT / 32, PPB = 4 / NWP;
+  hipLaunchKernelGGL((k_fwd3s<CIN, COUT, H, NWP>), dim3((unsigned)((B + PPB - 1) / PPB)), dim3(256), 0, st, zx,
+                     relu ? 1 : 0, W, B, z);
+  return hipGetLastError();
+}
+
 // W'[ci][co][tap] = W[co][ci][8 - tap]: the data gradient of a stride-1 3x3 conv is the same conv
 // of dY with these weights
 __global__ __launch_bounds__(256) void k_wflip(const float* __restrict__ w, int cout, int cin, float* __restrict__ wf) {
@@ -838,52 +930,65 @@ struct Fw2Cfg {
   static_assert(32 % HO == 0 && (2 * G * CIN * HI) % 64 == 0 && HO >= G, "geometry");
 };
 
-template <int CIN, int COUT, int HI>
+// NWP waves share one patch's ring and split its output-channel blocks (NWP > 1: 4 / NWP patches
+// per workgroup, workgroup barriers; NWP = 1: one patch per wave, wave barriers).
+template <int CIN, int COUT, int HI, int NWP>
 __global__ __launch_bounds__(256) void k_fwd2(const float* __restrict__ zx, int relu, const float* __restrict__ W,
                                               long B, float* __restrict__ z) {
   using C = Fw2Cfg<CIN, COUT, HI>;
-  constexpr int G = C::G, HO = C::HO, HHI = HI * HI;
-  __shared__ float smem[4 * C::WAVE_F];
+  constexpr int G = C::G, HO = C::HO, HHI = HI * HI, PPB = 4 / NWP, CPW = C::NCO / NWP, NLDT = C::NLD / NWP;
+  static_assert(C::NCO % NWP == 0 && C::NLD % NWP == 0, "split");
+  __shared__ float smem[PPB * C::WAVE_F];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
-  float* sx = smem + w * C::WAVE_F;  // [CIN][R slots][XW] (+pad); input row k in slot (k + 1) % R
-  for (int i = lane; i < C::WAVE_F; i += 64) sx[i] = 0.f;
-  __builtin_amdgcn_wave_barrier();
-  const long b = (long)blockIdx.x * 4 + w;
-  if (b >= B) return;
-  auto load_rows = [&](int y0, float (&v)[C::NLD]) {  // input rows y0 .. y0 + 2G - 1 (all in the patch)
+  const int lp = w / NWP, wp = w % NWP;
+  float* sx = smem + lp * C::WAVE_F;  // [CIN][R slots][XW] (+pad); input row k in slot (k + 1) % R
+  auto sync = [&] {
+    if constexpr (NWP > 1) __syncthreads();
+    else {
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+    }
+  };
+  for (int i = (NWP > 1 ? threadIdx.x : lane); i < (NWP > 1 ? PPB : 1) * C::WAVE_F; i += (NWP > 1 ? 256 : 64))
+    (NWP > 1 ? smem : sx)[i] = 0.f;
+  sync();
+  const long b = (long)blockIdx.x * PPB + lp;
+  const bool valid = b < B;
+  if (NWP == 1 && !valid) return;
+  auto load_rows = [&](int y0, float (&v)[NLDT]) {  // this wave's share of input rows y0 .. y0 + 2G - 1
 #pragma unroll
-    for (int i = 0; i < C::NLD; ++i) {
-      const int e = lane * C::NLD + i, c = e / (2 * G * HI), rr = (e / HI) % (2 * G), x = e % HI;
-      const float t = zx[((long)c * B + b) * HHI + (y0 + rr) * HI + x];
+    for (int i = 0; i < NLDT; ++i) {
+      const int e = (wp * 64 + lane) * NLDT + i, c = e / (2 * G * HI), rr = (e / HI) % (2 * G), x = e % HI;
+      const float t = valid ? zx[((long)c * B + b) * HHI + (y0 + rr) * HI + x] : 0.f;
       v[i] = relu ? fmaxf(t, 0.f) : t;
     }
   };
-  auto put_rows = [&](int y0, const float (&v)[C::NLD]) {
+  auto put_rows = [&](int y0, const float (&v)[NLDT]) {
 #pragma unroll
-    for (int i = 0; i < C::NLD; ++i) {
-      const int e = lane * C::NLD + i, c = e / (2 * G * HI), rr = (e / HI) % (2 * G), x = e % HI;
+    for (int i = 0; i < NLDT; ++i) {
+      const int e = (wp * 64 + lane) * NLDT + i, c = e / (2 * G * HI), rr = (e / HI) % (2 * G), x = e % HI;
       sx[c * C::RSX + ((y0 + rr + 1) % C::R) * C::XW + 1 + x] = v[i];
     }
   };
   {
-    float v[C::NLD];
+    float v[NLDT];
     load_rows(0, v);
     put_rows(0, v);
   }
-  __builtin_amdgcn_wave_barrier();
+  sync();
   const int rr0 = r / HO, x0 = r % HO;
-  const float* wl = W + (long)r * CIN * 9 + h * 9;  // W[co = cb * 32 + r][ci = 2 j + h][0..8]
+  const float* wl = W + (long)(wp * CPW * 32 + r) * CIN * 9 + h * 9;  // W[co = (wp CPW + cb) 32 + r][ci = 2 j + h]
 #pragma unroll 1
   for (int y = 0; y < HO; y += G) {
-    float nv[C::NLD];
+    float nv[NLDT];
     if (y + G < HO) load_rows(2 * (y + G), nv);
-    f32x16 acc[C::NCO];
+    f32x16 acc[CPW];
 #pragma unroll
-    for (int cb = 0; cb < C::NCO; ++cb) acc[cb] = f32x16{};
-    float wc[C::NCO][9], wn[C::NCO][9];
-    auto ldw = [&](int j, float (&wv)[C::NCO][9]) {
+    for (int cb = 0; cb < CPW; ++cb) acc[cb] = f32x16{};
+    float wc[CPW][9], wn[CPW][9];
+    auto ldw = [&](int j, float (&wv)[CPW][9]) {
 #pragma unroll
-      for (int cb = 0; cb < C::NCO; ++cb)
+      for (int cb = 0; cb < CPW; ++cb)
 #pragma unroll
         for (int t = 0; t < 9; ++t) wv[cb][t] = wl[(long)cb * 32 * CIN * 9 + j * 18 + t];
     };
@@ -898,36 +1003,41 @@ __global__ __launch_bounds__(256) void k_fwd2(const float* __restrict__ zx, int 
 #pragma unroll
         for (int dx = 0; dx < 3; ++dx) bv[dy * 3 + dx] = xc[((2 * (y + rr0) + dy) % C::R) * C::XW + 2 * x0 + dx];
 #pragma unroll
-      for (int cb = 0; cb < C::NCO; ++cb)
+      for (int cb = 0; cb < CPW; ++cb)
 #pragma unroll
         for (int t = 0; t < 9; ++t) acc[cb] = __builtin_amdgcn_mfma_f32_32x32x2f32(wc[cb][t], bv[t], acc[cb], 0, 0, 0);
       if (j + 1 < CIN / 2) {
 #pragma unroll
-        for (int cb = 0; cb < C::NCO; ++cb)
+        for (int cb = 0; cb < CPW; ++cb)
 #pragma unroll
           for (int t = 0; t < 9; ++t) wc[cb][t] = wn[cb][t];
       }
     }
+    if (valid)
 #pragma unroll
-    for (int cb = 0; cb < C::NCO; ++cb)
+      for (int cb = 0; cb < CPW; ++cb)
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
+        for (int q = 0; q < 4; ++q)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int co = 32 * cb + 8 * q + 4 * h + e;
-          z[((long)co * B + b) * (HO * HO) + (y + rr0) * HO + x0] = acc[cb][4 * q + e];
-        }
-    __builtin_amdgcn_wave_barrier();
-    asm volatile("" ::: "memory");
+          for (int e = 0; e < 4; ++e) {
+            const int co = 32 * (wp * CPW + cb) + 8 * q + 4 * h + e;
+            z[((long)co * B + b) * (HO * HO) + (y + rr0) * HO + x0] = acc[cb][4 * q + e];
+          }
+    sync();
     if (y + G < HO) put_rows(2 * (y + G), nv);
-    __builtin_amdgcn_wave_barrier();
-    asm volatile("" ::: "memory");
+    sync();
   }
 }
 
 template <int CIN, int COUT, int HI>
-hipError_t fwd2(const float* zx, bool relu, const float* W, long B, float* z, hipStream_t st) {
-  hipLaunchKernelGGL((k_fwd2<CIN, COUT, HI>), dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, zx, relu ? 1 : 0, W, B, z);
+hipError_t fwd2(const float* zx, bool relu, const float* W, long B, float* z, hipStream_t st, bool shared) {
+  constexpr int NWP = COUT / 32 >= 4 ? 4 : COUT / 32;
+  if (shared)
+    hipLaunchKernelGGL((k_fwd2<CIN, COUT, HI, NWP>), dim3((unsigned)((B + 4 / NWP - 1) / (4 / NWP))), dim3(256), 0,
+                       st, zx, relu ? 1 : 0, W, B, z);
+  else
+    hipLaunchKernelGGL((k_fwd2<CIN, COUT, HI, 1>), dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, zx, relu ? 1 : 0,
+                       W, B, z);
   return hipGetLastError();
 }
 
@@ -948,55 +1058,66 @@ struct Dg2Cfg {
   static_assert(32 % HO == 0 && (G * CO * HO) % 64 == 0 && HO >= G, "geometry");
 };
 
-template <int CO, int CI, int HO>
+template <int CO, int CI, int HO, int NWP>
 __global__ __launch_bounds__(256) void k_dgrad2(const float* __restrict__ dY, const float* __restrict__ W, long B,
                                                 float* __restrict__ din) {
   using C = Dg2Cfg<CO, CI, HO>;
-  constexpr int G = C::G, HI = 2 * HO, HH = HO * HO;
-  __shared__ float smem[4 * C::WAVE_F];
+  constexpr int G = C::G, HI = 2 * HO, HH = HO * HO, PPB = 4 / NWP, CPW = C::NCI / NWP, NLDT = C::NLD / NWP;
+  static_assert(C::NCI % NWP == 0 && C::NLD % NWP == 0, "split");
+  __shared__ float smem[PPB * C::WAVE_F];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
-  float* sx = smem + w * C::WAVE_F;  // [CO][R slots][XW]; dY row k in slot k % R
-  for (int i = lane; i < C::WAVE_F; i += 64) sx[i] = 0.f;
-  __builtin_amdgcn_wave_barrier();
-  const long b = (long)blockIdx.x * 4 + w;
-  if (b >= B) return;
-  auto load_rows = [&](int y0, float (&v)[C::NLD]) {  // dY rows y0 .. y0 + G - 1 (zero past the patch)
-#pragma unroll
-    for (int i = 0; i < C::NLD; ++i) {
-      const int e = lane * C::NLD + i, c = e / (G * HO), rr = (e / HO) % G, x = e % HO, y = y0 + rr;
-      v[i] = y < HO ? dY[((long)c * B + b) * HH + y * HO + x] : 0.f;
+  const int lp = w / NWP, wp = w % NWP;  // local patch, this wave's share of the input-channel blocks
+  float* sx = smem + lp * C::WAVE_F;  // [CO][R slots][XW]; dY row k in slot k % R
+  auto sync = [&] {
+    if constexpr (NWP > 1) __syncthreads();
+    else {
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
     }
   };
-  auto put_rows = [&](int y0, const float (&v)[C::NLD], int ymax) {
+  for (int i = (NWP > 1 ? threadIdx.x : lane); i < (NWP > 1 ? PPB : 1) * C::WAVE_F; i += (NWP > 1 ? 256 : 64))
+    (NWP > 1 ? smem : sx)[i] = 0.f;
+  sync();
+  const long b = (long)blockIdx.x * PPB + lp;
+  const bool valid = b < B;
+  if (NWP == 1 && !valid) return;
+  auto load_rows = [&](int y0, float (&v)[NLDT]) {  // dY rows y0 .. y0 + G - 1 (zero past the patch)
 #pragma unroll
-    for (int i = 0; i < C::NLD; ++i) {
-      const int e = lane * C::NLD + i, c = e / (G * HO), rr = (e / HO) % G, x = e % HO, y = y0 + rr;
+    for (int i = 0; i < NLDT; ++i) {
+      const int e = (wp * 64 + lane) * NLDT + i, c = e / (G * HO), rr = (e / HO) % G, x = e % HO, y = y0 + rr;
+      v[i] = valid && y < HO ? dY[((long)c * B + b) * HH + y * HO + x] : 0.f;
+    }
+  };
+  auto put_rows = [&](int y0, const float (&v)[NLDT], int ymax) {
+#pragma unroll
+    for (int i = 0; i < NLDT; ++i) {
+      const int e = (wp * 64 + lane) * NLDT + i, c = e / (G * HO), rr = (e / HO) % G, x = e % HO, y = y0 + rr;
       if (y <= ymax) sx[c * C::RSX + (y % C::R) * C::XW + x] = v[i];
     }
   };
   {  // prologue: rows 0 .. G
-    float v[C::NLD];
+    float v[NLDT];
     load_rows(0, v);
     put_rows(0, v, G);
     load_rows(G, v);
     put_rows(G, v, G);
   }
-  __builtin_amdgcn_wave_barrier();
+  sync();
   const int rr0 = r / HO, n0 = r % HO;
-  const float* wl = W + ((long)h * CI + r) * 9;  // W[co = 2 j + h][ci = cb * 32 + r][0..8]
+  const float* wl = W + ((long)h * CI + wp * CPW * 32 + r) * 9;  // W[co = 2 j + h][ci = (wp CPW + cb) 32 + r]
 #pragma unroll 1
   for (int y = 0; y < HO; y += G) {
-    float nv[C::NLD];
+    float nv[NLDT];
     if (y + G < HO) load_rows(y + G + 1, nv);
-    f32x16 acc[4][C::NCI];  // [2 py + px][ci block]
+    f32x16 acc[4][CPW];  // [2 py + px][ci block]
 #pragma unroll
     for (int k = 0; k < 4; ++k)
 #pragma unroll
-      for (int cb = 0; cb < C::NCI; ++cb) acc[k][cb] = f32x16{};
-    float wc[C::NCI][9], wn[C::NCI][9];
-    auto ldw = [&](int j, float (&wv)[C::NCI][9]) {
+      for (int cb = 0; cb < CPW; ++cb) acc[k][cb] = f32x16{};
+    float wc[CPW][9], wn[CPW][9];
+    auto ldw = [&](int j, float (&wv)[CPW][9]) {
 #pragma unroll
-      for (int cb = 0; cb < C::NCI; ++cb)
+      for (int cb = 0; cb < CPW; ++cb)
 #pragma unroll
         for (int t = 0; t < 9; ++t) wv[cb][t] = wl[(long)j * 2 * CI * 9 + cb * 32 * 9 + t];
     };
@@ -1008,7 +1129,7 @@ __global__ __launch_bounds__(256) void k_dgrad2(const float* __restrict__ dY, co
       const int s0 = ((y + rr0) % C::R) * C::XW + n0, s1 = ((y + rr0 + 1) % C::R) * C::XW + n0;
       const float b00 = xc[s0], b01 = xc[s0 + 1], b10 = xc[s1], b11 = xc[s1 + 1];
 #pragma unroll
-      for (int cb = 0; cb < C::NCI; ++cb) {
+      for (int cb = 0; cb < CPW; ++cb) {
         acc[0][cb] = __builtin_amdgcn_mfma_f32_32x32x2f32(wc[cb][4], b00, acc[0][cb], 0, 0, 0);
         acc[1][cb] = __builtin_amdgcn_mfma_f32_32x32x2f32(wc[cb][5], b00, acc[1][cb], 0, 0, 0);
         acc[2][cb] = __builtin_amdgcn_mfma_f32_32x32x2f32(wc[cb][7], b00, acc[2][cb], 0, 0, 0);
@@ -1021,35 +1142,39 @@ __global__ __launch_bounds__(256) void k_dgrad2(const float* __restrict__ dY, co
       }
       if (j + 1 < CO / 2) {
 #pragma unroll
-        for (int cb = 0; cb < C::NCI; ++cb)
+        for (int cb = 0; cb < CPW; ++cb)
 #pragma unroll
           for (int t = 0; t < 9; ++t) wc[cb][t] = wn[cb][t];
       }
     }
     // acc[2 py + px][cb][4q + e]: ci = 32 cb + 8q + 4h + e, input pixel (2 (y + rr0) + py, 2 n0 + px)
+    if (valid)
 #pragma unroll
-    for (int cb = 0; cb < C::NCI; ++cb)
+    for (int cb = 0; cb < CPW; ++cb)
 #pragma unroll
       for (int q = 0; q < 4; ++q)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const int ci = 32 * cb + 8 * q + 4 * h + e;
+          const int ci = 32 * (wp * CPW + cb) + 8 * q + 4 * h + e;
           float* o = din + ((long)ci * B + b) * (HI * HI) + 2 * (y + rr0) * HI + 2 * n0;
 #pragma unroll
           for (int py = 0; py < 2; ++py)
             *reinterpret_cast<float2*>(o + py * HI) = make_float2(acc[2 * py][cb][4 * q + e], acc[2 * py + 1][cb][4 * q + e]);
         }
-    __builtin_amdgcn_wave_barrier();
-    asm volatile("" ::: "memory");
+    sync();
     if (y + G < HO) put_rows(y + G + 1, nv, 1 << 30);
-    __builtin_amdgcn_wave_barrier();
-    asm volatile("" ::: "memory");
+    sync();
   }
 }
 
 template <int CO, int CI, int HO>
-hipError_t dgrad2(const float* dY, const float* W, long B, float* din, hipStream_t st) {
-  hipLaunchKernelGGL((k_dgrad2<CO, CI, HO>), dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, dY, W, B, din);
+hipError_t dgrad2(const float* dY, const float* W, long B, float* din, hipStream_t st, bool shared) {
+  constexpr int NWP = CI / 32 >= 4 ? 4 : CI / 32;
+  if (shared && NWP > 1)
+    hipLaunchKernelGGL((k_dgrad2<CO, CI, HO, NWP>), dim3((unsigned)((B + 4 / NWP - 1) / (4 / NWP))), dim3(256), 0,
+                       st, dY, W, B, din);
+  else
+    hipLaunchKernelGGL((k_dgrad2<CO, CI, HO, 1>), dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, dY, W, B, din);
   return hipGetLastError();
 }
 
@@ -1486,11 +1611,12 @@ hipError_t hn_train_forward(const float* in, long B, const float* const* W, floa
       HCK(conv_bf16x3(l, false, a.z, true, B, W[l], z, ws, L, st));
     else if ((l == 1 || l == 3 || l == 5) && !(tf & 8)) {  // stride-1 3x3: k_fwd3 (f32 MFMA)
       if (l == 1) HCK((fwd3<32, 32, 32>(a.z, true, W[l], B, z, st)));
-      if (l == 3) HCK((fwd3<64, 64, 16>(a.z, true, W[l], B, z, st)));
-      if (l == 5) HCK((fwd3<128, 128, 8>(a.z, true, W[l], B, z, st)));
+      const bool sh = !(tf & 128);  // conv3 / conv5: the shared-ring form
+      if (l == 3) HCK((sh ? fwd3s<64, 64, 16> : fwd3<64, 64, 16>)(a.z, true, W[l], B, z, st));
+      if (l == 5) HCK((sh ? fwd3s<128, 128, 8> : fwd3<128, 128, 8>)(a.z, true, W[l], B, z, st));
     } else if ((l == 2 || l == 4) && !(tf & 32)) {  // stride-2 3x3: k_fwd2 (f32 MFMA)
-      if (l == 2) HCK((fwd2<32, 64, 32>(a.z, true, W[l], B, z, st)));
-      if (l == 4) HCK((fwd2<64, 128, 16>(a.z, true, W[l], B, z, st)));
+      if (l == 2) HCK((fwd2<32, 64, 32>(a.z, true, W[l], B, z, st, !(tf & 128))));
+      if (l == 4) HCK((fwd2<64, 128, 16>(a.z, true, W[l], B, z, st, !(tf & 128))));
     } else
       HCK(conv_fwd_l(l, a, B, W[l], S.cout, z, reinterpret_cast<float*>(ws + L.part), st));  // Y = W . im2col(a)
     {
@@ -1570,8 +1696,9 @@ hipError_t hn_train_backward(const float* dout, long B, const float* const* W, f
                          S.cin, wf);
       HCK(hipGetLastError());
       if (l == 1) HCK((fwd3<32, 32, 32>(g, false, wf, B, gin, st)));
-      if (l == 3) HCK((fwd3<64, 64, 16>(g, false, wf, B, gin, st)));
-      if (l == 5) HCK((fwd3<128, 128, 8>(g, false, wf, B, gin, st)));
+      const bool sh = !(hn_knobs().train_f32 & 128);
+      if (l == 3) HCK((sh ? fwd3s<64, 64, 16> : fwd3<64, 64, 16>)(g, false, wf, B, gin, st));
+      if (l == 5) HCK((sh ? fwd3s<128, 128, 8> : fwd3<128, 128, 8>)(g, false, wf, B, gin, st));
     } else if (want_in && S.s == 1 && S.ks == 3 && l >= 1 && !(hn_knobs().train_f32 & 2)) {
       // stride-1 3x3 (conv1 / conv3 / conv5: Cin = Cout): the data gradient is the same conv with
       // the weights flipped and transposed, on the bf16x3 MFMA conv kernels
@@ -1581,8 +1708,9 @@ hipError_t hn_train_backward(const float* dout, long B, const float* const* W, f
       HCK(conv_dgrad_l(l, g, B, W[l], S.cout, reinterpret_cast<float*>(ws + L.wt), gin, st));
     } else if (want_in && (l == 2 || l == 4) && !(hn_knobs().train_f32 & 32)) {
       // stride-2 3x3: k_dgrad2 (the parity classes' taps only, f32 MFMA)
-      if (l == 2) HCK((dgrad2<64, 32, 16>(g, W[l], B, gin, st)));
-      if (l == 4) HCK((dgrad2<128, 64, 8>(g, W[l], B, gin, st)));
+      const bool sh = !(hn_knobs().train_f32 & 128);
+      if (l == 2) HCK((dgrad2<64, 32, 16>(g, W[l], B, gin, st, sh)));
+      if (l == 4) HCK((dgrad2<128, 64, 8>(g, W[l], B, gin, st, sh)));
     } else if (want_in) {
       // stride 2 (3 of 4 taps miss a given input pixel) and the 8x8 conv6 (one tap per pixel):
       // dcol [K][n hw] = W^T [K][Cout] . dY, then the gather col2im, in chunks of patches
