@@ -23,8 +23,9 @@ struct HnKnobs {
                                // bit 4: stride-1 dgrads not as k_fwd3 over dY (then bit 1 decides);
                                // bit 5: stride-2 layers as the generic GEMM + col2im (else k_fwd2 /
                                // k_wgrad2 / k_dgrad2); bit 6: conv0 as the generic GEMM (else
-                               // k_fwd0 / k_wgrad0); bit 7: conv3 / conv5 on k_fwd3 (one ring per
-                               // wave) instead of k_fwd3s (one ring per patch), and k_fwd2 / k_dgrad2 likewise
+                               // k_fwd0 / k_wgrad0); bit 7: swaps the one-ring-per-wave and the
+                               // shared-ring-per-patch forms (default shared: conv3 / conv5 k_fwd3s,
+                               // conv4 k_dgrad2; per wave: conv2 / conv4 k_fwd2)
   int c12_abl = 0;             // HN_C12_ABL (HN_EXPERIMENTS only)
   int dbg = 0;                 // HN_DEBUG (HN_EXPERIMENTS only)
 };
