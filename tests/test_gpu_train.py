@@ -217,3 +217,42 @@ def test_odd_batch_gradients(b, cuda_device):
     for i in (0, 3, 6, 9, 12, 15, 19):
         assert _rel2(mg.features[i].weight.grad, md.features[i].weight.grad) <= L2_BAR, i
     assert _rel2(xg.grad, xd.grad) <= L2_BAR
+
+
+_ALT_CHILD = r"""
+import sys, torch
+sys.path.insert(0, sys.argv[1])
+import test_gpu_train as T
+from fixtures import golden_inputs
+dev = torch.device("cuda:0")
+for b in (256, 37):
+    mg, _, fx = T._pair(dev, fresh=True)
+    md = T._model64(True)
+    x = torch.from_numpy(golden_inputs(fx)[:b])
+    c = torch.randn(b, 128, generator=torch.Generator().manual_seed(5))
+    xg, xd = x.to(dev).requires_grad_(True), x.double().requires_grad_(True)
+    for m, xx in ((mg, xg), (md, xd)):
+        (m(xx) * c.to(device=xx.device, dtype=xx.dtype)).sum().backward()
+    errs = [T._rel2(mg.features[i].weight.grad, md.features[i].weight.grad) for i in (0, 3, 6, 9, 12, 15, 19)]
+    errs.append(T._rel2(xg.grad, xd.grad))
+    print(b, ["%.2e" % e for e in errs])
+    assert max(errs) <= T.L2_BAR, errs
+"""
+
+
+@pytest.mark.parametrize("knobs", ["129", "127", "17"])
+def test_train_kernel_alternatives(knobs, cuda_device):
+    """The HN_TRAIN_F32 alternatives (read once per process, so each runs in a child process):
+    129 = the default kernels with the one-ring / shared-ring forms swapped; 127 = the generic
+    implicit-GEMM forwards, weight gradients and data gradients (stride-1 col2im gather, stride-2
+    and conv0 through the column GEMM); 17 = the stride-1 data gradients on the bf16x3 eval conv
+    kernels.  Smooth-objective gradients at 256 and 37 patches against fp64, the same bar."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, HN_TRAIN_F32=knobs)
+    r = subprocess.run([sys.executable, "-c", _ALT_CHILD, here], env=env, capture_output=True, text=True,
+                       timeout=110)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr[-3000:]
