@@ -323,13 +323,22 @@ int bn_slices(long C, long L) {
 __global__ __launch_bounds__(256) void k_bn_part(const float* __restrict__ y, long L, int NS, double* __restrict__ part) {
   __shared__ double sh[8];
   const int c = blockIdx.x, sl = blockIdx.y;
-  const long per = (L + NS - 1) / NS, b = sl * per, e = min(L, b + per);
   const float* row = y + (long)c * L;
   double s1 = 0.0, s2 = 0.0;
-  for (long i = b + threadIdx.x; i < e; i += 256) {
-    const double v = row[i];
-    s1 += v;
-    s2 += v * v;
+  if ((L & 3) == 0) {  // float4 loads: slices of a multiple of 4 elements (rows start 16-byte aligned)
+    const long per = ((L + NS - 1) / NS + 3) & ~3L, b = sl * per, e = min(L, b + per);
+    for (long i = b + 4 * threadIdx.x; i < e; i += 1024) {
+      const float4 v = *reinterpret_cast<const float4*>(row + i);
+      s1 += ((double)v.x + (double)v.y) + ((double)v.z + (double)v.w);
+      s2 += ((double)v.x * v.x + (double)v.y * v.y) + ((double)v.z * v.z + (double)v.w * v.w);
+    }
+  } else {
+    const long per = (L + NS - 1) / NS, b = sl * per, e = min(L, b + per);
+    for (long i = b + threadIdx.x; i < e; i += 256) {
+      const double v = row[i];
+      s1 += v;
+      s2 += v * v;
+    }
   }
   block_sum2(s1, s2, sh);
   if (threadIdx.x == 0) {
@@ -369,9 +378,9 @@ __global__ __launch_bounds__(256) void k_bn_apply(float* __restrict__ y, long C,
   }
 }
 
-// backward through [dropout o] ReLU o BN(train): g = da * relu'(z) [* mask] (written back), and
-// the slice sums of g and g z
-__global__ __launch_bounds__(256) void k_bn_bwd_part(float* __restrict__ da, const float* __restrict__ z, long L,
+// backward through [dropout o] ReLU o BN(train): g = da * relu'(z) [* mask] (recomputed by
+// k_bn_bwd_apply, not stored), and the slice sums of g and g z
+__global__ __launch_bounds__(256) void k_bn_bwd_part(const float* __restrict__ da, const float* __restrict__ z, long L,
                                                      int NS, int relu, float drop_p, unsigned long long seed,
                                                      double* __restrict__ part) {
   __shared__ double sh[8];
@@ -384,7 +393,6 @@ __global__ __launch_bounds__(256) void k_bn_bwd_part(float* __restrict__ da, con
     float v = da[base + i];
     if (relu && zv <= 0.f) v = 0.f;
     if (drop_p > 0.f) v *= drop_scale(seed, (unsigned long long)(base + i), drop_p);
-    da[base + i] = v;
     s1 += v;
     s2 += (double)v * zv;
   }
@@ -409,13 +417,18 @@ __global__ __launch_bounds__(256) void k_bn_bwd_final(const double* __restrict__
   m12[2 * c + 1] = (float)(s2 / (double)L);
 }
 
-// dy = rstd * (g - m1 - z m2), in place
+// dy = rstd * (g - m1 - z m2) with g = da * relu'(z) [* mask] as in k_bn_bwd_part, in place
 __global__ __launch_bounds__(256) void k_bn_bwd_apply(float* __restrict__ g, const float* __restrict__ z, long C, long L,
-                                                      const float* __restrict__ m12, const float* __restrict__ rstd) {
+                                                      const float* __restrict__ m12, const float* __restrict__ rstd,
+                                                      int relu, float drop_p, unsigned long long seed) {
   const long n = C * L;
   for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
     const long c = e / L;
-    g[e] = rstd[c] * (g[e] - m12[2 * c] - z[e] * m12[2 * c + 1]);
+    const float zv = z[e];
+    float v = g[e];
+    if (relu && zv <= 0.f) v = 0.f;
+    if (drop_p > 0.f) v *= drop_scale(seed, (unsigned long long)e, drop_p);
+    g[e] = rstd[c] * (v - m12[2 * c] - zv * m12[2 * c + 1]);
   }
 }
 
@@ -1662,7 +1675,8 @@ hipError_t hn_train_backward(const float* dout, long B, const float* const* W, f
                          l == 5 ? drop_p : 0.f, seed, part);
       hipLaunchKernelGGL(k_bn_bwd_final, dim3((S.cout + 255) / 256), dim3(256), 0, st, part, S.cout, NS, B * hw, m12);
       hipLaunchKernelGGL(k_bn_bwd_apply, dim3(grid_for(S.cout * B * hw)), dim3(256), 0, st, g, zl, (long)S.cout,
-                         B * hw, m12, reinterpret_cast<const float*>(ws + L.rstd[l]));
+                         B * hw, m12, reinterpret_cast<const float*>(ws + L.rstd[l]), l < 6 ? 1 : 0,
+                         l == 5 ? drop_p : 0.f, seed);
       HCK(hipGetLastError());
     }
     const ActIn a{l == 0 ? xn : reinterpret_cast<const float*>(ws + L.z[l - 1]), l > 0 ? 1 : 0,
