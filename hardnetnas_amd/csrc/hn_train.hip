@@ -762,6 +762,16 @@ __global__ __launch_bounds__(256) void k_fwd3(const float* __restrict__ zx, int 
   // this lane's output position within the step: row rr0 = r / H, column x0 = r % H
   const int rr0 = r / H, x0 = r % H;
   const float* wl = W + (long)r * CIN * 9 + h * 9;  // W[co = cb * 32 + r][ci = 2 j + h][0..8]
+  // conv1 (32 -> 32): the lane's whole weight slice (16 channel pairs x 9 taps) stays in registers
+  // for the kernel's lifetime, so the K-loop issues no L2 weight loads
+  constexpr bool WREG = C::NCO == 1 && CIN / 2 * 9 <= 144;
+  float wr[WREG ? CIN / 2 : 1][9];
+  if constexpr (WREG) {
+#pragma unroll
+    for (int j = 0; j < CIN / 2; ++j)
+#pragma unroll
+      for (int t = 0; t < 9; ++t) wr[j][t] = wl[j * 18 + t];
+  }
 #pragma unroll 1
   for (int y = 0; y < H; y += G) {
     float nv[C::NLD];
@@ -769,6 +779,18 @@ __global__ __launch_bounds__(256) void k_fwd3(const float* __restrict__ zx, int 
     f32x16 acc[C::NCO];
 #pragma unroll
     for (int cb = 0; cb < C::NCO; ++cb) acc[cb] = f32x16{};
+    if constexpr (WREG) {
+#pragma unroll
+      for (int j = 0; j < CIN / 2; ++j) {
+        const float* xc = sx + (2 * j + h) * C::RSX;
+#pragma unroll
+        for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+          for (int dx = 0; dx < 3; ++dx)
+            acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(
+                wr[j][dy * 3 + dx], xc[((y + rr0 + dy - 1 + 1 + C::R) % C::R) * C::XW + x0 + dx], acc[0], 0, 0, 0);
+      }
+    } else {
     float wc[C::NCO][9], wn[C::NCO][9];
     auto ldw = [&](int j, float (&wv)[C::NCO][9]) {
 #pragma unroll
@@ -797,6 +819,7 @@ __global__ __launch_bounds__(256) void k_fwd3(const float* __restrict__ zx, int 
 #pragma unroll
           for (int t = 0; t < 9; ++t) wc[cb][t] = wn[cb][t];
       }
+    }
     }
     // acc[cb][4q + e]: co = 32 cb + 8q + 4h + e, position r of the step -> CNHW
 #pragma unroll
