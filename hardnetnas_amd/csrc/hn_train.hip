@@ -1028,16 +1028,24 @@ __global__ __launch_bounds__(256) void k_fwd2(const float* __restrict__ zx, int 
 #pragma unroll
         for (int t = 0; t < 9; ++t) wv[cb][t] = wl[(long)cb * 32 * CIN * 9 + j * 18 + t];
     };
-    ldw(0, wc);
-#pragma unroll 1
-    for (int j = 0; j < CIN / 2; ++j) {
-      if (j + 1 < CIN / 2) ldw(j + 1, wn);
+    // the 9 shifted operands of channel pair j: input row 2 (y + rr0) + dy - 1 -> slot (2 (y + rr0) + dy) % R;
+    // read one pair ahead so the MFMA chain does not wait on the LDS latency
+    auto ldb = [&](int j, float (&bv)[9]) {
       const float* xc = sx + (2 * j + h) * C::RSX;
-      float bv[9];
 #pragma unroll
-      for (int dy = 0; dy < 3; ++dy)  // input row 2 (y + rr0) + dy - 1 -> slot (2 (y + rr0) + dy) % R
+      for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
         for (int dx = 0; dx < 3; ++dx) bv[dy * 3 + dx] = xc[((2 * (y + rr0) + dy) % C::R) * C::XW + 2 * x0 + dx];
+    };
+    float bv[9], bn[9];
+    ldw(0, wc);
+    ldb(0, bv);
+#pragma unroll 1
+    for (int j = 0; j < CIN / 2; ++j) {
+      if (j + 1 < CIN / 2) {
+        ldw(j + 1, wn);
+        ldb(j + 1, bn);
+      }
 #pragma unroll
       for (int cb = 0; cb < CPW; ++cb)
 #pragma unroll
@@ -1047,6 +1055,8 @@ __global__ __launch_bounds__(256) void k_fwd2(const float* __restrict__ zx, int 
         for (int cb = 0; cb < CPW; ++cb)
 #pragma unroll
           for (int t = 0; t < 9; ++t) wc[cb][t] = wn[cb][t];
+#pragma unroll
+        for (int t = 0; t < 9; ++t) bv[t] = bn[t];
       }
     }
     if (valid)
@@ -1065,9 +1075,8 @@ __global__ __launch_bounds__(256) void k_fwd2(const float* __restrict__ zx, int 
   }
 }
 
-template <int CIN, int COUT, int HI>
+template <int CIN, int COUT, int HI, int NWP = (COUT / 32 >= 4 ? 4 : COUT / 32)>
 hipError_t fwd2(const float* zx, bool relu, const float* W, long B, float* z, hipStream_t st, bool shared) {
-  constexpr int NWP = COUT / 32 >= 4 ? 4 : COUT / 32;
   if (shared)
     hipLaunchKernelGGL((k_fwd2<CIN, COUT, HI, NWP>), dim3((unsigned)((B + 4 / NWP - 1) / (4 / NWP))), dim3(256), 0,
                        st, zx, relu ? 1 : 0, W, B, z);
@@ -1651,9 +1660,10 @@ hipError_t hn_train_forward(const float* in, long B, const float* const* W, floa
       if (l == 3) HCK((sh ? fwd3s<64, 64, 16> : fwd3<64, 64, 16>)(a.z, true, W[l], B, z, st));
       if (l == 5) HCK((sh ? fwd3s<128, 128, 8> : fwd3<128, 128, 8>)(a.z, true, W[l], B, z, st));
     } else if ((l == 2 || l == 4) && !(tf & 32)) {  // stride-2 3x3: k_fwd2 (f32 MFMA)
-      // one ring per wave (the shared-ring form measured slower here: 0.64 / 0.52 vs 0.31 / 0.37 ms)
+      // conv2: one ring per wave (shared by 2 waves measured 0.64 vs 0.31 ms); conv4: one ring per two
+      // waves (one per wave needs 128 prefetch registers per lane and spills)
       if (l == 2) HCK((fwd2<32, 64, 32>(a.z, true, W[l], B, z, st, (tf & 128) != 0)));
-      if (l == 4) HCK((fwd2<64, 128, 16>(a.z, true, W[l], B, z, st, (tf & 128) != 0)));
+      if (l == 4) HCK((fwd2<64, 128, 16, 2>(a.z, true, W[l], B, z, st, !(tf & 128))));
     } else
       HCK(conv_fwd_l(l, a, B, W[l], S.cout, z, reinterpret_cast<float*>(ws + L.part), st));  // Y = W . im2col(a)
     {
