@@ -346,8 +346,12 @@ static std::vector<uint16_t> pack_conv3x3(const std::vector<float>& w, int cin, 
 
 // head conv (kernel kk x kk over an NHWC map): GEMM k = (y*kk + x)*cin + c,
 // fragments [ks][nt][plane][lane][8]
+// folded weights whose fp16 hi half is not finite (|w| >= 65520 or NaN): counted while a model is
+// packed (per calling thread), hn_create then fails instead of packing an infinite fragment
+static thread_local long tl_f16_out_of_range = 0;
 static void put_f16_split(float v, uint16_t* hi, uint16_t* lo) {  // hn_common.h split8_f16
   const _Float16 hv = (_Float16)v;
+  if (!std::isfinite((float)hv)) ++tl_f16_out_of_range;
   const _Float16 lv = (_Float16)(v - (float)hv);
   std::memcpy(hi, &hv, 2);
   std::memcpy(lo, &lv, 2);
@@ -758,10 +762,15 @@ extern "C" int hn_create(const hn_arch_desc* desc, const float* host_params, siz
   }
   (void)hipGetDevice(&m->device);
   Cursor cur{host_params, n_params};
+  tl_f16_out_of_range = 0;
   rc = desc->kind == HN_KIND_HARDNET ? build_hardnet(m, cur)
        : desc->kind == HN_KIND_NAS    ? build_nas(m, cur)
                                       : build_fdl(m, cur);
   if (!rc && cur.i != n_params) rc = fail(HN_ERR_ARG, "host_params not fully consumed");
+  if (!rc && tl_f16_out_of_range)
+    rc = fail(HN_ERR_ARG, std::to_string(tl_f16_out_of_range) +
+                              " BN-folded weights are outside the fp16 range of the fp16x3 kernels (|w| >= 65520 "
+                              "or not finite)");
   if (rc) {
     delete m;
     return rc;

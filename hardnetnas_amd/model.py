@@ -406,3 +406,41 @@ class HardNetNAS(_NativeMixin, nn.Module):
             elif k.startswith("first.") or k.startswith("last_stages."):
                 out[k] = v
         return self.load_state_dict(out, strict=strict)
+
+
+FP16_SPLIT_LIMIT = 65504.0  # largest finite fp16: the hi half of an fp16x3 operand
+
+
+@torch.no_grad()
+def fp16_split_margin(module: nn.Module, x: torch.Tensor) -> dict:
+    """Range check for the fp16x3 kernels of HardNetNAS / HardNetNeiMask.
+
+    Those kernels split every operand of their 1x1 / grouped convs, stem and head into fp16
+    hi + lo halves (csrc/hn_common.h ``split8_f16``), so an activation of magnitude >= 65520
+    entering such a layer overflows the hi half.  ``hn_create`` rejects BN-folded *weights* out of
+    that range; activations depend on the data, so this runs the module's own torch layers (a CPU
+    copy, fp32) over a calibration batch ``x`` and reports the largest |input| reaching any
+    non-depthwise conv.  ``margin = 65504 / peak`` must stay above 1 for the native forward to be
+    valid on data like ``x``; the golden checkpoints sit at margins of order 10^3.  (Stock
+    HardNet runs on bf16x3, whose range is fp32's: no limit applies.)
+
+    Returns ``{"peak": float, "layer": str, "margin": float}``.
+    """
+    import copy
+    m = copy.deepcopy(module).cpu().eval()
+    peak = {"peak": 0.0, "layer": ""}
+    hooks = []
+    for name, mod in m.named_modules():
+        if isinstance(mod, nn.Conv2d) and not (mod.groups == mod.in_channels and mod.in_channels > 1):
+            def hook(_mod, inp, _out, name=name):
+                v = float(inp[0].abs().max()) if inp[0].numel() else 0.0
+                if v > peak["peak"]:
+                    peak.update(peak=v, layer=name)
+            hooks.append(mod.register_forward_hook(hook))
+    try:
+        m(x.detach().to("cpu", torch.float32))
+    finally:
+        for h in hooks:
+            h.remove()
+    peak["margin"] = FP16_SPLIT_LIMIT / peak["peak"] if peak["peak"] > 0 else float("inf")
+    return peak
