@@ -228,31 +228,46 @@ __global__ __launch_bounds__(NW * 64) void k_pairdist_rows(
     if (tid < 32) reinterpret_cast<float*>(buf + 2 * PLANE)[half * 32 + tid] = psq[min(j0 + half * 32 + tid, B - 1)];
   };
   // One 32-column sub-tile's MFMA chain (bf16x3, K = 128) with the epilogue of the previous
-  // sub-tile woven into its gaps: two of that sub-tile's 16 accumulator entries per K-step
-  // (branch-free; pj = |p_j|^2 of this lane's column, dsel = column - g0: accumulator row rr(i)
-  // is on the diagonal iff rr(i) == dsel, -1000 when the sub-tile has no diagonal).  B
-  // fragments are read one K-step ahead.
+  // sub-tile woven into its gaps: two of that sub-tile's 16 accumulator entries per K-step become
+  // x (pj = |p_j|^2 of this lane's column) and enter the lane's running minimum lm.  After the
+  // chain, the sub-tile is "clean" unless it holds the diagonal (dsel = column - g0, -1000 when
+  // it has none: accumulator row rr(i) is on it iff rr(i) == dsel) or some lane saw x < X*
+  // (lm < xthr) -- both rare, and the test is wave-uniform.  A clean sub-tile has no +10 entry,
+  // so its row minima are plain fmins and its column minimum is lm; otherwise the masked
+  // form runs over the 16 kept x values.  B fragments are read one K-step ahead.
   float cu, cm;
-  auto epi_entry = [&](const f32x16& acc, int i, float pj, int dsel) {
-    const int rr = (i & 3) + 8 * (i >> 2) + 4 * h;
-    const float v = fmaf(-2.0f, acc[i], pj);
-    const bool m = v < xthr || rr == dsel;
-    const float tu = m ? INFINITY : v, tm = m ? v : INFINITY;
-    xu[i] = fminf(xu[i], tu);
-    xm[i] = fminf(xm[i], tm);
-    if constexpr (SWAP) {
-      cu = fminf(cu, tu);
-      cm = fminf(cm, tm);
+  auto epi_masked = [&](const f32x16& xv, int dsel) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int rr = (i & 3) + 8 * (i >> 2) + 4 * h;
+      const float v = xv[i];
+      const bool m = v < xthr || rr == dsel;
+      const float tu = m ? INFINITY : v, tm = m ? v : INFINITY;
+      xu[i] = fminf(xu[i], tu);
+      xm[i] = fminf(xm[i], tm);
+      if constexpr (SWAP) {
+        cu = fminf(cu, tu);
+        cm = fminf(cm, tm);
+      }
     }
   };
-  auto epi_close = [&](int cslot) {
+  auto epi_finish = [&](const f32x16& xv, float lm, int dsel, int cslot) {
+    cu = INFINITY;
+    cm = INFINITY;
+    if (__any(dsel != -1000 || lm < xthr)) {
+      epi_masked(xv, dsel);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) xu[i] = fminf(xu[i], xv[i]);
+      cu = lm;
+    }
     if constexpr (SWAP) {
       cu = fminf(cu, __shfl_xor(cu, 32, 64));
       cm = fminf(cm, __shfl_xor(cm, 32, 64));
       if (h == 0) (&cred[0][0][0])[cslot + r] = fminf(dm_of(cu), dm_of(cm) + 10.f);
     }
   };
-  auto chain_epi = [&](const char* cur, int nt, const f32x16& accp, float pj, int dsel, int cslot) {
+  auto chain_epi = [&](const char* cur, int nt, f32x16 accp, float pj, int dsel, int cslot) {
     f32x16 acc;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {  // accumulator rows 8q + 4h + {0..3}
@@ -262,8 +277,7 @@ __global__ __launch_bounds__(NW * 64) void k_pairdist_rows(
       acc[4 * q + 2] = v.z;
       acc[4 * q + 3] = v.w;
     }
-    cu = INFINITY;
-    cm = INFINITY;
+    float lm = INFINITY;
     const char* base = cur + (nt * 32 + r) * ROWB + h * 16;
     uint4 bh = *reinterpret_cast<const uint4*>(base);
     uint4 bl = *reinterpret_cast<const uint4*>(base + PLANE);
@@ -275,22 +289,25 @@ __global__ __launch_bounds__(NW * 64) void k_pairdist_rows(
         nl = *reinterpret_cast<const uint4*>(base + PLANE + (ks + 1) * 32);
       }
       acc = mfma3(ah[ks], al[ks], as_bf16x8(bh), as_bf16x8(bl), acc);
-      epi_entry(accp, 2 * ks, pj, dsel);
-      epi_entry(accp, 2 * ks + 1, pj, dsel);
+      accp[2 * ks] = fmaf(-2.0f, accp[2 * ks], pj);
+      accp[2 * ks + 1] = fmaf(-2.0f, accp[2 * ks + 1], pj);
+      lm = fminf(lm, fminf(accp[2 * ks], accp[2 * ks + 1]));
       if (ks + 1 < 8) {
         bh = nh;
         bl = nl;
       }
     }
-    epi_close(cslot);
+    epi_finish(accp, lm, dsel, cslot);
     return acc;
   };
-  auto epilogue = [&](const f32x16& accp, float pj, int dsel, int cslot) {
-    cu = INFINITY;
-    cm = INFINITY;
+  auto epilogue = [&](f32x16 accp, float pj, int dsel, int cslot) {
+    float lm = INFINITY;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) epi_entry(accp, i, pj, dsel);
-    epi_close(cslot);
+    for (int i = 0; i < 16; ++i) {
+      accp[i] = fmaf(-2.0f, accp[i], pj);
+      lm = fminf(lm, accp[i]);
+    }
+    epi_finish(accp, lm, dsel, cslot);
   };
   auto reduce_cols = [&](int t) {  // tile t's column minima over the 4 waves: one atomic per column
     const int j = t * TN + lane;
