@@ -368,14 +368,32 @@ __global__ __launch_bounds__(256) void k_bn_final(const double* __restrict__ par
   }
 }
 
-// y (in place) -> z = (y - mean) * rstd over [C][L]
-__global__ __launch_bounds__(256) void k_bn_apply(float* __restrict__ y, long C, long L,
-                                                  const float* __restrict__ mean, const float* __restrict__ rstd) {
-  const long n = C * L;
-  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
-    const long c = e / L;
-    y[e] = (y[e] - mean[c]) * rstd[c];
+// y (in place) -> z = (y - mean) * rstd over [C][L]; grid (C, S): workgroup (c, s) walks row c
+// (no per-element channel division), float4 when rows are 16-byte aligned
+__global__ __launch_bounds__(256) void k_bn_apply(float* __restrict__ y, long L, const float* __restrict__ mean,
+                                                  const float* __restrict__ rstd) {
+  const int c = blockIdx.x;
+  const float mu = mean[c], rs = rstd[c];
+  float* row = y + (long)c * L;
+  const long step = (long)gridDim.y * 256;
+  if ((L & 3) == 0) {
+    float4* r4 = reinterpret_cast<float4*>(row);
+    for (long i = (long)blockIdx.y * 256 + threadIdx.x; i < L / 4; i += step) {
+      float4 v = r4[i];
+      v.x = (v.x - mu) * rs;
+      v.y = (v.y - mu) * rs;
+      v.z = (v.z - mu) * rs;
+      v.w = (v.w - mu) * rs;
+      r4[i] = v;
+    }
+  } else {
+    for (long i = (long)blockIdx.y * 256 + threadIdx.x; i < L; i += step) row[i] = (row[i] - mu) * rs;
   }
+}
+// row-wise grid for the BN element passes: about 4,096 workgroups in all
+dim3 bn_row_grid(long C, long L) {
+  const long per_row = std::max<long>(1, std::min<long>((4096 + C - 1) / C, ((L + 3) / 4 + 255) / 256));
+  return dim3((unsigned)C, (unsigned)std::min<long>(per_row, 65535));
 }
 
 // backward through [dropout o] ReLU o BN(train): g = da * relu'(z) [* mask] (recomputed by
@@ -388,13 +406,24 @@ __global__ __launch_bounds__(256) void k_bn_bwd_part(const float* __restrict__ d
   const long per = (L + NS - 1) / NS, b = sl * per, e = min(L, b + per);
   const long base = (long)c * L;
   double s1 = 0.0, s2 = 0.0;
-  for (long i = b + threadIdx.x; i < e; i += 256) {
-    const float zv = z[base + i];
-    float v = da[base + i];
+  auto acc = [&](float v, float zv, long i) {
     if (relu && zv <= 0.f) v = 0.f;
     if (drop_p > 0.f) v *= drop_scale(seed, (unsigned long long)(base + i), drop_p);
     s1 += v;
     s2 += (double)v * zv;
+  };
+  if ((L & 3) == 0) {  // float4 loads over slices of a multiple of 4 elements
+    const long per4 = (per + 3) & ~3L, b4 = sl * per4, e4 = min(L, b4 + per4);
+    for (long i = b4 + 4 * threadIdx.x; i < e4; i += 1024) {
+      const float4 zv = *reinterpret_cast<const float4*>(z + base + i);
+      const float4 v = *reinterpret_cast<const float4*>(da + base + i);
+      acc(v.x, zv.x, i);
+      acc(v.y, zv.y, i + 1);
+      acc(v.z, zv.z, i + 2);
+      acc(v.w, zv.w, i + 3);
+    }
+  } else {
+    for (long i = b + threadIdx.x; i < e; i += 256) acc(da[base + i], z[base + i], i);
   }
   block_sum2(s1, s2, sh);
   if (threadIdx.x == 0) {
@@ -417,18 +446,33 @@ __global__ __launch_bounds__(256) void k_bn_bwd_final(const double* __restrict__
   m12[2 * c + 1] = (float)(s2 / (double)L);
 }
 
-// dy = rstd * (g - m1 - z m2) with g = da * relu'(z) [* mask] as in k_bn_bwd_part, in place
-__global__ __launch_bounds__(256) void k_bn_bwd_apply(float* __restrict__ g, const float* __restrict__ z, long C, long L,
+// dy = rstd * (g - m1 - z m2) with g = da * relu'(z) [* mask] as in k_bn_bwd_part, in place;
+// grid (C, S) as k_bn_apply
+__global__ __launch_bounds__(256) void k_bn_bwd_apply(float* __restrict__ g, const float* __restrict__ z, long L,
                                                       const float* __restrict__ m12, const float* __restrict__ rstd,
                                                       int relu, float drop_p, unsigned long long seed) {
-  const long n = C * L;
-  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
-    const long c = e / L;
-    const float zv = z[e];
-    float v = g[e];
+  const int c = blockIdx.x;
+  const float m1 = m12[2 * c], m2 = m12[2 * c + 1], rs = rstd[c];
+  const long base = (long)c * L, step = (long)gridDim.y * 256;
+  auto one = [&](float v, float zv, long i) {
     if (relu && zv <= 0.f) v = 0.f;
-    if (drop_p > 0.f) v *= drop_scale(seed, (unsigned long long)e, drop_p);
-    g[e] = rstd[c] * (v - m12[2 * c] - zv * m12[2 * c + 1]);
+    if (drop_p > 0.f) v *= drop_scale(seed, (unsigned long long)(base + i), drop_p);
+    return rs * (v - m1 - zv * m2);
+  };
+  if ((L & 3) == 0) {
+    float4* g4 = reinterpret_cast<float4*>(g + base);
+    const float4* z4 = reinterpret_cast<const float4*>(z + base);
+    for (long i = (long)blockIdx.y * 256 + threadIdx.x; i < L / 4; i += step) {
+      const float4 zv = z4[i];
+      float4 v = g4[i];
+      v.x = one(v.x, zv.x, 4 * i);
+      v.y = one(v.y, zv.y, 4 * i + 1);
+      v.z = one(v.z, zv.z, 4 * i + 2);
+      v.w = one(v.w, zv.w, 4 * i + 3);
+      g4[i] = v;
+    }
+  } else {
+    for (long i = (long)blockIdx.y * 256 + threadIdx.x; i < L; i += step) g[base + i] = one(g[base + i], z[base + i], i);
   }
 }
 
@@ -1674,8 +1718,7 @@ hipError_t hn_train_forward(const float* in, long B, const float* const* W, floa
       hipLaunchKernelGGL(k_bn_part, dim3(S.cout, NS), dim3(256), 0, st, z, B * hw, NS, part);
       hipLaunchKernelGGL(k_bn_final, dim3((S.cout + 255) / 256), dim3(256), 0, st, part, S.cout, NS, B * hw, bn_eps,
                          mom, rmean ? rmean[l] : nullptr, rvar ? rvar[l] : nullptr, mean, rstd);
-      hipLaunchKernelGGL(k_bn_apply, dim3(grid_for(S.cout * B * hw)), dim3(256), 0, st, z, (long)S.cout, B * hw,
-                         mean, rstd);
+      hipLaunchKernelGGL(k_bn_apply, bn_row_grid(S.cout, B * hw), dim3(256), 0, st, z, B * hw, mean, rstd);
       HCK(hipGetLastError());
     }
   }
@@ -1707,9 +1750,8 @@ hipError_t hn_train_backward(const float* dout, long B, const float* const* W, f
       hipLaunchKernelGGL(k_bn_bwd_part, dim3(S.cout, NS), dim3(256), 0, st, g, zl, B * hw, NS, l < 6 ? 1 : 0,
                          l == 5 ? drop_p : 0.f, seed, part);
       hipLaunchKernelGGL(k_bn_bwd_final, dim3((S.cout + 255) / 256), dim3(256), 0, st, part, S.cout, NS, B * hw, m12);
-      hipLaunchKernelGGL(k_bn_bwd_apply, dim3(grid_for(S.cout * B * hw)), dim3(256), 0, st, g, zl, (long)S.cout,
-                         B * hw, m12, reinterpret_cast<const float*>(ws + L.rstd[l]), l < 6 ? 1 : 0,
-                         l == 5 ? drop_p : 0.f, seed);
+      hipLaunchKernelGGL(k_bn_bwd_apply, bn_row_grid(S.cout, B * hw), dim3(256), 0, st, g, zl, B * hw, m12,
+                         reinterpret_cast<const float*>(ws + L.rstd[l]), l < 6 ? 1 : 0, l == 5 ? drop_p : 0.f, seed);
       HCK(hipGetLastError());
     }
     const ActIn a{l == 0 ? xn : reinterpret_cast<const float*>(ws + L.z[l - 1]), l > 0 ? 1 : 0,
