@@ -240,19 +240,6 @@ def cpu_baseline(name: str, model, seconds: float = 12.0, x_timed=None, y_timed=
     return out, None
 
 
-def read_traffic(name: str, stage: str, patches_per_launch: float):
-    """PMC-measured HBM bytes per launch of `stage` (profiles/pmc_traffic_<name>.json holds
-    bytes per patch from tools/pmc.sh + tools/pmc_traffic.py), or None."""
-    f = os.path.join(ROOT, "profiles", f"pmc_traffic_{name}.json")
-    if not os.path.exists(f):
-        return None
-    try:
-        e = json.load(open(f)).get(stage)
-        return int(e["bytes_per_patch"] * patches_per_launch) if e else None
-    except Exception:
-        return None
-
-
 def nas_stage_flop(name: str) -> dict:
     """Algorithmic FLOP per patch of each NAS / FDL stage class (summed over its launches in one
     forward), mirroring hn_api.hip::forward_nas (fused front = stem + layer 0; "irf" = every
@@ -280,10 +267,342 @@ def nas_stage_flop(name: str) -> dict:
     return out
 
 
-# PMC evidence of what binds the NAS kernels (profiles/r01_pmc_mfma_wang2.json: VALU vs MFMA
-# instructions per dispatch; MFMA busy 10-25 %): their roof is VALU issue, not HBM or MFMA
-NAS_BINDING = ("VALU issue (PMC, profiles/r01_pmc_mfma_wang2.json: k_front 209 M VALU vs 11 M MFMA "
-               "instructions per dispatch, MFMA busy 17.5 %; HBM traffic = algorithmic bytes)")
+def cpu_baseline_pairs(model, seconds: float = 8.0, pairs: int = 2048):
+    """Config 5 on the host cores (rank 0, N = 1): the oracle's HardNet forward of `pairs` anchor /
+    positive pairs (2 x `pairs` patches) followed by its loss_HardNet (Losses.py:87-154, anchor_swap,
+    the B x B matrix materialised as the reference does), at the quota's thread count.  ``value`` is
+    whole-step patches/s at that batch; the pair step alone is also timed at B = 4,096 pairs
+    (SURVEY/BASELINE.md's CPU pair-step row)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from oracle import hardnet_oracle as O
+    p = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    nproc = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = _cpu_quota()
+    threads = max(1, int(quota)) if 0 < quota < nproc else nproc
+    torch.set_num_threads(threads)
+    xa = torch.from_numpy(synth.synth_patches(pairs, seed=21))
+    xp = xa + 0.3 * torch.from_numpy(synth.synth_patches(pairs, seed=22))
+    g = torch.Generator().manual_seed(3)
+    da = torch.nn.functional.normalize(torch.randn(4096, 128, generator=g), dim=1)
+    dp = torch.nn.functional.normalize(da + 0.3 * torch.randn(4096, 128, generator=g), dim=1)
+
+    def step():
+        with torch.no_grad():
+            ya, yp = O.hardnet_forward(p, xa), O.hardnet_forward(p, xp)
+            return O.loss_hardnet(ya, yp, anchor_swap=True)
+
+    def pair_only():
+        with torch.no_grad():
+            return O.loss_hardnet(da, dp, anchor_swap=True)
+
+    step()
+    pair_only()
+    t_step, t_pair, t_start = [], [], time.perf_counter()
+    while time.perf_counter() - t_start < seconds or len(t_step) < 2:
+        t0 = time.perf_counter()
+        step()
+        t1 = time.perf_counter()
+        pair_only()
+        t_step.append(t1 - t0)
+        t_pair.append(time.perf_counter() - t1)
+    ms, mp = statistics.median(t_step), statistics.median(t_pair)
+    return {"value": round(2 * pairs / ms, 1), "unit": "patches/s", "cores": threads, "kind": "port",
+            "nproc": nproc, "cgroup_cpu_quota": quota or None, "model": _cpu_model_string(),
+            "pair_step_pairs_per_s_b4096": round(4096 / mp, 1), "pair_step_ms_b4096": round(mp * 1e3, 2),
+            "step_ms": round(ms * 1e3, 1),
+            "sample": f"oracle/hardnet_oracle.py: forward of {pairs} anchor + {pairs} positive patches then "
+                      f"loss_hardnet (anchor_swap, B x B matrix) at {threads} threads, median of {len(t_step)} "
+                      f"steps (~{seconds:.0f} s); the pair step alone (loss_hardnet over 4,096 random unit "
+                      "descriptor pairs) timed beside it"}
+
+
+def check_pairs(out, pairs, pos, min_neg, rows=1024):
+    """The timed config-5 step at its own size: the oracle's hardest_negative_rows (fp64) on a
+    strided row sample of the 65,536-pair batch against the GPU's pos / min_neg of those rows."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from oracle import hardnet_oracle as O
+    idx = torch.arange(0, pairs, max(1, pairs // rows))[:rows]
+    a = out[:pairs].detach().double().cpu()
+    p_ = out[pairs:2 * pairs].detach().double().cpu()
+    rp, rn = O.hardest_negative_rows(a, p_, idx, anchor_swap=True)
+    gp, gn = pos[idx.to(pos.device)].double().cpu(), min_neg[idx.to(min_neg.device)].double().cpu()
+    err = max(float((gp - rp).abs().max()), float((gn - rn).abs().max()))
+    return {"rows": int(len(idx)), "of": int(pairs), "max_abs_err_vs_oracle_fp64": err, "tol": 1e-4,
+            "what": "pos and min_neg (anchor_swap) of sampled rows vs oracle.hardest_negative_rows",
+            "ok": bool(err <= 1e-4)}
+
+
+def read_pmc(name: str):
+    """profiles/pmc_<name>.json (tools/pmc_stage.py: per-stage HBM bytes and instruction counts
+    per patch from rocprofv3 --pmc passes on the current build), or None."""
+    f = os.path.join(ROOT, "profiles", f"pmc_{name}.json")
+    if not os.path.exists(f):
+        return None
+    try:
+        return json.load(open(f))
+    except Exception:
+        return None
+
+
+CLOCK_GHZ = 2.4           # MI355X peak engine clock (MI355X_MICROARCH.md)
+SIMDS = 256 * 4
+VALU_ISSUE_CYC = 2        # cycles per wave64 VALU instruction on a SIMD-32 (MI355X_MICROARCH.md)
+
+
+def run(opts, world, rank, local, dev, on_gpu, backend):
+    """One measured configuration: W warmup steps, then K timed steps bracketed by a barrier and a
+    device synchronisation on both sides; max over ranks.  Returns rank 0's result dict."""
+    cfg5 = opts.config == 5
+    model = build_model(opts.model)
+    nm = NativeModel.from_module(model, dev) if on_gpu else None
+    pairs = None
+    if cfg5:
+        pairs = opts.batch or 65536
+        from hardnetnas_amd.distributed import shard_range, sharded_hardnet_loss
+        s0, e0 = shard_range(pairs, world, rank) if world > 1 else (0, pairs)
+        b = 2 * (e0 - s0)  # this rank's anchors and positives, one forward
+    else:
+        b = opts.batch
+        if b is None:
+            b = (CONFIG4_PER_RANK if (world > 1 and opts.model == "hardnet") else 262144) if on_gpu else 256
+    u8_mode = opts.input[3:] if opts.input.startswith("u8-") else None
+    x = synth_input_on_device(b, dev, seed=1000 + rank)
+    if u8_mode:
+        hw = 32 if u8_mode == "none" else 64
+        x8 = torch.randint(0, 256, (b, hw, hw), device=dev, dtype=torch.uint8,
+                           generator=torch.Generator(device=dev).manual_seed(1000 + rank))
+    if cfg5:  # positives = anchors + noise (the same patch seen twice), as a real pair batch
+        x[b // 2:] = x[: b // 2] + 0.3 * torch.randn(b // 2, 1, 32, 32, device=dev,
+                                                     generator=torch.Generator(device=dev).manual_seed(7 + rank))
+    out = torch.empty((b, 128), device=dev)
+    ws = torch.empty(nm.workspace_bytes_u8(b) if u8_mode else nm.workspace_bytes(b), device=dev,
+                     dtype=torch.uint8) if on_gpu else None
+    gathered = torch.empty((b * world, 128), device=dev) if (world > 1 and not cfg5) else None
+    last = {}
+
+    def forward():
+        if u8_mode:
+            nm.forward_u8(x8, resize=u8_mode, out=out, workspace=ws)
+        elif on_gpu:
+            nm.forward(x, out=out, workspace=ws)
+        else:
+            with torch.no_grad():
+                out.copy_(model(x))
+
+    def collective_or_pairs():
+        if cfg5:
+            n = b // 2
+            if world > 1:
+                last["loss"], last["pos"], last["min_neg"] = sharded_hardnet_loss(out[:n], out[n:], pairs,
+                                                                                  anchor_swap=True)
+            else:
+                from hardnetnas_amd._native import hardnet_loss, pairdist_rows
+                pos, rmin, cmin = pairdist_rows(out[:n], 0, out[n:], col_min=True)
+                last["loss"], last["min_neg"] = hardnet_loss(pos, rmin, cmin)
+                last["pos"] = pos
+        elif world > 1 and not opts.no_allgather:
+            if backend == "gloo":
+                dist.all_gather(list(gathered.chunk(world)), out)
+            else:
+                dist.all_gather_into_tensor(gathered, out)
+
+    if on_gpu:
+        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(opts.steps)]
+    cpu_phase = [0.0, 0.0]
+
+    def step(k=None):
+        if on_gpu and k is not None:
+            evs[k][0].record()
+        t0 = time.perf_counter()
+        forward()
+        if on_gpu and k is not None:
+            evs[k][1].record()
+        t1 = time.perf_counter()
+        collective_or_pairs()
+        if on_gpu and k is not None:
+            evs[k][2].record()
+        if not on_gpu and k is not None:
+            cpu_phase[0] += t1 - t0
+            cpu_phase[1] += time.perf_counter() - t1
+
+    for _ in range(opts.warmup):
+        step()
+    if on_gpu:
+        torch.cuda.synchronize()
+        nm.stage_times()  # clear
+        nm.set_profiling(True)
+    if world > 1:
+        dist.barrier()
+    if on_gpu:
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(opts.steps):
+        step(k)
+    if on_gpu:
+        torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if on_gpu:
+        nm.set_profiling(False)
+        stages = nm.stage_times()
+        phase = [sum(e[0].elapsed_time(e[1]) for e in evs), sum(e[1].elapsed_time(e[2]) for e in evs)]
+    else:
+        stages = {}
+        phase = [1e3 * cpu_phase[0], 1e3 * cpu_phase[1]]
+    ranks_seen = world
+    if world > 1:
+        t = torch.tensor([elapsed, phase[0], phase[1]], device=dev if backend == "nccl" else "cpu",
+                         dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, phase = t[0].item(), [t[1].item(), t[2].item()]
+        cnt = torch.ones(1, device=dev if backend == "nccl" else "cpu")
+        dist.all_reduce(cnt)
+        ranks_seen = int(cnt.item())
+
+    total = (pairs * 2 if cfg5 else b * world) * opts.steps
+    value = total / elapsed / 1e6
+    if rank != 0:
+        return None
+    roof = None
+    if on_gpu:
+        stages_ms = {k: round(v[0] / opts.steps, 3) for k, v in stages.items()}
+        if cfg5:
+            # the pair step's own roofline: distance FLOP (2 B^2 D, SURVEY 8(d)) over its time
+            pair_ms = phase[1] / opts.steps
+            flop = 2.0 * pairs * pairs * 128 / world
+            achieved = flop / (pair_ms * 1e-3) / 1e12
+            pmc = read_pmc("c5") or {}
+            tr = pmc.get("pairdist") if pmc.get("pairs") == pairs and world == 1 else None
+            roof = {"bound": "mfma", "kernel": "pair step (k_pairdist_rows + k_sq/k_pos/k_loss)",
+                    "achieved": round(achieved, 2), "peak": round(PEAK_BF16X3, 1), "unit": "TFLOP/s",
+                    "frac": round(achieved / PEAK_BF16X3, 4),
+                    "traffic": int(tr["bytes_per_launch"]) if tr else None,
+                    "traffic_source": "profiles/pmc_c5.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, separate "
+                                      "passes, k_pairdist_rows at this batch)" if tr else None,
+                    "avg_launch_ms": round(pair_ms, 4), "launches": opts.steps,
+                    "pairs_per_launch": int(pairs),
+                    "peak_basis": "bf16 MFMA dense 2.5 PFLOP/s / 3 (bf16x3 split-precision distance "
+                                  "dots); algorithmic FLOP = 2 * B^2 * 128 per step",
+                    "forward_stages_ms_per_step": stages_ms}
+        else:
+            # dominant kernel = stage with the largest summed device time
+            dom = max(stages, key=lambda k: stages[k][0])
+            dom_ms, dom_n = stages[dom]
+            avg_ms = dom_ms / max(dom_n, 1)
+            launches_per_step = dom_n / opts.steps
+            patches_per_launch = b / launches_per_step
+            pmc = read_pmc(opts.model) or {}
+            pst = pmc.get("stages", {}).get(dom)
+            traffic = int(pst["bytes_per_patch"] * patches_per_launch) if pst and "bytes_per_patch" in pst else None
+            if opts.model == "hardnet":
+                flop = 2 * HARDNET_STAGE_MAC[dom] * patches_per_launch
+                achieved = flop / (avg_ms * 1e-3) / 1e12
+                alg = HARDNET_STAGE_BYTES[dom] * patches_per_launch
+                roof = {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 2),
+                        "peak": round(PEAK_BF16X3, 1), "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16X3, 4)}
+                peak_basis = ("bf16 MFMA dense 2.5 PFLOP/s / 3 (bf16x3 split-precision fp32 products); "
+                              "algorithmic FLOP = 2*MAC")
+            else:
+                # A NAS / FDL stage class aggregates several layers' launches.  Its roofs: the fp16x3
+                # MFMA (algorithmic FLOP / summed time), HBM (PMC bytes / time) and VALU issue (PMC
+                # VALU instructions x 2 cycles / SIMD-cycles of the launch).  "bound" names whichever
+                # of MFMA / HBM it is closer to, "frac" is that fraction; all three are reported.
+                per_patch = nas_stage_flop(opts.model).get(dom, 0)
+                mfma_tf = per_patch * b * opts.steps / (dom_ms * 1e-3) / 1e12
+                alg = (fdl_stage_bytes(opts.model) if opts.model in FDL_MODELS
+                       else nas_stage_bytes(opts.model)).get(dom, 0) * patches_per_launch
+                hbm_gbps = (traffic if traffic else alg) / (avg_ms * 1e-3) / 1e9
+                mfma_frac, hbm_frac = mfma_tf / PEAK_BF16X3, hbm_gbps / PEAK_HBM
+                valu_frac = None
+                if pst and pst.get("valu_insts_per_patch"):
+                    valu_frac = (pst["valu_insts_per_patch"] * patches_per_launch * VALU_ISSUE_CYC
+                                 / (avg_ms * 1e-3 * CLOCK_GHZ * 1e9 * SIMDS))
+                if hbm_frac >= mfma_frac:
+                    roof = {"bound": "hbm", "kernel": dom, "achieved": round(hbm_gbps, 1), "peak": PEAK_HBM,
+                            "unit": "GB/s", "frac": round(hbm_frac, 4)}
+                else:
+                    roof = {"bound": "mfma", "kernel": dom, "achieved": round(mfma_tf, 2),
+                            "peak": round(PEAK_BF16X3, 1), "unit": "TFLOP/s", "frac": round(mfma_frac, 4)}
+                roof.update({"mfma_tflops": round(mfma_tf, 2), "mfma_frac": round(mfma_frac, 4),
+                             "hbm_gbps": round(hbm_gbps, 1), "hbm_frac": round(hbm_frac, 4),
+                             "hbm_bytes_basis": "PMC" if traffic else "algorithmic",
+                             "valu_issue_frac": round(valu_frac, 4) if valu_frac is not None else None,
+                             "mfma_busy_pmc": pst.get("mfma_busy") if pst else None})
+                peak_basis = ("fp16 MFMA dense 2.5 PFLOP/s / 3 (fp16x3 split-precision 1x1 convs; depthwise "
+                              "on the VALU); HBM 8 TB/s; VALU issue = 1,024 SIMDs x 2.4 GHz / 2 cycles per "
+                              "wave64 instruction; algorithmic FLOP = 2*MAC")
+            roof.update({"traffic": traffic, "avg_launch_ms": round(avg_ms, 4), "launches": dom_n,
+                         "patches_per_launch": int(patches_per_launch),
+                         "algorithmic_bytes_per_launch": int(alg) if alg else None,
+                         "hbm_gbps_algorithmic": round(alg / (avg_ms * 1e-3) / 1e9, 1) if alg else None,
+                         "pmc_source": f"profiles/pmc_{opts.model}.json" if pst else None,
+                         "peak_basis": peak_basis, "stages_ms_per_step": stages_ms})
+    if cfg5:
+        workload = (f"Stock HardNet forward of {pairs} anchor/positive pairs ({2 * pairs} patches) + "
+                    "fused masked distance / hardest negative (anchor_swap) / triplet margin loss")
+        if world > 1:
+            workload += f", pairs sharded over {world} ranks (RCCL all-gather of positives, all-reduce MIN/SUM)"
+    else:
+        workload = (("Stock HardNet forward" if opts.model == "hardnet"
+                     else f"FDLNet HardNetNeiMask {FDL_MODELS[opts.model]} forward"
+                     if opts.model in FDL_MODELS else f"hardnetNAS {opts.model} forward")
+                    + f", {b} synthetic 32x32 patches per GPU"
+                    + (" (BASELINE config 4 per-rank shard)" if world > 1 and b == CONFIG4_PER_RANK else "")
+                    + (", RCCL all-gather of descriptors" if world > 1 and not opts.no_allgather else ""))
+    if not on_gpu:
+        workload += " [CPU plumbing dry run: module torch layers, gloo; not a throughput figure]"
+    if u8_mode:
+        workload += (f" from uint8 {'32x32' if u8_mode == 'none' else '64x64'} patches, loader "
+                     f"preprocessing ({u8_mode}) fused into the forward")
+    result = {
+        "metric": METRIC, "value": round(value, 4 if on_gpu else 6), "unit": "Mpatches/s", "n_gpus": world,
+        "steps": opts.steps, "warmup": opts.warmup,
+        "ms_per_step": round(elapsed / opts.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "strong" if (cfg5 and world > 1) else "weak", "vs_baseline": None,
+        "dtype": ("bf16x3" if opts.model == "hardnet" else "fp16x3") if on_gpu else "f32",
+        "data": "synthetic",
+        "config": {"workload": workload, "model": opts.model,
+                   "baseline_config": 5 if cfg5 else (4 if world > 1 and b == CONFIG4_PER_RANK
+                                                      else (2 if opts.model == "hardnet" else 3)),
+                   "global_batch": pairs * 2 if cfg5 else b * world, "per_gpu_batch": b,
+                   "parallelism": f"dp{world}",
+                   "precision": "fp32 torch CPU layers (dry run)" if not on_gpu else
+                                ("bf16x3 split-precision MFMA (fp32-accurate: hi/lo bf16 operands, "
+                                 "3 products, fp32 accumulate)" if opts.model == "hardnet"
+                                 else "fp16x3 split-precision MFMA for 1x1 convs and head, fp32 VALU depthwise"
+                                 + (" and front" if opts.model in FDL_MODELS else "")),
+                   "flop_per_patch": flop_per_patch(opts.model)},
+        "ranks_seen": ranks_seen,
+        "compute_ms": round(phase[0] / opts.steps, 3),
+        ("pair_step_ms" if cfg5 else "allgather_ms"): round(phase[1] / opts.steps, 3),
+        "roofline": roof,
+        "cpu_baseline": None,
+    }
+    if cfg5:
+        result["pairs_per_s"] = round(pairs * opts.steps / elapsed, 1)
+        result["loss"] = float(last["loss"].item()) if "loss" in last else None
+    if world == 1 and on_gpu and not opts.no_cpu_baseline:
+        if cfg5:
+            cb, check = cpu_baseline_pairs(model, opts.cpu_seconds), check_pairs(out, pairs, last["pos"],
+                                                                                   last["min_neg"])
+        elif u8_mode:
+            cb, check = cpu_baseline(opts.model, model, opts.cpu_seconds)
+        else:
+            cb, check = cpu_baseline(opts.model, model, opts.cpu_seconds, x_timed=x, y_timed=out)
+        result["cpu_baseline"] = cb
+        result["gpu_vs_cpu"] = round(value * 1e6 / cb["value"], 1)
+        if check is not None:
+            result["check"] = check
+    del nm, ws, out, x
+    return result
+
+
+# the other BASELINE configurations measured after the headline one on a default 1-GPU run
+EXTRA_CONFIGS = [("3:wang2", "wang2", None), ("3:wang3", "wang3", None), ("3:wang4", "wang4", None),
+                 ("5", "hardnet", 5)]
+EXTRA_KEYS = ("value", "unit", "ms_per_step", "steps", "warmup", "dtype", "config", "compute_ms", "pair_step_ms",
+              "pairs_per_s", "loss", "roofline", "cpu_baseline", "gpu_vs_cpu", "check")
 
 
 def main():
@@ -311,10 +630,14 @@ def main():
     ap.add_argument("--no-allgather", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-extra-configs", action="store_true",
+                    help="default 1-GPU runs of config 2 also measure configs 3 (wang2/3/4) and 5 after the "
+                         "headline line and attach them under 'extra_configs'; this skips them")
     args = ap.parse_args()
-    cfg5 = args.config == 5
-    if cfg5 and args.model != "hardnet":
+    if args.config == 5 and args.model != "hardnet":
         ap.error("config 5 is the stock HardNet pair step")
+    if args.input.startswith("u8-") and (args.device != "cuda" or args.config == 5):
+        ap.error("--input u8-* is a GPU descriptor-forward mode")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -335,219 +658,20 @@ def main():
         else:
             dist.init_process_group("gloo")
 
-    model = build_model(args.model)
-    nm = NativeModel.from_module(model, dev) if on_gpu else None
-    if cfg5:
-        pairs = args.batch or 65536
-        from hardnetnas_amd.distributed import shard_range, sharded_hardnet_loss
-        s0, e0 = shard_range(pairs, world, rank) if world > 1 else (0, pairs)
-        b = 2 * (e0 - s0)  # this rank's anchors and positives, one forward
-    else:
-        b = args.batch
-        if b is None:
-            b = (CONFIG4_PER_RANK if (world > 1 and args.model == "hardnet") else 262144) if on_gpu else 256
-    u8_mode = args.input[3:] if args.input.startswith("u8-") else None
-    if u8_mode and (not on_gpu or cfg5):
-        ap.error("--input u8-* is a GPU descriptor-forward mode")
-    x = synth_input_on_device(b, dev, seed=1000 + rank)
-    if u8_mode:
-        hw = 32 if u8_mode == "none" else 64
-        x8 = torch.randint(0, 256, (b, hw, hw), device=dev, dtype=torch.uint8,
-                           generator=torch.Generator(device=dev).manual_seed(1000 + rank))
-    if cfg5:  # positives = anchors + noise (the same patch seen twice), as a real pair batch
-        x[b // 2:] = x[: b // 2] + 0.3 * torch.randn(b // 2, 1, 32, 32, device=dev,
-                                                     generator=torch.Generator(device=dev).manual_seed(7 + rank))
-    out = torch.empty((b, 128), device=dev)
-    ws = torch.empty(nm.workspace_bytes_u8(b) if u8_mode else nm.workspace_bytes(b), device=dev,
-                     dtype=torch.uint8) if on_gpu else None
-    gathered = torch.empty((b * world, 128), device=dev) if (world > 1 and not cfg5) else None
-    loss = None
-
-    def forward():
-        if u8_mode:
-            nm.forward_u8(x8, resize=u8_mode, out=out, workspace=ws)
-        elif on_gpu:
-            nm.forward(x, out=out, workspace=ws)
-        else:
-            with torch.no_grad():
-                out.copy_(model(x))
-
-    def collective_or_pairs():
-        nonlocal loss
-        if cfg5:
-            n = b // 2
-            if world > 1:
-                loss, _, _ = sharded_hardnet_loss(out[:n], out[n:], pairs, anchor_swap=True)
-            else:
-                from hardnetnas_amd._native import hardnet_loss, pairdist_rows
-                pos, rmin, cmin = pairdist_rows(out[:n], 0, out[n:], col_min=True)
-                loss, _ = hardnet_loss(pos, rmin, cmin)
-        elif world > 1 and not args.no_allgather:
-            if backend == "gloo":
-                dist.all_gather(list(gathered.chunk(world)), out)
-            else:
-                dist.all_gather_into_tensor(gathered, out)
-
-    if on_gpu:
-        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
-    cpu_phase = [0.0, 0.0]
-
-    def step(k=None):
-        if on_gpu and k is not None:
-            evs[k][0].record()
-        t0 = time.perf_counter()
-        forward()
-        if on_gpu and k is not None:
-            evs[k][1].record()
-        t1 = time.perf_counter()
-        collective_or_pairs()
-        if on_gpu and k is not None:
-            evs[k][2].record()
-        if not on_gpu and k is not None:
-            cpu_phase[0] += t1 - t0
-            cpu_phase[1] += time.perf_counter() - t1
-
-    for _ in range(args.warmup):
-        step()
-    if on_gpu:
-        torch.cuda.synchronize()
-        nm.stage_times()  # clear
-        nm.set_profiling(True)
-    if world > 1:
-        dist.barrier()
-    if on_gpu:
-        torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(k)
-    if on_gpu:
-        torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if on_gpu:
-        nm.set_profiling(False)
-        stages = nm.stage_times()
-        phase = [sum(e[0].elapsed_time(e[1]) for e in evs), sum(e[1].elapsed_time(e[2]) for e in evs)]
-    else:
-        stages = {}
-        phase = [1e3 * cpu_phase[0], 1e3 * cpu_phase[1]]
-    ranks_seen = world
-    if world > 1:
-        t = torch.tensor([elapsed, phase[0], phase[1]], device=dev if backend == "nccl" else "cpu",
-                         dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, phase = t[0].item(), [t[1].item(), t[2].item()]
-        cnt = torch.ones(1, device=dev if backend == "nccl" else "cpu")
-        dist.all_reduce(cnt)
-        ranks_seen = int(cnt.item())
-
-    total = (pairs * 2 if cfg5 else b * world) * args.steps
-    value = total / elapsed / 1e6
-    result = None
+    result = run(args, world, rank, local, dev, on_gpu, backend)
+    extras = (world == 1 and on_gpu and not args.no_extra_configs and args.model == "hardnet"
+              and args.config in (None, 2) and args.batch is None and args.input == "f32")
+    if extras:
+        result["extra_configs"] = {}
+        for key, model, cfg in EXTRA_CONFIGS:
+            o = argparse.Namespace(**vars(args))
+            o.model, o.config, o.batch = model, cfg, None
+            o.steps, o.warmup = max(3, args.steps // 2), max(1, args.warmup)
+            o.cpu_seconds = min(args.cpu_seconds, 5.0 if cfg is None else 8.0)
+            torch.cuda.empty_cache()
+            r = run(o, world, rank, local, dev, on_gpu, backend)
+            result["extra_configs"][key] = {k: r[k] for k in EXTRA_KEYS if k in r}
     if rank == 0:
-        roof = None
-        if on_gpu:
-            if cfg5:
-                # the pair step's own roofline: distance FLOP (2 B^2 D) over its time
-                pair_ms = phase[1] / args.steps
-                flop = 2.0 * pairs * pairs * 128 / world
-                achieved = flop / (pair_ms * 1e-3) / 1e12
-                roof = {"bound": "mfma", "kernel": "pair step (k_pairdist_rows + k_sq/k_pos/k_loss)",
-                        "achieved": round(achieved, 2), "peak": round(PEAK_BF16X3, 1), "unit": "TFLOP/s",
-                        "frac": round(achieved / PEAK_BF16X3, 4), "traffic": None,
-                        "avg_launch_ms": round(pair_ms, 4), "launches": args.steps,
-                        "pairs_per_launch": int(pairs),
-                        "peak_basis": "bf16 MFMA dense 2.5 PFLOP/s / 3 (bf16x3 split-precision distance "
-                                      "dots); algorithmic FLOP = 2 * B^2 * 128 per step",
-                        "stages_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in stages.items()}}
-            else:
-                # dominant kernel = stage with the largest summed device time
-                dom = max(stages, key=lambda k: stages[k][0])
-                dom_ms, dom_n = stages[dom]
-                avg_ms = dom_ms / max(dom_n, 1)
-                launches_per_step = dom_n / args.steps
-                patches_per_launch = b / launches_per_step
-                if args.model == "hardnet":
-                    flop = 2 * HARDNET_STAGE_MAC[dom] * patches_per_launch
-                    achieved = flop / (avg_ms * 1e-3) / 1e12
-                    alg = HARDNET_STAGE_BYTES[dom] * patches_per_launch
-                    binding = "MFMA (PMC: k_c12 58 % MFMA busy, profiles/r01_pmc_mfma_hardnet.json)"
-                else:
-                    # a NAS stage class aggregates different layers' launches: its summed
-                    # algorithmic FLOP / summed device time, against the fp16x3 MFMA roof
-                    per_patch = nas_stage_flop(args.model).get(dom, 0)
-                    achieved = per_patch * b * args.steps / (dom_ms * 1e-3) / 1e12
-                    alg = (fdl_stage_bytes(args.model) if args.model in FDL_MODELS
-                           else nas_stage_bytes(args.model)).get(dom, 0) * b / launches_per_step
-                    binding = NAS_BINDING
-                roof = {"bound": "mfma", "kernel": dom,
-                        "achieved": round(achieved, 2), "peak": round(PEAK_BF16X3, 1), "unit": "TFLOP/s",
-                        "frac": round(achieved / PEAK_BF16X3, 4),
-                        "traffic": read_traffic(args.model, dom, b / launches_per_step),
-                        "avg_launch_ms": round(avg_ms, 4), "launches": dom_n,
-                        "patches_per_launch": int(patches_per_launch),
-                        "algorithmic_bytes_per_launch": int(alg) if alg else None,
-                        "hbm_gbps_algorithmic": round(alg / (avg_ms * 1e-3) / 1e9, 1) if alg else None,
-                        "binding_counter": binding,
-                        "peak_basis": ("bf16 MFMA dense 2.5 PFLOP/s / 3 (bf16x3 split-precision fp32 "
-                                       "products)" if args.model == "hardnet" else
-                                       "fp16 MFMA dense 2.5 PFLOP/s / 3 (fp16x3 split-precision 1x1 "
-                                       "convs; depthwise on the VALU)") + "; algorithmic FLOP = 2*MAC",
-                        "stages_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in stages.items()}}
-        if cfg5:
-            workload = (f"Stock HardNet forward of {pairs} anchor/positive pairs ({2 * pairs} patches) + "
-                        "fused masked distance / hardest negative (anchor_swap) / triplet margin loss")
-            if world > 1:
-                workload += f", pairs sharded over {world} ranks (RCCL all-gather of positives, all-reduce MIN/SUM)"
-        else:
-            workload = (("Stock HardNet forward" if args.model == "hardnet"
-                         else f"FDLNet HardNetNeiMask {FDL_MODELS[args.model]} forward"
-                         if args.model in FDL_MODELS else f"hardnetNAS {args.model} forward")
-                        + f", {b} synthetic 32x32 patches per GPU"
-                        + (" (BASELINE config 4 per-rank shard)" if world > 1 and b == CONFIG4_PER_RANK else "")
-                        + (", RCCL all-gather of descriptors" if world > 1 and not args.no_allgather else ""))
-        if not on_gpu:
-            workload += " [CPU plumbing dry run: module torch layers, gloo; not a throughput figure]"
-        if u8_mode:
-            workload += (f" from uint8 {'32x32' if u8_mode == 'none' else '64x64'} patches, loader "
-                         f"preprocessing ({u8_mode}) fused into the forward")
-        result = {
-            "metric": METRIC, "value": round(value, 4 if on_gpu else 6), "unit": "Mpatches/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
-            "scaling": "strong" if (cfg5 and world > 1) else "weak", "vs_baseline": None,
-            "dtype": ("bf16x3" if args.model == "hardnet" else "fp16x3") if on_gpu else "f32",
-            "data": "synthetic",
-            "config": {"workload": workload, "model": args.model,
-                       "baseline_config": 5 if cfg5 else (4 if world > 1 and b == CONFIG4_PER_RANK
-                                                          else (2 if args.model == "hardnet" else 3)),
-                       "global_batch": pairs * 2 if cfg5 else b * world, "per_gpu_batch": b,
-                       "parallelism": f"dp{world}",
-                       "precision": "fp32 torch CPU layers (dry run)" if not on_gpu else
-                                    ("bf16x3 split-precision MFMA (fp32-accurate: hi/lo bf16 operands, "
-                                     "3 products, fp32 accumulate)" if args.model == "hardnet"
-                                     else "fp16x3 split-precision MFMA for 1x1 convs and head, fp32 VALU depthwise"
-                                     + (" and front" if args.model in FDL_MODELS else "")),
-                       "flop_per_patch": flop_per_patch(args.model)},
-            "ranks_seen": ranks_seen,
-            "compute_ms": round(phase[0] / args.steps, 3),
-            ("pair_step_ms" if cfg5 else "allgather_ms"): round(phase[1] / args.steps, 3),
-            "roofline": roof,
-            "cpu_baseline": None,
-        }
-        if cfg5:
-            result["pairs_per_s"] = round(pairs * args.steps / elapsed, 1)
-            result["loss"] = float(loss.item()) if loss is not None else None
-        if world == 1 and on_gpu and not args.no_cpu_baseline:
-            if cfg5 or u8_mode:
-                cb, check = cpu_baseline(args.model, model, args.cpu_seconds)
-            else:
-                cb, check = cpu_baseline(args.model, model, args.cpu_seconds, x_timed=x, y_timed=out)
-            result["cpu_baseline"] = cb
-            result["gpu_vs_cpu"] = round(value * 1e6 / cb["value"], 1)
-            if check is not None:
-                result["check"] = check
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.barrier()

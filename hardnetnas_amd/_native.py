@@ -30,6 +30,7 @@ HN_KIND_NAS = 1
 HN_KIND_FDL_NASNET = 2
 HN_KIND_FDL_NASNET01 = 3
 HN_MAX_LAYERS = 8
+ABI_VERSION = 2   # HN_ABI_VERSION of include/hardnet_mi355x.h
 
 
 class HnArchDesc(ctypes.Structure):
@@ -81,10 +82,10 @@ def load_library():
         lib.hn_forward.argtypes = [P, P, I64, P, P, S, P]
         lib.hn_workspace_bytes_u8.argtypes = [P, I64, ctypes.POINTER(S)]
         PP = ctypes.POINTER(P)
-        lib.hn_hardnet_train_workspace_bytes.argtypes = [I64, ctypes.POINTER(S)]
+        lib.hn_hardnet_train_workspace_bytes.argtypes = [I64, ctypes.POINTER(S), ctypes.POINTER(S)]
         lib.hn_hardnet_train_forward.argtypes = [P, I64, PP, PP, PP, ctypes.c_float, ctypes.c_float,
-                                                 ctypes.c_uint64, P, P, S, P]
-        lib.hn_hardnet_train_backward.argtypes = [P, I64, PP, PP, P, ctypes.c_float, ctypes.c_uint64, P, S, P]
+                                                 ctypes.c_uint64, P, P, S, P, S, P]
+        lib.hn_hardnet_train_backward.argtypes = [P, I64, PP, PP, P, ctypes.c_float, ctypes.c_uint64, P, S, P, S, P]
         lib.hn_forward_u8.argtypes = [P, P, I64, I32, I32, I32, ctypes.c_float, ctypes.c_float, P, P, S, P]
         lib.hn_pairdist_workspace_bytes.argtypes = [I64, ctypes.POINTER(S)]
         lib.hn_pairdist_hardneg.argtypes = [P, P, I64, I32, I32, P, P, P, S, P]
@@ -108,6 +109,8 @@ def load_library():
                      "hn_hardnet_train_workspace_bytes", "hn_hardnet_train_forward",
                      "hn_hardnet_train_backward"):
             getattr(lib, name).restype = ctypes.c_int
+        if lib.hn_abi_version() != ABI_VERSION:
+            raise RuntimeError(f"{path}: ABI version {lib.hn_abi_version()}, expected {ABI_VERSION}; rebuild it")
         _lib = lib
         return lib
 
@@ -463,20 +466,35 @@ def _ptr_array(ts):
     return (ctypes.c_void_p * len(ts))(*[t.data_ptr() for t in ts])
 
 
+def train_workspace_bytes(batch: int):
+    """(saved, scratch) bytes of hn_hardnet_train_forward / _backward for a batch."""
+    lib = load_library()
+    sv, sc = ctypes.c_size_t(), ctypes.c_size_t()
+    _check(lib.hn_hardnet_train_workspace_bytes(batch, ctypes.byref(sv), ctypes.byref(sc)),
+           "hn_hardnet_train_workspace_bytes")
+    return sv.value, sc.value
+
+
 class HardNetTrainFunction(torch.autograd.Function):
     """model.train() forward of the stock HardNet on the GPU kernels (BatchNorm batch
     statistics + running-statistics update, Dropout, L2Norm) and its backward to the 7 conv
     weights and the input -- what autograd does over the reference module in the training loop
     (hardnet/HardNet.py:379-441).  ``bn`` is a list of the 7 BatchNorm2d modules (their running
-    buffers are updated in place, num_batches_tracked incremented)."""
+    buffers are updated in place, num_batches_tracked incremented).
+
+    Each call keeps its own "saved" workspace (the BN outputs the backward reads) as a tensor
+    saved for backward, so the loop's two forwards (anchors, positives; HardNet.py:392-393) each
+    hold theirs until ``loss.backward()``, autograd frees it after the backward (or keeps it for
+    ``retain_graph=True``: the backward only reads it), and a second backward without
+    ``retain_graph`` raises torch's usual error.  The scratch workspace is transient."""
 
     @staticmethod
     def forward(ctx, x, drop_p, seed, bn, *weights):
         lib = load_library()
         b = x.shape[0]
-        n = ctypes.c_size_t()
-        _check(lib.hn_hardnet_train_workspace_bytes(b, ctypes.byref(n)), "hn_hardnet_train_workspace_bytes")
-        ws = torch.empty(n.value, device=x.device, dtype=torch.uint8)
+        n_sv, n_sc = train_workspace_bytes(b)
+        saved = torch.empty(n_sv, device=x.device, dtype=torch.uint8)
+        scratch = torch.empty(n_sc, device=x.device, dtype=torch.uint8)
         out = torch.empty((b, 128), device=x.device, dtype=torch.float32)
         ws_w = [w.detach().contiguous() for w in weights]
         rm = [m.running_mean for m in bn]
@@ -485,25 +503,29 @@ class HardNetTrainFunction(torch.autograd.Function):
         with torch.cuda.device(x.device):
             _check(lib.hn_hardnet_train_forward(x.data_ptr(), b, _ptr_array(ws_w), _ptr_array(rm), _ptr_array(rv),
                                                 float(bn[0].momentum), float(drop_p), int(seed), out.data_ptr(),
-                                                ws.data_ptr(), ws.numel(), stream), "hn_hardnet_train_forward")
+                                                saved.data_ptr(), saved.numel(), scratch.data_ptr(), scratch.numel(),
+                                                stream), "hn_hardnet_train_forward")
+        del scratch
         for m in bn:
             m.num_batches_tracked.add_(1)
-        ctx.ws, ctx.drop_p, ctx.seed, ctx.b = ws, float(drop_p), int(seed), b
-        ctx.save_for_backward(*ws_w)
+        ctx.drop_p, ctx.seed, ctx.b = float(drop_p), int(seed), b
+        ctx.save_for_backward(saved, *ws_w)
         return out
 
     @staticmethod
     def backward(ctx, dout):
         lib = load_library()
-        ws_w = ctx.saved_tensors
+        saved, *ws_w = ctx.saved_tensors
         dws = [torch.empty_like(w) for w in ws_w]
         need_x = ctx.needs_input_grad[0]
         din = torch.empty((ctx.b, 1, 32, 32), device=dout.device, dtype=torch.float32) if need_x else None
+        _, n_sc = train_workspace_bytes(ctx.b)
+        scratch = torch.empty(n_sc, device=dout.device, dtype=torch.uint8)
         stream = torch.cuda.current_stream(dout.device).cuda_stream
         with torch.cuda.device(dout.device):
             _check(lib.hn_hardnet_train_backward(dout.contiguous().data_ptr(), ctx.b, _ptr_array(ws_w),
                                                  _ptr_array(dws), din.data_ptr() if din is not None else None,
-                                                 ctx.drop_p, ctx.seed, ctx.ws.data_ptr(), ctx.ws.numel(), stream),
+                                                 ctx.drop_p, ctx.seed, saved.data_ptr(), saved.numel(),
+                                                 scratch.data_ptr(), scratch.numel(), stream),
                    "hn_hardnet_train_backward")
-        ctx.ws = None
         return (din, None, None, None, *dws)

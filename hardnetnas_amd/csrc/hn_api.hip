@@ -471,6 +471,7 @@ static std::vector<uint16_t> pack_c12(const std::vector<float>& w, int cout) {
   return a;
 }
 
+#ifdef HN_EXPERIMENTS
 // stride-1 3x3 conv (BN folded) as Winograd F(2x2,3x3) U = G g G^T (fp64, then bf16 hi/lo),
 // packed as the B operand of hn_wino.hip's 32x32x16 MFMAs: [cout/32][cin/16][xi 16][plane][lane
 // 64][8], lane (column l & 31 -> output channel, k-group l >> 5 -> input channels 8 (l >> 5) + j)
@@ -497,6 +498,7 @@ static std::vector<uint16_t> pack_wino(const std::vector<float>& w, int cin, int
           }
   return a;
 }
+#endif
 
 static int build_hardnet(hn_model* m, Cursor& cur) {
   static const int cin[7] = {1, 32, 32, 64, 64, 128, 128};
@@ -524,11 +526,13 @@ static int build_hardnet(hn_model* m, Cursor& cur) {
     if ((rc = m->upload(pk, &d))) return rc;
     m->hd.wpack[l] = d;
     if ((rc = m->upload(f.b, &m->hd.bias[l]))) return rc;
-    if (l == 3 || l == 5) {
+#ifdef HN_EXPERIMENTS
+    if (l == 3 || l == 5) {  // Winograd U fragments (experiments library only)
       uint16_t* c = nullptr;
       if ((rc = m->upload(pack_wino(f.w, cin[l], cout[l]), &c))) return rc;
       m->hd.wino[l] = c;
     }
+#endif
     if (l == 1 || l == 2) {
       uint16_t* c = nullptr;
       if ((rc = m->upload(pack_c12(f.w, cout[l]), &c))) return rc;
@@ -1020,18 +1024,25 @@ extern "C" int hn_forward_u8(hn_model* m, const uint8_t* d_in, int64_t batch, in
 // ---------------------------------------------------------------------------------------
 // train-mode stock HardNet (hn_train.hip)
 // ---------------------------------------------------------------------------------------
-extern "C" int hn_hardnet_train_workspace_bytes(int64_t batch, size_t* bytes_out) {
-  if (!bytes_out || batch < 2 || batch > (1 << 24)) return fail(HN_ERR_ARG, "batch must be 2 .. 2^24");
-  *bytes_out = hn_train_layout((long)batch).total;
+extern "C" int hn_hardnet_train_workspace_bytes(int64_t batch, size_t* saved_bytes_out, size_t* scratch_bytes_out) {
+  if (!saved_bytes_out || !scratch_bytes_out || batch < 2 || batch > (1 << 24))
+    return fail(HN_ERR_ARG, "batch must be 2 .. 2^24 (and both size pointers given)");
+  const HnTrainWs L = hn_train_layout((long)batch);
+  *saved_bytes_out = L.saved_total;
+  *scratch_bytes_out = L.scratch_total;
   return HN_OK;
 }
 
-static int train_args(int64_t batch, const void* const* ptrs, int n, void* ws, size_t ws_bytes) {
-  size_t need = 0;
-  int rc = hn_hardnet_train_workspace_bytes(batch, &need);
+static int train_args(int64_t batch, const void* const* ptrs, int n, void* saved, size_t saved_bytes, void* scratch,
+                      size_t scratch_bytes) {
+  size_t need_sv = 0, need_sc = 0;
+  int rc = hn_hardnet_train_workspace_bytes(batch, &need_sv, &need_sc);
   if (rc) return rc;
-  if (!ws) return fail(HN_ERR_ARG, "NULL workspace");
-  if (ws_bytes < need) return fail(HN_ERR_WORKSPACE, "workspace too small: need " + std::to_string(need) + " bytes");
+  if (!saved || !scratch) return fail(HN_ERR_ARG, "NULL workspace");
+  if (saved_bytes < need_sv)
+    return fail(HN_ERR_WORKSPACE, "saved workspace too small: need " + std::to_string(need_sv) + " bytes");
+  if (scratch_bytes < need_sc)
+    return fail(HN_ERR_WORKSPACE, "scratch workspace too small: need " + std::to_string(need_sc) + " bytes");
   if (!ptrs) return fail(HN_ERR_ARG, "NULL weight pointer array");
   for (int i = 0; i < n; ++i)
     if (!ptrs[i]) return fail(HN_ERR_ARG, "NULL weight pointer " + std::to_string(i));
@@ -1040,24 +1051,28 @@ static int train_args(int64_t batch, const void* const* ptrs, int n, void* ws, s
 
 extern "C" int hn_hardnet_train_forward(const float* d_in, int64_t batch, const float* const* d_weights,
                                         float* const* d_running_mean, float* const* d_running_var, float momentum,
-                                        float dropout_p, uint64_t seed, float* d_out, void* d_workspace,
-                                        size_t workspace_bytes, void* hip_stream) {
-  int rc = train_args(batch, reinterpret_cast<const void* const*>(d_weights), 7, d_workspace, workspace_bytes);
+                                        float dropout_p, uint64_t seed, float* d_out, void* d_saved,
+                                        size_t saved_bytes, void* d_scratch, size_t scratch_bytes,
+                                        void* hip_stream) {
+  int rc = train_args(batch, reinterpret_cast<const void* const*>(d_weights), 7, d_saved, saved_bytes, d_scratch,
+                      scratch_bytes);
   if (rc) return rc;
   if (!d_in || !d_out) return fail(HN_ERR_ARG, "NULL device pointer");
   if ((d_running_mean == nullptr) != (d_running_var == nullptr))
     return fail(HN_ERR_ARG, "running_mean and running_var must both be given or both NULL");
   if (!(dropout_p >= 0.f && dropout_p < 1.f)) return fail(HN_ERR_ARG, "dropout_p must be in [0, 1)");
   HIPCHK(hn_train_forward(d_in, (long)batch, d_weights, d_running_mean, d_running_var, momentum, 1e-5f, 1e-7f,
-                          1e-10f, dropout_p, (unsigned long long)seed, d_out, static_cast<char*>(d_workspace),
-                          static_cast<hipStream_t>(hip_stream)));
+                          1e-10f, dropout_p, (unsigned long long)seed, d_out, static_cast<char*>(d_saved),
+                          static_cast<char*>(d_scratch), static_cast<hipStream_t>(hip_stream)));
   return HN_OK;
 }
 
 extern "C" int hn_hardnet_train_backward(const float* d_dout, int64_t batch, const float* const* d_weights,
                                          float* const* d_dweights, float* d_din, float dropout_p, uint64_t seed,
-                                         void* d_workspace, size_t workspace_bytes, void* hip_stream) {
-  int rc = train_args(batch, reinterpret_cast<const void* const*>(d_weights), 7, d_workspace, workspace_bytes);
+                                         void* d_saved, size_t saved_bytes, void* d_scratch, size_t scratch_bytes,
+                                         void* hip_stream) {
+  int rc = train_args(batch, reinterpret_cast<const void* const*>(d_weights), 7, d_saved, saved_bytes, d_scratch,
+                      scratch_bytes);
   if (rc) return rc;
   if (!d_dout) return fail(HN_ERR_ARG, "NULL device pointer");
   if (!d_dweights) return fail(HN_ERR_ARG, "NULL gradient pointer array");
@@ -1065,7 +1080,7 @@ extern "C" int hn_hardnet_train_backward(const float* d_dout, int64_t batch, con
     if (!d_dweights[i]) return fail(HN_ERR_ARG, "NULL gradient pointer " + std::to_string(i));
   if (!(dropout_p >= 0.f && dropout_p < 1.f)) return fail(HN_ERR_ARG, "dropout_p must be in [0, 1)");
   HIPCHK(hn_train_backward(d_dout, (long)batch, d_weights, d_dweights, d_din, 1e-10f, dropout_p,
-                           (unsigned long long)seed, static_cast<char*>(d_workspace),
+                           (unsigned long long)seed, static_cast<char*>(d_saved), static_cast<char*>(d_scratch),
                            static_cast<hipStream_t>(hip_stream)));
   return HN_OK;
 }

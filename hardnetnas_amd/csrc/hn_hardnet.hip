@@ -1309,16 +1309,26 @@ constexpr int conv_lds() { return CFG::LDS + (STEM ? (34 * 34 + 8) * 4 : 0); }
 
 // variant 0 = default tiling; variant 1 = smaller LDS footprint / more workgroups per CU
 HN_CONV(conv1s_launch, true, 32, 32, 32, 1, 1, 8, 4, 1)
+#ifdef HN_EXPERIMENTS  // superseded tiling (experiments library only)
 HN_CONV(conv1s_v1, true, 32, 32, 32, 1, 1, 4, 4, 1)
+#endif
 HN_CONV(conv1_launch, false, 32, 32, 32, 1, 1, 8, 4, 1)
 HN_CONV(conv2_launch, false, 32, 64, 32, 2, 1, 8, 2, 2)
+#ifdef HN_EXPERIMENTS  // superseded tiling (experiments library only)
 HN_CONV(conv2_v1, false, 32, 64, 32, 2, 1, 4, 2, 2)
+#endif
 HN_CONV(conv3_launch, false, 64, 64, 16, 1, 1, 16, 2, 2)
+#ifdef HN_EXPERIMENTS  // superseded tiling (experiments library only)
 HN_CONV(conv3_v1, false, 64, 64, 16, 1, 1, 8, 2, 2)
+#endif
 HN_CONV(conv4_launch, false, 64, 128, 16, 2, 1, 8, 1, 4)
+#ifdef HN_EXPERIMENTS  // superseded tiling (experiments library only)
 HN_CONV(conv4_v1, false, 64, 128, 16, 2, 1, 4, 1, 4)
+#endif
 HN_CONV(conv5_launch, false, 128, 128, 8, 1, 2, 8, 1, 4)
+#ifdef HN_EXPERIMENTS  // superseded tiling (experiments library only)
 HN_CONV(conv5_v1, false, 128, 128, 8, 1, 1, 8, 1, 4)
+#endif
 
 // persistent launch: grid = min(tiles, resident workgroups) (occupancy query, cached)
 #define HN_PIPE(NAME, STEM, CIN, COUT, HIN, S, NP, TR, WM, WN) HN_PIPE_A(NAME, STEM, CIN, COUT, HIN, S, NP, TR, WM, WN, 0)
@@ -1346,6 +1356,7 @@ HN_CONV(conv5_v1, false, 128, 128, 8, 1, 1, 8, 1, 4)
     return NAME##_lo(in, out, wp, bias, P, sw, sb, eps, st, 0.f);                          \
   }
 
+#ifdef HN_EXPERIMENTS  // superseded tiling (experiments library only)
 HN_PIPE(pipe1s, true, 32, 32, 32, 1, 1, 4, 4, 1)
 HN_PIPE(pipe1s_t8, true, 32, 32, 32, 1, 1, 8, 4, 1)
 HN_PIPE(pipe2, false, 32, 64, 32, 2, 1, 4, 2, 2)
@@ -1356,6 +1367,7 @@ HN_PIPE(pipe4, false, 64, 128, 16, 2, 1, 4, 1, 4)
 HN_PIPE(pipe4_t8, false, 64, 128, 16, 2, 1, 8, 1, 4)
 HN_PIPE(pipe5, false, 128, 128, 8, 1, 1, 8, 1, 4)
 HN_PIPE(pipe5_np2, false, 128, 128, 8, 1, 2, 8, 1, 4)
+#endif
 HN_PIPE_C(pipe5_cst, false, 128, 128, 8, 1, 2, 8, 1, 4, 0, true)  // HN_VARIANT digit g at conv5
 
 #define HN_WS(NAME, CIN, COUT, HIN, S, NP, TR, WM, WN) HN_WS_S(NAME, false, CIN, COUT, HIN, S, NP, TR, WM, WN)
@@ -1397,8 +1409,10 @@ HN_WS(ws5, 128, 128, 8, 1, 1, 8, 1, 4)
 HN_WS(ws5_np2, 128, 128, 8, 1, 2, 8, 1, 4)
 // conv4 with the 64-byte swizzled window: two patches per stage (twice the weight reuse of ws4_t8)
 // -- HN_VARIANT digit d -- and the same layout at one patch (digit e)
+#ifdef HN_EXPERIMENTS  // superseded tiling (experiments library only)
 HN_WS_X(ws4_np2s, false, 64, 128, 16, 2, 2, 8, 1, 4, 0, 64)
 HN_WS_X(ws4_s, false, 64, 128, 16, 2, 1, 8, 1, 4, 0, 64)
+#endif
 HN_WS_X(ws4_np2s22, false, 64, 128, 16, 2, 2, 8, 2, 2, 0, 64)  // digit f: 2 x 2 waves
 // conv3 with the epilogue transposed through LDS for whole-row stores (CST): HN_VARIANT digit g
 // (the default, conv3 12.8 -> 12.1 ms).  The same on conv4's one-patch tiling (8.49 -> 8.35 ms)
@@ -1407,9 +1421,11 @@ HN_WS_X(ws4_np2s22, false, 64, 128, 16, 2, 2, 8, 2, 2, 0, 64)  // digit f: 2 x 2
 HN_WS_C(ws3_cst, false, 64, 64, 16, 1, 1, 16, 2, 2, 0, 80, true)
 
 // wider N tiles (fewer A-fragment reads, weights shared through L1)
+#ifdef HN_EXPERIMENTS  // superseded tiling (experiments library only)
 HN_WS(ws3_w8, 64, 64, 16, 1, 1, 16, 4, 1)
 HN_WS(ws4_w8, 64, 128, 16, 2, 1, 8, 2, 2)
 HN_WS(ws5_w8, 128, 128, 8, 1, 2, 8, 2, 2)
+#endif
 #ifdef HN_EXPERIMENTS
 // ablation builds (timing only, wrong results; the HN_EXPERIMENTS library only): weights
 // fetched once per stage
@@ -1437,27 +1453,27 @@ hipError_t hn_launch_stem(const float* in, float* out, const float* w, const flo
 // 1 = conv1 alone, 2..5 = conv2..conv5); mirrors the dispatch below.  Digits 4 / 8 / 9 are the
 // timing-only ablation builds of conv3..conv5 (HN_EXPERIMENTS library only).
 bool hn_hardnet_variant_ok(int layer, int v) {
+  // the product library: 0 (k_conv3x3), 5 / 6 (warp-specialised, smaller / larger tile), 15 (conv4
+  // on the 64-byte swizzled window, two patches per stage, 2 x 2 waves), 16 (conv3 / conv5 with
+  // epilogue stores through LDS).  The superseded tilings (1, 2, 3, 7, 13, 14), the Winograd
+  // kernels (17) and the timing-only ablations (4, 8, 9) exist only with -DHN_EXPERIMENTS.
   if (layer < 0 || layer > 5) return false;
-  if (v == 4 || v == 8 || v == 9) {
 #ifdef HN_EXPERIMENTS
-    return layer >= 3;
-#else
-    return false;
-#endif
-  }
-  if (v >= 13 && v <= 15) return layer == 4;
+  if (v == 4 || v == 8 || v == 9) return layer >= 3;
+  if (v == 13 || v == 14) return layer == 4;
   if (v == 17) return layer == 3 || layer == 5;  // Winograd F(2x2,3x3), hn_wino.hip
-  if (v == 16) return layer == 3 || layer == 5;
   if (v == 7) return layer >= 3;
-  if (v == 0 || v == 1) return true;
-  if (v == 2 || v == 3 || v == 5 || v == 6) return true;  // (layer 1 always runs conv1_launch)
+  if (v == 1 || v == 2 || v == 3) return true;
+#endif
+  if (v == 15) return layer == 4;
+  if (v == 16) return layer == 3 || layer == 5;
+  if (v == 0 || v == 5 || v == 6) return true;  // (layer 1 always runs conv1_launch)
   return false;
 }
 
 // layer 0 = fused stem (input_norm + conv0) + conv1 from the raw patches
 hipError_t hn_launch_hardnet_conv(int layer, int variant, const HardnetDev& d, const float* in,
                                   float* out, int P, float eps, hipStream_t st) {
-  const bool v1 = variant == 1;
   if (!hn_hardnet_variant_ok(layer, variant)) return hipErrorInvalidValue;
 #ifdef HN_EXPERIMENTS
   if (variant == 8 || variant == 9 || variant == 4) {  // ablation (timing only)
@@ -1470,24 +1486,29 @@ hipError_t hn_launch_hardnet_conv(int layer, int variant, const HardnetDev& d, c
     return hipErrorInvalidValue;
   }
 #endif
-  if (variant >= 13 && variant <= 15) {  // conv4, 64-byte swizzled window (2 / 1 / 2 patches per stage)
+  if (variant == 15) {  // conv4, 64-byte swizzled window, two patches per stage
     if (layer != 4) return hipErrorInvalidValue;
-    return (variant == 13 ? ws4_np2s : variant == 14 ? ws4_s : ws4_np2s22)(in, out, d.wpack[4], d.bias[4], P,
-                                                                          nullptr, nullptr, 0.f, st);
+    return ws4_np2s22(in, out, d.wpack[4], d.bias[4], P, nullptr, nullptr, 0.f, st);
+  }
+#ifdef HN_EXPERIMENTS
+  if (variant == 13 || variant == 14) {  // conv4, 64-byte swizzled window (2 / 1 patches per stage)
+    if (layer != 4) return hipErrorInvalidValue;
+    return (variant == 13 ? ws4_np2s : ws4_s)(in, out, d.wpack[4], d.bias[4], P, nullptr, nullptr, 0.f, st);
   }
   if (variant == 17) return hn_launch_wino(layer, d, in, out, P, st);
-  if (variant == 16) {  // coalesced epilogue stores
-    switch (layer) {
-      case 3: return ws3_cst(in, out, d.wpack[3], d.bias[3], P, nullptr, nullptr, 0.f, st);
-      case 5: return pipe5_cst(in, out, d.wpack[5], d.bias[5], P, nullptr, nullptr, 0.f, st);
-    }
-    return hipErrorInvalidValue;
-  }
   if (variant == 7) {  // warp-specialised, NT = 2
     switch (layer) {
       case 3: return ws3_w8(in, out, d.wpack[3], d.bias[3], P, nullptr, nullptr, 0.f, st);
       case 4: return ws4_w8(in, out, d.wpack[4], d.bias[4], P, nullptr, nullptr, 0.f, st);
       case 5: return ws5_w8(in, out, d.wpack[5], d.bias[5], P, nullptr, nullptr, 0.f, st);
+    }
+    return hipErrorInvalidValue;
+  }
+#endif
+  if (variant == 16) {  // coalesced epilogue stores
+    switch (layer) {
+      case 3: return ws3_cst(in, out, d.wpack[3], d.bias[3], P, nullptr, nullptr, 0.f, st);
+      case 5: return pipe5_cst(in, out, d.wpack[5], d.bias[5], P, nullptr, nullptr, 0.f, st);
     }
     return hipErrorInvalidValue;
   }
@@ -1503,6 +1524,7 @@ hipError_t hn_launch_hardnet_conv(int layer, int variant, const HardnetDev& d, c
     }
     return hipErrorInvalidValue;
   }
+#ifdef HN_EXPERIMENTS
   if (variant >= 2) {  // persistent pipelined kernels: 2 = smaller tile, 3 = larger tile
     const bool big = variant == 3;
     switch (layer) {
@@ -1515,19 +1537,25 @@ hipError_t hn_launch_hardnet_conv(int layer, int variant, const HardnetDev& d, c
     }
     return hipErrorInvalidValue;
   }
+#endif
+#ifdef HN_EXPERIMENTS
+  if (variant == 1) {
+    switch (layer) {
+      case 0: return conv1s_v1(in, out, d.wpack[1], d.bias[1], P, d.stem_w, d.stem_b, eps, st);
+      case 2: return conv2_v1(in, out, d.wpack[2], d.bias[2], P, nullptr, nullptr, 0.f, st);
+      case 3: return conv3_v1(in, out, d.wpack[3], d.bias[3], P, nullptr, nullptr, 0.f, st);
+      case 4: return conv4_v1(in, out, d.wpack[4], d.bias[4], P, nullptr, nullptr, 0.f, st);
+      case 5: return conv5_v1(in, out, d.wpack[5], d.bias[5], P, nullptr, nullptr, 0.f, st);
+    }
+  }
+#endif
   switch (layer) {
-    case 0:
-      return (v1 ? conv1s_v1 : conv1s_launch)(in, out, d.wpack[1], d.bias[1], P, d.stem_w,
-                                               d.stem_b, eps, st);
+    case 0: return conv1s_launch(in, out, d.wpack[1], d.bias[1], P, d.stem_w, d.stem_b, eps, st);
     case 1: return conv1_launch(in, out, d.wpack[1], d.bias[1], P, nullptr, nullptr, 0.f, st);
-    case 2:
-      return (v1 ? conv2_v1 : conv2_launch)(in, out, d.wpack[2], d.bias[2], P, nullptr, nullptr, 0.f, st);
-    case 3:
-      return (v1 ? conv3_v1 : conv3_launch)(in, out, d.wpack[3], d.bias[3], P, nullptr, nullptr, 0.f, st);
-    case 4:
-      return (v1 ? conv4_v1 : conv4_launch)(in, out, d.wpack[4], d.bias[4], P, nullptr, nullptr, 0.f, st);
-    case 5:
-      return (v1 ? conv5_v1 : conv5_launch)(in, out, d.wpack[5], d.bias[5], P, nullptr, nullptr, 0.f, st);
+    case 2: return conv2_launch(in, out, d.wpack[2], d.bias[2], P, nullptr, nullptr, 0.f, st);
+    case 3: return conv3_launch(in, out, d.wpack[3], d.bias[3], P, nullptr, nullptr, 0.f, st);
+    case 4: return conv4_launch(in, out, d.wpack[4], d.bias[4], P, nullptr, nullptr, 0.f, st);
+    case 5: return conv5_launch(in, out, d.wpack[5], d.bias[5], P, nullptr, nullptr, 0.f, st);
   }
   return hipErrorInvalidValue;
 }

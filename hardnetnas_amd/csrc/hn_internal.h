@@ -149,12 +149,14 @@ struct HnTrainLayer {
   int cin, cout, hin, ks, s, pad;
 };
 extern const HnTrainLayer kHardnetTrainLayers[7];
-struct HnTrainWs {  // byte offsets into the train workspace
-  size_t xn, inv_sd, z[7], rstd[7], g0, g1, col, part, bnpart, bnmean, wt, nhwc0, nhwc1, wpack, zero, total;
+struct HnTrainWs {  // byte offsets into the train workspace's saved region (xn .. rstd) / scratch region
+  size_t xn, inv_sd, z[7], rstd[7], saved_total;
+  size_t g0, g1, col, part, bnpart, bnmean, wt, nhwc0, nhwc1, wpack, zero, scratch_total;
 };
 HnTrainWs hn_train_layout(long B);
 hipError_t hn_train_forward(const float* in, long B, const float* const* W, float* const* rmean, float* const* rvar,
                             float mom, float bn_eps, float in_eps, float l2_eps, float drop_p,
-                            unsigned long long seed, float* out, char* ws, hipStream_t st);
+                            unsigned long long seed, float* out, char* saved, char* scratch, hipStream_t st);
 hipError_t hn_train_backward(const float* dout, long B, const float* const* W, float* const* dW, float* din,
-                             float l2_eps, float drop_p, unsigned long long seed, char* ws, hipStream_t st);
+                             float l2_eps, float drop_p, unsigned long long seed, char* saved, char* scratch,
+                             hipStream_t st);

@@ -1595,6 +1595,8 @@ static long chunk_of(const HnTrainLayer& l, long B) {
 }
 
 HnTrainWs hn_train_layout(long B) {
+  // Two regions.  "saved" holds what the backward reads (one per forward call: autograd keeps it
+  // until the backward has run); "scratch" is transient (the caller may reuse it between calls).
   HnTrainWs w{};
   size_t off = 0;
   auto take = [&](size_t bytes) {
@@ -1611,6 +1613,8 @@ HnTrainWs hn_train_layout(long B) {
     w.rstd[l] = take((size_t)kHardnetTrainLayers[l].cout * 4);
     maxact = std::max(maxact, (size_t)kHardnetTrainLayers[l].cout * B * ho * ho);
   }
+  w.saved_total = off;
+  off = 0;  // scratch offsets
   w.g0 = take(maxact * 4);
   w.g1 = take(maxact * 4);
   size_t col = 0;  // the strided / 8x8 dgrads' column chunk
@@ -1637,13 +1641,14 @@ HnTrainWs hn_train_layout(long B) {
   w.bnpart = take((size_t)128 * kBnSlices * 2 * sizeof(double));
   w.wt = take((size_t)128 * 128 * 64 * sizeof(float));  // a transposed weight (conv6 is the largest)
   w.bnmean = take((size_t)2 * 128 * sizeof(float));
-  // the bf16x3 conv path: NHWC in / out (the largest activation: 32 x 32 x 32 per patch), one
-  // packed layer (conv5: 128 x 128 x 9 x 2 bf16 pairs) and a zero bias
-  w.nhwc0 = take((size_t)B * 32 * 1024 * 4);
-  w.nhwc1 = take((size_t)B * 32 * 1024 * 4);
-  w.wpack = take((size_t)128 * 128 * 9 * 2 * 2 * 2);
+  // the bf16x3 conv path (HN_TRAIN_F32 bit 0 or 1 off): NHWC in / out (the largest activation:
+  // 32 x 32 x 32 per patch), one packed layer (conv5: 128 x 128 x 9 x 2 bf16 pairs), a zero bias
+  const bool bf16x3 = (hn_knobs().train_f32 & 3) != 3;
+  w.nhwc0 = take(bf16x3 ? (size_t)B * 32 * 1024 * 4 : 0);
+  w.nhwc1 = take(bf16x3 ? (size_t)B * 32 * 1024 * 4 : 0);
+  w.wpack = take(bf16x3 ? (size_t)128 * 128 * 9 * 2 * 2 * 2 : 0);
   w.zero = take(128 * sizeof(float));
-  w.total = off;
+  w.scratch_total = off;
   return w;
 }
 
@@ -1656,20 +1661,20 @@ HnTrainWs hn_train_layout(long B) {
 // conv layer l (1..5) as the inference kernels' bf16x3 MFMA conv over NHWC: CNHW `x` (relu'd if
 // asked) -> NHWC -> conv (flip: the data gradient, input = the conv's output space) -> CNHW `y`
 static hipError_t conv_bf16x3(int l, bool flip, const float* x, bool relu, long B, const float* W, float* y,
-                              char* ws, const HnTrainWs& L, hipStream_t st) {
+                              char* sc, const HnTrainWs& L, hipStream_t st) {
   const HnTrainLayer& S = kHardnetTrainLayers[l];
   const long ho = hout_of(S);
   const int cin = flip ? S.cout : S.cin, cout = flip ? S.cin : S.cout;
   const int hin = flip ? (int)ho : S.hin, hout = flip ? S.hin : (int)ho;
-  float* a = reinterpret_cast<float*>(ws + L.nhwc0);
-  float* o = reinterpret_cast<float*>(ws + L.nhwc1);
-  unsigned short* wp = reinterpret_cast<unsigned short*>(ws + L.wpack);
+  float* a = reinterpret_cast<float*>(sc + L.nhwc0);
+  float* o = reinterpret_cast<float*>(sc + L.nhwc1);
+  unsigned short* wp = reinterpret_cast<unsigned short*>(sc + L.wpack);
   hipLaunchKernelGGL(k_cnhw_to_nhwc, dim3(hin * hin / 64, (unsigned)B), dim3(256), 0, st, x, cin, B, hin * hin,
                      relu ? 1 : 0, a);
   hipLaunchKernelGGL(k_pack3x3, dim3((S.cin * S.cout * 9 + 255) / 256), dim3(256), 0, st, W, S.cin, S.cout,
                      flip ? 1 : 0, wp);
   HCK(hipGetLastError());
-  HCK(hn_launch_conv_raw(l, wp, reinterpret_cast<const float*>(ws + L.zero), a, o, (int)B, st));
+  HCK(hn_launch_conv_raw(l, wp, reinterpret_cast<const float*>(sc + L.zero), a, o, (int)B, st));
   hipLaunchKernelGGL(k_nhwc_to_cnhw, dim3(hout * hout / 64, (unsigned)B), dim3(256), 0, st, o, cout, B,
                      hout * hout, y);
   return hipGetLastError();
@@ -1677,27 +1682,27 @@ static hipError_t conv_bf16x3(int l, bool flip, const float* x, bool relu, long 
 
 hipError_t hn_train_forward(const float* in, long B, const float* const* W, float* const* rmean, float* const* rvar,
                             float mom, float bn_eps, float in_eps, float l2_eps, float drop_p,
-                            unsigned long long seed, float* out, char* ws, hipStream_t st) {
+                            unsigned long long seed, float* out, char* sv, char* sc, hipStream_t st) {
   const HnTrainWs L = hn_train_layout(B);
-  HCK(hipMemsetAsync(ws + L.zero, 0, 128 * sizeof(float), st));  // the bf16x3 convs' zero bias
-  float* xn = reinterpret_cast<float*>(ws + L.xn);
+  HCK(hipMemsetAsync(sc + L.zero, 0, 128 * sizeof(float), st));  // the bf16x3 convs' zero bias
+  float* xn = reinterpret_cast<float*>(sv + L.xn);
   hipLaunchKernelGGL(k_input_norm, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, in, B, in_eps, xn,
-                     reinterpret_cast<float*>(ws + L.inv_sd));
+                     reinterpret_cast<float*>(sv + L.inv_sd));
   HCK(hipGetLastError());
   for (int l = 0; l < 7; ++l) {
     const HnTrainLayer& S = kHardnetTrainLayers[l];
     const long ho = hout_of(S), hw = ho * ho;
     // this layer's input: the normalised patch, or relu(z) of the previous layer (x the dropout
     // mask before conv6, HardNet.py:299)
-    const ActIn a{l == 0 ? xn : reinterpret_cast<const float*>(ws + L.z[l - 1]), l > 0 ? 1 : 0,
+    const ActIn a{l == 0 ? xn : reinterpret_cast<const float*>(sv + L.z[l - 1]), l > 0 ? 1 : 0,
                   l == 6 ? drop_p : 0.f, seed};
-    float* z = reinterpret_cast<float*>(ws + L.z[l]);
+    float* z = reinterpret_cast<float*>(sv + L.z[l]);
     const int tf = hn_knobs().train_f32;
     if (l == 0 && !(tf & 64)) {  // conv0: k_fwd0 (taps as the MFMA's K)
       hipLaunchKernelGGL(k_fwd0, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, xn, W[0], B, z);
       HCK(hipGetLastError());
     } else if (l >= 1 && l <= 5 && !(tf & 1))  // conv1..5: the bf16x3 MFMA conv kernels
-      HCK(conv_bf16x3(l, false, a.z, true, B, W[l], z, ws, L, st));
+      HCK(conv_bf16x3(l, false, a.z, true, B, W[l], z, sc, L, st));
     else if ((l == 1 || l == 3 || l == 5) && !(tf & 8)) {  // stride-1 3x3: k_fwd3 (f32 MFMA)
       if (l == 1) HCK((fwd3<32, 32, 32>(a.z, true, W[l], B, z, st)));
       const bool sh = !(tf & 128);  // conv3 / conv5: the shared-ring form
@@ -1709,12 +1714,12 @@ hipError_t hn_train_forward(const float* in, long B, const float* const* W, floa
       if (l == 2) HCK((fwd2<32, 64, 32>(a.z, true, W[l], B, z, st, (tf & 128) != 0)));
       if (l == 4) HCK((fwd2<64, 128, 16, 2>(a.z, true, W[l], B, z, st, !(tf & 128))));
     } else
-      HCK(conv_fwd_l(l, a, B, W[l], S.cout, z, reinterpret_cast<float*>(ws + L.part), st));  // Y = W . im2col(a)
+      HCK(conv_fwd_l(l, a, B, W[l], S.cout, z, reinterpret_cast<float*>(sc + L.part), st));  // Y = W . im2col(a)
     {
       const int NS = bn_slices(S.cout, B * hw);
-      double* part = reinterpret_cast<double*>(ws + L.bnpart);
-      float* mean = reinterpret_cast<float*>(ws + L.bnmean);
-      float* rstd = reinterpret_cast<float*>(ws + L.rstd[l]);
+      double* part = reinterpret_cast<double*>(sc + L.bnpart);
+      float* mean = reinterpret_cast<float*>(sc + L.bnmean);
+      float* rstd = reinterpret_cast<float*>(sv + L.rstd[l]);
       hipLaunchKernelGGL(k_bn_part, dim3(S.cout, NS), dim3(256), 0, st, z, B * hw, NS, part);
       hipLaunchKernelGGL(k_bn_final, dim3((S.cout + 255) / 256), dim3(256), 0, st, part, S.cout, NS, B * hw, bn_eps,
                          mom, rmean ? rmean[l] : nullptr, rvar ? rvar[l] : nullptr, mean, rstd);
@@ -1723,43 +1728,43 @@ hipError_t hn_train_forward(const float* in, long B, const float* const* W, floa
     }
   }
   hipLaunchKernelGGL(k_l2_fwd, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st,
-                     reinterpret_cast<const float*>(ws + L.z[6]), B, l2_eps, out);
+                     reinterpret_cast<const float*>(sv + L.z[6]), B, l2_eps, out);
   return hipGetLastError();
 }
 
 hipError_t hn_train_backward(const float* dout, long B, const float* const* W, float* const* dW, float* din,
-                             float l2_eps, float drop_p, unsigned long long seed, char* ws, hipStream_t st) {
+                             float l2_eps, float drop_p, unsigned long long seed, char* sv, char* sc, hipStream_t st) {
   const HnTrainWs L = hn_train_layout(B);
-  HCK(hipMemsetAsync(ws + L.zero, 0, 128 * sizeof(float), st));
-  const float* xn = reinterpret_cast<const float*>(ws + L.xn);
-  float* gbuf[2] = {reinterpret_cast<float*>(ws + L.g0), reinterpret_cast<float*>(ws + L.g1)};
+  HCK(hipMemsetAsync(sc + L.zero, 0, 128 * sizeof(float), st));
+  const float* xn = reinterpret_cast<const float*>(sv + L.xn);
+  float* gbuf[2] = {reinterpret_cast<float*>(sc + L.g0), reinterpret_cast<float*>(sc + L.g1)};
   // g: gradient w.r.t. layer l's output activation a_l (a_6 = z_6 into the L2 norm; a_5 =
   // dropout(relu(z_5)); a_l = relu(z_l) below), then in place w.r.t. its conv output
   float* g = gbuf[0];
   hipLaunchKernelGGL(k_l2_bwd, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st,
-                     reinterpret_cast<const float*>(ws + L.z[6]), dout, B, l2_eps, g);
+                     reinterpret_cast<const float*>(sv + L.z[6]), dout, B, l2_eps, g);
   HCK(hipGetLastError());
   for (int l = 6; l >= 0; --l) {
     const HnTrainLayer& S = kHardnetTrainLayers[l];
     const long ho = hout_of(S), hw = ho * ho, K = (long)S.cin * S.ks * S.ks;
     {
       const int NS = bn_slices(S.cout, B * hw);
-      double* part = reinterpret_cast<double*>(ws + L.bnpart);
-      float* m12 = reinterpret_cast<float*>(ws + L.bnmean);
-      const float* zl = reinterpret_cast<const float*>(ws + L.z[l]);
+      double* part = reinterpret_cast<double*>(sc + L.bnpart);
+      float* m12 = reinterpret_cast<float*>(sc + L.bnmean);
+      const float* zl = reinterpret_cast<const float*>(sv + L.z[l]);
       hipLaunchKernelGGL(k_bn_bwd_part, dim3(S.cout, NS), dim3(256), 0, st, g, zl, B * hw, NS, l < 6 ? 1 : 0,
                          l == 5 ? drop_p : 0.f, seed, part);
       hipLaunchKernelGGL(k_bn_bwd_final, dim3((S.cout + 255) / 256), dim3(256), 0, st, part, S.cout, NS, B * hw, m12);
       hipLaunchKernelGGL(k_bn_bwd_apply, bn_row_grid(S.cout, B * hw), dim3(256), 0, st, g, zl, B * hw, m12,
-                         reinterpret_cast<const float*>(ws + L.rstd[l]), l < 6 ? 1 : 0, l == 5 ? drop_p : 0.f, seed);
+                         reinterpret_cast<const float*>(sv + L.rstd[l]), l < 6 ? 1 : 0, l == 5 ? drop_p : 0.f, seed);
       HCK(hipGetLastError());
     }
-    const ActIn a{l == 0 ? xn : reinterpret_cast<const float*>(ws + L.z[l - 1]), l > 0 ? 1 : 0,
+    const ActIn a{l == 0 ? xn : reinterpret_cast<const float*>(sv + L.z[l - 1]), l > 0 ? 1 : 0,
                   l == 6 ? drop_p : 0.f, seed};
     float* gin = gbuf[(7 - l) & 1];  // gradient w.r.t. this layer's input activation
     const bool want_in = l > 0 || din;
     // dW [Cout][K] = dY [Cout][B hw] . im2col(a)^T (split-K slices summed in fp64)
-    float* part = reinterpret_cast<float*>(ws + L.part);
+    float* part = reinterpret_cast<float*>(sc + L.part);
     if (l == 0 && !(hn_knobs().train_f32 & 64)) {  // conv0: k_wgrad0 (taps as the MFMA's N)
       const long ns = wgrad0_slices(B);
       hipLaunchKernelGGL(k_wgrad0, dim3((unsigned)(ns / 4)), dim3(256), 0, st, xn, g, B, part);
@@ -1768,12 +1773,12 @@ hipError_t hn_train_backward(const float* dout, long B, const float* const* W, f
       hipLaunchKernelGGL(k_splitk_sum, dim3((unsigned)((32 * 9 + 63) / 64)), dim3(1024), 0, st, gs, (int)ns, part);
       HCK(hipGetLastError());
     } else if ((l == 1 || l == 3 || l == 5) && !(hn_knobs().train_f32 & 4)) {  // stride-1 3x3: k_wgrad3
-      const float* zx = reinterpret_cast<const float*>(ws + L.z[l - 1]);
+      const float* zx = reinterpret_cast<const float*>(sv + L.z[l - 1]);
       if (l == 1) HCK((wgrad3<32, 32, 32>(zx, g, B, dW[l], part, st)));
       if (l == 3) HCK((wgrad3<64, 64, 16>(zx, g, B, dW[l], part, st)));
       if (l == 5) HCK((wgrad3<128, 128, 8>(zx, g, B, dW[l], part, st)));
     } else if ((l == 2 || l == 4) && !(hn_knobs().train_f32 & 32)) {  // stride-2 3x3: k_wgrad2
-      const float* zx = reinterpret_cast<const float*>(ws + L.z[l - 1]);
+      const float* zx = reinterpret_cast<const float*>(sv + L.z[l - 1]);
       if (l == 2) HCK((wgrad2<32, 64, 16>(zx, g, B, dW[l], part, st)));
       if (l == 4) HCK((wgrad2<64, 128, 8>(zx, g, B, dW[l], part, st)));
     } else {
@@ -1781,7 +1786,7 @@ hipError_t hn_train_backward(const float* dout, long B, const float* const* W, f
     }
     if (want_in && S.s == 1 && S.ks == 3 && l >= 1 && !(hn_knobs().train_f32 & 16)) {
       // stride-1 3x3 (Cin = Cout): the data gradient is k_fwd3 over dY with the flipped weights
-      float* wf = reinterpret_cast<float*>(ws + L.wt);
+      float* wf = reinterpret_cast<float*>(sc + L.wt);
       hipLaunchKernelGGL(k_wflip, dim3((unsigned)((S.cout * S.cin * 9 + 255) / 256)), dim3(256), 0, st, W[l], S.cout,
                          S.cin, wf);
       HCK(hipGetLastError());
@@ -1792,10 +1797,10 @@ hipError_t hn_train_backward(const float* dout, long B, const float* const* W, f
     } else if (want_in && S.s == 1 && S.ks == 3 && l >= 1 && !(hn_knobs().train_f32 & 2)) {
       // stride-1 3x3 (conv1 / conv3 / conv5: Cin = Cout): the data gradient is the same conv with
       // the weights flipped and transposed, on the bf16x3 MFMA conv kernels
-      HCK(conv_bf16x3(l, true, g, false, B, W[l], gin, ws, L, st));
+      HCK(conv_bf16x3(l, true, g, false, B, W[l], gin, sc, L, st));
     } else if (want_in && S.s == 1 && S.ks == 3) {
       // stride-1 3x3: d a_{l-1} [Cin][B H H] = implicit col2im-gather GEMM Wt . dY (every tap lands)
-      HCK(conv_dgrad_l(l, g, B, W[l], S.cout, reinterpret_cast<float*>(ws + L.wt), gin, st));
+      HCK(conv_dgrad_l(l, g, B, W[l], S.cout, reinterpret_cast<float*>(sc + L.wt), gin, st));
     } else if (want_in && (l == 2 || l == 4) && !(hn_knobs().train_f32 & 32)) {
       // stride-2 3x3: k_dgrad2 (the parity classes' taps only, f32 MFMA)
       const bool sh = !(hn_knobs().train_f32 & 128);
@@ -1804,7 +1809,7 @@ hipError_t hn_train_backward(const float* dout, long B, const float* const* W, f
     } else if (want_in) {
       // stride 2 (3 of 4 taps miss a given input pixel) and the 8x8 conv6 (one tap per pixel):
       // dcol [K][n hw] = W^T [K][Cout] . dY, then the gather col2im, in chunks of patches
-      float* col = reinterpret_cast<float*>(ws + L.col);
+      float* col = reinterpret_cast<float*>(sc + L.col);
       const long nc = chunk_of(S, B);
       for (long n0 = 0; n0 < B; n0 += nc) {
         const long n = std::min(nc, B - n0);
@@ -1824,7 +1829,7 @@ hipError_t hn_train_backward(const float* dout, long B, const float* const* W, f
   if (din) {
     // input_norm with detached mean / std (HardNet.py:309-310): d input = d xn / (std + eps)
     hipLaunchKernelGGL(k_scale_rows, dim3(grid_for(B * 1024)), dim3(256), 0, st, g, B,
-                       reinterpret_cast<const float*>(ws + L.inv_sd));
+                       reinterpret_cast<const float*>(sv + L.inv_sd));
     HCK(hipGetLastError());
     HCK(hipMemcpyAsync(din, g, (size_t)B * 1024 * 4, hipMemcpyDeviceToDevice, st));
   }

@@ -115,6 +115,22 @@ class _NativeMixin:
         return d
 
 
+def _dropout_seed(device: torch.device) -> int:
+    """A 64-bit dropout seed drawn from the CUDA generator of ``device`` -- where the reference's
+    nn.Dropout draws its mask on a HIP tensor -- without a device synchronisation and without
+    touching the CPU generator (so e.g. DataLoader shuffling sees the same CPU RNG stream as with
+    the reference module).  ``torch.manual_seed`` / ``torch.cuda.manual_seed`` make it
+    reproducible: the seed is a hash of the generator's seed and its Philox offset, which is then
+    advanced as a kernel launch that consumed 4 values per thread would advance it."""
+    g = torch.cuda.default_generators[device.index if device.index is not None else torch.cuda.current_device()]
+    off = g.get_offset()
+    g.set_offset(off + 4)
+    z = (g.initial_seed() * 0x9E3779B97F4A7C15 + off + 1) & 0xFFFFFFFFFFFFFFFF
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & 0xFFFFFFFFFFFFFFFF
+    return (z ^ (z >> 31)) & 0x3FFFFFFFFFFFFFFF
+
+
 class HardNet(_NativeMixin, nn.Module):
     """HardNet model definition (hardnet/HardNet.py:275-315)."""
 
@@ -158,15 +174,21 @@ class HardNet(_NativeMixin, nn.Module):
 
     def _train_native_eligible(self, x) -> bool:
         """model.train() on a HIP fp32 [B>=2,1,32,32] batch with the reference's BatchNorm setup
-        (momentum given, running statistics tracked) runs hn_hardnet_train_* (SURVEY 8(f) row 4)."""
+        (one momentum for all seven layers, running statistics tracked, eps 1e-5) and every conv
+        weight and BN running buffer fp32 on x's device runs hn_hardnet_train_* (SURVEY 8(f) row 4).
+        Anything else runs the module's torch layers, which raise the reference module's own
+        dtype / device errors."""
         if not (getattr(self, "native_train", True) and self.training and x.is_cuda
                 and x.dtype == torch.float32 and x.dim() == 4
                 and tuple(x.shape[1:]) == (1, 32, 32) and x.shape[0] >= 2):
             return False
         bns = [self.features[i] for i in (1, 4, 7, 10, 13, 16, 20)]
+        ts = [self.features[i].weight for i in (0, 3, 6, 9, 12, 15, 19)]
+        ts += [t for b in bns for t in (b.running_mean, b.running_var)]
         return (self.input_norm_eps == 1e-7 and self.l2_eps == 1e-10
-                and all(b.momentum is not None and b.track_running_stats and b.eps == 1e-5 for b in bns)
-                and all(self.features[i].weight.is_cuda for i in (0, 3, 6, 9, 12, 15, 19)))
+                and all(b.momentum is not None and b.track_running_stats and b.eps == 1e-5
+                        and not b.affine and b.momentum == bns[0].momentum for b in bns)
+                and all(t is not None and t.dtype == torch.float32 and t.device == x.device for t in ts))
 
     def _train_native_forward(self, x):
         from . import _native as N
@@ -174,7 +196,7 @@ class HardNet(_NativeMixin, nn.Module):
         ws = [self.features[i].weight for i in N.HARDNET_CONV_IDX]
         drop = self.features[18]
         p = drop.p if drop.training else 0.0
-        seed = int(torch.randint(0, 2 ** 62, (1,), device="cpu").item()) if p > 0 else 0
+        seed = _dropout_seed(x.device) if p > 0 else 0
         return N.HardNetTrainFunction.apply(x.contiguous(), p, seed, bns, *ws)
 
     def forward(self, input):

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define HN_ABI_VERSION 1
+#define HN_ABI_VERSION 2
 
 enum hn_status {
   HN_OK = 0,
@@ -172,18 +172,23 @@ int hn_forward_u8(hn_model* m, const uint8_t* d_in, int64_t batch, int32_t in_hw
  *  backward: d_dout [B,128] -> d_dweights[l] (each [Cout,Cin,k,k] like the module's weights,
  *            overwritten), and d_din [B,1,32,32] if not NULL.
  * d_weights / d_running_* / d_dweights are host arrays of 7 device pointers (features.{0,3,6,9,
- * 12,15,19}.weight and the matching BN buffers, fp32 contiguous).  The workspace holds what the
- * backward needs: keep it (unchanged) between a forward and its backward, with the same batch,
- * dropout_p and seed (the dropout mask is a counter hash of (seed, element), recomputed).
+ * 12,15,19}.weight and the matching BN buffers, fp32 contiguous).  The workspace has two parts:
+ *   d_saved   -- written by the forward, read by its backward: keep it unchanged between a
+ *                forward and its backward (the training loop's two forwards, anchors and
+ *                positives, HardNet.py:392-393, each need their own);
+ *   d_scratch -- transient: any buffer of the size asked for, reusable by every call.
+ * The backward must get the forward's batch, dropout_p and seed (the dropout mask is a counter
+ * hash of (seed, element), recomputed).  It only reads d_saved, so it may run more than once.
  * Batch >= 2 (train-mode BatchNorm of the 1x1 conv6 output needs more than one value). */
-int hn_hardnet_train_workspace_bytes(int64_t batch, size_t* bytes_out);
+int hn_hardnet_train_workspace_bytes(int64_t batch, size_t* saved_bytes_out, size_t* scratch_bytes_out);
 int hn_hardnet_train_forward(const float* d_in, int64_t batch, const float* const* d_weights,
                              float* const* d_running_mean, float* const* d_running_var, float momentum,
-                             float dropout_p, uint64_t seed, float* d_out, void* d_workspace,
-                             size_t workspace_bytes, void* hip_stream);
+                             float dropout_p, uint64_t seed, float* d_out, void* d_saved, size_t saved_bytes,
+                             void* d_scratch, size_t scratch_bytes, void* hip_stream);
 int hn_hardnet_train_backward(const float* d_dout, int64_t batch, const float* const* d_weights,
                               float* const* d_dweights, float* d_din, float dropout_p, uint64_t seed,
-                              void* d_workspace, size_t workspace_bytes, void* hip_stream);
+                              void* d_saved, size_t saved_bytes, void* d_scratch, size_t scratch_bytes,
+                              void* hip_stream);
 
 /* Per-stage timing (profiling aid used by bench.py): when enabled, hn_forward records a
  * hipEvent pair around every kernel launch on the caller's stream.  hn_stage_times

@@ -83,6 +83,24 @@ def hardnet_forward(p: Dict[str, torch.Tensor], x: torch.Tensor, dtype=torch.flo
     return (out, acts) if return_layers else out
 
 
+def hardnet_train_forward(p: Dict[str, torch.Tensor], x: torch.Tensor, running: Dict[str, torch.Tensor],
+                          momentum: float = 0.1, dtype=torch.float32):
+    """model.train() forward of HardNet (hardnet/HardNet.py:306-315 under :381): BatchNorm with the
+    batch's statistics (biased variance normalises; the running update uses the unbiased one with
+    ``momentum``, nn.BatchNorm2d), Dropout at p = 0.  ``running`` maps
+    ``features.{i}.running_{mean,var}`` to tensors updated in place.  The weights in ``p`` may
+    require grad: the result is differentiable (the training loop's backward, :421-423)."""
+    y = input_norm(x.to(dtype))
+    for ci, bi, s, pad, relu in _HARDNET_LAYERS:
+        w = p[f"features.{ci}.weight"]
+        y = F.conv2d(y, w if w.dtype == dtype else w.to(dtype), None, s, pad)
+        y = F.batch_norm(y, running[f"features.{bi}.running_mean"], running[f"features.{bi}.running_var"],
+                         None, None, True, momentum, BN_EPS)
+        if relu:
+            y = F.relu(y)
+    return l2norm(y.reshape(y.size(0), -1))
+
+
 # ---- hardnetNAS sampled descriptor ------------------------------------------------
 # fbnet_builder.py:36-191 restricted to CANDIDATE_BLOCKS:
 #   name -> (expansion, kernel, pw_group, se)   (shuffle iff pw_group > 1)

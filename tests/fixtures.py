@@ -58,3 +58,78 @@ def build_module(name: str):
             sd[k] = torch.from_numpy(p[k])
     m.load_state_dict(sd)
     return m.eval(), fx, p
+
+
+# ---- train-mode fixtures (tests/golden/train_*.npz, tests/golden/make_train_golden.py) -------
+GRAD_SAMPLE = 16384   # entries kept per weight gradient (all of them for the smaller layers)
+N_PROJ = 8            # +-1 projections of each full gradient (splitmix64 signs, seed 31 + layer)
+
+
+def train_pairs(n: int, seed_a: int, seed_n: int):
+    """Anchors and positives: synthetic patches; a positive is its anchor blended with another
+    patch (0.75 / 0.25), so positive distances sit below most negatives as in real pairs."""
+    a = synth.synth_patches(n, seed_a)
+    o = synth.synth_patches(n, seed_n)
+    return a, (0.75 * a + 0.25 * o).astype(np.float32)
+
+
+def grad_sample_index(n: int) -> np.ndarray:
+    """The entries of a flattened gradient a fixture keeps: every k-th, k = ceil(n / 16384)."""
+    k = -(-n // GRAD_SAMPLE)
+    return np.arange(0, n, k, dtype=np.int64)
+
+
+def grad_projection_signs(i: int, n: int) -> np.ndarray:
+    """[N_PROJ, n] +-1 matrix for gradient number ``i`` (regenerable without torch)."""
+    bits = synth.splitmix64(31 + i, N_PROJ * n) >> np.uint64(63)
+    return (1.0 - 2.0 * bits.astype(np.float64)).reshape(N_PROJ, n)
+
+
+def grad_errors(g, fx, prefix: str, i: int) -> dict:
+    """Errors of a full gradient ``g`` against a fixture's fp64 summary of the same gradient:
+    L2-relative error over the sampled entries, relative error of the L2 norm, and of the +-1
+    projections (RMS over the projections relative to the norm: a +-1 projection of an error
+    vector e has RMS |e|, so all three estimate the L2-relative error)."""
+    flat = np.asarray(g, dtype=np.float64).reshape(-1)
+    ref_s = fx[f"{prefix}g{i}_sample"].astype(np.float64)
+    got_s = flat[grad_sample_index(flat.size)]
+    norm = float(fx[f"{prefix}g{i}_norm"])
+    proj = grad_projection_signs(i, flat.size) @ flat
+    return {"sample_l2rel": float(np.linalg.norm(got_s - ref_s) / max(1e-30, np.linalg.norm(ref_s))),
+            "norm_rel": abs(float(np.linalg.norm(flat)) - norm) / max(1e-30, norm),
+            "proj_rel": float(np.linalg.norm(proj - fx[f"{prefix}g{i}_proj"]) / np.sqrt(N_PROJ)
+                              / max(1e-30, norm))}
+
+
+TRAIN_CONV_IDX = (0, 3, 6, 9, 12, 15, 19)
+TRAIN_BN_IDX = (1, 4, 7, 10, 13, 16, 20)
+
+
+def train_start(init: str):
+    """(HardNet module in train mode at a train fixture's starting point, fixture, anchors,
+    positives): "golden" = synthetic weights + calibrated running stats of hardnet.npz;
+    "fresh" = ``torch.manual_seed(0); HardNet()`` (the reference's own init, fresh buffers).
+    Dropout is set to p = 0 as in the fixture (tests/golden/make_train_golden.py)."""
+    fx = load("train_hardnet")
+    meta = fx["meta"]
+    if init == "golden":
+        m, _, _ = build_module("hardnet")
+    else:
+        torch.manual_seed(0)
+        m = HardNet()
+    for i in TRAIN_CONV_IDX:
+        w = m.features[i].weight.detach().numpy()
+        if init == "golden":  # splitmix64 weights: bit-exact everywhere
+            sha = meta["inits"][init]["weights_sha256"][f"features.{i}.weight"]
+            assert synth.sha256_f32(w) == sha, f"{init} weight drift at {i}"
+        else:  # torch's orthogonal_ (a LAPACK QR) reproduces to rounding on other CPUs
+            wf = w.reshape(-1).astype(np.float64)
+            ref = fx[f"fresh/w{i}_sample"].astype(np.float64)
+            got = wf[grad_sample_index(wf.size)]
+            assert np.abs(got - ref).max() <= 1e-5 * np.abs(ref).max(), f"fresh weight drift at {i}"
+            assert abs(np.linalg.norm(wf) - float(fx[f"fresh/w{i}_norm"])) <= 1e-5 * np.linalg.norm(wf)
+    m.train()
+    m.features[18].p = 0.0
+    a, p = train_pairs(meta["n_pairs"], meta["seed_a"], meta["seed_n"])
+    assert synth.sha256_f32(a) == meta["a_sha256"] and synth.sha256_f32(p) == meta["p_sha256"]
+    return m, fx, a, p

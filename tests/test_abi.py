@@ -28,7 +28,7 @@ def test_library_exports_every_symbol():
     lib = N.load_library()
     for s in _declared_symbols():
         assert hasattr(lib, s), s
-    assert lib.hn_abi_version() == 1
+    assert lib.hn_abi_version() == 2
 
 
 def test_param_count_hardnet_matches_state_dict():
@@ -140,8 +140,21 @@ def test_product_library_has_no_ablation_builds():
         assert int(args[0]) == 0, args
 
 
+def test_product_library_has_one_tiling_per_layer_plus_fallbacks():
+    """Measured-and-rejected kernels live only in the HN_EXPERIMENTS library:
+    no Winograd kernel (hn_wino.hip), and of k_conv_pipe only conv5's production instantiation
+    (the store-through-LDS form, CST = last template argument true)."""
+    import subprocess
+    out = subprocess.run(["nm", "-C", "--defined-only", N.lib_path()], capture_output=True,
+                         text=True, check=True).stdout
+    assert "k_wino" not in out
+    pipe = _kernel_template_args("k_conv_pipe")
+    assert pipe and all(a[-1].strip() == "true" for a in pipe), pipe
+
+
 @pytest.mark.parametrize("env,val", [("HN_VARIANT", "888888"), ("HN_VARIANT", "004000"),
-                                     ("HN_VARIANT", "00000z"), ("HN_C12_CFG", "13")])
+                                     ("HN_VARIANT", "00000z"), ("HN_VARIANT", "000h00"),
+                                     ("HN_VARIANT", "111111"), ("HN_C12_CFG", "13")])
 def test_create_rejects_ablation_and_unknown_builds(env, val, monkeypatch):
     """hn_create validates the A/B switches before touching the GPU: an ablation tiling or an
     unknown k_c12 configuration is HN_ERR_ARG, never a silently wrong model."""

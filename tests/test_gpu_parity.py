@@ -79,7 +79,8 @@ def test_chunked_forward_equals_unchunked(name, cuda_device, monkeypatch):
     assert torch.equal(full, chunked)
 
 
-@pytest.mark.parametrize("variant", ["111111", "010101", "101010", "202222", "303333", "202323", "005555", "006666", "505663", "605663", "6056d3", "6056e3", "6056f3", "605gf3", "605gfg", "605hfh", "605gfh", "605hfg"])
+@pytest.mark.parametrize("variant", ["000000", "005555", "006666", "505000", "605000", "6050f0", "605g0g",
+                                     "505gfg", "605gfg", "6056f6"])
 def test_tiling_variants_match_reference(variant, cuda_device, monkeypatch):
     from hardnetnas_amd._native import NativeModel
     m, fx, _ = build_module("hardnet")

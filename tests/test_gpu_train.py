@@ -256,3 +256,148 @@ def test_train_kernel_alternatives(knobs, cuda_device):
                        timeout=110)
     print(r.stdout)
     assert r.returncode == 0, r.stdout + r.stderr[-3000:]
+
+
+# ---- the reference training loop's own step, pinned by reference-generated fixtures ----------
+@pytest.mark.parametrize("init", ["golden", "fresh"])
+def test_reference_train_step(init, cuda_device):
+    """hardnet/HardNet.py:392-423 exactly: out_a = model(data_a); out_p = model(data_p) (two
+    HardNetTrainFunction nodes, two BN batch statistics, two running-stat updates, both saved
+    workspaces alive until the backward), loss_HardNet(anchor_swap=True), backward -- against
+    tests/golden/train_hardnet.npz, which the reference's own module and loss produced
+    (tests/golden/make_train_golden.py).  Bars: outputs 1e-4 max abs (north_star), running stats
+    1e-5 relative, num_batches_tracked 2, loss 1e-5, gradients L2-relative 5e-3 vs the fp64 step."""
+    from fixtures import TRAIN_BN_IDX, TRAIN_CONV_IDX, grad_errors, train_start
+    from hardnetnas_amd.losses import loss_HardNet
+    m, fx, a, p = train_start(init)
+    m = m.to(cuda_device)
+    out_a = m(torch.from_numpy(a).to(cuda_device))
+    out_p = m(torch.from_numpy(p).to(cuda_device))
+    for y in (out_a, out_p):
+        assert "HardNetTrainFunction" in type(y.grad_fn).__name__
+    loss = loss_HardNet(out_a, out_p, anchor_swap=True)
+    loss.backward()
+    pre = f"{init}/"
+    ea = np.abs(out_a.detach().cpu().numpy() - fx[pre + "out_a_32"]).max()
+    ep = np.abs(out_p.detach().cpu().numpy() - fx[pre + "out_p_32"]).max()
+    el = abs(loss.item() - float(fx[pre + "loss_64"]))
+    print(f"{init}: out_a {ea:.2e} out_p {ep:.2e} loss {el:.2e}")
+    assert ea <= 1e-4 and ep <= 1e-4 and el <= 1e-5
+    for i in TRAIN_BN_IDX:
+        bn = m.features[i]
+        for got, key in ((bn.running_mean, "rm"), (bn.running_var, "rv")):
+            ref = fx[f"{pre}{key}{i}_32"]
+            assert np.abs(got.cpu().numpy() - ref).max() / np.abs(ref).max() <= 1e-5, (key, i)
+        assert int(bn.num_batches_tracked) == 2
+    worst = 0.0
+    for i in TRAIN_CONV_IDX:
+        e = grad_errors(m.features[i].weight.grad.cpu().numpy(), fx, pre, i)
+        print(f"{init}: features.{i}.weight grad vs reference fp64: {e}")
+        worst = max(worst, *e.values())
+    assert worst <= L2_BAR
+
+
+def test_native_train_eligibility(cuda_device):
+    """the native train path runs only when every conv weight and BN buffer is fp32 on
+    x's device and the seven BN momenta agree; otherwise the module's torch layers run (and raise
+    the reference module's own errors)."""
+    from hardnetnas_amd.model import HardNet
+    x = torch.from_numpy(golden_inputs(build_module("hardnet")[1])[:8]).to(cuda_device)
+    torch.manual_seed(0)
+    m = HardNet().to(cuda_device).train()
+    assert "HardNetTrainFunction" in type(m(x).grad_fn).__name__
+    m64 = HardNet().to(cuda_device).double().train()
+    y = m64(x.double())
+    assert "HardNetTrainFunction" not in type(y.grad_fn).__name__ and y.dtype == torch.float64
+    with pytest.raises(RuntimeError):   # fp64 weights, fp32 input: torch's own dtype error
+        m64(x)
+    mc = HardNet().train()                # weights on the CPU, input on the GPU
+    with pytest.raises(RuntimeError):
+        mc(x)
+    mm = HardNet().to(cuda_device).train()
+    mm.features[4].momentum = 0.2
+    y = mm(x)
+    assert "HardNetTrainFunction" not in type(y.grad_fn).__name__
+
+
+def test_backward_twice_with_retain_graph(cuda_device):
+    """The saved workspace is a tensor saved for backward: retain_graph=True allows a second
+    backward (gradients accumulate to exactly twice), without it torch raises its usual error."""
+    mg, _, fx = _pair(cuda_device, fresh=True)
+    x = torch.from_numpy(golden_inputs(fx)[:64]).to(cuda_device)
+    y = mg(x)
+    c = torch.randn(64, 128, generator=torch.Generator().manual_seed(9)).to(cuda_device)
+    (y * c).sum().backward(retain_graph=True)
+    g1 = [mg.features[i].weight.grad.clone() for i in (0, 3, 6, 9, 12, 15, 19)]
+    (y * c).sum().backward()
+    for g, i in zip(g1, (0, 3, 6, 9, 12, 15, 19)):
+        assert torch.allclose(mg.features[i].weight.grad, 2 * g, rtol=1e-6, atol=0), i
+    y2 = mg(x)
+    (y2 * c).sum().backward()
+    with pytest.raises(RuntimeError):
+        (y2 * c).sum().backward()
+
+
+def _dropout_mask(seed: int, p: float, b: int) -> np.ndarray:
+    """csrc/hn_train.hip drop_scale restated: the mask of element e of dropout's input, which is
+    relu(z5) in the kernels' CNHW layout [128][B][8][8]; returned as NCHW [B,128,8,8]."""
+    e = np.arange(128 * b * 64, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = np.uint64(seed) ^ (e * np.uint64(0x9E3779B97F4A7C15))
+        z ^= z >> np.uint64(30)
+        z *= np.uint64(0xBF58476D1CE4E5B9)
+        z ^= z >> np.uint64(27)
+        z *= np.uint64(0x94D049BB133111EB)
+        z ^= z >> np.uint64(31)
+    u = (z >> np.uint64(40)).astype(np.float32) * np.float32(1.0 / 16777216.0)
+    scale = np.float32(1.0) / (np.float32(1.0) - np.float32(p))
+    m = np.where(u < np.float32(p), np.float32(0.0), scale).astype(np.float32)
+    return m.reshape(128, b, 8, 8).transpose(1, 0, 2, 3).copy()
+
+
+def test_dropout_mask_matches_its_restatement(cuda_device):
+    """at p = 0.3 the forward mask (applied in the im2col loader of conv6) and the
+    backward mask (recomputed in k_bn_bwd_part / k_bn_bwd_apply from the CNHW index of z5) are the
+    same hash mask: an fp64 restatement of the module with that mask applied after features[17]
+    matches the HIP outputs (1e-4) and weight / input gradients (L2 5e-3), and the mask drops
+    ~30 % of the elements with the 1/(1-p) scale on the kept ones."""
+    from hardnetnas_amd import _native as N
+    p, seed, b = 0.3, 0x1234_5678_9ABC, 96
+    mg, _, fx = _pair(cuda_device, fresh=True)
+    md = _model64(True)
+    x = torch.from_numpy(golden_inputs(fx)[:b])
+    mask = _dropout_mask(seed, p, b)
+    frac = float((mask == 0).mean())
+    print(f"dropout: dropped fraction {frac:.4f}")
+    assert abs(frac - p) < 0.01
+    assert np.allclose(mask[mask != 0], 1.0 / 0.7, rtol=1e-6)
+    xg = x.to(cuda_device).requires_grad_(True)
+    bns = [mg.features[i] for i in N.HARDNET_BN_IDX]
+    ws = [mg.features[i].weight for i in N.HARDNET_CONV_IDX]
+    yg = N.HardNetTrainFunction.apply(xg, p, seed, bns, *ws)
+    xd = x.double().requires_grad_(True)
+    h = md.features[:18](md.input_norm(xd)) * torch.from_numpy(mask).double()
+    h = md.features[20](md.features[19](h)).reshape(b, -1)
+    yd = h / torch.sqrt((h * h).sum(dim=1, keepdim=True) + 1e-10)
+    assert (yg.detach().cpu().double() - yd.detach()).abs().max().item() <= 1e-4
+    c = torch.randn(b, 128, generator=torch.Generator().manual_seed(6))
+    (yg * c.to(cuda_device)).sum().backward()
+    (yd * c.double()).sum().backward()
+    for i in N.HARDNET_CONV_IDX:
+        assert _rel2(mg.features[i].weight.grad, md.features[i].weight.grad) <= L2_BAR, i
+    assert _rel2(xg.grad, xd.grad) <= L2_BAR
+
+
+def test_dropout_seed_leaves_the_cpu_rng_alone(cuda_device):
+    """the dropout seed comes from the CUDA generator of x's device; the CPU generator's
+    stream is the same as without the call, and torch.manual_seed makes the step reproducible."""
+    mg, _, fx = _pair(cuda_device, dropout=0.3)
+    x = torch.from_numpy(golden_inputs(fx)[:32]).to(cuda_device)
+    torch.manual_seed(5)
+    ref = torch.rand(4)
+    torch.manual_seed(5)
+    y1 = mg(x)
+    assert torch.equal(torch.rand(4), ref)
+    torch.manual_seed(5)
+    y2 = mg(x)
+    assert torch.equal(y1, y2)

@@ -1,6 +1,6 @@
 """Train step of the stock HardNet: model.train() forward + loss_HardNet
 (anchor_swap, triplet margin) + backward + SGD step at the reference's batch of 1024 pairs
-(hardnet/HardNet.py:379-441: 2 x 1024 patches per step), on the HIP train kernels vs the same
+(hardnet/HardNet.py:379-441: out_a = model(data_a); out_p = model(data_p), 2 x 1024 patches per step), on the HIP train kernels vs the same
 module's torch layers on the same GPU (MIOpen).  Prints one JSON line."""
 import json
 import os
@@ -16,7 +16,7 @@ from hardnetnas_amd.model import HardNet  # noqa: E402
 
 dev = torch.device("cuda:0")
 pairs = int(os.environ.get("PAIRS", "1024"))
-steps = int(os.environ.get("STEPS", "10"))
+steps = int(os.environ.get("TRAIN_STEPS", "10"))
 legs = os.environ.get("LEGS", "hip,torch_miopen").split(",")  # LEGS=hip: profile the HIP leg alone
 res = {"config": f"HardNet train step, {pairs} pairs ({2 * pairs} patches), loss_HardNet + SGD"}
 for name, native in (("hip", True), ("torch_miopen", False)):
@@ -26,11 +26,13 @@ for name, native in (("hip", True), ("torch_miopen", False)):
     m = HardNet().to(dev).train()
     m.native_train = native
     opt = torch.optim.SGD(m.features.parameters(), lr=0.1, momentum=0.9, dampening=0.9, weight_decay=1e-4)
-    x = torch.randn(2 * pairs, 1, 32, 32, device=dev)
+    xa = torch.randn(pairs, 1, 32, 32, device=dev)
+    xp = xa + 0.5 * torch.randn(pairs, 1, 32, 32, device=dev)
 
-    def step():
-        y = m(x)
-        loss = loss_HardNet(y[:pairs], y[pairs:], anchor_swap=True)
+    def step():  # the reference loop's shape: two model calls, HardNet.py:392-393
+        out_a = m(xa)
+        out_p = m(xp)
+        loss = loss_HardNet(out_a, out_p, anchor_swap=True)
         opt.zero_grad()
         loss.backward()
         opt.step()

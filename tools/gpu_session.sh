@@ -1,5 +1,5 @@
 #!/bin/bash
-# One GPU session on the gpurun box: tests, smoke, bench, rocprof kernel stats.
+# One GPU session on the gpurun box: tests, smoke, bench, rocprof kernel stats, PMC passes.
 # Each GPU step has its own time limit; a crash/abort/timeout (exit not 0 or 1) stops the
 # session, test failures (exit 1) do not.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
@@ -16,10 +16,12 @@ run() {  # name, seconds, command...
   return 0
 }
 STEPS=${STEPS:-pytest,smoke,bench,prof}
-[[ $STEPS == *pytest* ]] && run pytest_gpu 500 python -m pytest ${PYTEST_FILES:-tests} -m gpu -q -rf
+[[ $STEPS == *pytest* ]] && run pytest_gpu 500 python -u -m pytest ${PYTEST_FILES:-tests} -m gpu -q -rf --timeout 120 --timeout-method thread ${PYTEST_ARGS:-}
 [[ $STEPS == *smoke* ]] && run smoke 200 python -c "import __graft_entry__ as g; g.smoke()"
-[[ $STEPS == *bench* ]] && run bench 300 python bench.py ${BENCH_ARGS:-}
-[[ $STEPS == *prof* ]] && run rocprof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 3 --warmup 1 ${BENCH_ARGS:-}
+[[ $STEPS == *bench* ]] && run bench 300 python bench.py ${BENCH_ARGS:---steps 20 --warmup 5}
+[[ $STEPS == *prof* ]] && run rocprof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --no-cpu-baseline ${BENCH_ARGS:---steps 20 --warmup 5}
+[[ $STEPS == *pmc* ]] && run pmc 900 bash tools/pmc_all.sh
 [[ $STEPS == *pre* ]] && run bench_pre 200 python tools/bench_preprocess.py
 [[ $STEPS == *pairs* ]] && run bench_pairs 200 python tools/bench_pairs.py
+[[ $STEPS == *train* ]] && run bench_train 200 python tools/bench_train.py
 exit 0
