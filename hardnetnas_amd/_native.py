@@ -29,6 +29,7 @@ HN_KIND_HARDNET = 0
 HN_KIND_NAS = 1
 HN_KIND_FDL_NASNET = 2
 HN_KIND_FDL_NASNET01 = 3
+HN_KIND_NAS_SUPERNET = 4  # train mode only (hn_nas_train_*)
 HN_MAX_LAYERS = 8
 ABI_VERSION = 2   # HN_ABI_VERSION of include/hardnet_mi355x.h
 
@@ -51,7 +52,8 @@ EXPORTED = ["hn_param_count", "hn_create", "hn_workspace_bytes", "hn_forward",
             "hn_pairdist_workspace_bytes", "hn_pairdist_hardneg", "hn_pairdist_rows_workspace_bytes",
             "hn_pairdist_rows", "hn_hardnet_loss", "hn_workspace_bytes_u8", "hn_forward_u8",
             "hn_hardnet_train_workspace_bytes", "hn_hardnet_train_forward", "hn_hardnet_train_backward",
-            "hn_fpr95_workspace_bytes",
+            "hn_nas_train_tensor_count", "hn_nas_train_workspace_bytes", "hn_nas_train_forward",
+            "hn_nas_train_backward", "hn_fpr95_workspace_bytes",
             "hn_fpr95", "hn_preprocess", "hn_set_profiling",
             "hn_stage_times", "hn_destroy", "hn_last_error", "hn_abi_version"]
 
@@ -87,6 +89,11 @@ def load_library():
                                                  ctypes.c_uint64, P, P, S, P, S, P]
         lib.hn_hardnet_train_backward.argtypes = [P, I64, PP, PP, P, ctypes.c_float, ctypes.c_uint64, P, S, P, S, P]
         lib.hn_forward_u8.argtypes = [P, P, I64, I32, I32, I32, ctypes.c_float, ctypes.c_float, P, P, S, P]
+        D = ctypes.POINTER(HnArchDesc)
+        lib.hn_nas_train_tensor_count.argtypes = [D, ctypes.POINTER(S)]
+        lib.hn_nas_train_workspace_bytes.argtypes = [D, I64, ctypes.POINTER(S), ctypes.POINTER(S)]
+        lib.hn_nas_train_forward.argtypes = [D, P, I64, PP, ctypes.c_float, P, P, P, S, P, S, P]
+        lib.hn_nas_train_backward.argtypes = [D, P, P, I64, PP, P, PP, P, P, S, P, S, P]
         lib.hn_pairdist_workspace_bytes.argtypes = [I64, ctypes.POINTER(S)]
         lib.hn_pairdist_hardneg.argtypes = [P, P, I64, I32, I32, P, P, P, S, P]
         lib.hn_pairdist_rows_workspace_bytes.argtypes = [I64, I64, ctypes.POINTER(S)]
@@ -107,7 +114,8 @@ def load_library():
                      "hn_fpr95", "hn_pairdist_rows_workspace_bytes", "hn_pairdist_rows",
                      "hn_hardnet_loss", "hn_workspace_bytes_u8", "hn_forward_u8",
                      "hn_hardnet_train_workspace_bytes", "hn_hardnet_train_forward",
-                     "hn_hardnet_train_backward"):
+                     "hn_hardnet_train_backward", "hn_nas_train_tensor_count", "hn_nas_train_workspace_bytes",
+                     "hn_nas_train_forward", "hn_nas_train_backward"):
             getattr(lib, name).restype = ctypes.c_int
         if lib.hn_abi_version() != ABI_VERSION:
             raise RuntimeError(f"{path}: ABI version {lib.hn_abi_version()}, expected {ABI_VERSION}; rebuild it")
@@ -529,3 +537,83 @@ class HardNetTrainFunction(torch.autograd.Function):
                                                  scratch.data_ptr(), scratch.numel(), stream),
                    "hn_hardnet_train_backward")
         return (din, None, None, None, *dws)
+
+
+# ----------------------------------------------------------------------------------
+# train-mode hardnetNAS (hn_nas_train_*): the sampled descriptor and the supernet
+# ----------------------------------------------------------------------------------
+def supernet_desc(layers=None) -> HnArchDesc:
+    """HN_KIND_NAS_SUPERNET: every layer a MixedOperation over all 17 CANDIDATE_BLOCKS
+    (model_supernet.py:10-36, 53-68)."""
+    layers = layers or A.SEARCH_SPACE2
+    d = nas_desc(["skip"] * len(layers), layers)
+    d.kind = HN_KIND_NAS_SUPERNET
+    return d
+
+
+def train_tensors(module):
+    """The float state_dict tensors the train ABI walks, in order (num_batches_tracked and the
+    supernet's thetas left out), as (names, tensors)."""
+    names, ts = [], []
+    for k, v in module.state_dict(keep_vars=True).items():
+        if k.endswith("num_batches_tracked") or k.endswith(".thetas"):
+            continue
+        names.append(k)
+        ts.append(v)
+    return names, ts
+
+
+class NasTrainFunction(torch.autograd.Function):
+    """model.train() forward of a hardnetNAS descriptor (``desc`` kind NAS) or of the supernet
+    (kind NAS_SUPERNET, with the per-layer soft weights ``soft`` [n_layers, 17]) on the GPU
+    kernels, and its backward to every parameter (and to ``soft``) -- what autograd does over the
+    reference modules in hardnetNAS/supernet_functions/training_functions_supernet.py:88-103.
+    ``tensors`` is the module's float state_dict in order (train_tensors); ``params`` are the ones
+    among them that are parameters, in the same order; running buffers are updated in place."""
+
+    @staticmethod
+    def forward(ctx, x, soft, desc, tensors, momentum, *params):
+        lib = load_library()
+        b = x.shape[0]
+        sv, sc = ctypes.c_size_t(), ctypes.c_size_t()
+        _check(lib.hn_nas_train_workspace_bytes(ctypes.byref(desc), b, ctypes.byref(sv), ctypes.byref(sc)),
+               "hn_nas_train_workspace_bytes")
+        saved = torch.empty(sv.value, device=x.device, dtype=torch.uint8)
+        scratch = torch.empty(sc.value, device=x.device, dtype=torch.uint8)
+        out = torch.empty((b, 128), device=x.device, dtype=torch.float32)
+        soft_c = soft.detach().contiguous() if soft is not None else None
+        stream = torch.cuda.current_stream(x.device).cuda_stream
+        with torch.cuda.device(x.device):
+            _check(lib.hn_nas_train_forward(ctypes.byref(desc), x.data_ptr(), b, _ptr_array(tensors), float(momentum),
+                                            soft_c.data_ptr() if soft_c is not None else None, out.data_ptr(),
+                                            saved.data_ptr(), saved.numel(), scratch.data_ptr(), scratch.numel(),
+                                            stream), "hn_nas_train_forward")
+        del scratch
+        ctx.desc, ctx.tensors, ctx.b = desc, tensors, b
+        ctx.is_param = [t.requires_grad for t in tensors]
+        ctx.has_soft = soft is not None
+        ctx.save_for_backward(saved, x, soft_c if soft_c is not None else x.new_empty(0), *params)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        lib = load_library()
+        saved, x, soft_c, *params = ctx.saved_tensors
+        grads = [torch.empty_like(p) for p in params]
+        it = iter(grads)
+        gptrs = [next(it) if isp else None for isp in ctx.is_param]
+        sv, sc = ctypes.c_size_t(), ctypes.c_size_t()
+        _check(lib.hn_nas_train_workspace_bytes(ctypes.byref(ctx.desc), ctx.b, ctypes.byref(sv), ctypes.byref(sc)),
+               "hn_nas_train_workspace_bytes")
+        scratch = torch.empty(sc.value, device=dout.device, dtype=torch.uint8)
+        dsoft = torch.empty_like(soft_c) if ctx.has_soft else None
+        stream = torch.cuda.current_stream(dout.device).cuda_stream
+        gp = (ctypes.c_void_p * len(gptrs))(*[g.data_ptr() if g is not None else None for g in gptrs])
+        with torch.cuda.device(dout.device):
+            _check(lib.hn_nas_train_backward(ctypes.byref(ctx.desc), dout.contiguous().data_ptr(), x.data_ptr(), ctx.b,
+                                             _ptr_array(ctx.tensors),
+                                             soft_c.data_ptr() if ctx.has_soft else None, gp,
+                                             dsoft.data_ptr() if dsoft is not None else None, saved.data_ptr(),
+                                             saved.numel(), scratch.data_ptr(), scratch.numel(), stream),
+                   "hn_nas_train_backward")
+        return (None, dsoft, None, None, None, *grads)

@@ -97,15 +97,9 @@ static int fail(int code, const std::string& msg) {
       return fail(HN_ERR_HIP, std::string(#x) + ": " + hipGetErrorString(e_));             \
   } while (0)
 
-namespace {
-
 // candidate op table, restating hardnetNAS/fbnet_building_blocks/fbnet_builder.py:36-191
 // for CANDIDATE_BLOCKS (lookup_table_builder.py:18-20), in that index order.
-struct OpSpec {
-  const char* name;
-  int skip, e, k, g, se;
-};
-const OpSpec kOps[17] = {
+const HnOpSpec kHnOps[17] = {
     {"skip", 1, 0, 0, 0, 0},        {"ir_k3_e1", 0, 1, 3, 1, 0},    {"ir_k3_e3", 0, 3, 3, 1, 0},
     {"ir_k3_s4", 0, 4, 3, 4, 0},    {"ir_k5_e1", 0, 1, 5, 1, 0},    {"ir_k5_e3", 0, 3, 5, 1, 0},
     {"ir_k5_s4", 0, 4, 5, 4, 0},    {"ir_k3_e1_se", 0, 1, 3, 1, 1}, {"ir_k3_e3_se", 0, 3, 3, 1, 1},
@@ -113,6 +107,11 @@ const OpSpec kOps[17] = {
     {"ir_k5_s4_se", 0, 4, 5, 4, 1}, {"ir_k3_s2", 0, 1, 3, 2, 0},    {"ir_k5_s2", 0, 1, 5, 2, 0},
     {"ir_k3_s2_se", 0, 1, 3, 2, 1}, {"ir_k5_s2_se", 0, 1, 5, 2, 1},
 };
+
+namespace {
+
+using OpSpec = HnOpSpec;
+const OpSpec* const kOps = kHnOps;
 
 struct NasLayer {
   int op = 0, cin = 0, cout = 0, stride = 1, hin = 0, hout = 0;
@@ -1082,6 +1081,91 @@ extern "C" int hn_hardnet_train_backward(const float* d_dout, int64_t batch, con
   HIPCHK(hn_train_backward(d_dout, (long)batch, d_weights, d_dweights, d_din, 1e-10f, dropout_p,
                            (unsigned long long)seed, static_cast<char*>(d_saved), static_cast<char*>(d_scratch),
                            static_cast<hipStream_t>(hip_stream)));
+  return HN_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+// train-mode hardnetNAS (hn_nas_train.hip)
+// ---------------------------------------------------------------------------------------
+static int nas_train_desc_ok(const hn_arch_desc* d) {
+  if (!d) return fail(HN_ERR_ARG, "NULL desc");
+  if (d->kind != HN_KIND_NAS && d->kind != HN_KIND_NAS_SUPERNET)
+    return fail(HN_ERR_ARG, "train mode: desc kind must be HN_KIND_NAS or HN_KIND_NAS_SUPERNET");
+  if (d->n_layers < 1 || d->n_layers > HN_MAX_LAYERS) return fail(HN_ERR_ARG, "bad n_layers");
+  int hw = 32, c = 32;
+  for (int i = 0; i < d->n_layers; ++i) {
+    if (d->kind == HN_KIND_NAS && (d->op[i] < 0 || d->op[i] >= 17)) return fail(HN_ERR_ARG, "bad op index");
+    if (d->c_in[i] != c || (d->stride[i] != 1 && d->stride[i] != 2) || hw % d->stride[i])
+      return fail(HN_ERR_ARG, "layer " + std::to_string(i) + ": channels / stride do not chain");
+    if (d->c_out[i] < 1 || d->c_out[i] > 128 || d->c_in[i] % 4 || d->c_out[i] % 4)
+      return fail(HN_ERR_ARG, "layer " + std::to_string(i) + ": channel count");
+    c = d->c_out[i];
+    hw /= d->stride[i];
+  }
+  if (hw != 4) return fail(HN_ERR_ARG, "the layers must reduce 32x32 to the 4x4 head input");
+  return HN_OK;
+}
+
+extern "C" int hn_nas_train_tensor_count(const hn_arch_desc* desc, size_t* n_out) {
+  int rc = nas_train_desc_ok(desc);
+  if (rc) return rc;
+  if (!n_out) return fail(HN_ERR_ARG, "NULL n_out");
+  hn_nas_train_plan(*desc, 2, n_out, nullptr, nullptr);
+  return HN_OK;
+}
+
+extern "C" int hn_nas_train_workspace_bytes(const hn_arch_desc* desc, int64_t batch, size_t* saved_bytes_out,
+                                            size_t* scratch_bytes_out) {
+  int rc = nas_train_desc_ok(desc);
+  if (rc) return rc;
+  if (!saved_bytes_out || !scratch_bytes_out || batch < 2 || batch > (1 << 22))
+    return fail(HN_ERR_ARG, "batch must be 2 .. 2^22 (and both size pointers given)");
+  hn_nas_train_plan(*desc, (long)batch, nullptr, saved_bytes_out, scratch_bytes_out);
+  return HN_OK;
+}
+
+static int nas_train_args(const hn_arch_desc* desc, int64_t batch, float* const* tensors, void* saved,
+                          size_t saved_bytes, void* scratch, size_t scratch_bytes, const float* soft) {
+  size_t need_sv = 0, need_sc = 0, nt = 0;
+  int rc = hn_nas_train_workspace_bytes(desc, batch, &need_sv, &need_sc);
+  if (rc) return rc;
+  hn_nas_train_plan(*desc, (long)batch, &nt, nullptr, nullptr);
+  if (!saved || !scratch) return fail(HN_ERR_ARG, "NULL workspace");
+  if (saved_bytes < need_sv)
+    return fail(HN_ERR_WORKSPACE, "saved workspace too small: need " + std::to_string(need_sv) + " bytes");
+  if (scratch_bytes < need_sc)
+    return fail(HN_ERR_WORKSPACE, "scratch workspace too small: need " + std::to_string(need_sc) + " bytes");
+  if (!tensors) return fail(HN_ERR_ARG, "NULL tensor pointer array");
+  for (size_t i = 0; i < nt; ++i)
+    if (!tensors[i]) return fail(HN_ERR_ARG, "NULL tensor pointer " + std::to_string(i));
+  if (desc->kind == HN_KIND_NAS_SUPERNET && !soft) return fail(HN_ERR_ARG, "the supernet needs d_soft");
+  return HN_OK;
+}
+
+extern "C" int hn_nas_train_forward(const hn_arch_desc* desc, const float* d_in, int64_t batch, float* const* d_tensors,
+                                    float momentum, const float* d_soft, float* d_out, void* d_saved,
+                                    size_t saved_bytes, void* d_scratch, size_t scratch_bytes, void* hip_stream) {
+  int rc = nas_train_args(desc, batch, d_tensors, d_saved, saved_bytes, d_scratch, scratch_bytes, d_soft);
+  if (rc) return rc;
+  if (!d_in || !d_out) return fail(HN_ERR_ARG, "NULL device pointer");
+  HIPCHK(hn_nas_train_forward_impl(*desc, d_in, (long)batch, d_tensors, momentum, d_soft, d_out,
+                                   static_cast<char*>(d_saved), static_cast<char*>(d_scratch),
+                                   static_cast<hipStream_t>(hip_stream)));
+  return HN_OK;
+}
+
+extern "C" int hn_nas_train_backward(const hn_arch_desc* desc, const float* d_dout, const float* d_in, int64_t batch,
+                                     float* const* d_tensors, const float* d_soft, float* const* d_grads,
+                                     float* d_dsoft, void* d_saved, size_t saved_bytes, void* d_scratch,
+                                     size_t scratch_bytes, void* hip_stream) {
+  int rc = nas_train_args(desc, batch, d_tensors, d_saved, saved_bytes, d_scratch, scratch_bytes, d_soft);
+  if (rc) return rc;
+  if (!d_dout || !d_in) return fail(HN_ERR_ARG, "NULL device pointer");
+  if (!d_grads) return fail(HN_ERR_ARG, "NULL gradient pointer array");
+  if (desc->kind == HN_KIND_NAS_SUPERNET && !d_dsoft) return fail(HN_ERR_ARG, "the supernet needs d_dsoft");
+  HIPCHK(hn_nas_train_backward_impl(*desc, d_dout, (long)batch, d_in, d_tensors, d_soft, d_grads, d_dsoft,
+                                    static_cast<char*>(d_saved), static_cast<char*>(d_scratch),
+                                    static_cast<hipStream_t>(hip_stream)));
   return HN_OK;
 }
 

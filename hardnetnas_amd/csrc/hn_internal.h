@@ -2,6 +2,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include "hardnet_mi355x.h"
+
 // A/B switches of the launchers.  Read from the environment once per model in hn_create (and
 // once per process for the model-less entry points); hn_forward makes the calling model's
 // set current for the duration of the call (thread-local), so launchers never call getenv.
@@ -149,11 +151,27 @@ struct HnTrainLayer {
   int cin, cout, hin, ks, s, pad;
 };
 extern const HnTrainLayer kHardnetTrainLayers[7];
+// CANDIDATE_BLOCKS (lookup_table_builder.py:18-20) as (skip, expansion, kernel, pw groups, SE);
+// the ChannelShuffle runs iff groups > 1 (fbnet_builder.py:36-191); defined in hn_api.hip
+struct HnOpSpec {
+  const char* name;
+  int skip, e, k, g, se;
+};
+extern const HnOpSpec kHnOps[17];
+
 struct HnTrainWs {  // byte offsets into the train workspace's saved region (xn .. rstd) / scratch region
   size_t xn, inv_sd, z[7], rstd[7], saved_total;
   size_t g0, g1, col, part, bnpart, bnmean, wt, nhwc0, nhwc1, wpack, zero, scratch_total;
 };
 HnTrainWs hn_train_layout(long B);
+// train-mode hardnetNAS (hn_nas_train.hip): tensors consumed, saved / scratch workspace bytes
+int hn_nas_train_plan(const hn_arch_desc& d, long B, size_t* n_tensors, size_t* saved, size_t* scratch);
+hipError_t hn_nas_train_forward_impl(const hn_arch_desc& d, const float* in, long B, float* const* tensors,
+                                     float momentum, const float* soft, float* out, char* saved, char* scratch,
+                                     hipStream_t st);
+hipError_t hn_nas_train_backward_impl(const hn_arch_desc& d, const float* dout, long B, const float* in,
+                                      float* const* tensors, const float* soft, float* const* grads, float* dsoft,
+                                      char* saved, char* scratch, hipStream_t st);
 hipError_t hn_train_forward(const float* in, long B, const float* const* W, float* const* rmean, float* const* rvar,
                             float mom, float bn_eps, float in_eps, float l2_eps, float drop_p,
                             unsigned long long seed, float* out, char* saved, char* scratch, hipStream_t st);

@@ -12,7 +12,7 @@ from __future__ import annotations
 
 import torch
 
-__all__ = ["distance_matrix_vector", "loss_HardNet"]
+__all__ = ["distance_matrix_vector", "loss_HardNet", "SupernetLoss"]
 
 
 def distance_matrix_vector(anchor: torch.Tensor, positive: torch.Tensor) -> torch.Tensor:
@@ -50,3 +50,21 @@ def loss_HardNet(anchor: torch.Tensor, positive: torch.Tensor, anchor_swap: bool
     else:
         raise ValueError(f"unknown loss_type {loss_type!r}")
     return loss.mean()
+
+
+class SupernetLoss(torch.nn.Module):
+    """The supernet search loss (hardnetNAS/supernet_functions/model_supernet.py:88-110):
+    alpha * (loss_HardNet(outs, targets) + clamp(log(latency^beta) * (log(((sample_latency - target)
+    / target)^2) + 5) * 0.2, 0)), with the hardnetNAS loss_HardNet (general_functions/Losses.py:27-51:
+    anchor swap always on, margin 1).  alpha 0.2, beta 0.6 (config_for_supernet.py)."""
+
+    def __init__(self, alpha: float = 0.2, beta: float = 0.6):
+        super().__init__()
+        self.alpha, self.beta = alpha, beta
+
+    def forward(self, outs, targets, latency, sample_latency, target):
+        ce = loss_HardNet(outs, targets, anchor_swap=True)
+        lat = torch.clamp(torch.log(latency ** self.beta) * (torch.log(((sample_latency - target) / target) ** 2) + 5)
+                          * 0.2, 0)
+        loss = self.alpha * (ce + lat)
+        return loss, ce, lat

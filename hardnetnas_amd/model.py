@@ -403,6 +403,8 @@ class HardNetNAS(_NativeMixin, nn.Module):
         y = self._dispatch_native(x)
         if y is not None:
             return y
+        if _nas_train_native_eligible(self, x, self.layers):
+            return _nas_train_native_forward(self, x, None)
         y = self.first(x)
         for op in self.stages:
             y = op(y)
@@ -428,6 +430,116 @@ class HardNetNAS(_NativeMixin, nn.Module):
             elif k.startswith("first.") or k.startswith("last_stages."):
                 out[k] = v
         return self.load_state_dict(out, strict=strict)
+
+
+def _nas_train_native_eligible(module: nn.Module, x: torch.Tensor, layers) -> bool:
+    """model.train() of HardNetNAS / HardNetNASSupernet on a HIP fp32 [B>=2,1,32,32] batch that
+    needs no input gradient, with the reference's BatchNorm setup (one momentum, running statistics
+    tracked, eps 1e-5) and every parameter / buffer fp32 contiguous on x's device, runs
+    hn_nas_train_* (SURVEY 8(f) row 4).  Anything else runs the module's torch layers."""
+    if not (getattr(module, "native_train", True) and module.training and x.is_cuda
+            and x.dtype == torch.float32 and x.dim() == 4 and tuple(x.shape[1:]) == (1, 32, 32)
+            and x.shape[0] >= 2 and not (torch.is_grad_enabled() and x.requires_grad)
+            and list(layers) == list(A.SEARCH_SPACE2)):
+        return False
+    bns = [m for m in module.modules() if isinstance(m, nn.BatchNorm2d)]
+    if not all(b.momentum is not None and b.track_running_stats and b.eps == 1e-5
+               and b.momentum == bns[0].momentum for b in bns):
+        return False
+    ts = list(module.parameters()) + [b for b in module.buffers() if b.dtype != torch.int64]
+    return all(t.dtype == torch.float32 and t.device == x.device and t.is_contiguous() for t in ts)
+
+
+def _nas_train_native_forward(module: nn.Module, x: torch.Tensor, soft):
+    from . import _native as N
+    bns = [m for m in module.modules() if isinstance(m, nn.BatchNorm2d)]
+    desc = N.supernet_desc() if soft is not None else N.nas_desc(module.arch_ops, module.layers)
+    _, tensors = N.train_tensors(module)
+    params = [t for t in tensors if t.requires_grad]
+    y = N.NasTrainFunction.apply(x.contiguous(), soft, desc, tensors, bns[0].momentum, *params)
+    for b in bns:
+        b.num_batches_tracked.add_(1)
+    return y
+
+
+class MixedOperation(nn.Module):
+    """One searchable layer of the supernet (hardnetNAS/supernet_functions/model_supernet.py:10-50):
+    all 17 CANDIDATE_BLOCKS on the same input, output sum_j m_j op_j(x) with m the Gumbel-softmax of
+    ``thetas`` (initialised to 1/17), plus the latency bookkeeping of the reference."""
+
+    def __init__(self, c_in, c_out, stride, latency=None):
+        super().__init__()
+        self.ops = nn.ModuleList([make_op(op, c_in, c_out, stride) for op in A.CANDIDATE_BLOCKS])
+        self.latency = list(latency) if latency is not None else [1.0] * len(A.CANDIDATE_BLOCKS)
+        self.thetas = nn.Parameter(torch.Tensor([1.0 / len(A.CANDIDATE_BLOCKS)] * len(A.CANDIDATE_BLOCKS)))
+
+    def softnms(self, variables, ksize, strength):
+        """model_supernet.py:38-50 (1-D soft NMS over the op probabilities)."""
+        maxk = F.max_pool1d(variables, ksize, stride=1, padding=ksize // 2)
+        max_all, _ = maxk.max(dim=-1, keepdim=True)
+        exp_maps = torch.exp(strength * (variables - max_all))
+        exp_maps_pad = F.pad(exp_maps, [ksize // 2, ksize // 2], mode="replicate")
+        sum_exp = F.conv1d(exp_maps_pad, weight=torch.ones([1, 1, ksize]).to(exp_maps.device), stride=1)
+        return exp_maps / sum_exp
+
+    def latency_terms(self, m, latency_to_accumulate):
+        """model_supernet.py:27-35: the soft latency, its soft-NMS and hard-sample forms."""
+        latency = sum(mj * lat for mj, lat in zip(m, self.latency))
+        nmsprobs = self.softnms(m.unsqueeze(0).unsqueeze(0), len(self.latency), 50)
+        soft = sum(p * lat for p, lat in zip(nmsprobs.squeeze(), self.latency))
+        hard = self.latency[torch.argmax(m).item()]
+        return latency_to_accumulate + latency, soft, hard
+
+    def forward(self, x, temperature, latency_to_accumulate, m=None):
+        if m is None:
+            m = F.gumbel_softmax(self.thetas, temperature)
+        out = sum(mj * op(x) for mj, op in zip(m, self.ops))
+        lat, soft, hard = self.latency_terms(m, latency_to_accumulate)
+        return out, lat, soft, hard
+
+
+class HardNetNASSupernet(nn.Module):
+    """FBNet_Stochastic_SuperNet (hardnetNAS/supernet_functions/model_supernet.py:53-85) with the
+    reference's module names (``first``, ``stages_to_search.{i}.ops.{j}`` / ``.thetas``,
+    ``last_stages``), so its checkpoints load unchanged.  ``latency``: per layer, the 17 op
+    latencies of the lookup table (default 1.0).
+
+    ``forward(x, temperature, latency_to_accumulate, soft_weights=None)`` returns
+    ``(y, latency_to_accumulate, soft, hard)`` like the reference.  ``soft_weights`` ([6, 17],
+    may require grad) replaces the per-layer Gumbel-softmax draw of ``thetas`` -- a caller that
+    wants thetas' gradient passes ``softmax((thetas + g) / tau)`` with its own Gumbel noise g.  In
+    train() on a HIP batch the descriptor runs on hn_nas_train_* (every op of every layer, the
+    weighted sum, train-mode BatchNorm, and the backward to every parameter and to the soft
+    weights); otherwise the module's torch layers run."""
+
+    def __init__(self, latency=None, layers: Sequence = None):
+        super().__init__()
+        self.layers = list(layers) if layers is not None else list(A.SEARCH_SPACE2)
+        lat = latency if latency is not None else [None] * len(self.layers)
+        self.first = ConvBNRelu(1, A.STEM_CHANNELS, 3, 1, 1, relu=True)
+        self.stages_to_search = nn.ModuleList([MixedOperation(ci, co, s, lat[i])
+                                               for i, (ci, co, s) in enumerate(self.layers)])
+        self.last_stages = nn.Sequential(OrderedDict([
+            ("conv_k1", nn.Conv2d(self.layers[-1][1], A.DESC_DIM, kernel_size=A.HEAD_KERNEL, bias=False)),
+            ("batchnorm", nn.BatchNorm2d(A.DESC_DIM, affine=False)),
+            ("flatten", Flatten()),
+        ]))
+
+    def forward(self, x, temperature, latency_to_accumulate, soft_weights=None):
+        if soft_weights is None:
+            soft_weights = torch.stack([F.gumbel_softmax(st.thetas, temperature) for st in self.stages_to_search])
+        soft, hard = 0, 0
+        for i, st in enumerate(self.stages_to_search):
+            latency_to_accumulate, s_i, h_i = st.latency_terms(soft_weights[i], latency_to_accumulate)
+            soft, hard = soft + s_i, hard + h_i
+        if _nas_train_native_eligible(self, x, self.layers):
+            y = _nas_train_native_forward(self, x, soft_weights.to(device=x.device, dtype=torch.float32))
+            return y, latency_to_accumulate, soft, hard
+        y = self.first(x)
+        for i, st in enumerate(self.stages_to_search):
+            y = sum(mj * op(y) for mj, op in zip(soft_weights[i], st.ops))
+        y = self.last_stages(y)
+        return y / torch.norm(y, p=2, dim=-1, keepdim=True), latency_to_accumulate, soft, hard
 
 
 FP16_SPLIT_LIMIT = 65504.0  # largest finite fp16: the hi half of an fp16x3 operand

@@ -46,7 +46,9 @@ enum hn_kind {
   HN_KIND_HARDNET = 0,      /* stock HardNet, hardnet/HardNet.py:275-304 */
   HN_KIND_NAS = 1,          /* sampled hardnetNAS net, model_supernet.py:53-85 */
   HN_KIND_FDL_NASNET = 2,   /* FDLNet HardNetNeiMask, FDLNet-master/latency/NASNet/model/des.py:8-55 */
-  HN_KIND_FDL_NASNET01 = 3  /* FDLNet HardNetNeiMask, FDLNet-master/latency/NASNet_0.1/model/des.py:10-55 */
+  HN_KIND_FDL_NASNET01 = 3, /* FDLNet HardNetNeiMask, FDLNet-master/latency/NASNet_0.1/model/des.py:10-55 */
+  HN_KIND_NAS_SUPERNET = 4  /* train mode only: FBNet_Stochastic_SuperNet, model_supernet.py:53-85 (every layer
+                               a MixedOperation over all 17 CANDIDATE_BLOCKS, :10-36) */
 };
 
 #define HN_MAX_LAYERS 8
@@ -189,6 +191,36 @@ int hn_hardnet_train_backward(const float* d_dout, int64_t batch, const float* c
                               float* const* d_dweights, float* d_din, float dropout_p, uint64_t seed,
                               void* d_saved, size_t saved_bytes, void* d_scratch, size_t scratch_bytes,
                               void* hip_stream);
+
+/* Train-mode hardnetNAS (second half; hardnetNAS/supernet_functions/
+ * training_functions_supernet.py:88-103 runs the module in train() through autograd):
+ *   desc->kind HN_KIND_NAS           the sampled descriptor (op[i] per layer), model_supernet.py:53-85
+ *                                    with each MixedOperation replaced by its arch op;
+ *   desc->kind HN_KIND_NAS_SUPERNET  the supernet: layer i outputs sum_j m[i][j] op_j(x) over all 17
+ *                                    CANDIDATE_BLOCKS (MixedOperation.forward, model_supernet.py:23-36);
+ *                                    d_soft = the soft weights m [n_layers][17] (the caller's
+ *                                    Gumbel-softmax draw, :24), d_dsoft receives d loss / d m.
+ * forward : stem ConvBNRelu -> 6 layers -> 4x4 head conv -> BatchNorm2d(affine=False) -> y / ||y||,
+ *           every BatchNorm with the batch's statistics (running stats updated with `momentum`,
+ *           unbiased variance).  d_in [B,1,32,32] fp32 (no input_norm; the NAS loaders normalise).
+ * backward: d_dout [B,128] -> d_grads (every conv weight, BN weight / bias and SE weight / bias,
+ *           overwritten); no input gradient.
+ * d_tensors: host array of hn_nas_train_tensor_count() device pointers, one per float tensor of the
+ * module's state_dict in order (num_batches_tracked and the supernet's `thetas` left out): conv
+ * weights, BN weight, bias, running_mean, running_var (updated in place), SE weights / biases.
+ * d_grads: the same length; entries for running buffers are ignored (may be NULL).
+ * Workspace: d_saved is written by the forward and read by its backward (one per forward call);
+ * d_scratch is transient. */
+int hn_nas_train_tensor_count(const hn_arch_desc* desc, size_t* n_out);
+int hn_nas_train_workspace_bytes(const hn_arch_desc* desc, int64_t batch, size_t* saved_bytes_out,
+                                 size_t* scratch_bytes_out);
+int hn_nas_train_forward(const hn_arch_desc* desc, const float* d_in, int64_t batch, float* const* d_tensors,
+                         float momentum, const float* d_soft, float* d_out, void* d_saved, size_t saved_bytes,
+                         void* d_scratch, size_t scratch_bytes, void* hip_stream);
+int hn_nas_train_backward(const hn_arch_desc* desc, const float* d_dout, const float* d_in, int64_t batch,
+                          float* const* d_tensors, const float* d_soft, float* const* d_grads, float* d_dsoft,
+                          void* d_saved, size_t saved_bytes, void* d_scratch, size_t scratch_bytes,
+                          void* hip_stream);
 
 /* Per-stage timing (profiling aid used by bench.py): when enabled, hn_forward records a
  * hipEvent pair around every kernel launch on the caller's stream.  hn_stage_times

@@ -73,9 +73,9 @@ def train_pairs(n: int, seed_a: int, seed_n: int):
     return a, (0.75 * a + 0.25 * o).astype(np.float32)
 
 
-def grad_sample_index(n: int) -> np.ndarray:
-    """The entries of a flattened gradient a fixture keeps: every k-th, k = ceil(n / 16384)."""
-    k = -(-n // GRAD_SAMPLE)
+def grad_sample_index(n: int, cap: int = GRAD_SAMPLE) -> np.ndarray:
+    """The entries of a flattened gradient a fixture keeps: every k-th, k = ceil(n / cap)."""
+    k = -(-n // cap)
     return np.arange(0, n, k, dtype=np.int64)
 
 
@@ -85,20 +85,40 @@ def grad_projection_signs(i: int, n: int) -> np.ndarray:
     return (1.0 - 2.0 * bits.astype(np.float64)).reshape(N_PROJ, n)
 
 
-def grad_errors(g, fx, prefix: str, i: int) -> dict:
-    """Errors of a full gradient ``g`` against a fixture's fp64 summary of the same gradient:
-    L2-relative error over the sampled entries, relative error of the L2 norm, and of the +-1
-    projections (RMS over the projections relative to the norm: a +-1 projection of an error
-    vector e has RMS |e|, so all three estimate the L2-relative error)."""
+def name_seed(name: str) -> int:
+    """Projection seed of a named tensor (the NAS fixtures key gradients by state_dict name)."""
+    import zlib
+    return 1000 + zlib.crc32(name.encode())
+
+
+def summary(g: np.ndarray, seed: int, cap: int = GRAD_SAMPLE) -> dict:
+    """(sample, norm, proj) of a tensor: the fixture form of a gradient (tests/golden/make_train_golden.py)."""
     flat = np.asarray(g, dtype=np.float64).reshape(-1)
-    ref_s = fx[f"{prefix}g{i}_sample"].astype(np.float64)
-    got_s = flat[grad_sample_index(flat.size)]
-    norm = float(fx[f"{prefix}g{i}_norm"])
-    proj = grad_projection_signs(i, flat.size) @ flat
-    return {"sample_l2rel": float(np.linalg.norm(got_s - ref_s) / max(1e-30, np.linalg.norm(ref_s))),
-            "norm_rel": abs(float(np.linalg.norm(flat)) - norm) / max(1e-30, norm),
-            "proj_rel": float(np.linalg.norm(proj - fx[f"{prefix}g{i}_proj"]) / np.sqrt(N_PROJ)
-                              / max(1e-30, norm))}
+    return {"sample": flat[grad_sample_index(flat.size, cap)].astype(np.float32),
+            "norm": np.float64(np.linalg.norm(flat)), "proj": grad_projection_signs(seed, flat.size) @ flat}
+
+
+def summary_errors(g, fx, key: str, seed: int, cap: int = GRAD_SAMPLE) -> dict:
+    """Errors of a full tensor ``g`` against a fixture's fp64 summary of it (keys key_sample /
+    key_norm / key_proj): L2-relative error over the sampled entries, relative error of the L2 norm,
+    and of the +-1 projections (RMS over the projections relative to the norm: a +-1 projection of
+    an error vector e has RMS |e|, so all three estimate the L2-relative error).  Entries whose
+    reference norm is zero report the absolute norm instead."""
+    flat = np.asarray(g, dtype=np.float64).reshape(-1)
+    ref_s = fx[f"{key}_sample"].astype(np.float64)
+    got_s = flat[grad_sample_index(flat.size, cap)]
+    norm = float(fx[f"{key}_norm"])
+    proj = grad_projection_signs(seed, flat.size) @ flat
+    if norm == 0.0:
+        return {"abs_norm": float(np.linalg.norm(flat))}
+    return {"sample_l2rel": float(np.linalg.norm(got_s - ref_s) / max(1e-30 * norm, np.linalg.norm(ref_s))),
+            "norm_rel": abs(float(np.linalg.norm(flat)) - norm) / norm,
+            "proj_rel": float(np.linalg.norm(proj - fx[f"{key}_proj"]) / np.sqrt(N_PROJ) / norm)}
+
+
+def grad_errors(g, fx, prefix: str, i: int) -> dict:
+    """summary_errors for the stock HardNet fixture's gradient of features.{i}.weight."""
+    return summary_errors(g, fx, f"{prefix}g{i}", i)
 
 
 TRAIN_CONV_IDX = (0, 3, 6, 9, 12, 15, 19)
@@ -133,3 +153,79 @@ def train_start(init: str):
     a, p = train_pairs(meta["n_pairs"], meta["seed_a"], meta["seed_n"])
     assert synth.sha256_f32(a) == meta["a_sha256"] and synth.sha256_f32(p) == meta["p_sha256"]
     return m, fx, a, p
+
+
+# ---- hardnetNAS train fixtures (tests/golden/train_nas.npz) ----------------------------------
+def nas_train_start(name: str):
+    """(HardNetNAS in train mode at the fixture's starting point: golden synthetic weights +
+    calibrated running statistics, BN momentum 0.1; fixture; anchors; positives)."""
+    fx = load("train_nas")
+    meta = fx["meta"][name]
+    m, _, _ = build_module(name)
+    m.train()
+    a, p = train_pairs(meta["n_pairs"], meta["seed_a"], meta["seed_n"])
+    return m, fx, a, p
+
+
+def supernet_start():
+    """(HardNetNASSupernet in train mode with the fixture's synthetic weights, fresh BatchNorm
+    buffers and latencies; fixture; X; Y)."""
+    from hardnetnas_amd.model import HardNetNASSupernet
+    fx = load("train_nas")
+    meta = fx["meta"]["supernet"]
+    lat = fx["super/latency"]
+    m = HardNetNASSupernet(latency=[list(map(float, lat[i])) for i in range(6)])
+    sd = m.state_dict()
+    tmpl = {k: tuple(v.shape) for k, v in sd.items() if not k.endswith(".thetas")}
+    w = synth.synth_state_dict(tmpl, 1234)
+    sd.update({k: torch.from_numpy(v) for k, v in w.items()})
+    m.load_state_dict(sd)
+    m.train()
+    a, p = train_pairs(meta["n_pairs"], meta["seed_a"], meta["seed_n"])
+    return m, fx, a, p
+
+
+def supernet_step(m, fx, x, y, device=None):
+    """The supernet training step of training_functions_supernet.py:88-103 with the fixture's Gumbel
+    noise: soft weights softmax((thetas + g) / T) per call (so thetas get their gradient), outs_X with
+    grad, outs_Y under no_grad, SupernetLoss, backward.  Returns (outs_X, outs_Y, loss, ce, lat)."""
+    from hardnetnas_amd.losses import SupernetLoss
+    meta = fx["meta"]["supernet"]
+    T = meta["temperature"]
+    dev = device or torch.device("cpu")
+    g = torch.from_numpy(fx["super/noise"]).to(dev)
+    thetas = torch.stack([st.thetas for st in m.stages_to_search])
+    soft_x = ((thetas + g[:6]) / T).softmax(-1)
+    lat0 = torch.tensor([[0.0]], device=dev, requires_grad=True)
+    ox, lacc, soft1, _ = m(torch.from_numpy(x).to(dev), T, lat0, soft_weights=soft_x)
+    with torch.no_grad():
+        soft_y = ((thetas + g[6:]) / T).softmax(-1)
+        oy, _, _, _ = m(torch.from_numpy(y).to(dev), T, lacc, soft_weights=soft_y)
+    loss, ce, lat = SupernetLoss()(ox, oy, lacc, soft1, meta["target_latency"])
+    loss.backward()
+    return ox, oy, loss, ce, lat
+
+
+def nas_grad_check(named_grads, fx, prefix: str, cap: int = GRAD_SAMPLE, bar: float = 5e-3):
+    """Worst summary error of every parameter gradient against the fixture's fp64 summaries, in
+    units where ``bar`` is the pass mark (an error is scaled by bar / max(bar, 3 x the reference's
+    own fp32-vs-fp64 error of that gradient)).  A
+    gradient whose fp64 norm is ~0 (a BN bias right before a linear map into another BatchNorm,
+    whose mean subtraction cancels it exactly) is checked in absolute terms against the layer
+    scale instead.  Returns (worst relative error, name)."""
+    scale = max(float(fx[f"{prefix}g/{k}_norm"]) for k, _ in named_grads)
+    ref_err = dict(zip([str(n) for n in fx[f"{prefix}grad_names"]], fx[f"{prefix}fp32_err"]))
+    worst, where = 0.0, ""
+    for k, g in named_grads:
+        key = f"{prefix}g/{k}"
+        norm = float(fx[f"{key}_norm"])
+        if norm < 1e-9 * scale:
+            e = float(np.linalg.norm(np.asarray(g, dtype=np.float64))) / scale
+            assert e <= 1e-6, (k, e)
+            continue
+        # relative to the bar, or to 3x the reference's own fp32 error on this gradient when that is
+        # larger (a ReLU kink the fp32 reference itself lands on the other side of)
+        e = max(summary_errors(g, fx, key, name_seed(k), cap).values()) / max(bar, 3.0 * float(ref_err[k])) * bar
+        if e > worst:
+            worst, where = e, k
+    return worst, where

@@ -1,0 +1,113 @@
+"""Train-mode hardnetNAS on MI355X (second half): hn_nas_train_* through
+HardNetNAS.train() and HardNetNASSupernet.train(), against the reference's own training steps
+(tests/golden/train_nas.npz, made by tests/golden/make_train_golden.py from
+hardnetNAS/supernet_functions/model_supernet.py + training_functions_supernet.py:88-103).
+
+Bars: descriptors 1e-4 max abs (north_star), running statistics 1e-5 relative, the loss 1e-5,
+every gradient L2-relative 5e-3 against the reference's fp64 step (or 3x the reference's own fp32
+error on that gradient where a ReLU kink makes that larger; tests/fixtures.py::nas_grad_check)."""
+import numpy as np
+import pytest
+import torch
+
+from fixtures import nas_grad_check, nas_train_start, supernet_start, supernet_step
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("name", ["wang2", "cov_b"])
+def test_nas_train_step_matches_reference(name, cuda_device):
+    """A sampled descriptor (wang2; cov_b: SE and ChannelShuffle in every layer) in the loop's shape:
+    two train() calls, the hardnetNAS loss_HardNet (anchor swap), backward."""
+    from hardnetnas_amd.losses import loss_HardNet
+    m, fx, a, p = nas_train_start(name)
+    m = m.to(cuda_device)
+    oa = m(torch.from_numpy(a).to(cuda_device))
+    op_ = m(torch.from_numpy(p).to(cuda_device))
+    assert "NasTrainFunction" in type(oa.grad_fn).__name__
+    loss = loss_HardNet(oa, op_, anchor_swap=True)
+    loss.backward()
+    pre = f"nas_{name}/"
+    ea = np.abs(oa.detach().cpu().numpy() - fx[pre + "out_a_32"]).max()
+    ep = np.abs(op_.detach().cpu().numpy() - fx[pre + "out_p_32"]).max()
+    el = abs(loss.item() - float(fx[pre + "loss_64"]))
+    print(f"{name}: out_a {ea:.2e} out_p {ep:.2e} loss {el:.2e}")
+    assert ea <= 1e-4 and ep <= 1e-4 and el <= 1e-5
+    worst_stat = 0.0
+    for k, v in m.state_dict().items():
+        if "running" in k:
+            ref = fx[f"{pre}stat/{k}_32"]
+            worst_stat = max(worst_stat, float(np.abs(v.cpu().numpy() - ref).max() / max(1.0, np.abs(ref).max())))
+        if k.endswith("num_batches_tracked"):
+            assert int(v) == 2, k
+    print(f"{name}: running stats worst rel {worst_stat:.2e}")
+    assert worst_stat <= 1e-5
+    worst, where = nas_grad_check([(k, t.grad.cpu().numpy()) for k, t in m.named_parameters()], fx, pre)
+    print(f"{name}: worst gradient error {worst:.2e} at {where}")
+    assert worst <= 5e-3, (where, worst)
+
+
+def test_supernet_step_matches_reference(cuda_device):
+    """The supernet search step itself: every layer runs all 17 CANDIDATE_BLOCKS (so every op at
+    every layer is exercised, forward and backward), the soft weights come from the fixture's
+    recorded Gumbel noise, outs_Y runs under no_grad, the SupernetLoss latency term and the thetas
+    gradient flow through the HIP op's soft-weight gradient."""
+    m, fx, x, y = supernet_start()
+    m = m.to(cuda_device)
+    ox, oy, loss, ce, lat = supernet_step(m, fx, x, y, device=cuda_device)
+    assert "NasTrainFunction" in type(ox.grad_fn).__name__
+    ex = np.abs(ox.detach().cpu().numpy() - fx["super/out_x_32"]).max()
+    ey = np.abs(oy.detach().cpu().numpy() - fx["super/out_y_32"]).max()
+    print(f"supernet: out_x {ex:.2e} out_y {ey:.2e} loss {loss.item():.6f} vs {float(fx['super/loss_64']):.6f}")
+    assert ex <= 1e-4 and ey <= 1e-4
+    for k, v in (("loss", loss), ("ce", ce), ("lat", lat)):
+        assert abs(float(v.item()) - float(fx[f"super/{k}_64"])) <= 1e-5, k
+    tg = torch.stack([st.thetas.grad for st in m.stages_to_search]).cpu().numpy()
+    ref = fx["super/thetas_grad_64"]
+    et = np.linalg.norm(tg - ref) / np.linalg.norm(ref)
+    print(f"supernet: thetas grad L2-rel {et:.2e}")
+    assert et <= 5e-3
+    named = [(k, t.grad.cpu().numpy()) for k, t in m.named_parameters() if not k.endswith("thetas")]
+    worst, where = nas_grad_check(named, fx, "super/", cap=fx["meta"]["supernet"]["sample"])
+    print(f"supernet: worst gradient error {worst:.2e} at {where}")
+    assert worst <= 5e-3, (where, worst)
+    names = [str(n) for n in fx["super/stat_names"]]
+    sd = m.state_dict()
+    for n, ref in zip(names, fx["super/stat_norms_64"]):
+        got = float(sd[n].double().norm())
+        assert abs(got - ref) <= 1e-5 * max(1.0, ref), n
+
+
+def test_nas_train_eligibility(cuda_device):
+    """Input gradients, CPU tensors and eval mode take the module's torch layers."""
+    m, fx, a, _ = nas_train_start("wang2")
+    m = m.to(cuda_device)
+    x = torch.from_numpy(a[:8]).to(cuda_device)
+    assert "NasTrainFunction" in type(m(x).grad_fn).__name__
+    xr = x.clone().requires_grad_(True)
+    assert "NasTrainFunction" not in type(m(xr).grad_fn).__name__
+    m.native_train = False
+    assert "NasTrainFunction" not in type(m(x).grad_fn).__name__
+
+
+def test_nas_train_matches_torch_layers_on_gpu(cuda_device):
+    """The HIP train path against the same module's torch layers on the GPU (MIOpen) over wang3
+    (maxpool + 1x1 skip ops) at 96 patches: descriptors and gradients."""
+    from fixtures import build_module
+    from hardnetnas_amd.losses import loss_HardNet
+    from hardnetnas_amd import synth
+    res = {}
+    x = torch.from_numpy(synth.synth_patches(96, seed=41)).to(cuda_device)
+    for native in (True, False):
+        m, _, _ = build_module("wang3")
+        m = m.to(cuda_device).train()
+        m.native_train = native
+        torch.backends.cudnn.allow_tf32 = False
+        y = m(x)
+        loss_HardNet(y[:48], y[48:], anchor_swap=True).backward()
+        res[native] = (y.detach(), {k: t.grad.detach().clone() for k, t in m.named_parameters()})
+    assert (res[True][0] - res[False][0]).abs().max().item() <= 1e-4
+    for k, g in res[False][1].items():
+        n = g.norm().item()
+        if n > 1e-6:
+            assert (res[True][1][k] - g).norm().item() / n <= 2e-2, k

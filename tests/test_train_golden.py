@@ -70,3 +70,46 @@ def test_fixture_fp32_reference_gradient_error_is_recorded():
     for init in ("golden", "fresh"):
         errs = meta["inits"][init]["fp32_grad_l2rel_vs_fp64"]
         assert len(errs) == 7 and max(errs.values()) < 2.5e-3
+
+
+
+# ---- hardnetNAS: the sampled descriptors and the supernet ------------------------------------
+@pytest.mark.parametrize("name", ["wang2", "cov_b"])
+def test_module_torch_nas_train_step_matches_reference(name):
+    """HardNetNAS's torch layers (the CPU path of train()) in the supernet training loop's shape
+    (two calls, hardnetNAS loss_HardNet = anchor swap, backward) against the reference's step."""
+    from fixtures import nas_grad_check, nas_train_start
+    from hardnetnas_amd.losses import loss_HardNet
+    m, fx, a, p = nas_train_start(name)
+    oa, op_ = m(torch.from_numpy(a)), m(torch.from_numpy(p))
+    loss = loss_HardNet(oa, op_, anchor_swap=True)
+    loss.backward()
+    pre = f"nas_{name}/"
+    assert np.abs(oa.detach().numpy() - fx[pre + "out_a_32"]).max() <= 1e-5
+    assert np.abs(op_.detach().numpy() - fx[pre + "out_p_32"]).max() <= 1e-5
+    assert abs(loss.item() - float(fx[pre + "loss_64"])) <= 1e-5
+    for k, v in m.state_dict().items():
+        if "running" in k:
+            ref = fx[f"{pre}stat/{k}_32"]
+            assert np.abs(v.numpy() - ref).max() <= 1e-5 * max(1.0, np.abs(ref).max()), k
+    worst, where = nas_grad_check([(k, t.grad.numpy()) for k, t in m.named_parameters()], fx, pre)
+    assert worst <= 5e-3, (where, worst)
+
+
+def test_supernet_module_torch_step_matches_reference():
+    """HardNetNASSupernet (torch layers) with the recorded Gumbel noise reproduces the reference
+    supernet's training step (FBNet_Stochastic_SuperNet + SupernetLoss): descriptors, the loss and
+    its latency term, the thetas gradient and every weight gradient."""
+    from fixtures import nas_grad_check, supernet_start, supernet_step
+    m, fx, x, y = supernet_start()
+    ox, oy, loss, ce, lat = supernet_step(m, fx, x, y)
+    assert np.abs(ox.detach().numpy() - fx["super/out_x_32"]).max() <= 1e-5
+    assert np.abs(oy.detach().numpy() - fx["super/out_y_32"]).max() <= 1e-5
+    for k in ("loss", "ce", "lat"):
+        assert abs(float({"loss": loss, "ce": ce, "lat": lat}[k].item()) - float(fx[f"super/{k}_64"])) <= 1e-5, k
+    tg = torch.stack([st.thetas.grad for st in m.stages_to_search]).numpy()
+    ref = fx["super/thetas_grad_64"]
+    assert np.linalg.norm(tg - ref) / np.linalg.norm(ref) <= 5e-3
+    named = [(k, t.grad.numpy()) for k, t in m.named_parameters() if not k.endswith("thetas")]
+    worst, where = nas_grad_check(named, fx, "super/", cap=fx["meta"]["supernet"]["sample"])
+    assert worst <= 5e-3, (where, worst)
