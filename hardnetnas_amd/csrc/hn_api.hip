@@ -36,6 +36,7 @@ void hn_read_knobs(HnKnobs* k) {
   k->naive_dw = std::getenv("HN_NAIVE_DW") != nullptr;
   k->no_skipfuse = std::getenv("HN_NO_SKIPFUSE") != nullptr;
   k->pairdist_valu = std::getenv("HN_PAIRDIST_VALU") != nullptr;
+  k->pairdist_reg = env_int("HN_PAIRDIST_REG", 0) != 0;
   k->train_splitk = std::max(32, env_int("HN_TRAIN_SPLITK", 1024)) / 32 * 32;
   k->train_f32 = env_int("HN_TRAIN_F32", 1) & 255;
 #ifdef HN_EXPERIMENTS
@@ -1171,9 +1172,9 @@ extern "C" int hn_nas_train_backward(const hn_arch_desc* desc, const float* d_do
 
 extern "C" int hn_pairdist_workspace_bytes(int64_t batch, size_t* bytes_out) {
   if (!bytes_out || batch < 0) return fail(HN_ERR_ARG, "bad argument");
-  // column minima + |a|^2 + |p|^2 (each padded to 64 entries)
-  const size_t n = (size_t)((batch > 0 ? batch : 1) + 63) / 64 * 64;
-  *bytes_out = 3 * n * sizeof(float);
+  // column minima (padded to 64 entries) + the row kernel's workspace (hn_pairdist_rows_ws_bytes)
+  const long b = batch > 0 ? (long)batch : 1;
+  *bytes_out = (size_t)((b + 63) / 64 * 64) * sizeof(float) + hn_pairdist_rows_ws_bytes(b, b);
   return HN_OK;
 }
 
@@ -1196,7 +1197,7 @@ extern "C" int hn_pairdist_hardneg(const float* d_anchor, const float* d_positiv
 extern "C" int hn_pairdist_rows_workspace_bytes(int64_t n_rows, int64_t batch, size_t* bytes_out) {
   if (!bytes_out || n_rows < 1 || batch < 2 || batch > (1 << 30) || n_rows > batch)
     return fail(HN_ERR_ARG, "bad n_rows / batch");
-  *bytes_out = (size_t)((n_rows + 63) / 64 * 64 + (batch + 63) / 64 * 64) * sizeof(float);
+  *bytes_out = hn_pairdist_rows_ws_bytes((long)n_rows, (long)batch);
   return HN_OK;
 }
 

@@ -17,6 +17,7 @@ struct HnKnobs {
   bool naive_dw = false;       // HN_NAIVE_DW: untiled depthwise kernel
   bool no_skipfuse = false;    // HN_NO_SKIPFUSE: maxpool + pw instead of k_skip_s2
   bool pairdist_valu = false;  // HN_PAIRDIST_VALU: fp32 VALU pair-distance kernel
+  bool pairdist_reg = false;   // HN_PAIRDIST_REG: register-staged positives instead of the LDS-DMA ring
   int train_splitk = 1024;     // HN_TRAIN_SPLITK: K per split-K slice of the train GEMMs
   int train_f32 = 1;           // HN_TRAIN_F32: bit 0 train forward convs, bit 1 stride-1 dgrads as f32-MFMA
                                // GEMMs (else the bf16x3 conv kernels); default 1 = every product f32;
@@ -96,6 +97,7 @@ hipError_t hn_launch_pairdist(const float* a, const float* p, int B, int D, int 
                               float* pos, float* minneg, void* ws, hipStream_t st);
 // rows [row0, row0 + NA) of the B x B matrix (a = those NA anchors, p = all B positives);
 // colmin (float bits, atomicMin; may be NULL) gets the column minima over these rows
+size_t hn_pairdist_rows_ws_bytes(long NA, long B);
 hipError_t hn_launch_pairdist_rows(const float* a, int NA, int row0, const float* p, int B, float* pos,
                                    float* rowmin, float* colmin, void* ws, hipStream_t st);
 hipError_t hn_launch_loss(const float* pos, const float* rmin, const float* cmin, int n, float margin,

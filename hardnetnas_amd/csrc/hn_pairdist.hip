@@ -394,6 +394,249 @@ __global__ __launch_bounds__(NW * 64) void k_pairdist_rows(
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// The same computation with the positives pre-split ONCE (k_split_planes: bf16 hi / lo planes
+// [B][128] in the workspace) and staged by LDS-DMA (global_load_lds, 16 B per lane) into a ring
+// of three tile buffers: no register staging, no per-tile split, two tiles in flight while the
+// waves compute on the third.  A buffer's rows are 256 B, the 16-byte chunk c of row j stored at
+// chunk c ^ (j & 15) (the swizzle is applied on the per-lane SOURCE address, the LDS image being
+// lane-linear), so each 16-lane ds_read_b128 group of a B-fragment read (16 consecutive rows, one
+// logical chunk) hits 16 distinct chunks: conflict-free.  Each buffer is its own __shared__ object
+// and the tile loop is unrolled by three, so every ds_read names its buffer at compile time and
+// hipcc does not wait for the in-flight DMA into the other buffers; the waits are counted
+// s_waitcnt vmcnt(N) (N = this wave's DMA instructions for the tile issued after the one to
+// retire) followed by a raw s_barrier.
+// ---------------------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+__global__ __launch_bounds__(256) void k_split_planes(const float* __restrict__ p, int B, uint16_t* __restrict__ ph,
+                                                      uint16_t* __restrict__ pl) {
+  const long e = ((long)blockIdx.x * 256 + threadIdx.x) * 8;  // 8 consecutive values per thread
+  if (e >= (long)B * 128) return;
+  const float4 x0 = *reinterpret_cast<const float4*>(p + e), x1 = *reinterpret_cast<const float4*>(p + e + 4);
+  uint4 hi, lo;
+  split8(x0, x1, hi, lo);
+  *reinterpret_cast<uint4*>(ph + e) = hi;
+  *reinterpret_cast<uint4*>(pl + e) = lo;
+}
+
+template <int N>
+HN_DEV void wait_vm() {  // s_waitcnt vmcnt(N), lgkmcnt / expcnt untouched
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+template <bool SWAP, int NW>
+__global__ __launch_bounds__(NW * 64) void k_pairdist_ring(
+    const float* __restrict__ a, int NA, int row0, const uint16_t* __restrict__ ph, const uint16_t* __restrict__ pl,
+    int B, const float* __restrict__ asq, const float* __restrict__ psq, float xthr, float* __restrict__ rowmin,
+    unsigned* __restrict__ colmin) {
+  constexpr int TN = 64, ROWB = 256, PLANE = TN * ROWB, BUF = 2 * PLANE + TN * 4;
+  constexpr int G = 2 * PLANE / 1024 / NW;  // DMA instructions per wave per tile (4 at NW = 8)
+  static_assert(G * NW * 1024 == 2 * PLANE, "tile split");
+  __shared__ __attribute__((aligned(16))) char sb0[BUF], sb1[BUF], sb2[BUF];
+  __shared__ float cred[3][NW][TN];
+  __shared__ __attribute__((aligned(16))) float ainit[NW][32];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int i0 = blockIdx.x * (32 * NW) + wave * 32;
+  const int g0 = row0 + i0;
+  bf16x8 ah[8], al[8];
+  {
+    const int ia = min(i0 + r, NA - 1);
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      const float4 x0 = *reinterpret_cast<const float4*>(a + (size_t)ia * 128 + ks * 16 + h * 8);
+      const float4 x1 = *reinterpret_cast<const float4*>(a + (size_t)ia * 128 + ks * 16 + h * 8 + 4);
+      uint4 hi, lo;
+      split8(x0, x1, hi, lo);
+      ah[ks] = as_bf16x8(hi);
+      al[ks] = as_bf16x8(lo);
+    }
+  }
+  if (lane < 32) ainit[wave][lane] = i0 + lane < NA ? -0.5f * asq[i0 + lane] : -INFINITY;
+  float xu[16], xm[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) { xu[i] = INFINITY; xm[i] = INFINITY; }
+
+  // tile j0's rows (clamped to B - 1) into a buffer: wave instruction gi = wave * G + k covers plane
+  // gi / 16, rows 4 (gi % 16) .. +3; lane L fills row 4 (gi % 16) + L / 16, chunk L % 16 with the
+  // row's logical chunk (L % 16) ^ (row & 15); wave 0 adds |p_j|^2 of the 64 rows (4 B per lane)
+  // The DMA goes through inline asm (the guide's glds16 recipe: M0 set and restored in the same
+  // statement), so hipcc does not track it as a pending LDS write: its alias analysis would
+  // otherwise wait vmcnt(0) before LDS reads of the other buffers; the waits here are explicit.
+  const unsigned wv = __builtin_amdgcn_readfirstlane(wave);
+  auto issue = [&](char* buf, int j0) {
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+      const int gi = wave * G + k, plane = gi >> 4, r4 = (gi & 15) * 4;
+      const int row = r4 + (lane >> 4), d = lane & 15;
+      const int jr = min(j0 + row, B - 1);
+      const uint16_t* src = (plane ? pl : ph) + (size_t)jr * 128 + ((d ^ (row & 15)) << 3);
+      const int gu = (int)wv * G + k;
+      const unsigned dst = (unsigned)(uintptr_t)(lds_ptr_t)(buf + (gu >> 4) * PLANE + (gu & 15) * 4 * ROWB);
+      unsigned keep;
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
+    }
+    if (wv == 0) {
+      const float* src = psq + min(j0 + lane, B - 1);
+      const unsigned dst = (unsigned)(uintptr_t)(lds_ptr_t)(buf + 2 * PLANE);
+      unsigned keep;
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
+    }
+  };
+  // this wave's share of the older tile's DMA retired, then every wave's (LDS reads of the buffer
+  // about to be refilled are complete before the barrier: lgkmcnt(0))
+  auto sync_tile = [&](bool more) {
+    if (more) {
+      if (wv == 0) wait_vm<G + 1>(); else wait_vm<G>();
+    } else {
+      wait_vm<0>();
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  };
+  float cu, cm;
+  auto epi_masked = [&](const f32x16& xv, int dsel) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int rr = (i & 3) + 8 * (i >> 2) + 4 * h;
+      const float v = xv[i];
+      const bool m = v < xthr || rr == dsel;
+      const float tu = m ? INFINITY : v, tm = m ? v : INFINITY;
+      xu[i] = fminf(xu[i], tu);
+      xm[i] = fminf(xm[i], tm);
+      if constexpr (SWAP) {
+        cu = fminf(cu, tu);
+        cm = fminf(cm, tm);
+      }
+    }
+  };
+  auto epi_finish = [&](const f32x16& xv, float lm, int dsel, int cslot) {
+    cu = INFINITY;
+    cm = INFINITY;
+    if (__any(dsel != -1000 || lm < xthr)) {
+      epi_masked(xv, dsel);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) xu[i] = fminf(xu[i], xv[i]);
+      cu = lm;
+    }
+    if constexpr (SWAP) {
+      cu = fminf(cu, __shfl_xor(cu, 32, 64));
+      cm = fminf(cm, __shfl_xor(cm, 32, 64));
+      if (h == 0) (&cred[0][0][0])[cslot + r] = fminf(dm_of(cu), dm_of(cm) + 10.f);
+    }
+  };
+  // one 32-column sub-tile's bf16x3 chain (K = 128) with the previous sub-tile's epilogue woven in
+  auto chain_epi = [&](const char* cur, int nt, f32x16 accp, float pj, int dsel, int cslot) {
+    f32x16 acc;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 v = *reinterpret_cast<const float4*>(&ainit[wave][8 * q + 4 * h]);
+      acc[4 * q] = v.x;
+      acc[4 * q + 1] = v.y;
+      acc[4 * q + 2] = v.z;
+      acc[4 * q + 3] = v.w;
+    }
+    float lm = INFINITY;
+    const int row = nt * 32 + r, sw = row & 15;
+    const char* base = cur + row * ROWB;
+    uint4 bh = *reinterpret_cast<const uint4*>(base + ((h ^ sw) << 4));
+    uint4 bl = *reinterpret_cast<const uint4*>(base + PLANE + ((h ^ sw) << 4));
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      uint4 nh, nl;
+      if (ks + 1 < 8) {
+        const int off = ((2 * (ks + 1) + h) ^ sw) << 4;
+        nh = *reinterpret_cast<const uint4*>(base + off);
+        nl = *reinterpret_cast<const uint4*>(base + PLANE + off);
+      }
+      acc = mfma3(ah[ks], al[ks], as_bf16x8(bh), as_bf16x8(bl), acc);
+      accp[2 * ks] = fmaf(-2.0f, accp[2 * ks], pj);
+      accp[2 * ks + 1] = fmaf(-2.0f, accp[2 * ks + 1], pj);
+      lm = fminf(lm, fminf(accp[2 * ks], accp[2 * ks + 1]));
+      if (ks + 1 < 8) {
+        bh = nh;
+        bl = nl;
+      }
+    }
+    epi_finish(accp, lm, dsel, cslot);
+    return acc;
+  };
+  auto reduce_cols = [&](int t) {
+    const int j = t * TN + lane;
+    const float* c = cred[t % 3][0];
+    float ce = c[lane];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) ce = fminf(ce, c[w * TN + lane]);
+    if (j < B && ce < INFINITY) atomicMin(colmin + j, __float_as_uint(ce));
+  };
+  auto sub_meta = [&](const float* ps, int j0, int nt, float& pj, int& dsel, int& cslot, int t) {
+    const int jb = j0 + nt * 32;
+    pj = ps[nt * 32 + r];
+    const int jlo = min(jb, B - 1), jhi = min(jb + 31, B - 1);
+    dsel = (jlo < g0 + 32 && jhi >= g0) ? min(jb + r, B - 1) - g0 : -1000;
+    cslot = ((t % 3) * NW + wave) * TN + nt * 32;
+  };
+
+  const int ntile = (B + TN - 1) / TN;
+  f32x16 accp{};
+  float pjp = INFINITY;
+  int dselp = -1000, cslotp = wave * TN + 32;
+  // prologue: tiles 0 and 1 in flight, wait for tile 0 (ainit, written above, is read after it)
+  issue(sb0, 0);
+  if (ntile > 1) issue(sb1, TN);
+  sync_tile(ntile > 1);
+  // tile t on buffer t % 3 (compile-time within the unrolled step): tile t + 2's DMA goes into the
+  // buffer tile t - 1 was read from (every wave passed the barrier after reading it)
+  auto step = [&](const char* cur, char* nxt2, int t) {
+    const int j0 = t * TN;
+    if (SWAP && t >= 2 && wave == (t - 2) % NW) reduce_cols(t - 2);
+    const bool more2 = t + 2 < ntile;
+    if (more2) issue(nxt2, j0 + 2 * TN);
+    const float* ps = reinterpret_cast<const float*>(cur + 2 * PLANE);
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      accp = chain_epi(cur, nt, accp, pjp, dselp, cslotp);
+      sub_meta(ps, j0, nt, pjp, dselp, cslotp, t);
+    }
+    sync_tile(more2);  // retire tile t + 1's DMA, leaving tile t + 2's in flight
+  };
+#pragma unroll 1
+  for (int t = 0; t < ntile; t += 3) {
+    step(sb0, sb2, t);
+    if (t + 1 < ntile) step(sb1, sb0, t + 1);
+    if (t + 2 < ntile) step(sb2, sb1, t + 2);
+  }
+  {  // the last sub-tile's epilogue
+    float lm = INFINITY;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      accp[i] = fmaf(-2.0f, accp[i], pjp);
+      lm = fminf(lm, accp[i]);
+    }
+    epi_finish(accp, lm, dselp, cslotp);
+  }
+  if (SWAP) {
+    __syncthreads();
+    if (ntile >= 2 && wave == (ntile - 2) % NW) reduce_cols(ntile - 2);
+    if (wave == (ntile - 1) % NW) reduce_cols(ntile - 1);
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    float u = xu[i], m = xm[i];
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) {
+      u = fminf(u, __shfl_xor(u, o, 64));
+      m = fminf(m, __shfl_xor(m, o, 64));
+    }
+    const int row = i0 + (i & 3) + 8 * (i >> 2) + 4 * h;
+    if (r == 0 && row < NA) rowmin[row] = fminf(dm_of(u), dm_of(m) + 10.f);
+  }
+}
+
 // The margin losses of loss_HardNet (Losses.py:142-153) over the 'min' reduce, one workgroup
 // (fixed summation order: deterministic); min_neg = min(row_min, col_min) when col_min is given.
 __global__ __launch_bounds__(1024) void k_loss(const float* __restrict__ pos, const float* __restrict__ rmin,
@@ -448,24 +691,41 @@ float mask_threshold_x() {
 
 }  // namespace
 
+// workspace: |a|^2 [NA] | |p|^2 [B] | (ring form) bf16 hi / lo planes of the positives [B][128] each
+size_t hn_pairdist_rows_ws_bytes(long NA, long B) {
+  return (size_t)((NA + 63) / 64 * 64 + (B + 63) / 64 * 64) * sizeof(float) + (size_t)B * 128 * 2 * sizeof(uint16_t);
+}
+
 hipError_t hn_launch_pairdist_rows(const float* a, int NA, int row0, const float* p, int B, float* pos,
                                    float* rowmin, float* colmin, void* ws, hipStream_t st) {
   float* asq = static_cast<float*>(ws);
   float* psq = asq + ((NA + 63) / 64) * 64;
+  uint16_t* ph = reinterpret_cast<uint16_t*>(psq + ((B + 63) / 64) * 64);
+  uint16_t* pl = ph + (size_t)B * 128;
   static const float xthr = mask_threshold_x();
   if (colmin) hipLaunchKernelGGL(k_colmin_init, dim3((B + 255) / 256), dim3(256), 0, st,
                                  reinterpret_cast<unsigned*>(colmin), B);
   hipLaunchKernelGGL(k_sq, dim3((NA + 3) / 4), dim3(256), 0, st, a, NA, asq);
   hipLaunchKernelGGL(k_sq, dim3((B + 3) / 4), dim3(256), 0, st, p, B, psq);
   hipLaunchKernelGGL(k_pos, dim3((NA + 3) / 4), dim3(256), 0, st, a, p, asq, psq, NA, row0, pos);
+  const bool ring = !hn_knobs().pairdist_reg;  // HN_PAIRDIST_REG=1: the register-staged form
+  if (ring)
+    hipLaunchKernelGGL(k_split_planes, dim3((unsigned)(((long)B * 16 + 255) / 256)), dim3(256), 0, st, p, B, ph, pl);
   // 8-wave workgroups when they still give every CU one (NA >= 65,536 anchors), else 4-wave
   // ones (twice the workgroups: a row shard of a sharded batch)
   auto go = [&](auto nw) {
     constexpr int NW = decltype(nw)::value;
     const dim3 grid((NA + 32 * NW - 1) / (32 * NW)), block(64 * NW);
-    if (colmin)
+    unsigned* cm = reinterpret_cast<unsigned*>(colmin);
+    if (ring && colmin)
+      hipLaunchKernelGGL((k_pairdist_ring<true, NW>), grid, block, 0, st, a, NA, row0, ph, pl, B, asq, psq, xthr,
+                         rowmin, cm);
+    else if (ring)
+      hipLaunchKernelGGL((k_pairdist_ring<false, NW>), grid, block, 0, st, a, NA, row0, ph, pl, B, asq, psq, xthr,
+                         rowmin, nullptr);
+    else if (colmin)
       hipLaunchKernelGGL((k_pairdist_rows<true, NW>), grid, block, 0, st, a, NA, row0, p, B, asq, psq, xthr,
-                         rowmin, reinterpret_cast<unsigned*>(colmin));
+                         rowmin, cm);
     else
       hipLaunchKernelGGL((k_pairdist_rows<false, NW>), grid, block, 0, st, a, NA, row0, p, B, asq, psq, xthr,
                          rowmin, nullptr);
@@ -485,7 +745,7 @@ hipError_t hn_launch_pairdist(const float* a, const float* p, int B, int D_, int
   const bool valu = hn_knobs().pairdist_valu;  // HN_PAIRDIST_VALU (A/B), read once per process
   if (!valu) {
     float* colmin = swap ? reinterpret_cast<float*>(cm) : nullptr;
-    hipError_t e = hn_launch_pairdist_rows(a, B, 0, p, B, pos, minneg, colmin, cm + ((B + 63) / 64) * 64, st);
+    hipError_t e = hn_launch_pairdist_rows(a, B, 0, p, B, pos, minneg, colmin, cm + ((B + 63) / 64) * 64, st);  // (ws: hn_pairdist_rows_ws_bytes)
     if (e != hipSuccess) return e;
     if (swap) hipLaunchKernelGGL(k_combine, dim3(g), dim3(256), 0, st, minneg, cm, B);
     return hipGetLastError();

@@ -83,3 +83,40 @@ def test_hardnet_loss_matches_reference(loss_type, swap, cuda_device):
     assert abs(loss.item() - ref) < 1e-5
     _, rmn = O.hardest_negative(a.double(), p.double(), swap)
     assert (mn.cpu().double() - rmn).abs().max().item() < 1e-4
+
+
+_REG_CHILD = r"""
+import sys, torch
+sys.path.insert(0, sys.argv[1])
+from test_gpu_pairs import _pairs
+from hardnetnas_amd._native import pairdist_rows
+dev = torch.device("cuda:0")
+out = {}
+for b, swap in ((1000, True), (65536 + 37, True), (4097, False)):
+    a, p = _pairs(b, 11, dup=[(3, 9)])
+    pos, rmin, cmin = pairdist_rows(a.to(dev), 0, p.to(dev), col_min=swap)
+    out[f"{b}_{swap}"] = [pos.cpu(), rmin.cpu()] + ([cmin.cpu()] if cmin is not None else [])
+torch.save(out, sys.argv[2])
+"""
+
+
+def test_lds_dma_ring_equals_register_staged_form(tmp_path, cuda_device):
+    """The LDS-DMA ring pair kernel (default) and the register-staged one (HN_PAIRDIST_REG=1, read
+    once per process: a child process) stage the same bf16 hi / lo values and run the same MFMA
+    chains: pos, row minima and column minima agree bit for bit, including a batch that is not a
+    multiple of the 64-column tile and the 8-wave (>= 65,536 anchors) form."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    res = {}
+    for tag, env in (("ring", {}), ("reg", {"HN_PAIRDIST_REG": "1"})):
+        f = str(tmp_path / f"{tag}.pt")
+        r = subprocess.run([sys.executable, "-c", _REG_CHILD, here, f], env=dict(os.environ, **env),
+                           capture_output=True, text=True, timeout=110)
+        assert r.returncode == 0, r.stderr[-3000:]
+        res[tag] = torch.load(f, weights_only=True)
+    for k in res["ring"]:
+        for x, y in zip(res["ring"][k], res["reg"][k]):
+            if x is not None:
+                assert torch.equal(x, y), k
