@@ -57,6 +57,36 @@ HARDNET_STAGE_BYTES = {"stem": 4096 + 131072, "conv1": 2 * 131072, "stem+conv1":
                        "conv5": 2 * 32768, "head": 32768 + 512}
 
 
+# hn_irf.hip HN_IRF2_SHAPES: (C_A, H, k_A, mid_A, C_B, k_B, mid_B) of the two-block fused kernel k_irf2
+IRF2_SHAPES = {(32, 16, ka, 32, 64, kb, 32) for ka in (3, 5) for kb in (3, 5)} | \
+              {(64, 8, ka, 64, 128, kb, 64) for ka in (3, 5) for kb in (3, 5)}
+
+
+def irf2_pairs(ops) -> set:
+    """First layers of the block pairs hn_api.hip::forward_nas runs as one k_irf2 (a stride-1 block
+    without SE followed by a stride-2 block at the same resolution), unless HN_NO_IRF2 / HN_NO_IRF."""
+    if os.environ.get("HN_NO_IRF2", "0") not in ("", "0") or os.environ.get("HN_NO_IRF", "0") not in ("", "0"):
+        return set()
+    ops = A.arch_ops(ops)
+    out, hw, i = set(), 32, 0
+    hws = []
+    for (ci, co, s) in A.SEARCH_SPACE2:
+        hws.append(hw)
+        hw //= s
+    i = 1
+    while i + 1 < len(ops):
+        a, b = A.OP_SPECS[ops[i]], A.OP_SPECS[ops[i + 1]]
+        (ci, co, s), (cb_in, cb, sb) = A.SEARCH_SPACE2[i], A.SEARCH_SPACE2[i + 1]
+        if (a.kind != "skip" and b.kind != "skip" and not a.se and s == 1 and ci == co and sb == 2 and
+                (ci, hws[i], a.kernel, A.ir_mid(ci, a.expansion), cb, b.kernel,
+                 A.ir_mid(cb_in, b.expansion)) in IRF2_SHAPES):
+            out.add(i)
+            i += 2
+        else:
+            i += 1
+    return out
+
+
 def nas_stage_bytes(ops) -> dict:
     """Algorithmic HBM bytes per patch of each NAS stage class, summed over its launches in
     one forward (fp32 NHWC in + out (+ residual read)), mirroring hn_api.hip::forward_nas
@@ -64,16 +94,31 @@ def nas_stage_bytes(ops) -> dict:
     fused "irf" blocks unless HN_NO_IRF=1)."""
     front = os.environ.get("HN_NO_FRONT", "0") in ("", "0")
     irf = os.environ.get("HN_NO_IRF", "0") in ("", "0")
-    out = {"stem": 0 if front else 4096 + 32 * 32 * 32 * 4, "front": 0, "irf": 0, "pw": 0,
+    out = {"stem": 0 if front else 4096 + 32 * 32 * 32 * 4, "front": 0, "irf": 0, "irf2": 0, "skip": 0, "pw": 0,
            "dw": 0, "pwl": 0, "maxpool": 0, "se": 0, "head": 0}
+    pairs = irf2_pairs(ops)
     hw = 32
     for i, (op, (ci, co, s)) in enumerate(zip(A.arch_ops(ops), A.SEARCH_SPACE2)):
         spec = A.OP_SPECS[op]
         ho = hw // s
+        if i in pairs:  # k_irf2: this block's input in, the next block's output out
+            _, co2, s2 = A.SEARCH_SPACE2[i + 1]
+            out["irf2"] += 4 * ci * hw * hw + 4 * co2 * (hw // s2) ** 2
+            hw = ho
+            continue
+        if i - 1 in pairs:
+            if spec.se:
+                out["se"] += 4 * 2 * co * ho * ho
+            hw = ho
+            continue
         fused = front and i == 0
         if spec.kind == "skip":
             if fused:
                 out["front"] += 4096 + 4 * ci * ho * ho
+            elif s == 2 and ci != co and os.environ.get("HN_NO_SKIPFUSE", "0") in ("", "0"):
+                out["skip"] += 4 * (ci * hw * hw + co * ho * ho)  # k_skip_s2: maxpool + 1x1 fused
+                hw = ho
+                continue
             elif s == 2:
                 out["maxpool"] += 4 * (ci * hw * hw + ci * ho * ho)
             if ci != co:
@@ -253,11 +298,14 @@ def nas_stage_flop(name: str) -> dict:
             hw //= st
         return {"front": 2 * front, "irf": 2 * irf, "head": 2 * 128 * 128 * 16}
     ops = A.arch_ops(name)
-    out = {"front": 0, "irf": 0, "skip": 0, "head": 2 * A.SEARCH_SPACE2[-1][1] * 128 * 16}
+    out = {"front": 0, "irf": 0, "irf2": 0, "skip": 0, "head": 2 * A.SEARCH_SPACE2[-1][1] * 128 * 16}
+    pairs = irf2_pairs(ops)
     hw = 32
     for i, (op, (ci, co, st)) in enumerate(zip(ops, A.SEARCH_SPACE2)):
         macs = A.layer_macs(ci, co, st, op, hw)
-        if i == 0:
+        if i in pairs or i - 1 in pairs:
+            out["irf2"] += 2 * macs
+        elif i == 0:
             out["front"] += 2 * (9 * 32 * 32 * 32 + macs)
         elif A.OP_SPECS[op].kind == "skip":
             out["skip"] += 2 * macs

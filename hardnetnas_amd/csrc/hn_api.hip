@@ -235,6 +235,7 @@ struct hn_model {
   int front = 0;  // NAS: 1 = stem + layer-0 IRF pw/dw fused, 2 = stem + layer-0 maxpool fused
   bool no_front = false;  // HN_NO_FRONT=1: unfused NAS stem/layer 0 (A/B, debugging)
   bool no_irf = false;    // HN_NO_IRF=1: layer-by-layer pw/dw/pwl kernels (A/B, debugging)
+  bool no_irf2 = false;   // HN_NO_IRF2=1: one k_irf launch per block (no two-block fusion)
   // conv tiling per layer (index 0 = stem+conv1, 2..5 = conv2..5); defaults are the best
   // measured on MI355X (tools/tune_variants.py); HN_VARIANT="003303" style override
   int variant[6] = {6, 0, 5, 16, 15, 16};  // 16 = epilogue stores through LDS (conv3 whole rows, conv5 64-byte rows); conv4: 15 = two patches per stage, 64-byte swizzled window
@@ -746,6 +747,7 @@ extern "C" int hn_create(const hn_arch_desc* desc, const float* host_params, siz
   if (const char* e = std::getenv("HN_NO_C12")) m->c12 = std::atoi(e) == 0;
   if (const char* e = std::getenv("HN_SUBCHUNK")) m->subchunk = std::max(64, std::atoi(e));
   if (const char* e = std::getenv("HN_NO_IRF")) m->no_irf = std::atoi(e) != 0;
+  if (const char* e = std::getenv("HN_NO_IRF2")) m->no_irf2 = std::atoi(e) != 0;
   if (const char* e = std::getenv("HN_VARIANT")) {
     int i = 0;
     for (const char* c = e; *c && i < 6; ++c)
@@ -901,6 +903,24 @@ static int forward_nas(hn_model* m, const float* in, int P, int pmax, float* out
         std::swap(x, t1);
       }
       continue;
+    }
+    if (L.irf_pwl_a && li + 1 < m->layers.size() && !m->no_irf2) {
+      // this block and the next in one kernel (k_irf2) when this one is stride 1 without SE and
+      // the next is a stride-2 block at the same resolution: the activation between them stays in LDS
+      const NasLayer& N = m->layers[li + 1];
+      if (!L.se && N.irf_pwl_a && L.stride == 1 && L.cin == L.cout && N.stride == 2 && N.cin == L.cout &&
+          N.hin == L.hin && hn_irf2_supported(L.cin, L.hin, L.k, L.mid, N.cout, N.k, N.mid)) {
+        const HnIrfArgs ia{x, nullptr, reinterpret_cast<const uint4*>(L.irf_pw_a), L.irf_pw_b, L.dw_w, L.dw_b,
+                           reinterpret_cast<const uint4*>(L.irf_pwl_a), L.pwl_b};
+        const HnIrfArgs ib{nullptr, y, reinterpret_cast<const uint4*>(N.irf_pw_a), N.irf_pw_b, N.dw_w, N.dw_b,
+                           reinterpret_cast<const uint4*>(N.irf_pwl_a), N.pwl_b};
+        STAGE("irf2", hn_launch_irf2(ia, ib, P, L.cin, L.hin, L.k, L.mid, N.cout, N.k, N.mid, st));
+        if (N.se)
+          STAGE("se", hn_launch_se(y, N.se_w1, N.se_b1, N.se_w2, N.se_b2, P, N.hout * N.hout, N.cout, N.semid, st));
+        std::swap(x, y);
+        ++li;
+        continue;
+      }
     }
     if (L.irf_pwl_a) {
       const HnIrfArgs ia{x, y, reinterpret_cast<const uint4*>(L.irf_pw_a), L.irf_pw_b, L.dw_w, L.dw_b,

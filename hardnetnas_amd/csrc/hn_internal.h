@@ -141,6 +141,10 @@ struct HnIrfArgs {
   const float* pwl_b;  // [COUT]
 };
 bool hn_irf_supported(int cin, int cout, int hin, int s, int k, int mid);
+// two consecutive blocks in one kernel (hn_irf.hip k_irf2): A (ca -> ca, stride 1) then B (ca -> cb, stride 2)
+bool hn_irf2_supported(int ca, int hi, int ka, int ma, int cb, int kb, int mb);
+hipError_t hn_launch_irf2(const HnIrfArgs& a, const HnIrfArgs& b, int P, int ca, int hi, int ka, int ma, int cb,
+                          int kb, int mb, hipStream_t st);
 hipError_t hn_launch_irf(const HnIrfArgs& a, int P, int cin, int cout, int hin, int s, int k, int mid,
                          hipStream_t st);
 hipError_t hn_launch_preprocess(const uint8_t* in, int64_t n, int resize, int norm, float mean,

@@ -33,85 +33,43 @@ struct IrfTile {
   static constexpr int NI = NPB * HIN * HIN;  // input pixels per workgroup
 };
 
-// The 64 -> 128 stride-2 and the 128-channel (4x4) blocks are held to 168 VGPRs, three
-// workgroups per CU (their LDS allows three; the k5 forms spill 20-25 dwords and still gain):
-// wang2 / wang4 / FDLNet irf -1 to -2 %.  The 32 -> 64 stride-2 blocks lose with the same cap
-// (+6 % irf: their register prefetch of the next tile spills).
 template <int CIN, int COUT, int HIN, int S, int K, int MID>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((CIN == 64 && S == 2) || CIN == 128 ? 3 : 1))) void k_irf(const float* __restrict__ x, float* __restrict__ y,
-                                             const uint4* __restrict__ pw_a,   // [MID/32][CIN/16][2][64]
-                                             const float* __restrict__ pw_b,   // [MID] dw order
-                                             const float* __restrict__ dw_w,   // [K*K][MID]
-                                             const float* __restrict__ dw_b,   // [MID]
-                                             const uint4* __restrict__ pwl_a,  // [COUT/32][MID/16][2][64]
-                                             const float* __restrict__ pwl_b,  // [COUT]
-                                             int P) {
-  constexpr int HOUT = HIN / S, PAD = K / 2;
-  constexpr int NPB = IrfTile<CIN, HIN>::NPB, NI = IrfTile<CIN, HIN>::NI;
-  constexpr int NO = NPB * HOUT * HOUT;           // output pixels per workgroup
-  constexpr int TI = NI / 32 / 4;                 // pw pixel tiles per wave
-  constexpr int KS = CIN / 16;                    // pw K-steps
-  constexpr int NOT = NO / 32, NCT = COUT / 32;   // pwl pixel tiles, cout tiles
-  constexpr int TW = NOT * NCT / 4;               // pwl tiles per wave
-  constexpr int R = S == 1 ? 4 : 2;               // dw run length (output pixels per thread)
-  constexpr int RUNS = NO / R;                    // runs per chunk (x 8 channel quads)
-  constexpr int WIN = (R - 1) * S + K;            // input columns of a run window
-  constexpr bool RES = S == 1 && CIN == COUT;
+struct IrfShape {
+  static constexpr int HOUT = HIN / S, PAD = K / 2;
+  static constexpr int NPB = IrfTile<CIN, HIN>::NPB, NI = IrfTile<CIN, HIN>::NI;
+  static constexpr int NO = NPB * HOUT * HOUT;           // output pixels per workgroup
+  static constexpr int TI = NI / 32 / 4;                 // pw pixel tiles per wave
+  static constexpr int KS = CIN / 16;                    // pw K-steps
+  static constexpr int NOT = NO / 32, NCT = COUT / 32;   // pwl pixel tiles, cout tiles
+  static constexpr int TW = NOT * NCT / 4;               // pwl tiles per wave
+  static constexpr int R = S == 1 ? 4 : 2;               // dw run length (output pixels per thread)
+  static constexpr int RUNS = NO / R;                    // runs per chunk (x 8 channel quads)
+  static constexpr int WIN = (R - 1) * S + K;            // input columns of a run window
+  static constexpr bool RES = S == 1 && CIN == COUT;
   static_assert(NI % 128 == 0 && NO % 32 == 0 && (NOT * NCT) % 4 == 0, "tile shape");
   static_assert(HOUT % R == 0, "dw run must stay in one row");
-  __shared__ __attribute__((aligned(16))) float s_pw[NI * PS];
-  __shared__ __attribute__((aligned(16))) float s_dw[NO * PS];
-  __shared__ __attribute__((aligned(16))) float s_w[K * K * 32 + 32];
+  static constexpr int LDS_PW = NI * PS, LDS_DW = NO * PS, LDS_W = K * K * 32 + 32;  // floats
+};
 
+// The block's work on one tile once its pw B operands (x split into fp16 hi / lo, pixel tiles
+// 4i + w of the tile, lane: pixel, 8 channels) are in registers: per 32-channel chunk of MID the
+// pw (fp16x3 MFMA, bias + ReLU -> LDS), the dw (VALU, register window), the pwl accumulated in
+// registers; then the residual as identity-weight K-steps.  Leaves the pwl output (bias included)
+// in acc[i] = 32 x 32 tile (pixel tile (4i + w) % NOT, channel tile (4i + w) / NOT); lane (px, h):
+// acc[4q + r] = channel 8q + 4h + r of pixel px.  Ends with a barrier (s_pw / s_dw free).
+template <int CIN, int COUT, int HIN, int S, int K, int MID>
+HN_DEV void irf_core(const uint4 (&bh)[IrfShape<CIN, COUT, HIN, S, K, MID>::TI][CIN / 16],
+                     const uint4 (&bl)[IrfShape<CIN, COUT, HIN, S, K, MID>::TI][CIN / 16],
+                     f32x16 (&acc)[IrfShape<CIN, COUT, HIN, S, K, MID>::TW], const uint4* __restrict__ pw_a,
+                     const float* __restrict__ pw_b, const float* __restrict__ dw_w, const float* __restrict__ dw_b,
+                     const uint4* __restrict__ pwl_a, const float* __restrict__ pwl_b, float* s_pw, float* s_dw,
+                     float* s_w) {
+  using Sh = IrfShape<CIN, COUT, HIN, S, K, MID>;
+  constexpr int HOUT = Sh::HOUT, PAD = Sh::PAD, TI = Sh::TI, KS = Sh::KS, NOT = Sh::NOT, TW = Sh::TW, R = Sh::R,
+                RUNS = Sh::RUNS, WIN = Sh::WIN;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int px = lane & 31, h = lane >> 5;
-  // persistent: a contiguous range of tiles per workgroup; the next tile's input is
-  // prefetched into registers while the current one is computed
-  // register prefetch + persistence only where the VGPR budget allows it without losing
-  // occupancy (CIN = 32); otherwise one tile per workgroup
-  constexpr bool PREF = CIN == 32;
-  const int ntiles = (P + NPB - 1) / NPB;
-  const int per = PREF ? (ntiles + (int)gridDim.x - 1) / (int)gridDim.x : 1;
-  const int tbeg = (int)blockIdx.x * per, tend = PREF ? min(ntiles, tbeg + per) : tbeg + 1;
-  if (tbeg >= ntiles) return;  // workgroup-uniform
-
-  float4 pa[TI][KS], pb[TI][KS];
-#define HN_IRF_LOAD(TILE)                                                                   \
-  {                                                                                         \
-    const long q0 = (long)(TILE) * NPB;                                                     \
-    const int nv = (int)min<long>(NPB, P - q0);                                             \
-    _Pragma("unroll") for (int i = 0; i < TI; ++i) {                                        \
-      const int p = (4 * i + w) * 32 + px;                                                  \
-      const bool ok = p < nv * HIN * HIN;                                                   \
-      _Pragma("unroll") for (int s = 0; s < KS; ++s) {                                      \
-        pa[i][s] = pb[i][s] = make_float4(0.f, 0.f, 0.f, 0.f);                              \
-        if (ok) {                                                                           \
-          const float4* src = reinterpret_cast<const float4*>(                              \
-              x + (q0 * (HIN * HIN) + p) * CIN + 16 * s + 8 * h);                           \
-          pa[i][s] = src[0];                                                                \
-          pb[i][s] = src[1];                                                                \
-        }                                                                                   \
-      }                                                                                     \
-    }                                                                                       \
-  }
-  if (PREF) HN_IRF_LOAD(tbeg)
-#pragma unroll 1
-  for (int tile = tbeg; tile < tend; ++tile) {
-  if (!PREF) HN_IRF_LOAD(tile)
-  const long p0 = (long)tile * NPB;  // first patch of the tile
-  const int npv = (int)min<long>(NPB, P - p0);
-
-  // ---- pw B operands: pixel tiles 4i + w of the workgroup tile (lane: pixel, 8 channels) --
-  uint4 bh[TI][KS], bl[TI][KS];
-#pragma unroll
-  for (int i = 0; i < TI; ++i)
-#pragma unroll
-    for (int s = 0; s < KS; ++s) split8_f16(pa[i][s], pb[i][s], bh[i][s], bl[i][s]);
-  if (PREF && tile + 1 < tend) HN_IRF_LOAD(tile + 1)
-
-  // pwl accumulators start at the pwl bias (lane (px, h): acc[4q + r] = channel 8q + 4h + r
-  // of the tile's 32 output channels), so the epilogue is stores only
-  f32x16 acc[TW];
+  // pwl accumulators start at the pwl bias, so the epilogue is stores only
 #pragma unroll
   for (int i = 0; i < TW; ++i) {
     const int ct = (4 * i + w) / NOT;
@@ -121,7 +79,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((CIN == 64 
       acc[i][4 * q] = b.x; acc[i][4 * q + 1] = b.y; acc[i][4 * q + 2] = b.z; acc[i][4 * q + 3] = b.w;
     }
   }
-
 #pragma unroll 1
   for (int m = 0; m < MID / 32; ++m) {
     // dw weights + bias of the chunk
@@ -216,7 +173,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((CIN == 64 
   // ---- residual: y += x as two more MFMA K-steps per tile with an identity A operand
   // against the x B operands already in registers (x = hi + lo to ~2^-22; no second read of
   // x from HBM).  With S = 1, NI = NO, so the wave's pwl pixel tiles are its pw tiles.
-  if (RES) {
+  if constexpr (Sh::RES) {
 #pragma unroll
     for (int i = 0; i < TW; ++i) {
       constexpr int TPW = NOT / 4;  // pixel tiles per wave (= TI)
@@ -231,12 +188,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((CIN == 64 
       }
     }
   }
+}
 
-  // ---- epilogue (the bias is in the accumulators): each 32-pixel x 32-channel tile goes through
-  // a per-wave scratch in s_pw (free after the last chunk's barrier), so that every float4 store
-  // instruction writes 8 whole 128-byte pixel rows instead of 32 pixels x 32 bytes ---------------
+// pwl output tiles -> y in HBM: each 32-pixel x 32-channel tile goes through a per-wave scratch in
+// s_pw (free after the core's last barrier), so that every float4 store instruction writes 8 whole
+// 128-byte pixel rows instead of 32 pixels x 32 bytes.  Ends with a barrier.
+template <int CIN, int COUT, int HIN, int S, int K, int MID>
+HN_DEV void irf_store(const f32x16 (&acc)[IrfShape<CIN, COUT, HIN, S, K, MID>::TW], float* __restrict__ y, long p0,
+                      int npv, float* s_pw) {
+  using Sh = IrfShape<CIN, COUT, HIN, S, K, MID>;
+  constexpr int HOUT = Sh::HOUT, NOT = Sh::NOT, TW = Sh::TW;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, px = lane & 31, h = lane >> 5;
   float* scr = s_pw + w * 32 * PS;
-  static_assert(NI * PS >= 4 * 32 * PS, "scratch fits in s_pw");
+  static_assert(Sh::NI * PS >= 4 * 32 * PS, "scratch fits in s_pw");
 #pragma unroll
   for (int i = 0; i < TW; ++i) {
     const int tile = 4 * i + w, pt = tile % NOT, ct = tile / NOT;
@@ -257,8 +221,152 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((CIN == 64 
     asm volatile("" ::: "memory");
   }
   __syncthreads();  // the scratch (s_pw) is rewritten by the next tile's pw
-  }  // tile loop
-#undef HN_IRF_LOAD
+}
+
+// The block's input tile from HBM into registers (pixel tiles 4i + w, 8 channels per lane), zero
+// past the batch's last patch
+template <int CIN, int COUT, int HIN, int S, int K, int MID>
+HN_DEV void irf_load(float4* pa, float4* pb, const float* __restrict__ x, long tile, int P) {  // [TI][KS]
+  using Sh = IrfShape<CIN, COUT, HIN, S, K, MID>;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, px = lane & 31, h = lane >> 5;
+  const long q0 = tile * Sh::NPB;
+  const int nv = (int)min<long>(Sh::NPB, P - q0);
+#pragma unroll
+  for (int i = 0; i < Sh::TI; ++i) {
+    const int p = (4 * i + w) * 32 + px;
+    const bool ok = p < nv * HIN * HIN;
+#pragma unroll
+    for (int s = 0; s < Sh::KS; ++s) {
+      pa[i * Sh::KS + s] = pb[i * Sh::KS + s] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (ok) {
+        const float4* src = reinterpret_cast<const float4*>(x + (q0 * (HIN * HIN) + p) * CIN + 16 * s + 8 * h);
+        pa[i * Sh::KS + s] = src[0];
+        pb[i * Sh::KS + s] = src[1];
+      }
+    }
+  }
+}
+
+// The block's shared memory: pw rows, dw outputs, dw weights (one array, carved)
+template <int CIN, int COUT, int HIN, int S, int K, int MID>
+constexpr int irf_lds_floats() {
+  using Sh = IrfShape<CIN, COUT, HIN, S, K, MID>;
+  return Sh::LDS_PW + Sh::LDS_DW + Sh::LDS_W;
+}
+
+// The 64 -> 128 stride-2 and the 128-channel (4x4) blocks are held to 168 VGPRs, three
+// workgroups per CU (their LDS allows three; the k5 forms spill 20-25 dwords and still gain):
+// wang2 / wang4 / FDLNet irf -1 to -2 %.  The 32 -> 64 stride-2 blocks lose with the same cap
+// (+6 % irf: their register prefetch of the next tile spills).
+template <int CIN, int COUT, int HIN, int S, int K, int MID>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((CIN == 64 && S == 2) || CIN == 128 ? 3 : 1))) void k_irf(const float* __restrict__ x, float* __restrict__ y,
+                                             const uint4* __restrict__ pw_a,   // [MID/32][CIN/16][2][64]
+                                             const float* __restrict__ pw_b,   // [MID] dw order
+                                             const float* __restrict__ dw_w,   // [K*K][MID]
+                                             const float* __restrict__ dw_b,   // [MID]
+                                             const uint4* __restrict__ pwl_a,  // [COUT/32][MID/16][2][64]
+                                             const float* __restrict__ pwl_b,  // [COUT]
+                                             int P) {
+  using Sh = IrfShape<CIN, COUT, HIN, S, K, MID>;
+  constexpr int NPB = Sh::NPB, TI = Sh::TI, KS = Sh::KS, TW = Sh::TW;
+  __shared__ __attribute__((aligned(16))) float smem[irf_lds_floats<CIN, COUT, HIN, S, K, MID>()];
+  float* s_pw = smem;
+  float* s_dw = smem + Sh::LDS_PW;
+  float* s_w = s_dw + Sh::LDS_DW;
+  // persistent: a contiguous range of tiles per workgroup; the next tile's input is
+  // prefetched into registers while the current one is computed
+  // register prefetch + persistence only where the VGPR budget allows it without losing
+  // occupancy (CIN = 32); otherwise one tile per workgroup
+  constexpr bool PREF = CIN == 32;
+  const int ntiles = (P + NPB - 1) / NPB;
+  const int per = PREF ? (ntiles + (int)gridDim.x - 1) / (int)gridDim.x : 1;
+  const int tbeg = (int)blockIdx.x * per, tend = PREF ? min(ntiles, tbeg + per) : tbeg + 1;
+  if (tbeg >= ntiles) return;  // workgroup-uniform
+
+  float4 pa[TI][KS], pb[TI][KS];
+  if (PREF) irf_load<CIN, COUT, HIN, S, K, MID>(&pa[0][0], &pb[0][0], x, tbeg, P);
+#pragma unroll 1
+  for (int tile = tbeg; tile < tend; ++tile) {
+    if (!PREF) irf_load<CIN, COUT, HIN, S, K, MID>(&pa[0][0], &pb[0][0], x, tile, P);
+    const long p0 = (long)tile * NPB;  // first patch of the tile
+    const int npv = (int)min<long>(NPB, P - p0);
+    uint4 bh[TI][KS], bl[TI][KS];
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int s = 0; s < KS; ++s) split8_f16(pa[i][s], pb[i][s], bh[i][s], bl[i][s]);
+    if (PREF && tile + 1 < tend) irf_load<CIN, COUT, HIN, S, K, MID>(&pa[0][0], &pb[0][0], x, tile + 1, P);
+    f32x16 acc[TW];
+    irf_core<CIN, COUT, HIN, S, K, MID>(bh, bl, acc, pw_a, pw_b, dw_w, dw_b, pwl_a, pwl_b, s_pw, s_dw, s_w);
+    irf_store<CIN, COUT, HIN, S, K, MID>(acc, y, p0, npv, s_pw);
+  }
+}
+
+// Two consecutive blocks on the same tile (A at stride 1, so its output tile is B's input tile:
+// SEARCH_SPACE2 layers 1 -> 2 at 16x16 and 3 -> 4 at 8x8): A's pwl output goes to LDS (over A's
+// then free pw / dw buffers) instead of HBM, B's pw B operands are read back from there -- the
+// A -> B activation (32 / 16 KB per patch each way) never reaches HBM.
+template <int CA, int HI, int KA, int MA, int CB, int KB, int MB>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CA == 64 ? 2 : 1))) void k_irf2(
+    const float* __restrict__ x, float* __restrict__ y, HnIrfArgs A, HnIrfArgs Bk, int P) {
+  using SA = IrfShape<CA, CA, HI, 1, KA, MA>;
+  using SB = IrfShape<CA, CB, HI, 2, KB, MB>;
+  static_assert(SA::NPB == SB::NPB && SA::NO == SB::NI, "A's output tile is B's input tile");
+  constexpr int NPB = SA::NPB, XS = CA + 4;  // A -> B tile in LDS: [pixel][CA + 4 floats]
+  constexpr int LA = irf_lds_floats<CA, CA, HI, 1, KA, MA>(), LB = irf_lds_floats<CA, CB, HI, 2, KB, MB>();
+  constexpr int LX = SA::NO * XS;
+  constexpr int LDS = LA > LB ? (LA > LX ? LA : LX) : (LB > LX ? LB : LX);
+  __shared__ __attribute__((aligned(16))) float smem[LDS];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, px = lane & 31, h = lane >> 5;
+  constexpr bool PREF = CA == 32;
+  const int ntiles = (P + NPB - 1) / NPB;
+  const int per = PREF ? (ntiles + (int)gridDim.x - 1) / (int)gridDim.x : 1;
+  const int tbeg = (int)blockIdx.x * per, tend = PREF ? min(ntiles, tbeg + per) : tbeg + 1;
+  if (tbeg >= ntiles) return;  // workgroup-uniform
+
+  float4 pa[SA::TI][SA::KS], pb[SA::TI][SA::KS];
+  if (PREF) irf_load<CA, CA, HI, 1, KA, MA>(&pa[0][0], &pb[0][0], x, tbeg, P);
+#pragma unroll 1
+  for (int tile = tbeg; tile < tend; ++tile) {
+    if (!PREF) irf_load<CA, CA, HI, 1, KA, MA>(&pa[0][0], &pb[0][0], x, tile, P);
+    const long p0 = (long)tile * NPB;
+    const int npv = (int)min<long>(NPB, P - p0);
+    {
+      uint4 bh[SA::TI][SA::KS], bl[SA::TI][SA::KS];
+#pragma unroll
+      for (int i = 0; i < SA::TI; ++i)
+#pragma unroll
+        for (int s = 0; s < SA::KS; ++s) split8_f16(pa[i][s], pb[i][s], bh[i][s], bl[i][s]);
+      if (PREF && tile + 1 < tend) irf_load<CA, CA, HI, 1, KA, MA>(&pa[0][0], &pb[0][0], x, tile + 1, P);
+      f32x16 acc[SA::TW];
+      irf_core<CA, CA, HI, 1, KA, MA>(bh, bl, acc, A.pw_a, A.pw_b, A.dw_w, A.dw_b, A.pwl_a, A.pwl_b, smem,
+                                      smem + SA::LDS_PW, smem + SA::LDS_PW + SA::LDS_DW);
+      // A's output tile -> LDS [pixel][XS] (lane (px, h): channels 8q + 4h .. + 3 of pixel px)
+#pragma unroll
+      for (int i = 0; i < SA::TW; ++i) {
+        const int tl = 4 * i + w, pt = tl % SA::NOT, ct = tl / SA::NOT;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          *reinterpret_cast<float4*>(smem + (pt * 32 + px) * XS + 32 * ct + 8 * q + 4 * h) =
+              make_float4(acc[i][4 * q], acc[i][4 * q + 1], acc[i][4 * q + 2], acc[i][4 * q + 3]);
+      }
+    }
+    __syncthreads();
+    // B's pw B operands from the LDS tile (pixel tiles 4i + w, 8 channels per lane), then B
+    uint4 bh[SB::TI][SB::KS], bl[SB::TI][SB::KS];
+#pragma unroll
+    for (int i = 0; i < SB::TI; ++i)
+#pragma unroll
+      for (int s = 0; s < SB::KS; ++s) {
+        const float4* src = reinterpret_cast<const float4*>(smem + ((4 * i + w) * 32 + px) * XS + 16 * s + 8 * h);
+        split8_f16(src[0], src[1], bh[i][s], bl[i][s]);
+      }
+    __syncthreads();  // the tile's LDS is B's pw / dw buffers from here
+    f32x16 acc[SB::TW];
+    irf_core<CA, CB, HI, 2, KB, MB>(bh, bl, acc, Bk.pw_a, Bk.pw_b, Bk.dw_w, Bk.dw_b, Bk.pwl_a, Bk.pwl_b, smem,
+                                    smem + SB::LDS_PW, smem + SB::LDS_PW + SB::LDS_DW);
+    irf_store<CA, CB, HI, 2, KB, MB>(acc, y, p0, npv, smem);
+  }
 }
 
 template <int CIN, int COUT, int HIN, int S, int K, int MID>
@@ -274,7 +382,44 @@ hipError_t irf_launch(const HnIrfArgs& a, int P, hipStream_t st) {
   return hipGetLastError();
 }
 
+template <int CA, int HI, int KA, int MA, int CB, int KB, int MB>
+hipError_t irf2_launch(const HnIrfArgs& a, const HnIrfArgs& b, int P, hipStream_t st) {
+  constexpr int NPB = IrfTile<CA, HI>::NPB;
+  const void* fn = reinterpret_cast<const void*>(&k_irf2<CA, HI, KA, MA, CB, KB, MB>);
+  int resident = 0;
+  const hipError_t e = hn_resident_blocks(fn, 256, 0, &resident);
+  if (e != hipSuccess) return e;
+  const int grid = CA == 32 ? std::min((P + NPB - 1) / NPB, resident) : (P + NPB - 1) / NPB;
+  hipLaunchKernelGGL((k_irf2<CA, HI, KA, MA, CB, KB, MB>), dim3(grid), dim3(256), 0, st, a.x, b.y, a, b, P);
+  return hipGetLastError();
+}
+
 }  // namespace
+
+// two consecutive blocks fused (k_irf2): A = (CA -> CA, stride 1, kernel KA, mid MA) at HI x HI,
+// B = (CA -> CB, stride 2, KB, MB); e = 1 / s2 ops (mid = CA) at SEARCH_SPACE2 layers 1 -> 2 and 3 -> 4
+#define HN_IRF2_SHAPES(X) \
+  X(32, 16, 3, 32, 64, 3, 32) X(32, 16, 3, 32, 64, 5, 32) X(32, 16, 5, 32, 64, 3, 32) X(32, 16, 5, 32, 64, 5, 32) \
+  X(64, 8, 3, 64, 128, 3, 64) X(64, 8, 3, 64, 128, 5, 64) X(64, 8, 5, 64, 128, 3, 64) X(64, 8, 5, 64, 128, 5, 64)
+
+bool hn_irf2_supported(int ca, int hi, int ka, int ma, int cb, int kb, int mb) {
+#define HN_IRF2_SUP(CA, HI, KA, MA, CB, KB, MB) \
+  if (ca == CA && hi == HI && ka == KA && ma == MA && cb == CB && kb == KB && mb == MB) return true;
+  HN_IRF2_SHAPES(HN_IRF2_SUP)
+#undef HN_IRF2_SUP
+  return false;
+}
+
+hipError_t hn_launch_irf2(const HnIrfArgs& a, const HnIrfArgs& b, int P, int ca, int hi, int ka, int ma, int cb,
+                          int kb, int mb, hipStream_t st) {
+  if (P <= 0) return hipSuccess;
+#define HN_IRF2_GO(CA, HI, KA, MA, CB, KB, MB) \
+  if (ca == CA && hi == HI && ka == KA && ma == MA && cb == CB && kb == KB && mb == MB) \
+    return irf2_launch<CA, HI, KA, MA, CB, KB, MB>(a, b, P, st);
+  HN_IRF2_SHAPES(HN_IRF2_GO)
+#undef HN_IRF2_GO
+  return hipErrorInvalidValue;
+}
 
 // SEARCH_SPACE2 layers 1..5 (cin, cout, hin, stride) x k in {3,5} x e in {1,3,4}
 #define HN_IRF_SHAPES(X, K)                                                                     \

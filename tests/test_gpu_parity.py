@@ -9,6 +9,8 @@ import os
 
 import numpy as np
 import pytest
+
+from hardnetnas_amd import arch as A
 import torch
 
 from fixtures import FDL_NAMES, NAS_NAMES, build_module, load, golden_inputs
@@ -350,12 +352,16 @@ ALL_OPS = ["skip", "ir_k3_e1", "ir_k3_e3", "ir_k3_s4", "ir_k5_e1", "ir_k5_e3", "
 
 
 @pytest.mark.parametrize("op", ALL_OPS[1:])
-def test_every_candidate_op_at_every_layer_fused_irf(op, cuda_device):
+@pytest.mark.parametrize("pairs", [True, False])
+def test_every_candidate_op_at_every_layer_fused_irf(op, pairs, cuda_device, monkeypatch):
     """The op at all six slots: layer 0 through the fused front, layers 1..5 through the
-    fused IRF block kernel (every SEARCH_SPACE2 shape incl. 16/8/4 px and e3/e4 MID); ragged
-    batch 37 exercises partial tiles (NPB = 1/4/8 patches per workgroup)."""
+    fused IRF block kernel (every SEARCH_SPACE2 shape incl. 16/8/4 px and e3/e4 MID) -- with the
+    two-block kernel k_irf2 for layers 1+2 and 3+4 where the op qualifies, and without
+    (HN_NO_IRF2=1); ragged batch 37 exercises partial tiles (NPB = 1/4/8 patches per workgroup)."""
     from hardnetnas_amd import synth
     from hardnetnas_amd._native import NativeModel
+    if not pairs:
+        monkeypatch.setenv("HN_NO_IRF2", "1")
     ops = [op] * 6
     m, p = _synth_nas(ops, seed=7)
     x = torch.from_numpy(synth.synth_patches(37, seed=9))
@@ -364,8 +370,31 @@ def test_every_candidate_op_at_every_layer_fused_irf(op, cuda_device):
     nm.set_profiling(True)
     y = nm(x.to(cuda_device)).cpu().numpy()
     st = nm.stage_times()
-    assert st["irf"][1] == 5 and "pw" not in st
+    n1, n2 = st.get("irf", (0, 0))[1], st.get("irf2", (0, 0))[1]
+    assert n1 + 2 * n2 == 5 and "pw" not in st
+    spec = A.OP_SPECS[op]
+    fusable = pairs and not spec.se and A.ir_mid(32, spec.expansion) == 32 and A.ir_mid(64, spec.expansion) == 64
+    assert n2 == (2 if fusable else 0), (op, st)
     assert np.abs(y - ref).max() <= NAS_TOL
+
+
+@pytest.mark.parametrize("name", ["wang2", "wang4"])
+def test_two_block_kernel_is_bit_identical(name, cuda_device, monkeypatch):
+    """k_irf2 (layers 1+2 / 3+4 in one kernel, the activation between them in LDS) computes exactly
+    what the two k_irf launches do (the same fp32 values are split and multiplied): bit-identical
+    descriptors, on the golden patches and a ragged batch."""
+    from hardnetnas_amd._native import NativeModel
+    m, fx, _ = build_module(name)
+    x = torch.from_numpy(golden_inputs(fx)).to(cuda_device)
+    nm = NativeModel.from_module(m, cuda_device)
+    nm.set_profiling(True)
+    y = nm(x)
+    assert "irf2" in nm.stage_times()
+    monkeypatch.setenv("HN_NO_IRF2", "1")
+    nm1 = NativeModel.from_module(m, cuda_device)
+    assert torch.equal(y, nm1(x))
+    assert torch.equal(nm(x[:37]), nm1(x[:37]))
+    assert np.abs(y.cpu().numpy() - fx["y"]).max() <= NAS_TOL
 
 
 @pytest.mark.parametrize("name", ["wang2", "wang4"])

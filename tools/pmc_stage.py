@@ -22,8 +22,10 @@ from pmc_traffic import stage_of  # noqa: E402
 
 
 def stage(name: str):
-    if "k_pairdist_rows<" in name:
+    if "k_pairdist_rows<" in name or "k_pairdist_ring<" in name:
         return "pairdist"
+    if "k_irf2<" in name:
+        return "irf2"
     if "k_skip_s2<" in name or "k_skip_s2(" in name:
         return "skip"
     if "k_fdl_front" in name:
