@@ -37,6 +37,7 @@ void hn_read_knobs(HnKnobs* k) {
   k->no_skipfuse = std::getenv("HN_NO_SKIPFUSE") != nullptr;
   k->pairdist_valu = std::getenv("HN_PAIRDIST_VALU") != nullptr;
   k->pairdist_reg = env_int("HN_PAIRDIST_REG", 0) != 0;
+  k->front_fold = env_int("HN_FRONT_FOLD", 0) != 0;
   k->train_splitk = std::max(32, env_int("HN_TRAIN_SPLITK", 1024)) / 32 * 32;
   k->train_f32 = env_int("HN_TRAIN_F32", 1) & 255;
 #ifdef HN_EXPERIMENTS
@@ -122,6 +123,7 @@ struct NasLayer {
   float *pwl_w = nullptr, *pwl_b = nullptr;
   float *se_w1 = nullptr, *se_b1 = nullptr, *se_w2 = nullptr, *se_b2 = nullptr;
   uint16_t* front_a = nullptr;  // fused front (layer 0): pw as MFMA A operand, dw channel order
+  uint16_t* front_pwl16 = nullptr;  // fused front: pwl as 16x16x32 A operands
   float* front_b = nullptr;
   uint16_t *irf_pw_a = nullptr, *irf_pwl_a = nullptr;  // fused IRF block (layers >= 1)
   float* irf_pw_b = nullptr;
@@ -452,6 +454,25 @@ static std::vector<uint16_t> pack_1x1_a(const std::vector<float>& w, int cout, i
   return a;
 }
 
+// 1x1 conv (cout = 32, groups densified) as 16x16x32 fp16 hi/lo A operands: [cin/32][out tile 2][plane]
+// [lane 64][8], lane (row = l & 15 -> output channel 16 tile + row, k-group l >> 4 -> input
+// channels 32 chunk + 8 (l >> 4) + j) -- the NAS front's pwl (hn_front.hip, no-fold form)
+static std::vector<uint16_t> pack_1x1_a16(const std::vector<float>& w, int cout, int cin, int g) {
+  const int kg = cin / g;
+  std::vector<uint16_t> a((size_t)cin / 32 * (cout / 16) * 2 * 64 * 8, 0);
+  for (int ch = 0; ch < cin / 32; ++ch)
+    for (int tt = 0; tt < cout / 16; ++tt)
+      for (int lane = 0; lane < 64; ++lane)
+        for (int j = 0; j < 8; ++j) {
+          const int c = 16 * tt + (lane & 15), k = 32 * ch + 8 * (lane >> 4) + j;
+          const int grp = c / (cout / g);
+          const float v = (k >= grp * kg && k < (grp + 1) * kg) ? w[(size_t)c * kg + (k - grp * kg)] : 0.f;
+          const size_t o = ((((size_t)ch * (cout / 16) + tt) * 2) * 64 + lane) * 8 + j;
+          put_f16_split(v, &a[o], &a[o + 64 * 8]);
+        }
+  return a;
+}
+
 // 3x3 conv (cin = 32, BN folded) as 16x16x32 bf16 hi/lo A operands for k_c12:
 // [tap 9][group of 16 output channels][plane][lane 64][8], lane (row = l & 15 -> output
 // channel 16 g + row, k-group l >> 4 -> input channels 8 (l >> 4) + j).
@@ -686,6 +707,8 @@ static int build_nas_layers(hn_model* m, Cursor& cur, int hw, size_t maxf) {
       if ((L.irf_pw_a || (i == 0 && L.front_a)) &&
           (rc = m->upload(pack_1x1_a(f.w, L.cout, L.mid, L.g, [](int c) { return c; }), &L.irf_pwl_a)))
         return rc;
+      if (i == 0 && L.front_a && (rc = m->upload(pack_1x1_a16(f.w, L.cout, L.mid, L.g), &L.front_pwl16)))
+        return rc;
       if (L.se) {
         L.semid = L.cout / 4 > 8 ? L.cout / 4 : 8;
         const size_t n1 = (size_t)L.semid * L.cout;
@@ -872,7 +895,8 @@ static int forward_nas(hn_model* m, const float* in, int P, int pmax, float* out
     const bool mp = m->front == 2;
     const HnFrontArgs fa{in, x, reinterpret_cast<const uint4*>(m->front_spack), m->stem_b,
                          reinterpret_cast<const uint4*>(L.front_a), L.front_b, L.dw_w, L.dw_b,
-                         reinterpret_cast<const uint4*>(L.irf_pwl_a), L.pwl_b};
+                         reinterpret_cast<const uint4*>(L.irf_pwl_a), L.pwl_b,
+                         reinterpret_cast<const uint4*>(L.front_pwl16)};
     STAGE("front", hn_launch_front(fa, P, L.k, L.mid, mp, ineps >= 0.f, ineps, st));
     if (!mp && L.se)
       STAGE("se", hn_launch_se(x, L.se_w1, L.se_b1, L.se_w2, L.se_b2, P, L.hout * L.hout, L.cout,

@@ -84,6 +84,15 @@ HN_DEV f32x16 mfma3_f16(const f16x8& ah, const f16x8& al, const f16x8& bh, const
   return acc;
 }
 
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+// the same split-precision product on the 16x16x32 f16 MFMA (4 accumulator entries per lane)
+HN_DEV f32x4_t mfma3_f16_16(const f16x8& ah, const f16x8& al, const f16x8& bh, const f16x8& bl, f32x4_t acc) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, acc, 0, 0, 0);
+  return acc;
+}
+
 // Blocks are dispatched round-robin over the 8 XCDs (block b -> XCD b % 8); remap so that
 // consecutive logical tiles run on the same XCD and share its L2.
 HN_DEV int xcd_remap(int bid, int nblocks) {

@@ -51,7 +51,11 @@ __constant__ unsigned char kDwLane[64] = {
 // RING (MID = 32 and the maxpool form): the chunk's pw rows live in an LDS ring of IR rows
 // (slot (y + PAD) % IR) that persists across the 4 bands of a patch, so a band computes only
 // its 8 new stem/pw rows.  MID > 32 recomputes the band's halo rows for every chunk.
-template <int K, int MID, int MODE, bool NORM>
+// NF (no fold, the default): the pwl runs as 16x16x32 tiles -- wave w owns the band's output row w
+// (16 pixels), lane (pixel l & 15, channels 8 (l >> 4) .. + 7) computes its dw channels and is directly
+// that MFMA's B operand -- so no wave holds a partial K sum and the fold through LDS (two barriers
+// per band) goes; for MID = 32 the dw weights are loaded into LDS once per workgroup.
+template <int K, int MID, int MODE, bool NORM, bool NF>
 __global__ __launch_bounds__(256) void k_front(const float* __restrict__ in,
                                                float* __restrict__ out,
                                                const uint4* __restrict__ spack,  // stem A operand
@@ -62,6 +66,7 @@ __global__ __launch_bounds__(256) void k_front(const float* __restrict__ in,
                                                const float* __restrict__ dw_b,  // [MID]
                                                const uint4* __restrict__ pwl_a,  // [1][MID/16][2][64]
                                                const float* __restrict__ pwl_b,  // [32]
+                                               const uint4* __restrict__ pwl_a16,  // [MID/32][2][2][64]
                                                int P, float eps) {
   constexpr int KK = MODE == FRONT_MAXPOOL ? 3 : K;
   constexpr int PAD = KK / 2;
@@ -127,6 +132,17 @@ __global__ __launch_bounds__(256) void k_front(const float* __restrict__ in,
   const int lm = kDwLane[lane], dq = lm & 7, dox = lm >> 3;
   auto slot_of = [](int y) { return (y + PAD + IR) % IR; };  // ring slot of pw row y
 
+  constexpr bool DW_ONCE = NF && MID == 32 && MODE == FRONT_IRF;  // one chunk: its dw weights never change
+  if constexpr (DW_ONCE) {
+    for (int i = t; i < KK * KK * 8 + 8; i += 256) {
+      float4 wv;
+      if (i < KK * KK * 8)
+        wv = *reinterpret_cast<const float4*>(dw_w + (i >> 3) * MID + 4 * (i & 7));
+      else
+        wv = *reinterpret_cast<const float4*>(dw_b + 4 * (i - KK * KK * 8));
+      reinterpret_cast<float4*>(s_dw)[i] = wv;
+    }
+  }
   float4 vnext = reinterpret_cast<const float4*>(in + pb * 1024)[t];
 #pragma unroll 1
   for (long patch = pb; patch < pe; ++patch) {
@@ -238,9 +254,18 @@ __global__ __launch_bounds__(256) void k_front(const float* __restrict__ in,
 
       // ---- phases B/C/D per 32-channel chunk of MID -------------------------------------
       f32x16 oacc = {};
+      f32x4_t o16[2];  // NF: pwl output channels 16 tile + 4 (lane >> 4) + j of pixel lane & 15, from the bias
+      if constexpr (NF) {
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt) {
+          const float4 b = *reinterpret_cast<const float4*>(pwl_b + 16 * tt + 4 * (lane >> 4));
+          o16[tt] = f32x4_t{b.x, b.y, b.z, b.w};
+        }
+      }
 #pragma unroll 1
       for (int m = 0; m < MID / 32; ++m) {
         // dw weights + bias of the chunk
+        if (!DW_ONCE)
         for (int i = t; i < KK * KK * 8 + 8; i += 256) {
           float4 wv;
           if (i < KK * KK * 8)
@@ -268,6 +293,33 @@ __global__ __launch_bounds__(256) void k_front(const float* __restrict__ in,
                                        fmaxf(acc[4 * q + 2], 0.f), fmaxf(acc[4 * q + 3], 0.f));
         }
         __syncthreads();
+        if constexpr (NF) {  // dw of band row w, 8 channels of pixel lane & 15 -> 16x16x32 pwl
+          const int ox = lane & 15, c0 = 8 * (lane >> 4);
+          f32x4 a0 = *reinterpret_cast<const f32x4*>(s_dw + KK * KK * 32 + c0);
+          f32x4 a1 = *reinterpret_cast<const f32x4*>(s_dw + KK * KK * 32 + c0 + 4);
+#pragma unroll DYU
+          for (int dy = 0; dy < KK; ++dy) {
+            const float* rp = s_pw + slot_of(2 * (r0 + w) - PAD + dy) * RS + c0;
+#pragma unroll
+            for (int dx = 0; dx < KK; ++dx) {
+              const float* wp = s_dw + (dy * KK + dx) * 32 + c0;
+              const float* ip = rp + ((dx & 1) ? HALF + ox + (dx >> 1) : ox + (dx >> 1)) * PS;
+              a0 = __builtin_elementwise_fma(*reinterpret_cast<const f32x4*>(wp), *reinterpret_cast<const f32x4*>(ip), a0);
+              a1 = __builtin_elementwise_fma(*reinterpret_cast<const f32x4*>(wp + 4), *reinterpret_cast<const f32x4*>(ip + 4), a1);
+            }
+          }
+          a0 = __builtin_elementwise_max(a0, f32x4{});
+          a1 = __builtin_elementwise_max(a1, f32x4{});
+          uint4 xh, xl;
+          split8_f16(make_float4(a0.x, a0.y, a0.z, a0.w), make_float4(a1.x, a1.y, a1.z, a1.w), xh, xl);
+          const uint4* lp = pwl_a16 + (size_t)m * 4 * 64 + lane;
+#pragma unroll
+          for (int tt = 0; tt < 2; ++tt)
+            o16[tt] = mfma3_f16_16(as_f16x8(lp[128 * tt]), as_f16x8(lp[128 * tt + 64]), as_f16x8(xh), as_f16x8(xl),
+                                   o16[tt]);
+          __syncthreads();  // s_dw (and, without the ring, s_pw) is rewritten next
+          continue;
+        }
         // dw straight into the pwl B-operand layout: wave w owns band pixel tile (w & 1) and
         // K-step (w >> 1) of this chunk; lane (px, h) computes channels 16*(w>>1) + 8h .. +7
         // of band pixel 32*(w&1) + px, splits them and multiplies with the pwl weights of
@@ -296,6 +348,13 @@ __global__ __launch_bounds__(256) void k_front(const float* __restrict__ in,
           oacc = mfma3_f16(as_f16x8(lp[0]), as_f16x8(lp[64]), as_f16x8(xh), as_f16x8(xl), oacc);
         }
         __syncthreads();  // s_dw (and, without the ring, s_pw) is rewritten next
+      }
+      if constexpr (NF) {  // band row r0 + w, pixel lane & 15: 4 consecutive channels per tile
+        float* dst = out + ((patch * 16 + r0 + w) * 16 + (lane & 15)) * OC + 4 * (lane >> 4);
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt)
+          *reinterpret_cast<float4*>(dst + 16 * tt) = make_float4(o16[tt][0], o16[tt][1], o16[tt][2], o16[tt][3]);
+        continue;
       }
       // fold the odd-K-step partial sums of waves 2/3 into waves 0/1 through the interior
       // of the ring slots of rows ybeg, ybeg + 1 (recomputed by the next band, never the
@@ -329,15 +388,24 @@ __global__ __launch_bounds__(256) void k_front(const float* __restrict__ in,
   }
 }
 
-template <int K, int MID, int MODE, bool NORM>
-hipError_t front_launch_t(const HnFrontArgs& a, int P, float eps, hipStream_t st) {
+template <int K, int MID, int MODE, bool NORM, bool NF>
+hipError_t front_launch_nf(const HnFrontArgs& a, int P, float eps, hipStream_t st) {
   int resident = 0;  // persistent grid: every workgroup resident at once
   const hipError_t e =
-      hn_resident_blocks(reinterpret_cast<const void*>(&k_front<K, MID, MODE, NORM>), 256, 0, &resident);
+      hn_resident_blocks(reinterpret_cast<const void*>(&k_front<K, MID, MODE, NORM, NF>), 256, 0, &resident);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((k_front<K, MID, MODE, NORM>), dim3(std::min(P, resident)), dim3(256), 0, st, a.in,
-                     a.out, a.spack, a.stem_b, a.apack, a.pw_b, a.dw_w, a.dw_b, a.pwl_a, a.pwl_b, P, eps);
+  hipLaunchKernelGGL((k_front<K, MID, MODE, NORM, NF>), dim3(std::min(P, resident)), dim3(256), 0, st, a.in,
+                     a.out, a.spack, a.stem_b, a.apack, a.pw_b, a.dw_w, a.dw_b, a.pwl_a, a.pwl_b, a.pwl_a16, P,
+                     eps);
   return hipGetLastError();
+}
+
+template <int K, int MID, int MODE, bool NORM>
+hipError_t front_launch_t(const HnFrontArgs& a, int P, float eps, hipStream_t st) {
+  // HN_FRONT_FOLD=1: the 32x32x16 pwl with the partial-sum fold through LDS (the round-2 form)
+  if (MODE == FRONT_IRF && !hn_knobs().front_fold && a.pwl_a16)
+    return front_launch_nf<K, MID, MODE, NORM, true>(a, P, eps, st);
+  return front_launch_nf<K, MID, MODE, NORM, false>(a, P, eps, st);
 }
 
 template <int K, int MID, int MODE>

@@ -18,6 +18,7 @@ struct HnKnobs {
   bool no_skipfuse = false;    // HN_NO_SKIPFUSE: maxpool + pw instead of k_skip_s2
   bool pairdist_valu = false;  // HN_PAIRDIST_VALU: fp32 VALU pair-distance kernel
   bool pairdist_reg = false;   // HN_PAIRDIST_REG: register-staged positives instead of the LDS-DMA ring
+  bool front_fold = false;     // HN_FRONT_FOLD: the NAS front's pwl with the LDS partial-sum fold
   int train_splitk = 1024;     // HN_TRAIN_SPLITK: K per split-K slice of the train GEMMs
   int train_f32 = 1;           // HN_TRAIN_F32: bit 0 train forward convs, bit 1 stride-1 dgrads as f32-MFMA
                                // GEMMs (else the bf16x3 conv kernels); default 1 = every product f32;
@@ -116,6 +117,7 @@ struct HnFrontArgs {
   const float* dw_b;
   const uint4* pwl_a;   // pwl A operand, [1][MID/16][plane 2][lane 64] x 8 fp16
   const float* pwl_b;   // [32]
+  const uint4* pwl_a16; // pwl A operand for 16x16x32: [MID/32][out tile 2][plane 2][lane 64] x 8 fp16
 };
 bool hn_front_supported(int k, int mid);
 hipError_t hn_launch_front(const HnFrontArgs& a, int P, int k, int mid, bool maxpool, bool norm,
