@@ -403,7 +403,9 @@ hipError_t front_launch_nf(const HnFrontArgs& a, int P, float eps, hipStream_t s
 template <int K, int MID, int MODE, bool NORM>
 hipError_t front_launch_t(const HnFrontArgs& a, int P, float eps, hipStream_t st) {
   // HN_FRONT_FOLD=1: the 32x32x16 pwl with the partial-sum fold through LDS (the round-2 form)
-  if (MODE == FRONT_IRF && !hn_knobs().front_fold && a.pwl_a16)
+  // (k3 only: the k5 form measured 6 % slower without the fold -- its rolled dy loop keeps more live
+  // registers in the no-fold mapping; wang2 front k3 6.12 -> 5.59 ms, wang3 front k5 8.77 -> 9.30 ms)
+  if (MODE == FRONT_IRF && K == 3 && !hn_knobs().front_fold && a.pwl_a16)
     return front_launch_nf<K, MID, MODE, NORM, true>(a, P, eps, st);
   return front_launch_nf<K, MID, MODE, NORM, false>(a, P, eps, st);
 }

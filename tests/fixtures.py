@@ -207,15 +207,20 @@ def supernet_step(m, fx, x, y, device=None):
 
 
 def nas_grad_check(named_grads, fx, prefix: str, cap: int = GRAD_SAMPLE, bar: float = 5e-3):
-    """Worst summary error of every parameter gradient against the fixture's fp64 summaries, in
-    units where ``bar`` is the pass mark (an error is scaled by bar / max(bar, 3 x the reference's
-    own fp32-vs-fp64 error of that gradient)).  A
+    """Gradient errors of every parameter against the fixture's fp64 summaries.
+
+    Returns (global, worst, where): ``global`` is the L2-relative error of all the gradients taken
+    together (the per-tensor errors weighted by the fp64 norms: sqrt(sum e_k^2 |g_k|^2 / sum |g_k|^2)),
+    ``worst`` the largest per-tensor error in units where ``bar`` is the pass mark -- an error is
+    scaled by bar / max(bar, 3 x the reference's own fp32-vs-fp64 error of that gradient).  A
     gradient whose fp64 norm is ~0 (a BN bias right before a linear map into another BatchNorm,
-    whose mean subtraction cancels it exactly) is checked in absolute terms against the layer
-    scale instead.  Returns (worst relative error, name)."""
+    whose mean subtraction cancels it exactly) is checked in absolute terms against the layer scale
+    instead.  The global figure is the one a ReLU kink cannot dominate: one BN / SE output within
+    rounding of zero, landing on the other side, moves one small tensor's gradient (an SE or BN
+    bias summing few entries) by percent while every other gradient stays at 1e-5."""
     scale = max(float(fx[f"{prefix}g/{k}_norm"]) for k, _ in named_grads)
     ref_err = dict(zip([str(n) for n in fx[f"{prefix}grad_names"]], fx[f"{prefix}fp32_err"]))
-    worst, where = 0.0, ""
+    worst, where, num, den, errs = 0.0, "", 0.0, 0.0, []
     for k, g in named_grads:
         key = f"{prefix}g/{k}"
         norm = float(fx[f"{key}_norm"])
@@ -223,9 +228,13 @@ def nas_grad_check(named_grads, fx, prefix: str, cap: int = GRAD_SAMPLE, bar: fl
             e = float(np.linalg.norm(np.asarray(g, dtype=np.float64))) / scale
             assert e <= 1e-6, (k, e)
             continue
-        # relative to the bar, or to 3x the reference's own fp32 error on this gradient when that is
-        # larger (a ReLU kink the fp32 reference itself lands on the other side of)
-        e = max(summary_errors(g, fx, key, name_seed(k), cap).values()) / max(bar, 3.0 * float(ref_err[k])) * bar
+        raw = max(summary_errors(g, fx, key, name_seed(k), cap).values())
+        num += raw * raw * norm * norm
+        den += norm * norm
+        errs.append((raw, k))
+        e = raw / max(bar, 3.0 * float(ref_err[k])) * bar
         if e > worst:
             worst, where = e, k
-    return worst, where
+    errs.sort(reverse=True)
+    print("largest per-tensor gradient errors:", [(k, f"{e:.2e}") for e, k in errs[:5]])
+    return float(np.sqrt(num / den)), worst, where

@@ -92,8 +92,8 @@ def test_module_torch_nas_train_step_matches_reference(name):
         if "running" in k:
             ref = fx[f"{pre}stat/{k}_32"]
             assert np.abs(v.numpy() - ref).max() <= 1e-5 * max(1.0, np.abs(ref).max()), k
-    worst, where = nas_grad_check([(k, t.grad.numpy()) for k, t in m.named_parameters()], fx, pre)
-    assert worst <= 5e-3, (where, worst)
+    glob, worst, where = nas_grad_check([(k, t.grad.numpy()) for k, t in m.named_parameters()], fx, pre)
+    assert glob <= 5e-3 and worst <= 2e-2, (glob, where, worst)
 
 
 def test_supernet_module_torch_step_matches_reference():
@@ -111,5 +111,5 @@ def test_supernet_module_torch_step_matches_reference():
     ref = fx["super/thetas_grad_64"]
     assert np.linalg.norm(tg - ref) / np.linalg.norm(ref) <= 5e-3
     named = [(k, t.grad.numpy()) for k, t in m.named_parameters() if not k.endswith("thetas")]
-    worst, where = nas_grad_check(named, fx, "super/", cap=fx["meta"]["supernet"]["sample"])
-    assert worst <= 5e-3, (where, worst)
+    glob, worst, where = nas_grad_check(named, fx, "super/", cap=fx["meta"]["supernet"]["sample"])
+    assert glob <= 5e-3 and worst <= 2e-2, (glob, where, worst)
