@@ -30,7 +30,7 @@ static int env_int(const char* name, int dflt) {
 void hn_read_knobs(HnKnobs* k) {
   *k = HnKnobs{};
   k->c12_cfg = env_int("HN_C12_CFG", 12);
-  k->head_v1 = std::getenv("HN_HEAD_V1") != nullptr;
+  k->head = std::getenv("HN_HEAD_V1") ? 1 : env_int("HN_HEAD", 3);
   k->fdl_valu = std::getenv("HN_FDL_VALU") != nullptr;
   k->naive_pw = std::getenv("HN_NAIVE_PW") != nullptr;
   k->naive_dw = std::getenv("HN_NAIVE_DW") != nullptr;
@@ -789,6 +789,10 @@ extern "C" int hn_create(const hn_arch_desc* desc, const float* host_params, siz
     delete m;
     return fail(HN_ERR_ARG, "HN_C12_CFG / HN_C12_ABL: no such k_c12 build in this library");
   }
+  if (m->knobs.head < 1 || m->knobs.head > 3) {
+    delete m;
+    return fail(HN_ERR_ARG, "HN_HEAD: head GEMM form must be 1, 2 or 3");
+  }
   (void)hipGetDevice(&m->device);
   Cursor cur{host_params, n_params};
   tl_f16_out_of_range = 0;
@@ -879,7 +883,7 @@ static int forward_hardnet(hn_model* m, const float* in, int P, int pmax, float*
 }
 
 static int forward_nas(hn_model* m, const float* in, int P, int pmax, float* out, float* ws,
-                       hipStream_t st) {
+                       hipStream_t st, const HnU8In* u8 = nullptr) {
   const size_t per = m->ws_floats_per_patch * (size_t)pmax;
   float* x = ws;
   float* t1 = ws + per;
@@ -897,7 +901,7 @@ static int forward_nas(hn_model* m, const float* in, int P, int pmax, float* out
                          reinterpret_cast<const uint4*>(L.front_a), L.front_b, L.dw_w, L.dw_b,
                          reinterpret_cast<const uint4*>(L.irf_pwl_a), L.pwl_b,
                          reinterpret_cast<const uint4*>(L.front_pwl16)};
-    STAGE("front", hn_launch_front(fa, P, L.k, L.mid, mp, ineps >= 0.f, ineps, st));
+    STAGE("front", hn_launch_front(fa, P, L.k, L.mid, mp, ineps >= 0.f, ineps, st, u8));
     if (!mp && L.se)
       STAGE("se", hn_launch_se(x, L.se_w1, L.se_b1, L.se_w2, L.se_b2, P, L.hout * L.hout, L.cout,
                                L.semid, st));
@@ -1003,9 +1007,13 @@ extern "C" int hn_forward(hn_model* m, const float* d_in, int64_t batch, float* 
   return HN_OK;
 }
 
-// uint8 input: the stock HardNet's fused k_c12 preprocesses in its patch
-// load; every other model / configuration runs hn_preprocess into the workspace tail first.
-static bool u8_fused(const hn_model* m) {
+// uint8 input: the stock HardNet's fused k_c12 (every resize mode) and the NAS
+// models' fused front (NONE / CV2) preprocess in their patch loads; every other model / mode /
+// configuration (FDLNet, NAS PIL, HN_NO_FRONT, HN_FRONT_FOLD, the A/B configurations) runs
+// hn_preprocess into the workspace tail first.
+static bool u8_fused(const hn_model* m, int resize) {
+  if (m->desc.kind == HN_KIND_NAS)  // the fused front's patch load (hn_front.hip): no input_norm, not PIL
+    return resize != HN_RESIZE_PIL_BILINEAR && m->front && m->desc.input_norm_eps < 0.f && !m->knobs.front_fold;
   return m->desc.kind == HN_KIND_HARDNET && m->c12 && !m->unfused_stem && m->knobs.c12_cfg == 12 &&
          !m->knobs.c12_abl;
 }
@@ -1013,7 +1021,8 @@ static bool u8_fused(const hn_model* m) {
 extern "C" int hn_workspace_bytes_u8(const hn_model* m, int64_t batch, size_t* bytes_out) {
   int rc = hn_workspace_bytes(m, batch, bytes_out);
   if (rc) return rc;
-  if (!u8_fused(m)) *bytes_out += (size_t)std::min<int64_t>(batch, m->chunk) * 1024 * sizeof(float);
+  // (the fp32 tail for hn_preprocess unless every resize mode is fused)
+  if (!u8_fused(m, HN_RESIZE_PIL_BILINEAR)) *bytes_out += (size_t)std::min<int64_t>(batch, m->chunk) * 1024 * sizeof(float);
   return HN_OK;
 }
 
@@ -1040,7 +1049,7 @@ extern "C" int hn_forward_u8(hn_model* m, const uint8_t* d_in, int64_t batch, in
     return fail(HN_ERR_WORKSPACE, "workspace too small: need " + std::to_string(need) + " bytes");
   hipStream_t st = static_cast<hipStream_t>(hip_stream);
   KnobScope knobs(&m->knobs);
-  const bool fused = u8_fused(m);
+  const bool fused = u8_fused(m, resize);
   const size_t inb = (size_t)in_hw * in_hw;
   float* ws = static_cast<float*>(d_workspace);
   size_t base = 0;
@@ -1054,7 +1063,8 @@ extern "C" int hn_forward_u8(hn_model* m, const uint8_t* d_in, int64_t batch, in
     int rc;
     if (fused) {
       const HnU8In u8{in, resize, normalize, mean, stdv};
-      rc = forward_hardnet(m, nullptr, P, pmax, out, ws, st, &u8);
+      rc = m->desc.kind == HN_KIND_HARDNET ? forward_hardnet(m, nullptr, P, pmax, out, ws, st, &u8)
+                                           : forward_nas(m, nullptr, P, pmax, out, ws, st, &u8);
     } else {
       STAGE("preprocess", hn_launch_preprocess(in, P, resize, normalize, mean, stdv, pre, st));
       rc = m->desc.kind == HN_KIND_HARDNET ? forward_hardnet(m, pre, P, pmax, out, ws, st)

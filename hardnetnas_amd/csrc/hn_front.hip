@@ -22,6 +22,7 @@
 // accumulates over the MID chunks in registers; only the 32-channel block output reaches HBM.
 #include "hn_common.h"
 #include "hn_internal.h"
+#include "hn_preproc.h"
 
 #include <algorithm>
 #include <cstdlib>
@@ -55,8 +56,14 @@ __constant__ unsigned char kDwLane[64] = {
 // (16 pixels), lane (pixel l & 15, channels 8 (l >> 4) .. + 7) computes its dw channels and is directly
 // that MFMA's B operand -- so no wave holds a partial K sum and the fold through LDS (two barriers
 // per band) goes; for MID = 32 the dw weights are loaded into LDS once per workgroup.
-template <int K, int MID, int MODE, bool NORM, bool NF>
-__global__ __launch_bounds__(256) void k_front(const float* __restrict__ in,
+// U8 (preprocessing fused into the patch load, as k_c12): -1 = fp32 [P,1,32,32]
+// input; HN_RESIZE_NONE / _CV2_LINEAR = uint8 patches (32x32 / 64x64) resized, /255'd and
+// Normalize'd in the load by hn_preproc.h (the arithmetic of hn_preprocess), so the input costs
+// 1 / 4 KiB of HBM per patch and no intermediate fp32 tensor exists.  (PIL mode stays unfused:
+// its 12 prefetched byte registers took the k3 front from three workgroups per CU to two, wang2
+// front 5.7 -> 7.2 ms, against 0.46 ms for the separate hn_preprocess.)
+template <int K, int MID, int MODE, bool NORM, bool NF, int U8 = -1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRONT_IRF && K == 3 && MID == 32 ? 3 : 1))) void k_front(const void* __restrict__ in_,
                                                float* __restrict__ out,
                                                const uint4* __restrict__ spack,  // stem A operand
                                                const float* __restrict__ stem_b,  // [32]
@@ -67,7 +74,7 @@ __global__ __launch_bounds__(256) void k_front(const float* __restrict__ in,
                                                const uint4* __restrict__ pwl_a,  // [1][MID/16][2][64]
                                                const float* __restrict__ pwl_b,  // [32]
                                                const uint4* __restrict__ pwl_a16,  // [MID/32][2][2][64]
-                                               int P, float eps) {
+                                               int P, float eps, float pmean, float pstd, int pnorm) {
   constexpr int KK = MODE == FRONT_MAXPOOL ? 3 : K;
   constexpr int PAD = KK / 2;
   constexpr int IR = 2 * (RB - 1) + KK;  // pw rows a band reads (ring size)
@@ -143,12 +150,33 @@ __global__ __launch_bounds__(256) void k_front(const float* __restrict__ in,
       reinterpret_cast<float4*>(s_dw)[i] = wv;
     }
   }
-  float4 vnext = reinterpret_cast<const float4*>(in + pb * 1024)[t];
+  const float* in = static_cast<const float*>(in_);
+  const uint8_t* in8 = static_cast<const uint8_t*>(in_);
+  constexpr int INB = U8 == HN_RESIZE_NONE ? 1024 : 4096;  // bytes per uint8 patch
+  const int iy = t >> 3, ix = 4 * (t & 7);                  // this thread's 4 pixels (iy, ix ..)
+  // the next patch's pixels are fetched one patch ahead (U8: its raw bytes -- 1 / 4 registers for
+  // NONE / CV2, as many as the fp32 form -- resized at use)
+  static_assert(U8 != HN_RESIZE_PIL_BILINEAR, "PIL's 12 prefetch registers cost the k3 front its third workgroup");
+  float4 vnext;
+  hnpre::U8Px<U8 < 0 ? HN_RESIZE_NONE : U8, 4> rnext;
+  if constexpr (U8 < 0)
+    vnext = reinterpret_cast<const float4*>(in + pb * 1024)[t];
+  else
+    rnext.load(in8 + pb * INB, iy, ix);
 #pragma unroll 1
   for (long patch = pb; patch < pe; ++patch) {
     // ---- patch (+ input_norm) to LDS; the next patch's pixels are prefetched ---------------
-    const float4 v = vnext;
-    if (patch + 1 < pe) vnext = reinterpret_cast<const float4*>(in + (patch + 1) * 1024)[t];
+    float4 v;
+    if constexpr (U8 < 0) {
+      v = vnext;
+      if (patch + 1 < pe) vnext = reinterpret_cast<const float4*>(in + (patch + 1) * 1024)[t];
+    } else {
+      int q[4];
+      rnext.resized(iy, ix, q);
+      v = make_float4(hnpre::to_input(q[0], pmean, pstd, pnorm), hnpre::to_input(q[1], pmean, pstd, pnorm),
+                      hnpre::to_input(q[2], pmean, pstd, pnorm), hnpre::to_input(q[3], pmean, pstd, pnorm));
+      if (patch + 1 < pe) rnext.load(in8 + (patch + 1) * INB, iy, ix);
+    }
     float mean = 0.f, sd = 1.f;
     if (NORM) {  // (x - mean) / (std_unbiased + eps), as k_stem
       const float s = wave_sum(v.x + v.y + v.z + v.w);
@@ -388,32 +416,51 @@ __global__ __launch_bounds__(256) void k_front(const float* __restrict__ in,
   }
 }
 
-template <int K, int MID, int MODE, bool NORM, bool NF>
-hipError_t front_launch_nf(const HnFrontArgs& a, int P, float eps, hipStream_t st) {
+template <int K, int MID, int MODE, bool NORM, bool NF, int U8 = -1>
+hipError_t front_launch_nf(const HnFrontArgs& a, int P, float eps, hipStream_t st, const HnU8In* u8 = nullptr) {
   int resident = 0;  // persistent grid: every workgroup resident at once
   const hipError_t e =
-      hn_resident_blocks(reinterpret_cast<const void*>(&k_front<K, MID, MODE, NORM, NF>), 256, 0, &resident);
+      hn_resident_blocks(reinterpret_cast<const void*>(&k_front<K, MID, MODE, NORM, NF, U8>), 256, 0, &resident);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((k_front<K, MID, MODE, NORM, NF>), dim3(std::min(P, resident)), dim3(256), 0, st, a.in,
+  const void* src = u8 ? static_cast<const void*>(u8->in) : static_cast<const void*>(a.in);
+  hipLaunchKernelGGL((k_front<K, MID, MODE, NORM, NF, U8>), dim3(std::min(P, resident)), dim3(256), 0, st, src,
                      a.out, a.spack, a.stem_b, a.apack, a.pw_b, a.dw_w, a.dw_b, a.pwl_a, a.pwl_b, a.pwl_a16, P,
-                     eps);
+                     eps, u8 ? u8->mean : 0.f, u8 ? u8->stdv : 1.f, u8 ? u8->normalize : 0);
   return hipGetLastError();
 }
 
+// the production form of (K, MODE): the no-fold pwl for k3 IRF fronts
+template <int K, int MODE>
+constexpr bool front_nf() { return MODE == FRONT_IRF && K == 3; }
+
 template <int K, int MID, int MODE, bool NORM>
-hipError_t front_launch_t(const HnFrontArgs& a, int P, float eps, hipStream_t st) {
+hipError_t front_launch_t(const HnFrontArgs& a, int P, float eps, hipStream_t st, const HnU8In* u8) {
   // HN_FRONT_FOLD=1: the 32x32x16 pwl with the partial-sum fold through LDS (the round-2 form)
   // (k3 only: the k5 form measured 6 % slower without the fold -- its rolled dy loop keeps more live
   // registers in the no-fold mapping; wang2 front k3 6.12 -> 5.59 ms, wang3 front k5 8.77 -> 9.30 ms)
-  if (MODE == FRONT_IRF && K == 3 && !hn_knobs().front_fold && a.pwl_a16)
-    return front_launch_nf<K, MID, MODE, NORM, true>(a, P, eps, st);
+  const bool nf = MODE == FRONT_IRF && K == 3 && !hn_knobs().front_fold && a.pwl_a16;
+  if (u8) {  // uint8 loads (NONE / CV2): the production form without input_norm only (hn_api.hip u8_fused)
+    if constexpr (NORM) {
+      return hipErrorInvalidValue;
+    } else {
+      if (nf != front_nf<K, MODE>()) return hipErrorInvalidValue;
+      constexpr bool NFD = front_nf<K, MODE>();
+      switch (u8->resize) {
+        case HN_RESIZE_NONE: return front_launch_nf<K, MID, MODE, false, NFD, HN_RESIZE_NONE>(a, P, eps, st, u8);
+        case HN_RESIZE_CV2_LINEAR:
+          return front_launch_nf<K, MID, MODE, false, NFD, HN_RESIZE_CV2_LINEAR>(a, P, eps, st, u8);
+      }
+      return hipErrorInvalidValue;
+    }
+  }
+  if (nf) return front_launch_nf<K, MID, MODE, NORM, true>(a, P, eps, st);
   return front_launch_nf<K, MID, MODE, NORM, false>(a, P, eps, st);
 }
 
 template <int K, int MID, int MODE>
-hipError_t front_launch(const HnFrontArgs& a, int P, bool norm, float eps, hipStream_t st) {
-  return norm ? front_launch_t<K, MID, MODE, true>(a, P, eps, st)
-              : front_launch_t<K, MID, MODE, false>(a, P, eps, st);
+hipError_t front_launch(const HnFrontArgs& a, int P, bool norm, float eps, hipStream_t st, const HnU8In* u8) {
+  return norm ? front_launch_t<K, MID, MODE, true>(a, P, eps, st, u8)
+              : front_launch_t<K, MID, MODE, false>(a, P, eps, st, u8);
 }
 
 }  // namespace
@@ -423,11 +470,11 @@ bool hn_front_supported(int k, int mid) {
 }
 
 hipError_t hn_launch_front(const HnFrontArgs& a, int P, int k, int mid, bool maxpool, bool norm,
-                           float eps, hipStream_t st) {
+                           float eps, hipStream_t st, const HnU8In* u8) {
   if (P <= 0) return hipSuccess;
-  if (maxpool) return front_launch<3, 32, FRONT_MAXPOOL>(a, P, norm, eps, st);
+  if (maxpool) return front_launch<3, 32, FRONT_MAXPOOL>(a, P, norm, eps, st, u8);
 #define HN_FRONT(KK, MM) \
-  if (k == KK && mid == MM) return front_launch<KK, MM, FRONT_IRF>(a, P, norm, eps, st);
+  if (k == KK && mid == MM) return front_launch<KK, MM, FRONT_IRF>(a, P, norm, eps, st, u8);
   HN_FRONT(3, 32) HN_FRONT(3, 96) HN_FRONT(3, 128) HN_FRONT(5, 32) HN_FRONT(5, 96) HN_FRONT(5, 128)
 #undef HN_FRONT
   return hipErrorInvalidValue;

@@ -1279,6 +1279,156 @@ __global__ __launch_bounds__(256) void k_head2(const float* __restrict__ a, floa
 }
 
 // ------------------------------------------------------------------------------------
+// k_head3: the same GEMM + bias + L2 fed by LDS-DMA (global_load_lds_dwordx4) into rings of
+// K-chunks, so no register holds a staged operand: A (the activations, from HBM) in a DA-deep
+// ring and B (the weights, L2 / MALL) in a DB-deep one.  128 patches per workgroup, 8 waves =
+// 4 (M: 32 patches) x 2 (N: 64 columns); at the HardNet chunk of 32,768 patches one workgroup
+// per CU.
+//   A (fp32): 128 rows x 128 B per chunk; the 16-byte piece c of row j lands at piece
+//     c ^ ((j >> 1) & 7) (the swizzle rides on the per-lane SOURCE address, the DMA image being
+//     lane-linear), so each 16-lane ds_read_b128 group of a fragment read (16 consecutive rows,
+//     one logical piece) hits 16 distinct bank slots; each wave splits its own fragments to
+//     hi / lo at read time.
+//   B: the chunk's 16 KB of pre-split fragments ([ks][4 n-tiles][hi, lo][64 lanes], the k_head2
+//     packing) copied linearly.
+// Iteration j issues B(j + DB - 1) and then A(j + DA - 1) (2 + 2 DMA instructions per wave; the
+// prologue is iterations 1 - max(DA, DB) .. -1).  vmcnt retires in issue order, so at the top of
+// iteration c the wave waits until only the instructions issued after the later of A(c) / B(c)
+// are outstanding -- B first in each iteration lets a shallow B ring keep the deeper A chunks in
+// flight -- then lgkmcnt(0) + s_barrier (every wave's chunk c landed; chunk c - 1's slots free
+// for the refills).  The DMA is inline asm (M0 set and restored in the same statement) so hipcc
+// does not track it as an LDS write.  Accumulation order = k_head2's (bit-identical results).
+// ------------------------------------------------------------------------------------
+template <int N>
+HN_DEV void head_wait_vm() {  // s_waitcnt vmcnt(N), lgkmcnt / expcnt untouched
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+template <int K, bool F16, int DA, int DB>
+__global__ __launch_bounds__(512) void k_head3(const float* __restrict__ a, float* __restrict__ out,
+                                               const uint4* __restrict__ wp,
+                                               const float* __restrict__ bias, int P, float l2eps) {
+  constexpr int KC = 32, NCH = K / KC, M = 128;
+  constexpr int ABYTES = M * KC * 4;           // 16 KB per A chunk
+  constexpr int BBYTES = 2 * 4 * 2 * 64 * 16;  // 16 KB per B chunk
+  static_assert(ABYTES == 16 * 1024 && BBYTES == 16 * 1024, "two DMA instructions per wave each");
+  static_assert(DA >= 2 && DB >= 2 && NCH >= DA && NCH >= DB && (DA + DB) * 16 <= 152, "rings");
+  typedef __attribute__((address_space(3))) void* lds_ptr_t;
+  __shared__ __attribute__((aligned(16))) char sa[DA * ABYTES];
+  __shared__ __attribute__((aligned(16))) char sbw[DB * BBYTES];
+  __shared__ float ssq[2][M];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int r = lane & 31, h = lane >> 5;
+  const int pbase = blockIdx.x * M;
+
+  // this wave's DMA instructions 2 wave + k (k = 0, 1) of each chunk; chunk c adds c * KC floats
+  // (A) / c * 1024 uint4 (B) to the source
+  const float* asrc[2];
+  const uint4* bsrc[2];
+  unsigned adst[2], bdst[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int gi = 2 * wave + k, s = gi * 64 + lane, row = s >> 3, c = (s & 7) ^ ((row >> 1) & 7);
+    asrc[k] = a + (size_t)min(pbase + row, P - 1) * K + c * 4;
+    bsrc[k] = wp + gi * 64 + lane;
+    adst[k] = (unsigned)(uintptr_t)(lds_ptr_t)(sa + gi * 1024);
+    bdst[k] = (unsigned)(uintptr_t)(lds_ptr_t)(sbw + gi * 1024);
+  }
+  auto dma = [](const void* src, unsigned dst) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
+  };
+  auto live = [](int chunk) { return chunk >= 0 && chunk < NCH; };
+  auto issue = [&](int j) {  // iteration j's DMA: B(j + DB - 1), then A(j + DA - 1)
+    const int cb = j + DB - 1, ca = j + DA - 1;
+    if (live(cb)) {
+      const unsigned so = (unsigned)(cb % DB) * BBYTES;
+      dma(bsrc[0] + (size_t)cb * 1024, bdst[0] + so);
+      dma(bsrc[1] + (size_t)cb * 1024, bdst[1] + so);
+    }
+    if (live(ca)) {
+      const unsigned so = (unsigned)(ca % DA) * ABYTES;
+      dma(asrc[0] + (size_t)ca * KC, adst[0] + so);
+      dma(asrc[1] + (size_t)ca * KC, adst[1] + so);
+    }
+  };
+  // DMA instructions issued after the later of A(c) / B(c) (this wave's own; even, <= 2 (DA + DB))
+  auto after = [&](int c) {
+    constexpr int MN = DA < DB ? DA : DB;
+    int n = 0;
+    for (int i = c - MN + 2; i < c; ++i) n += 2 * live(i + DB - 1) + 2 * live(i + DA - 1);
+    if (DB < DA) n += 2 * live(c - DB + 1 + DA - 1);  // the A half of B(c)'s iteration
+    return n;
+  };
+  const int arow = 32 * wm + r, asw = (arow >> 1) & 7;
+  f32x16 acc[2] = {f32x16{}, f32x16{}};
+  for (int j = 1 - (DA > DB ? DA : DB); j < 0; ++j) issue(j);
+#pragma unroll 1
+  for (int c = 0; c < NCH; ++c) {
+    switch (after(c)) {
+      case 0: head_wait_vm<0>(); break;
+      case 2: head_wait_vm<2>(); break;
+      case 4: head_wait_vm<4>(); break;
+      case 6: head_wait_vm<6>(); break;
+      case 8: head_wait_vm<8>(); break;
+      case 10: head_wait_vm<10>(); break;
+      case 12: head_wait_vm<12>(); break;
+      default: head_wait_vm<14>(); break;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    issue(c);
+    const char* ast = sa + (c % DA) * ABYTES + arow * (KC * 4);
+    const char* bst = sbw + (c % DB) * BBYTES;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int p0 = 4 * ks + 2 * h;
+      const float4 x0 = *reinterpret_cast<const float4*>(ast + ((p0 ^ asw) << 4));
+      const float4 x1 = *reinterpret_cast<const float4*>(ast + (((p0 + 1) ^ asw) << 4));
+      uint4 ah, al;
+      if (F16) split8_f16(x0, x1, ah, al);
+      else split8(x0, x1, ah, al);
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        const char* bp = bst + ((((ks * 4 + wn * 2 + nt) * 2) * 64 + lane) << 4);
+        const uint4 bh = *reinterpret_cast<const uint4*>(bp);
+        const uint4 bl = *reinterpret_cast<const uint4*>(bp + 1024);
+        if (F16)
+          acc[nt] = mfma3_f16(as_f16x8(ah), as_f16x8(al), as_f16x8(bh), as_f16x8(bl), acc[nt]);
+        else
+          acc[nt] = mfma3(as_bf16x8(ah), as_bf16x8(al), as_bf16x8(bh), as_bf16x8(bl), acc[nt]);
+      }
+    }
+  }
+  const float b0 = bias[wn * 64 + r], b1 = bias[wn * 64 + 32 + r];
+  float part[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    acc[0][i] += b0;
+    acc[1][i] += b1;
+    part[i] = half_sum(acc[0][i] * acc[0][i] + acc[1][i] * acc[1][i]);
+  }
+  if (r == 0) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) ssq[wn][wm * 32 + (i & 3) + 8 * (i >> 2) + 4 * h] = part[i];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int row = (i & 3) + 8 * (i >> 2) + 4 * h;
+    const int p = pbase + wm * 32 + row;
+    const float norm = sqrtf(ssq[0][wm * 32 + row] + ssq[1][wm * 32 + row] + l2eps);
+    if (p < P) {
+      out[(size_t)p * 128 + wn * 64 + r] = acc[0][i] / norm;
+      out[(size_t)p * 128 + wn * 64 + 32 + r] = acc[1][i] / norm;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
 // host launchers
 // ------------------------------------------------------------------------------------
 // stem-fused kernels carry the normalised patch (34x34 fp32) + 8 reduction floats
@@ -1580,9 +1730,21 @@ hipError_t hn_launch_conv_raw(int layer, const void* wp, const float* zero_bias,
 hipError_t hn_launch_head(const float* a, float* out, const void* wp, const float* bias, int P,
                           int K, float l2eps, hipStream_t st, bool f16) {
   const int grid = (P + 63) / 64;
-  const bool old = hn_knobs().head_v1;
+  const int form = hn_knobs().head;  // HN_HEAD: 1 k_head, 2 k_head2, 3 k_head3 (default)
   const uint4* w = static_cast<const uint4*>(wp);
-  if (K == 8192 && !f16 && old)
+#define HN_HEAD3(KK, F, DA, DB)                                                                              \
+  if (K == KK && f16 == F) {                                                                                 \
+    hipLaunchKernelGGL((k_head3<KK, F, DA, DB>), dim3((P + 127) / 128), dim3(512), 0, st, a, out, w, bias, P, \
+                       l2eps);                                                                               \
+    return hipGetLastError();                                                                                \
+  }
+  // both rings 4 deep (128 KB): same-box A/B of the HardNet head at A / B depths 4 / 4, 5 / 3, 5 / 4,
+  // 4 / 5 = 2.11, 2.29, 2.33, 2.31 ms (k_head2 2.33)
+  if (form == 3) {
+    HN_HEAD3(8192, false, 4, 4) HN_HEAD3(2048, true, 4, 4)
+  }
+#undef HN_HEAD3
+  if (K == 8192 && !f16 && form == 1)
     hipLaunchKernelGGL(k_head<8192>, dim3(grid), dim3(256), 0, st, a, out, w, bias, P, l2eps);
   else if (K == 8192 && !f16)
     hipLaunchKernelGGL((k_head2<8192, false>), dim3(grid), dim3(256), 0, st, a, out, w, bias, P, l2eps);

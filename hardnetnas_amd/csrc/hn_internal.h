@@ -11,7 +11,7 @@
 // dbg: timing-only builds with wrong results) exist only in the HN_EXPERIMENTS library.
 struct HnKnobs {
   int c12_cfg = 12;            // HN_C12_CFG: k_c12 configuration (0..12, all exact)
-  bool head_v1 = false;        // HN_HEAD_V1: the first HardNet head GEMM
+  int head = 3;                // HN_HEAD: head GEMM form (1 k_head, 2 k_head2, 3 k_head3 LDS-DMA rings)
   bool fdl_valu = false;       // HN_FDL_VALU: FDLNet front as fp32 VALU
   bool naive_pw = false;       // HN_NAIVE_PW: untiled 1x1 conv kernel
   bool naive_dw = false;       // HN_NAIVE_DW: untiled depthwise kernel
@@ -120,8 +120,10 @@ struct HnFrontArgs {
   const uint4* pwl_a16; // pwl A operand for 16x16x32: [MID/32][out tile 2][plane 2][lane 64] x 8 fp16
 };
 bool hn_front_supported(int k, int mid);
+// u8: uint8 patches preprocessed in the front's patch load (the production forms without
+// input_norm, HN_FRONT_FOLD off; hn_api.hip u8_fused)
 hipError_t hn_launch_front(const HnFrontArgs& a, int P, int k, int mid, bool maxpool, bool norm,
-                           float eps, hipStream_t st);
+                           float eps, hipStream_t st, const HnU8In* u8 = nullptr);
 // FDLNet HardNetNeiMask front (32x32 patch -> 8x8x64), hn_fdl.hip; mode 0 = NASNet, 1 = NASNet_0.1
 struct HnFdlFrontArgs {
   const float* in;

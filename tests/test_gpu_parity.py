@@ -378,6 +378,25 @@ def test_every_candidate_op_at_every_layer_fused_irf(op, pairs, cuda_device, mon
     assert np.abs(y - ref).max() <= NAS_TOL
 
 
+@pytest.mark.parametrize("name", ["hardnet", "wang2", "fdl_NASNet"])
+def test_head_forms_are_bit_identical(name, cuda_device, monkeypatch):
+    """k_head3 (LDS-DMA ring, 128-patch workgroups) accumulates the K-chunks in the same order as
+    k_head2 (HN_HEAD=2): bit-identical descriptors for the HardNet (bf16x3, K = 8192) and the NAS /
+    FDL (fp16x3, K = 2048) heads, at a ragged batch whose last workgroup is partial."""
+    from hardnetnas_amd._native import NativeModel
+    m, fx, _ = build_module(name)
+    x = torch.from_numpy(golden_inputs(fx)).to(cuda_device)
+    xr = torch.from_numpy(np.concatenate([golden_inputs(fx)] * 40)[:301]).to(cuda_device)
+    nm = NativeModel.from_module(m, cuda_device)
+    y, yr = nm(x), nm(xr)
+    for form in ("2", "1"):  # k_head2; k_head (no LDS staging)
+        monkeypatch.setenv("HN_HEAD", form)
+        nm2 = NativeModel.from_module(m, cuda_device)
+        assert torch.equal(y, nm2(x)), form
+        assert torch.equal(yr, nm2(xr)), form
+    assert np.abs(y.cpu().numpy() - fx["y"]).max() <= _tol(name)
+
+
 @pytest.mark.parametrize("name", ["wang2", "wang4"])
 def test_two_block_kernel_is_bit_identical(name, cuda_device, monkeypatch):
     """k_irf2 (layers 1+2 / 3+4 in one kernel, the activation between them in LDS) computes exactly

@@ -140,13 +140,14 @@ def _u8_batch(n, seed, hw=64):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["hardnet", "wang2"])
+@pytest.mark.parametrize("name", ["hardnet", "wang2", "wang3", "wang4", "fdl_NASNet"])
 @pytest.mark.parametrize("resize,normalize", [("pil", False), ("pil", True), ("cv2", True), ("none", True)])
 @pytest.mark.parametrize("n", [1, 37, 3001])
 def test_forward_u8_equals_preprocess_then_forward(name, resize, normalize, n, cuda_device):
     """hn_forward_u8 == hn_preprocess followed by hn_forward, bit for bit (HardNet: fused into
-    k_c12's patch load; NAS: preprocessed into the workspace); 3,001 patches run every
-    persistent k_c12 workgroup over several patches and end on a ragged one."""
+    k_c12's patch load; NAS: fused into k_front's in NONE / CV2 mode -- wang2 the k3 no-fold form,
+    wang3 k5, wang4 the maxpool form; FDLNet and NAS PIL: preprocessed into the workspace); 3,001 patches run every
+    persistent workgroup over several patches and end on a ragged one."""
     m, _, _ = build_module(name)
     nm = N.NativeModel.from_module(m, cuda_device)
     hw = 32 if resize == "none" else 64
@@ -155,8 +156,22 @@ def test_forward_u8_equals_preprocess_then_forward(name, resize, normalize, n, c
     nm.set_profiling(True)
     got = nm.forward_u8(u, resize=resize, normalize=normalize)
     st = nm.stage_times()
-    assert ("preprocess" in st) == (name != "hardnet")
+    assert ("preprocess" in st) == (name.startswith("fdl") or (name != "hardnet" and resize == "pil"))
     assert torch.equal(got, ref)
+
+
+@pytest.mark.gpu
+def test_forward_u8_nas_fold_form_preprocesses_apart(cuda_device, monkeypatch):
+    """HN_FRONT_FOLD (the round-2 front, no uint8 load) takes the hn_preprocess path, same result."""
+    m, _, _ = build_module("wang2")
+    u = torch.from_numpy(_u8_batch(37, 5, 64)).to(cuda_device)
+    ref = N.NativeModel.from_module(m, cuda_device).forward_u8(u, resize="cv2")
+    monkeypatch.setenv("HN_FRONT_FOLD", "1")
+    nm = N.NativeModel.from_module(m, cuda_device)
+    nm.set_profiling(True)
+    got = nm.forward_u8(u, resize="cv2")
+    assert "preprocess" in nm.stage_times()
+    assert (got - ref).abs().max().item() <= 2e-5
 
 
 @pytest.mark.gpu
