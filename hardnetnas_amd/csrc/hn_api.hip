@@ -1144,12 +1144,14 @@ extern "C" int hn_hardnet_train_backward(const float* d_dout, int64_t batch, con
 // ---------------------------------------------------------------------------------------
 static int nas_train_desc_ok(const hn_arch_desc* d) {
   if (!d) return fail(HN_ERR_ARG, "NULL desc");
-  if (d->kind != HN_KIND_NAS && d->kind != HN_KIND_NAS_SUPERNET)
-    return fail(HN_ERR_ARG, "train mode: desc kind must be HN_KIND_NAS or HN_KIND_NAS_SUPERNET");
+  const bool fdl = d->kind == HN_KIND_FDL_NASNET || d->kind == HN_KIND_FDL_NASNET01;
+  if (d->kind != HN_KIND_NAS && d->kind != HN_KIND_NAS_SUPERNET && !fdl)
+    return fail(HN_ERR_ARG, "train mode: desc kind must be HN_KIND_NAS, HN_KIND_NAS_SUPERNET or an FDL kind");
   if (d->n_layers < 1 || d->n_layers > HN_MAX_LAYERS) return fail(HN_ERR_ARG, "bad n_layers");
-  int hw = 32, c = 32;
+  if (fdl && !(d->input_norm_eps >= 0.f)) return fail(HN_ERR_ARG, "FDL: input_norm_eps must be >= 0");
+  int hw = fdl ? 8 : 32, c = fdl ? 64 : 32;  // the FDL fronts leave 64 channels at 8x8
   for (int i = 0; i < d->n_layers; ++i) {
-    if (d->kind == HN_KIND_NAS && (d->op[i] < 0 || d->op[i] >= 17)) return fail(HN_ERR_ARG, "bad op index");
+    if (d->kind != HN_KIND_NAS_SUPERNET && (d->op[i] < 0 || d->op[i] >= 17)) return fail(HN_ERR_ARG, "bad op index");
     if (d->c_in[i] != c || (d->stride[i] != 1 && d->stride[i] != 2) || hw % d->stride[i])
       return fail(HN_ERR_ARG, "layer " + std::to_string(i) + ": channels / stride do not chain");
     if (d->c_out[i] < 1 || d->c_out[i] > 128 || d->c_in[i] % 4 || d->c_out[i] % 4)
@@ -1157,7 +1159,7 @@ static int nas_train_desc_ok(const hn_arch_desc* d) {
     c = d->c_out[i];
     hw /= d->stride[i];
   }
-  if (hw != 4) return fail(HN_ERR_ARG, "the layers must reduce 32x32 to the 4x4 head input");
+  if (hw != 4) return fail(HN_ERR_ARG, "the layers must reduce the front's output to the 4x4 head input");
   return HN_OK;
 }
 

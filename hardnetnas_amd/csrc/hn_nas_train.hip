@@ -282,6 +282,25 @@ __global__ __launch_bounds__(256) void k_maxpool_bwd(const float* __restrict__ d
   }
 }
 
+// the stride-2 1x1 convs of the FDLNet fronts read every other pixel: y [R][H/2][H/2] = x[R][2i][2j]
+// (CNHW rows R = C x B); the backward scatters back with zeros in between
+__global__ __launch_bounds__(256) void k_sub2(const float* __restrict__ x, long R, int H, float* __restrict__ y) {
+  const int HO = H / 2;
+  const long total = R * HO * HO;
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
+    const int ox = (int)(e % HO), oy = (int)((e / HO) % HO);
+    y[e] = x[(e / ((long)HO * HO)) * H * H + 2 * oy * H + 2 * ox];
+  }
+}
+__global__ __launch_bounds__(256) void k_unsub2(const float* __restrict__ dy, long R, int H, float* __restrict__ dx) {
+  const int HO = H / 2;
+  const long total = R * H * H;
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
+    const int ix = (int)(e % H), iy = (int)((e / H) % H);
+    dx[e] = ((ix | iy) & 1) ? 0.f : dy[(e / ((long)H * H)) * HO * HO + (iy / 2) * HO + ix / 2];
+  }
+}
+
 // y = (acc ? y : 0) + c x, c = coef ? *coef : 1
 __global__ __launch_bounds__(256) void k_axpy(long n, const float* __restrict__ coef, const float* __restrict__ x,
                                               float* __restrict__ y, int acc) {
@@ -431,9 +450,15 @@ struct LayerPlan {
 struct Plan {
   long B = 0;
   bool super = false;
+  int fdl = 0;  // FDLNet HardNetNeiMask front: 1 NASNet, 2 NASNet_0.1 (0: the NAS stem)
+  float in_eps = 0.f;
   int nt = 0;  // tensors consumed
   int stem_w = -1, stem_bn = -1, head_w = -1, head_rm = -1;
-  size_t x0z = 0, x0r = 0, x0a = 0;    // stem
+  size_t x0z = 0, x0r = 0, x0a = 0;    // stem (FDL: conv0 output + bias; NASNet: its BN's z, in place)
+  // FDL front: input_norm; NASNet: BN(affine=False) -> 1x1 s2 32->32 BN ReLU -> 1x1 s2 32->64 BN ReLU;
+  // NASNet_0.1: MaxPool(3, 2, 1) -> 1x1 s2 32->64 BN ReLU (FDLIdentity)
+  int stem_b = -1, f_bn0 = -1, f_w1 = -1, f_bn1 = -1, f_w2 = -1, f_bn2 = -1;
+  size_t xn = 0, xsd = 0, f_xs1 = 0, f_z1 = 0, f_r1 = 0, f_a1 = 0, f_mp = 0, f_xs2 = 0, f_z2 = 0, f_r2 = 0, f_a2 = 0;
   size_t hz = 0, hr = 0;               // head
   std::vector<LayerPlan> layers;
   size_t saved = 0;
@@ -461,13 +486,48 @@ Plan make_plan(const hn_arch_desc& d, long B) {
   auto wg = [&](long M, long N, long K) { part = std::max(part, (size_t)(M * N * gemm_slices(M, N, K))); };
   int nt = 0;
   auto bn = [&]() { const int t = nt; nt += 4; return t; };
-  // stem ConvBNRelu(1 -> 32, 3x3): conv.weight, bn.{weight, bias, running_mean, running_var}
-  P.stem_w = nt++;
-  P.stem_bn = bn();
-  P.x0z = take(act(32, 32));
-  P.x0r = take(32 * sizeof(float));
-  P.x0a = take(act(32, 32));
+  P.fdl = d.kind == HN_KIND_FDL_NASNET ? 1 : d.kind == HN_KIND_FDL_NASNET01 ? 2 : 0;
   int hw = 32;
+  if (P.fdl) {
+    // FDLNet fronts (des.py), in state_dict order: features.0.{weight, bias}, then
+    //   NASNet    : features.1.{running_mean, running_var}, .2.weight, .3.{w, b, rm, rv}, .5.weight, .6.{...}
+    //   NASNet_0.1: features.3.conv.conv.weight, features.3.conv.bn.{...}
+    P.in_eps = d.input_norm_eps;
+    P.xn = take((size_t)B * 1024 * sizeof(float));
+    P.xsd = take((size_t)B * sizeof(float));
+    P.stem_w = nt++;
+    P.stem_b = nt++;
+    P.x0z = take(act(32, 32));
+    if (P.fdl == 1) {
+      P.f_bn0 = nt;
+      nt += 2;
+      P.x0r = take(32 * sizeof(float));
+      P.f_xs1 = take(act(32, 16));
+      P.f_w1 = nt++;
+      P.f_bn1 = bn();
+      P.f_z1 = take(act(32, 16));
+      P.f_r1 = take(32 * sizeof(float));
+      P.f_a1 = take(act(32, 16));
+      wg(32, 32, B * 256);
+    } else {
+      P.f_mp = take(act(32, 16));
+    }
+    P.f_xs2 = take(act(32, 8));
+    P.f_w2 = nt++;
+    P.f_bn2 = bn();
+    P.f_z2 = take(act(64, 8));
+    P.f_r2 = take(64 * sizeof(float));
+    P.f_a2 = take(act(64, 8));
+    wg(64, 32, B * 64);
+    hw = 8;
+  } else {
+    // stem ConvBNRelu(1 -> 32, 3x3): conv.weight, bn.{weight, bias, running_mean, running_var}
+    P.stem_w = nt++;
+    P.stem_bn = bn();
+    P.x0z = take(act(32, 32));
+    P.x0r = take(32 * sizeof(float));
+    P.x0a = take(act(32, 32));
+  }
   for (int i = 0; i < d.n_layers; ++i) {
     LayerPlan L;
     L.cin = d.c_in[i];
@@ -807,13 +867,49 @@ hipError_t op_bwd(const Ctx& c, const OpPlan& o, const float* x, float* dO, floa
 // ------------------------------------------------------------------------------------------
 // whole network
 // ------------------------------------------------------------------------------------------
+// FDLNet front (des.py:8-55 / NASNet_0.1 des.py:10-55) -> the first block's input [64][B][8][8]
+hipError_t fdl_front_fwd(Ctx& c, Plan& P, const float* in) {
+  const long B = P.B;
+  // input_norm (des.py:40-47, mean / std detached), conv0 3x3 (k_fwd0) + its bias
+  hipLaunchKernelGGL(k_input_norm, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, c.st, in, B, P.in_eps, c.f(P.xn),
+                     c.f(P.xsd));
+  hipLaunchKernelGGL(k_fwd0, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, c.st, c.f(P.xn), c.T[P.stem_w], B,
+                     c.f(P.x0z));
+  hipLaunchKernelGGL(k_bias_act, dim3(grid_of(32 * B * 1024)), dim3(256), 0, c.st, c.f(P.x0z), 32, B * 1024,
+                     c.T[P.stem_b], 0);
+  HCK(hipGetLastError());
+  const float* s2in;  // the input of the stride-2 1x1 conv to 64 channels, [32][B][16][16]
+  if (P.fdl == 1) {
+    // BatchNorm2d(32, affine=False), no ReLU: z in place is the next input
+    HCK(bn_fwd(c, c.f(P.x0z), 32, B * 1024, P.f_bn0, false, false, nullptr, nullptr, c.f(P.x0r)));
+    hipLaunchKernelGGL(k_sub2, dim3(grid_of(32 * B * 256)), dim3(256), 0, c.st, c.f(P.x0z), 32 * B, 32, c.f(P.f_xs1));
+    HCK(pw_fwd(c, c.T[P.f_w1], 32, 32, 1, c.f(P.f_xs1), B * 256, c.f(P.f_z1)));
+    HCK(bn_fwd(c, c.f(P.f_z1), 32, B * 256, P.f_bn1, true, true, nullptr, c.f(P.f_a1), c.f(P.f_r1)));
+    s2in = c.f(P.f_a1);
+  } else {
+    hipLaunchKernelGGL(k_maxpool_fwd, dim3(grid_of(32 * B * 256)), dim3(256), 0, c.st, c.f(P.x0z), 32 * B, 32,
+                       c.f(P.f_mp));
+    s2in = c.f(P.f_mp);  // FDLIdentity(32, 32, 1): nothing
+  }
+  hipLaunchKernelGGL(k_sub2, dim3(grid_of(32 * B * 64)), dim3(256), 0, c.st, s2in, 32 * B, 16, c.f(P.f_xs2));
+  HCK(pw_fwd(c, c.T[P.f_w2], 64, 32, 1, c.f(P.f_xs2), B * 64, c.f(P.f_z2)));
+  return bn_fwd(c, c.f(P.f_z2), 64, B * 64, P.f_bn2, true, true, nullptr, c.f(P.f_a2), c.f(P.f_r2));
+}
+
+// the input of the first searched layer
+const float* first_input(const Ctx& c, const Plan& P) { return P.fdl ? c.f(P.f_a2) : c.f(P.x0a); }
+
 hipError_t nas_fwd(Ctx& c, Plan& P, const float* in, const float* soft, float* out) {
   const long B = P.B;
-  // stem: conv (k_fwd0 on the raw 32x32 patches, taps as the MFMA's K) -> BN -> ReLU
-  hipLaunchKernelGGL(k_fwd0, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, c.st, in, c.T[P.stem_w], B, c.f(P.x0z));
-  HCK(hipGetLastError());
-  HCK(bn_fwd(c, c.f(P.x0z), 32, B * 1024, P.stem_bn, true, true, nullptr, c.f(P.x0a), c.f(P.x0r)));
-  const float* x = c.f(P.x0a);
+  if (P.fdl) {
+    HCK(fdl_front_fwd(c, P, in));
+  } else {
+    // stem: conv (k_fwd0 on the raw 32x32 patches, taps as the MFMA's K) -> BN -> ReLU
+    hipLaunchKernelGGL(k_fwd0, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, c.st, in, c.T[P.stem_w], B, c.f(P.x0z));
+    HCK(hipGetLastError());
+    HCK(bn_fwd(c, c.f(P.x0z), 32, B * 1024, P.stem_bn, true, true, nullptr, c.f(P.x0a), c.f(P.x0r)));
+  }
+  const float* x = first_input(c, P);
   for (size_t i = 0; i < P.layers.size(); ++i) {
     LayerPlan& L = P.layers[i];
     if (!P.super) {
@@ -851,7 +947,7 @@ hipError_t nas_bwd(Ctx& c, Plan& P, const float* in, const float* soft, const fl
   const long K = (long)cl * 16;
   const float* xl = P.super ? c.f(P.layers.back().sum) : nullptr;
   if (!P.super) {  // the sampled net's last layer output: its op's out (or its input, for an identity)
-    const float* x = c.f(P.x0a);
+    const float* x = first_input(c, P);
     for (size_t i = 0; i + 1 < P.layers.size(); ++i) {
       const OpPlan& o = P.layers[i].ops[0];
       x = o.out_is_input ? x : c.f(o.out);
@@ -868,7 +964,7 @@ hipError_t nas_bwd(Ctx& c, Plan& P, const float* in, const float* soft, const fl
   // layer inputs, front to back
   std::vector<const float*> xin(P.layers.size());
   {
-    const float* x = c.f(P.x0a);
+    const float* x = first_input(c, P);
     for (size_t i = 0; i < P.layers.size(); ++i) {
       xin[i] = x;
       if (P.super) x = c.f(P.layers[i].sum);
@@ -897,10 +993,35 @@ hipError_t nas_bwd(Ctx& c, Plan& P, const float* in, const float* soft, const fl
     }
     std::swap(g, gx);
   }
-  // stem: ReLU o BN -> conv weight gradient (k_wgrad0; the input gradient is not formed)
-  HCK(bn_bwd(c, g, c.f(P.x0z), c.f(P.x0r), 32, B * 1024, P.stem_bn, true, true, gx));
+  const float* x0 = in;  // conv0's input
+  if (P.fdl) {
+    // g = d front output [64][B][8][8]: ReLU o BN -> 1x1 s2 conv (weight grad; data grad scattered)
+    float* t1 = c.s(P.t1);
+    float* t2 = c.s(P.t2);
+    HCK(bn_bwd(c, g, c.f(P.f_z2), c.f(P.f_r2), 64, B * 64, P.f_bn2, true, true, t1));
+    HCK(pw_wgrad(c, t1, c.f(P.f_xs2), 64, 32, 1, B * 64, c.G[P.f_w2]));
+    HCK(pw_dgrad(c, c.T[P.f_w2], t1, 64, 32, 1, B * 64, t2, false));
+    hipLaunchKernelGGL(k_unsub2, dim3(grid_of(32 * B * 256)), dim3(256), 0, c.st, t2, 32 * B, 16, t1);  // [32][B][256]
+    if (P.fdl == 1) {
+      HCK(bn_bwd(c, t1, c.f(P.f_z1), c.f(P.f_r1), 32, B * 256, P.f_bn1, true, true, t2));
+      HCK(pw_wgrad(c, t2, c.f(P.f_xs1), 32, 32, 1, B * 256, c.G[P.f_w1]));
+      HCK(pw_dgrad(c, c.T[P.f_w1], t2, 32, 32, 1, B * 256, t1, false));
+      hipLaunchKernelGGL(k_unsub2, dim3(grid_of(32 * B * 1024)), dim3(256), 0, c.st, t1, 32 * B, 32, g);
+      HCK(bn_bwd(c, g, c.f(P.x0z), c.f(P.x0r), 32, B * 1024, P.f_bn0, false, false, gx));  // BN(affine=False)
+    } else {
+      HCK(hipMemsetAsync(gx, 0, (size_t)32 * B * 1024 * sizeof(float), c.st));
+      hipLaunchKernelGGL(k_maxpool_bwd, dim3(grid_of(32 * B * 1024)), dim3(256), 0, c.st, t1, c.f(P.x0z), 32 * B, 32,
+                         gx);
+    }
+    hipLaunchKernelGGL(k_rowsum, dim3(32), dim3(256), 0, c.st, gx, B * 1024, c.G[P.stem_b]);  // conv0 bias
+    HCK(hipGetLastError());
+    x0 = c.f(P.xn);
+  } else {
+    // stem: ReLU o BN -> conv weight gradient (k_wgrad0; the input gradient is not formed)
+    HCK(bn_bwd(c, g, c.f(P.x0z), c.f(P.x0r), 32, B * 1024, P.stem_bn, true, true, gx));
+  }
   const long ns = wgrad0_slices(B);
-  hipLaunchKernelGGL(k_wgrad0, dim3((unsigned)(ns / 4)), dim3(256), 0, c.st, in, gx, B, c.s(P.part));
+  hipLaunchKernelGGL(k_wgrad0, dim3((unsigned)(ns / 4)), dim3(256), 0, c.st, x0, gx, B, c.s(P.part));
   HCK(hipGetLastError());
   GemmArgs gs{nullptr, nullptr, c.G[P.stem_w], 32, 9, 0, 0, 0, 0, 0, 9, 1, 1.f, 0.f};
   hipLaunchKernelGGL(k_splitk_sum, dim3((unsigned)((32 * 9 + 63) / 64)), dim3(1024), 0, c.st, gs, (int)ns,

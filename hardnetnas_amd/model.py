@@ -370,6 +370,8 @@ class HardNetNeiMask(_NativeMixin, nn.Module):
         y = self._dispatch_native(input)
         if y is not None:
             return y
+        if _nas_train_native_eligible(self, input, A.FDL_LAYERS, A.FDL_LAYERS):
+            return _nas_train_native_forward(self, input, None)
         x_features = self.features(self.input_norm(input))
         x = x_features.view(x_features.size(0), -1)
         return x / torch.norm(x, p=2, dim=-1, keepdim=True)
@@ -432,15 +434,16 @@ class HardNetNAS(_NativeMixin, nn.Module):
         return self.load_state_dict(out, strict=strict)
 
 
-def _nas_train_native_eligible(module: nn.Module, x: torch.Tensor, layers) -> bool:
-    """model.train() of HardNetNAS / HardNetNASSupernet on a HIP fp32 [B>=2,1,32,32] batch that
-    needs no input gradient, with the reference's BatchNorm setup (one momentum, running statistics
-    tracked, eps 1e-5) and every parameter / buffer fp32 contiguous on x's device, runs
-    hn_nas_train_* (SURVEY 8(f) row 4).  Anything else runs the module's torch layers."""
+def _nas_train_native_eligible(module: nn.Module, x: torch.Tensor, layers, expect=A.SEARCH_SPACE2) -> bool:
+    """model.train() of HardNetNAS / HardNetNASSupernet / HardNetNeiMask on a HIP fp32
+    [B>=2,1,32,32] batch that needs no input gradient, with the reference's BatchNorm setup (one
+    momentum, running statistics tracked, eps 1e-5) and every parameter / buffer fp32 contiguous on
+    x's device, runs hn_nas_train_* (SURVEY 8(f) row 4).  Anything else runs the module's torch
+    layers."""
     if not (getattr(module, "native_train", True) and module.training and x.is_cuda
             and x.dtype == torch.float32 and x.dim() == 4 and tuple(x.shape[1:]) == (1, 32, 32)
             and x.shape[0] >= 2 and not (torch.is_grad_enabled() and x.requires_grad)
-            and list(layers) == list(A.SEARCH_SPACE2)):
+            and list(layers) == list(expect)):
         return False
     bns = [m for m in module.modules() if isinstance(m, nn.BatchNorm2d)]
     if not all(b.momentum is not None and b.track_running_stats and b.eps == 1e-5
@@ -453,7 +456,7 @@ def _nas_train_native_eligible(module: nn.Module, x: torch.Tensor, layers) -> bo
 def _nas_train_native_forward(module: nn.Module, x: torch.Tensor, soft):
     from . import _native as N
     bns = [m for m in module.modules() if isinstance(m, nn.BatchNorm2d)]
-    desc = N.supernet_desc() if soft is not None else N.nas_desc(module.arch_ops, module.layers)
+    desc = N.supernet_desc() if soft is not None else N.desc_for_module(module)
     _, tensors = N.train_tensors(module)
     params = [t for t in tensors if t.requires_grad]
     y = N.NasTrainFunction.apply(x.contiguous(), soft, desc, tensors, bns[0].momentum, *params)

@@ -201,9 +201,14 @@ int hn_hardnet_train_backward(const float* d_dout, int64_t batch, const float* c
  *                                    CANDIDATE_BLOCKS (MixedOperation.forward, model_supernet.py:23-36);
  *                                    d_soft = the soft weights m [n_layers][17] (the caller's
  *                                    Gumbel-softmax draw, :24), d_dsoft receives d loss / d m.
- * forward : stem ConvBNRelu -> 6 layers -> 4x4 head conv -> BatchNorm2d(affine=False) -> y / ||y||,
+ *   desc->kind HN_KIND_FDL_NASNET / _FDL_NASNET01  FDLNet HardNetNeiMask (des.py:8-55 / NASNet_0.1
+ *                                    des.py:10-55): input_norm (desc->input_norm_eps), conv0 3x3 + bias,
+ *                                    then BN(affine=False) -> 1x1 s2 BN ReLU -> 1x1 s2 BN ReLU (NASNet) or
+ *                                    MaxPool(3,2,1) -> 1x1 s2 BN ReLU (NASNet_0.1), then the layers at 8x8.
+ * forward : front -> the layers -> 4x4 head conv -> BatchNorm2d(affine=False) -> y / ||y||,
  *           every BatchNorm with the batch's statistics (running stats updated with `momentum`,
- *           unbiased variance).  d_in [B,1,32,32] fp32 (no input_norm; the NAS loaders normalise).
+ *           unbiased variance).  d_in [B,1,32,32] fp32 (NAS: no input_norm, the NAS loaders normalise;
+ *           FDL: input_norm in the forward).
  * backward: d_dout [B,128] -> d_grads (every conv weight, BN weight / bias and SE weight / bias,
  *           overwritten); no input gradient.
  * d_tensors: host array of hn_nas_train_tensor_count() device pointers, one per float tensor of the

@@ -167,6 +167,19 @@ def nas_train_start(name: str):
     return m, fx, a, p
 
 
+def fdl_train_start(variant: str):
+    """(HardNetNeiMask in train mode at the FDL train fixture's starting point: the golden synthetic
+    weights + calibrated running statistics of fdl_<variant>.npz, BN momentum 0.1; fixture; anchors;
+    positives)."""
+    tag = variant.replace(".", "")
+    fx = load("train_fdl")
+    meta = fx["meta"][tag]
+    m, _, _ = build_module("fdl_" + tag)
+    m.train()
+    a, p = train_pairs(meta["n_pairs"], meta["seed_a"], meta["seed_n"])
+    return m, fx, a, p
+
+
 def supernet_start():
     """(HardNetNASSupernet in train mode with the fixture's synthetic weights, fresh BatchNorm
     buffers and latencies; fixture; X; Y)."""

@@ -1,7 +1,8 @@
 """Train-mode fixtures from the REFERENCE code (survey container only).
 
 Run from the repo root:  python tests/golden/make_train_golden.py
-Writes tests/golden/train_hardnet.npz (data only; the reference is executed, never copied).
+Writes tests/golden/train_hardnet.npz, train_nas.npz and train_fdl.npz (data only; the reference is
+executed, never copied).
 
 One step of the reference training loop, in its own shape (hardnet/HardNet.py:379-423):
 
@@ -337,6 +338,91 @@ def make_train_supernet(out):
                       "training_functions_supernet.py:88-103 (imported, torch %s CPU)" % torch.__version__}
 
 
+def _fdl_ref(variant):
+    """FDLNet HardNetNeiMask (latency/<variant>/model/des.py), imported with its package root on
+    sys.path, as tests/golden/make_golden.py::make_fdl does."""
+    for k in [k for k in sys.modules if k.split(".")[0] in ("model", "utils")]:
+        del sys.modules[k]
+    sys.path.insert(0, os.path.join(G.REF, "FDLNet-master", "latency", variant))
+    try:
+        from model.des import HardNetNeiMask as RefNet
+    finally:
+        sys.path.pop(0)
+    return RefNet
+
+
+def make_train_fdl(out, variant):
+    """One train step of FDLNet's HardNetNeiMask in the loop shape the other fixtures use (two
+    train() calls, the hardnetNAS loss_HardNet, backward; FDLNet's own neighbour-mask loss is out of
+    scope), at the golden synthetic weights + calibrated running statistics of
+    fdl_<variant>.npz, BN momentum 0.1."""
+    from hardnetnas_amd.model import HardNetNeiMask
+    _, _, _, NL = _nas_ref()
+    RefNet = _fdl_ref(variant)
+    tag = variant.replace(".", "")
+    fx = np.load(os.path.join(HERE, f"fdl_{tag}.npz"), allow_pickle=False)
+    tmpl = {k: tuple(v.shape) for k, v in HardNetNeiMask(variant=variant).state_dict().items()}
+    w = synth.synth_state_dict(tmpl, G.WEIGHT_SEED)
+    a, p = F.train_pairs(NAS_PAIRS, SEED_A + 20, SEED_N + 20)
+    res = {}
+    for dt, dtype in (("32", torch.float32), ("64", torch.float64)):
+        torch.manual_seed(0)
+        model = RefNet(1.0, 1.0)
+        sd = model.state_dict()
+        assert tmpl == {k: tuple(v.shape) for k, v in sd.items()}, "state_dict layout differs"
+        for k, v in w.items():
+            sd[k] = torch.from_numpy(fx["bn/" + k] if "running" in k else v)
+        model.load_state_dict(sd)
+        model = model.to(dtype).train()
+        oa = model(torch.from_numpy(a).to(dtype))
+        op_ = model(torch.from_numpy(p).to(dtype))
+        loss = NL.loss_HardNet(oa, op_)
+        loss.backward()
+        msd = model.state_dict(keep_vars=True)
+        r = {"out_a": oa.detach().numpy(), "out_p": op_.detach().numpy(), "loss": np.float64(loss.item()),
+             "stats": {}, "grads": {}}
+        for k in tmpl:
+            t = msd[k]
+            if "running" in k:
+                r["stats"][k] = t.detach().numpy()
+            elif not k.endswith("num_batches_tracked"):
+                r["grads"][k] = t.grad.numpy()
+        res[dt] = r
+    pre = f"fdl_{tag}/"
+    for dt in ("32", "64"):
+        r = res[dt]
+        cast = (lambda v: v.astype(np.float32)) if dt == "32" else (lambda v: v)
+        out[f"{pre}out_a_{dt}"], out[f"{pre}out_p_{dt}"] = cast(r["out_a"]), cast(r["out_p"])
+        out[f"{pre}loss_{dt}"] = r["loss"]
+        for k, v in r["stats"].items():
+            out[f"{pre}stat/{k}_{dt}"] = cast(v)
+    fp32_err = {}
+    gmax = max(np.linalg.norm(v) for v in res["64"]["grads"].values())
+    for k, g64 in res["64"]["grads"].items():
+        for kk, v in F.summary(g64, F.name_seed(k)).items():
+            out[f"{pre}g/{k}_{kk}"] = v
+        g32 = res["32"]["grads"][k].astype(np.float64)
+        n = np.linalg.norm(g64)
+        fp32_err[k] = float(np.linalg.norm(g32 - g64) / n) if n > 1e-9 * gmax else 0.0
+    out[f"{pre}grad_names"] = np.array(sorted(fp32_err))
+    out[f"{pre}fp32_err"] = np.array([fp32_err[k] for k in sorted(fp32_err)])
+    print("fdl", variant, "loss", res["32"]["loss"], res["64"]["loss"], "worst fp32 grad err",
+          max(fp32_err.values()))
+    return {"variant": variant, "n_pairs": NAS_PAIRS, "seed_a": SEED_A + 20, "seed_n": SEED_N + 20,
+            "momentum": 0.1, "fp32_grad_l2rel_vs_fp64": fp32_err,
+            "source": "FDLNet-master/latency/%s/model/des.py HardNetNeiMask + hardnetNAS "
+                      "general_functions/Losses.py:27-51 (imported, torch %s CPU)" % (variant, torch.__version__)}
+
+
+def make_train_fdl_all():
+    torch.Tensor.cuda = lambda self, *a, **k: self  # the loss's eye().cuda(): CPU fixture generation
+    out, meta = {}, {}
+    for v in G.A.FDL_VARIANTS:
+        meta[v.replace(".", "")] = make_train_fdl(out, v)
+    out["meta"] = json.dumps(meta)
+    np.savez_compressed(os.path.join(HERE, "train_fdl.npz"), **out)
+
+
 def make_train_nas_all():
     torch.Tensor.cuda = lambda self, *a, **k: self  # the losses' eye().cuda(): CPU fixture generation
     out, meta = {}, {}
@@ -355,3 +441,5 @@ if __name__ == "__main__":
         make_train_hardnet()
     if len(sys.argv) < 2 or sys.argv[1] == "nas":
         make_train_nas_all()
+    if len(sys.argv) < 2 or sys.argv[1] == "fdl":
+        make_train_fdl_all()

@@ -194,3 +194,27 @@ def test_cpu_and_train_calls_use_the_torch_layers():
     y = m(torch.randn(4, 1, 32, 32))
     y.sum().backward()
     assert getattr(m, "_hn_handle", None) is None
+
+
+@pytest.mark.parametrize("kind", ["wang2", "cov_b", "supernet", "fdl_NASNet", "fdl_NASNet_01"])
+def test_train_tensor_count_matches_module(kind):
+    """hn_nas_train_tensor_count walks the same float tensors, in the same order, as the module's
+    state_dict minus num_batches_tracked / thetas (_native.train_tensors): NAS, supernet, FDLNet."""
+    from hardnetnas_amd.model import HardNetNASSupernet
+    if kind == "supernet":
+        m, d = HardNetNASSupernet(), N.supernet_desc()
+    else:
+        m, _, _ = build_module(kind)
+        d = N.desc_for_module(m)
+    n = ctypes.c_size_t()
+    assert N.load_library().hn_nas_train_tensor_count(ctypes.byref(d), ctypes.byref(n)) == 0, \
+        N.load_library().hn_last_error()
+    assert n.value == len(N.train_tensors(m)[1])
+
+
+def test_train_rejects_fdl_without_input_norm():
+    d = N.fdl_desc("NASNet")
+    d.input_norm_eps = -1.0
+    n = ctypes.c_size_t()
+    assert N.load_library().hn_nas_train_tensor_count(ctypes.byref(d), ctypes.byref(n)) == 1
+    assert b"input_norm" in N.load_library().hn_last_error()

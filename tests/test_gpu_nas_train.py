@@ -113,3 +113,37 @@ def test_nas_train_matches_torch_layers_on_gpu(cuda_device):
         n = g.norm().item()
         if n > 1e-6:
             assert (res[True][1][k] - g).norm().item() / n <= 2e-2, k
+
+
+@pytest.mark.parametrize("variant", ["NASNet", "NASNet_0.1"])
+def test_fdl_train_step_matches_reference(variant, cuda_device):
+    """FDLNet HardNetNeiMask.train() on hn_nas_train_* (input_norm, conv0 + bias, the NASNet front's
+    BN(affine=False) and stride-2 1x1 convs or the NASNet_0.1 max-pool front, three IRF blocks, the
+    4x4 head) against the reference FDLNet module's step (tests/golden/train_fdl.npz)."""
+    from fixtures import fdl_train_start
+    from hardnetnas_amd.losses import loss_HardNet
+    m, fx, a, p = fdl_train_start(variant)
+    m = m.to(cuda_device)
+    oa = m(torch.from_numpy(a).to(cuda_device))
+    op_ = m(torch.from_numpy(p).to(cuda_device))
+    assert "NasTrainFunction" in type(oa.grad_fn).__name__
+    loss = loss_HardNet(oa, op_, anchor_swap=True)
+    loss.backward()
+    pre = f"fdl_{variant.replace('.', '')}/"
+    ea = np.abs(oa.detach().cpu().numpy() - fx[pre + "out_a_32"]).max()
+    ep = np.abs(op_.detach().cpu().numpy() - fx[pre + "out_p_32"]).max()
+    el = abs(loss.item() - float(fx[pre + "loss_64"]))
+    print(f"{variant}: out_a {ea:.2e} out_p {ep:.2e} loss {el:.2e}")
+    assert ea <= 1e-4 and ep <= 1e-4 and el <= 1e-5
+    worst_stat = 0.0
+    for k, v in m.state_dict().items():
+        if "running" in k:
+            ref = fx[f"{pre}stat/{k}_32"]
+            worst_stat = max(worst_stat, float(np.abs(v.cpu().numpy() - ref).max() / max(1.0, np.abs(ref).max())))
+        if k.endswith("num_batches_tracked"):
+            assert int(v) == 2, k
+    print(f"{variant}: running stats worst rel {worst_stat:.2e}")
+    assert worst_stat <= 1e-5
+    glob, worst, where = nas_grad_check([(k, t.grad.cpu().numpy()) for k, t in m.named_parameters()], fx, pre)
+    print(f"{variant}: gradients L2-rel (all) {glob:.2e}, worst tensor {worst:.2e} at {where}")
+    assert glob <= 5e-3 and worst <= 2e-2, (glob, where, worst)

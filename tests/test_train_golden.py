@@ -96,6 +96,28 @@ def test_module_torch_nas_train_step_matches_reference(name):
     assert glob <= 5e-3 and worst <= 2e-2, (glob, where, worst)
 
 
+@pytest.mark.parametrize("variant", ["NASNet", "NASNet_0.1"])
+def test_module_torch_fdl_train_step_matches_reference(variant):
+    """HardNetNeiMask's torch layers (the CPU path of train()) against the reference FDLNet module's
+    train step (tests/golden/train_fdl.npz: two calls, hardnetNAS loss_HardNet, backward)."""
+    from fixtures import fdl_train_start, nas_grad_check
+    from hardnetnas_amd.losses import loss_HardNet
+    m, fx, a, p = fdl_train_start(variant)
+    oa, op_ = m(torch.from_numpy(a)), m(torch.from_numpy(p))
+    loss = loss_HardNet(oa, op_, anchor_swap=True)
+    loss.backward()
+    pre = f"fdl_{variant.replace('.', '')}/"
+    assert np.abs(oa.detach().numpy() - fx[pre + "out_a_32"]).max() <= 1e-5
+    assert np.abs(op_.detach().numpy() - fx[pre + "out_p_32"]).max() <= 1e-5
+    assert abs(loss.item() - float(fx[pre + "loss_64"])) <= 1e-5
+    for k, v in m.state_dict().items():
+        if "running" in k:
+            ref = fx[f"{pre}stat/{k}_32"]
+            assert np.abs(v.numpy() - ref).max() <= 1e-5 * max(1.0, np.abs(ref).max()), k
+    glob, worst, where = nas_grad_check([(k, t.grad.numpy()) for k, t in m.named_parameters()], fx, pre)
+    assert glob <= 5e-3 and worst <= 2e-2, (glob, where, worst)
+
+
 def test_supernet_module_torch_step_matches_reference():
     """HardNetNASSupernet (torch layers) with the recorded Gumbel noise reproduces the reference
     supernet's training step (FBNet_Stochastic_SuperNet + SupernetLoss): descriptors, the loss and
