@@ -245,3 +245,49 @@ def test_swizzled_window_reads_and_writes_conflict_free(layer):
             continue
         slots = {(a // 16) % 16 for a in addr[k:k + 8]}
         assert len(slots) == 8, (layer, k)
+
+
+def _band_sw(p):  # hn_irf.hip band_sw
+    return ((p >> 1) & 1) | (((p >> 4) & 1) << 1) | (((p >> 2) & 1) << 2)
+
+
+def test_irf_band_buffer_conflict_free():
+    """k_irf2's band buffer (IRF_BAND, 128 pixels x 32 floats, chunk c of pixel p at c ^ band_sw(p)):
+    the pwl's ds_read_b128 operand reads (lane: pixel 32 t + (l & 31), chunks 4 s + 2 (l >> 5) + k)
+    hit 16 distinct 16-byte slots per group, and the dw's ds_write_b128 stores (8-lane groups; lane
+    -> run, channel quad as in irf_core) 8 distinct slots of the 128-byte write row."""
+    for pt in range(4):
+        for s in range(2):
+            for k in range(2):
+                for g in GROUPS:
+                    slots = set()
+                    for l in g:
+                        p, c = pt * 32 + (l & 31), 4 * s + 2 * (l >> 5) + k
+                        slots.add((p * 8 + (c ^ _band_sw(p))) % 16)
+                    assert len(slots) == 16, (pt, s, k)
+    for band in range(2):
+        for w in range(4):
+            for r in range(4):
+                for g0 in range(0, 64, 8):
+                    slots = set()
+                    for lane in range(g0, g0 + 8):
+                        it = w * 64 + lane + 256 * band
+                        q = (lane & 3) | ((lane >> 5) << 2)
+                        run = (it >> 6) * 8 + ((lane >> 2) & 7)
+                        p = (run * 4 + r) & 127
+                        slots.add((q ^ _band_sw(p)) % 8)
+                    assert len(slots) == 8, (band, w, r, g0)
+
+
+def test_irf_weight_pad_slots_conflict_free():
+    """IRF_WPAD: dw weight float4 i in the pad slot of s_pw pixel i (byte 144 i + 128); a 16-lane read
+    group touches 4 channel quads of one tap (broadcast within a quad): 4 distinct slots."""
+    for k in (3, 5):
+        for tap in range(k * k):
+            for g in GROUPS:
+                addrs = {}
+                for l in g:
+                    q = (l & 3) | ((l >> 5) << 2)
+                    a = (tap * 8 + q) * 144 + 128
+                    addrs.setdefault((a // 16) % 16, set()).add(a)
+                assert all(len(v) == 1 for v in addrs.values()), (k, tap)
