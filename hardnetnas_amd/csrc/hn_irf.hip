@@ -27,16 +27,20 @@ namespace {
 
 constexpr int PS = 36;  // floats per pixel in the LDS tiles (32 channels + 4 pad)
 
-template <int CIN, int HIN>
+// 256 input pixels per tile; 128 for the 128-channel blocks and the 64-channel e1 blocks (the
+// wang2 / wang4 irf2 pair at 8x8: three workgroups per CU in 40 KB, 156-166 VGPRs; same-box A/B
+// irf2 -1.2 / -2.7 %).  The 64-channel e3 / e4 blocks keep 256 (FDLNet's irf +4 % at 128: half the
+// weight reuse of their 192 / 256-channel 1x1 operands).
+template <int CIN, int HIN, int MID>
 struct IrfTile {
-  static constexpr int NPB = CIN == 128 ? 128 / (HIN * HIN) : 256 / (HIN * HIN);
+  static constexpr int NPB = (CIN == 128 || (CIN == 64 && MID == 64)) ? 128 / (HIN * HIN) : 256 / (HIN * HIN);
   static constexpr int NI = NPB * HIN * HIN;  // input pixels per workgroup
 };
 
 template <int CIN, int COUT, int HIN, int S, int K, int MID>
 struct IrfShape {
   static constexpr int HOUT = HIN / S, PAD = K / 2;
-  static constexpr int NPB = IrfTile<CIN, HIN>::NPB, NI = IrfTile<CIN, HIN>::NI;
+  static constexpr int NPB = IrfTile<CIN, HIN, MID>::NPB, NI = IrfTile<CIN, HIN, MID>::NI;
   static constexpr int NO = NPB * HOUT * HOUT;           // output pixels per workgroup
   static constexpr int TI = NI / 32 / 4;                 // pw pixel tiles per wave
   static constexpr int KS = CIN / 16;                    // pw K-steps
@@ -315,7 +319,7 @@ constexpr int irf_smem_floats() {
 }
 
 template <int CIN, int COUT, int HIN, int S, int K, int MID>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((CIN == 64 && S == 2) || CIN == 128 || CIN == 32 ? 3 : 1))) void k_irf(const float* __restrict__ x, float* __restrict__ y,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CIN == 64 && S == 1 && MID != 64 ? 1 : 3))) void k_irf(const float* __restrict__ x, float* __restrict__ y,
                                              const uint4* __restrict__ pw_a,   // [MID/32][CIN/16][2][64]
                                              const float* __restrict__ pw_b,   // [MID] dw order
                                              const float* __restrict__ dw_w,   // [K*K][MID]
@@ -326,7 +330,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((CIN == 64 
   using Sh = IrfShape<CIN, COUT, HIN, S, K, MID>;
   constexpr int NPB = Sh::NPB, TI = Sh::TI, KS = Sh::KS, TW = Sh::TW, MODE = irf_mode<CIN, S>();
   constexpr int SMEM = irf_smem_floats<CIN, COUT, HIN, S, K, MID>();
-  static_assert(CIN != 32 || 3 * SMEM * 4 <= 160 * 1024, "three workgroups per CU");
+  static_assert((CIN == 64 && S == 1 && MID != 64) || 3 * SMEM * 4 <= 160 * 1024, "three workgroups per CU");
   __shared__ __attribute__((aligned(16))) float smem[SMEM];
   float* s_pw = smem;
   float* s_dw = smem + Sh::LDS_PW;
@@ -360,7 +364,7 @@ template <int CA>
 constexpr int irf2_mode_b() { return CA == 32 ? IRF_WPAD : IRF_PLAIN; }
 
 template <int CA, int HI, int KA, int MA, int CB, int KB, int MB>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CA == 32 ? 3 : 2))) void k_irf2(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_irf2(
     const float* __restrict__ x, float* __restrict__ y, HnIrfArgs A, HnIrfArgs Bk, int P) {
   using SA = IrfShape<CA, CA, HI, 1, KA, MA>;
   using SB = IrfShape<CA, CB, HI, 2, KB, MB>;
@@ -371,7 +375,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CA == 32 ? 
   constexpr int LB = MB_ == IRF_WPAD ? SB::LDS_PW + SB::LDS_DW : irf_lds_floats<CA, CB, HI, 2, KB, MB>();
   constexpr int LX = SA::NO * XS;
   constexpr int LDS = LA > LB ? (LA > LX ? LA : LX) : (LB > LX ? LB : LX);
-  static_assert(CA != 32 || 3 * LDS * 4 <= 160 * 1024, "three workgroups per CU");
+  static_assert(3 * LDS * 4 <= 160 * 1024, "three workgroups per CU");
   __shared__ __attribute__((aligned(16))) float smem[LDS];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, px = lane & 31, h = lane >> 5;
   // one tile per workgroup (not persistent, no register prefetch of the next tile: the other
@@ -423,7 +427,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CA == 32 ? 
 
 template <int CIN, int COUT, int HIN, int S, int K, int MID>
 hipError_t irf_launch(const HnIrfArgs& a, int P, hipStream_t st) {
-  constexpr int NPB = IrfTile<CIN, HIN>::NPB;
+  constexpr int NPB = IrfTile<CIN, HIN, MID>::NPB;
   hipLaunchKernelGGL((k_irf<CIN, COUT, HIN, S, K, MID>), dim3((P + NPB - 1) / NPB), dim3(256), 0, st, a.x, a.y,
                      a.pw_a, a.pw_b, a.dw_w, a.dw_b, a.pwl_a, a.pwl_b, P);
   return hipGetLastError();
@@ -431,7 +435,7 @@ hipError_t irf_launch(const HnIrfArgs& a, int P, hipStream_t st) {
 
 template <int CA, int HI, int KA, int MA, int CB, int KB, int MB>
 hipError_t irf2_launch(const HnIrfArgs& a, const HnIrfArgs& b, int P, hipStream_t st) {
-  constexpr int NPB = IrfTile<CA, HI>::NPB;
+  constexpr int NPB = IrfTile<CA, HI, MA>::NPB;
   hipLaunchKernelGGL((k_irf2<CA, HI, KA, MA, CB, KB, MB>), dim3((P + NPB - 1) / NPB), dim3(256), 0, st, a.x, b.y, a,
                      b, P);
   return hipGetLastError();
