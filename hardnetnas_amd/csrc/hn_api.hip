@@ -398,13 +398,19 @@ static std::vector<float> transpose_pw(const std::vector<float>& w, int cout, in
 
 // Fused-front stem weights as the MFMA A operand: [plane hi/lo][lane][8] fp16, lane
 // (r = l & 31 = output channel, h = l >> 5) holding taps 8h..8h+7 (taps >= 9 are zero).
+// The fused front's stem as 32x32x16 A operands [op][plane hi/lo][lane][8] fp16, lane (channel
+// r = l & 31, K slots 8 (l >> 5) ..): op 0 = the 9 taps in K slots 0..8 (one image row per MFMA);
+// op 1 = the same taps shifted to K slots 3..11, so that one B operand holding the 4 x 3 input
+// window of two adjacent rows (slot 3 dy + dx, dy = 0..3) feeds row y (op 0) and row y + 1 (op 1).
 static std::vector<uint16_t> pack_front_stem(const Folded& f) {
-  std::vector<uint16_t> a(2 * 64 * 8, 0);
-  for (int lane = 0; lane < 64; ++lane)
-    for (int j = 0; j < 8; ++j) {
-      const int r = lane & 31, tap = 8 * (lane >> 5) + j;
-      put_f16_split(tap < 9 ? f.w[(size_t)r * 9 + tap] : 0.f, &a[lane * 8 + j], &a[64 * 8 + lane * 8 + j]);
-    }
+  std::vector<uint16_t> a(2 * 2 * 64 * 8, 0);
+  for (int op = 0; op < 2; ++op)
+    for (int lane = 0; lane < 64; ++lane)
+      for (int j = 0; j < 8; ++j) {
+        const int r = lane & 31, tap = 8 * (lane >> 5) + j - 3 * op;
+        uint16_t* d = &a[(size_t)op * 2 * 64 * 8];
+        put_f16_split(tap >= 0 && tap < 9 ? f.w[(size_t)r * 9 + tap] : 0.f, &d[lane * 8 + j], &d[64 * 8 + lane * 8 + j]);
+      }
   return a;
 }
 

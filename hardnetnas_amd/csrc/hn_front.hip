@@ -120,6 +120,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRO
   }
   const f16x8 sah = as_f16x8(spack[lane]), sal = as_f16x8(spack[64 + lane]);
   constexpr bool LDSB = LEAN;
+  // PAIR (the k3 no-fold front): wave w computes the band's stem rows 2w, 2w + 1 from ONE B operand,
+  // the 4 x 3 input window of the two rows (K slot 3 dy + dx, dy = 0..3; slots 12..15 carry any valid
+  // input against zero weights), with the row-y taps in K slots 0..8 (spack op 0) and the row-(y + 1)
+  // taps in slots 3..11 (op 1): one gather and one hi / lo split per two rows
+  constexpr bool PAIR = LEAN && NF;
+  f16x8 sah2{}, sal2{};
+  int toff[8] = {};  // PAIR: this lane's s_in offsets of its 8 K slots, from (row y0, column px)
+  if constexpr (PAIR) {
+    sah2 = as_f16x8(spack[128 + lane]);
+    sal2 = as_f16x8(spack[192 + lane]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = min(8 * h + j, 11);
+      toff[j] = (k / 3) * 34 + k % 3;
+    }
+  }
   if (t < 32) s_sb[t] = stem_b[t];
   else if (t < 64 && MID == 32) s_pwb[t - 32] = pw_b[t - 32];
   // (visible after the first patch's barriers)
@@ -226,9 +242,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRO
         for (int y = ybeg + w; y <= ylast; y += 4)
           if (y < 0 || y >= 32) zero_row(y);
       uint4 bh[NT][2], bl[NT][2];
+      // row tile i of this wave: band row 2w + i (PAIR) or w + 4i
+      auto row_of = [&](int i) { return PAIR ? 2 * w + i : w + 4 * i; };
+      if constexpr (PAIR) {
+        static_assert(!PAIR || NT == 2, "two rows per wave");
+        const int y0 = yr0 + 2 * w;  // rows y0, y0 + 1: real (LEAN bands hold 8 real rows)
+        const float* sb = s_in + y0 * 34 + px;
+        float tp[8];
 #pragma unroll
-      for (int i = 0; i < NT; ++i) {
-        const int ri = w + 4 * i, y = yr0 + ri;
+        for (int j = 0; j < 8; ++j) tp[j] = sb[toff[j]];
+        uint4 xh, xl;
+        split8_f16(make_float4(tp[0], tp[1], tp[2], tp[3]), make_float4(tp[4], tp[5], tp[6], tp[7]), xh, xl);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const f32x16 c = i == 0 ? mfma3_f16(sah, sal, as_f16x8(xh), as_f16x8(xl), bias16(s_sb))
+                                  : mfma3_f16(sah2, sal2, as_f16x8(xh), as_f16x8(xl), bias16(s_sb));
+          float4 o[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            o[q] = make_float4(fmaxf(c[4 * q], 0.f), fmaxf(c[4 * q + 1], 0.f), fmaxf(c[4 * q + 2], 0.f),
+                               fmaxf(c[4 * q + 3], 0.f));
+          split8_f16(o[0], o[1], bh[i][0], bl[i][0]);
+          split8_f16(o[2], o[3], bh[i][1], bl[i][1]);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < (PAIR ? 0 : NT); ++i) {
+        const int ri = row_of(i), y = yr0 + ri;
         if (ri >= nreal) continue;  // wave-uniform; such tiles are never read
         if (!LEAN && (y < 0 || y >= 32)) {
           zero_row(y);
@@ -309,7 +349,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRO
         if constexpr (!LDSB) bias = bias16(pw_b + 32 * m);
 #pragma unroll
         for (int i = 0; i < NT; ++i) {
-          const int ri = w + 4 * i, y = yr0 + ri;
+          const int ri = row_of(i), y = yr0 + ri;
           if (ri >= nreal || y < 0 || y >= 32) continue;
           if constexpr (LDSB) bias = bias16(s_pwb);
           f32x16 acc = mfma3_f16(ah0, al0, as_f16x8(bh[i][0]), as_f16x8(bl[i][0]), bias);
