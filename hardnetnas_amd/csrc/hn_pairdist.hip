@@ -17,6 +17,15 @@
 #include <type_traits>
 
 namespace {
+
+// min(v[l], v[l ^ 32]) with v_permlane32_swap (VALU; __shfl_xor(v, 32) is an LDS ds_bpermute round
+// trip on the epilogue's critical path)
+HN_DEV float half_swap_min(float v) {
+  const unsigned u = __float_as_uint(v);
+  const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return fminf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+
 constexpr int TM = 64, TN = 64, D = 128, LDP = D + 4;
 
 __global__ __launch_bounds__(256) void k_colmin_init(unsigned* cm, int B) {
@@ -176,7 +185,7 @@ __global__ __launch_bounds__(NW * 64) void k_pairdist_rows(
     float* __restrict__ rowmin, unsigned* __restrict__ colmin) {
   constexpr int TN = 64, ROWB = 272, PLANE = TN * ROWB, BUF = 2 * PLANE + TN * 4;
   __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
-  __shared__ float cred[3][NW][TN];  // per-wave column minima of a tile (SWAP), tile % 3
+  __shared__ float2 cred[3][NW][TN];  // per-wave squared column minima (unmasked, masked) of a tile (SWAP), tile % 3
   __shared__ __attribute__((aligned(16))) float ainit[NW][32];  // -|a_i|^2 / 2 per wave row
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
@@ -266,9 +275,9 @@ __global__ __launch_bounds__(NW * 64) void k_pairdist_rows(
       cu = lm;
     }
     if constexpr (SWAP) {
-      cu = fminf(cu, __shfl_xor(cu, 32, 64));
-      cm = fminf(cm, __shfl_xor(cm, 32, 64));
-      if (h == 0) (&cred[0][0][0])[cslot + r] = fminf(dm_of(cu), dm_of(cm) + 10.f);
+      cu = half_swap_min(cu);
+      cm = half_swap_min(cm);
+      if (h == 0) (&cred[0][0][0])[cslot + r] = make_float2(cu, cm);
     }
   };
   auto chain_epi = [&](const char* cur, int nt, f32x16 accp, float pj, int dsel, int cslot) {
@@ -315,11 +324,17 @@ __global__ __launch_bounds__(NW * 64) void k_pairdist_rows(
   };
   auto reduce_cols = [&](int t) {  // tile t's column minima over the 4 waves: one atomic per column
     const int j = t * TN + lane;
-    const float* c = cred[t % 3][0];
-    float ce = c[lane];
+    const float2* c = cred[t % 3][0];
+    float2 ce = c[lane];
 #pragma unroll
-    for (int w = 1; w < NW; ++w) ce = fminf(ce, c[w * TN + lane]);
-    if (j < B && ce < INFINITY) atomicMin(colmin + j, __float_as_uint(ce));
+    for (int w = 1; w < NW; ++w) {
+      const float2 x = c[w * TN + lane];
+      ce.x = fminf(ce.x, x.x);
+      ce.y = fminf(ce.y, x.y);
+    }
+    // dm_of is monotone: the distance of the squared minimum is the minimum distance
+    const float d = fminf(dm_of(ce.x), dm_of(ce.y) + 10.f);
+    if (j < B && d < INFINITY) atomicMin(colmin + j, __float_as_uint(d));
   };
   auto sub_meta = [&](const float* ps, int j0, int nt, float& pj, int& dsel, int& cslot, int t) {
     const int jb = j0 + nt * 32;
@@ -409,6 +424,7 @@ __global__ __launch_bounds__(NW * 64) void k_pairdist_rows(
 // ---------------------------------------------------------------------------------------
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
+
 __global__ __launch_bounds__(256) void k_split_planes(const float* __restrict__ p, int B, uint16_t* __restrict__ ph,
                                                       uint16_t* __restrict__ pl) {
   const long e = ((long)blockIdx.x * 256 + threadIdx.x) * 8;  // 8 consecutive values per thread
@@ -435,8 +451,9 @@ __global__ __launch_bounds__(NW * 64) void k_pairdist_ring(
   constexpr int G = 2 * PLANE / 1024 / NW;  // DMA instructions per wave per tile (4 at NW = 8)
   static_assert(G * NW * 1024 == 2 * PLANE, "tile split");
   __shared__ __attribute__((aligned(16))) char sb0[BUF], sb1[BUF], sb2[BUF];
-  __shared__ float cred[3][NW][TN];
+  __shared__ float2 cred[3][NW][TN];
   __shared__ __attribute__((aligned(16))) float ainit[NW][32];
+  __shared__ float xms[NW][16][64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
   const int i0 = blockIdx.x * (32 * NW) + wave * 32;
@@ -455,9 +472,13 @@ __global__ __launch_bounds__(NW * 64) void k_pairdist_ring(
     }
   }
   if (lane < 32) ainit[wave][lane] = i0 + lane < NA ? -0.5f * asq[i0 + lane] : -INFINITY;
-  float xu[16], xm[16];
+  // row minima of the unmasked entries in registers; those of the masked entries (rare: only the
+  // masked sub-tiles touch them) in LDS, each lane its own 16 slots, so that the common epilogue
+  // path and the masked one leave the same registers live (no per-sub-tile copies at the join)
+  float xu[16];
+  float* xm = &xms[wave][0][lane];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) { xu[i] = INFINITY; xm[i] = INFINITY; }
+  for (int i = 0; i < 16; ++i) { xu[i] = INFINITY; xm[64 * i] = INFINITY; }
 
   // tile j0's rows (clamped to B - 1) into a buffer: wave instruction gi = wave * G + k covers plane
   // gi / 16, rows 4 (gi % 16) .. +3; lane L fills row 4 (gi % 16) + L / 16, chunk L % 16 with the
@@ -506,7 +527,7 @@ __global__ __launch_bounds__(NW * 64) void k_pairdist_ring(
       const bool m = v < xthr || rr == dsel;
       const float tu = m ? INFINITY : v, tm = m ? v : INFINITY;
       xu[i] = fminf(xu[i], tu);
-      xm[i] = fminf(xm[i], tm);
+      xm[64 * i] = fminf(xm[64 * i], tm);
       if constexpr (SWAP) {
         cu = fminf(cu, tu);
         cm = fminf(cm, tm);
@@ -524,9 +545,9 @@ __global__ __launch_bounds__(NW * 64) void k_pairdist_ring(
       cu = lm;
     }
     if constexpr (SWAP) {
-      cu = fminf(cu, __shfl_xor(cu, 32, 64));
-      cm = fminf(cm, __shfl_xor(cm, 32, 64));
-      if (h == 0) (&cred[0][0][0])[cslot + r] = fminf(dm_of(cu), dm_of(cm) + 10.f);
+      cu = half_swap_min(cu);
+      cm = half_swap_min(cm);
+      if (h == 0) (&cred[0][0][0])[cslot + r] = make_float2(cu, cm);
     }
   };
   // one 32-column sub-tile's bf16x3 chain (K = 128) with the previous sub-tile's epilogue woven in
@@ -567,11 +588,17 @@ __global__ __launch_bounds__(NW * 64) void k_pairdist_ring(
   };
   auto reduce_cols = [&](int t) {
     const int j = t * TN + lane;
-    const float* c = cred[t % 3][0];
-    float ce = c[lane];
+    const float2* c = cred[t % 3][0];
+    float2 ce = c[lane];
 #pragma unroll
-    for (int w = 1; w < NW; ++w) ce = fminf(ce, c[w * TN + lane]);
-    if (j < B && ce < INFINITY) atomicMin(colmin + j, __float_as_uint(ce));
+    for (int w = 1; w < NW; ++w) {
+      const float2 x = c[w * TN + lane];
+      ce.x = fminf(ce.x, x.x);
+      ce.y = fminf(ce.y, x.y);
+    }
+    // dm_of is monotone: the distance of the squared minimum is the minimum distance
+    const float d = fminf(dm_of(ce.x), dm_of(ce.y) + 10.f);
+    if (j < B && d < INFINITY) atomicMin(colmin + j, __float_as_uint(d));
   };
   auto sub_meta = [&](const float* ps, int j0, int nt, float& pj, int& dsel, int& cslot, int t) {
     const int jb = j0 + nt * 32;
@@ -626,7 +653,7 @@ __global__ __launch_bounds__(NW * 64) void k_pairdist_ring(
   }
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
-    float u = xu[i], m = xm[i];
+    float u = xu[i], m = xm[64 * i];
 #pragma unroll
     for (int o = 16; o > 0; o >>= 1) {
       u = fminf(u, __shfl_xor(u, o, 64));
