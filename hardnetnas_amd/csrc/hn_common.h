@@ -67,6 +67,12 @@ HN_DEV uint4 buf_load16(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff) 
   const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
   return make_uint4(v.x, v.y, v.z, v.w);
 }
+// a store beyond the resource's byte count is dropped by the hardware (no branch, so the
+// compiler's vmcnt accounting stays exact)
+HN_DEV void buf_store16(__amdgpu_buffer_rsrc_t r, const uint4& v, unsigned voff, unsigned soff) {
+  const u32x4 x = {v.x, v.y, v.z, v.w};
+  __builtin_amdgcn_raw_buffer_store_b128(x, r, voff, soff, 0);
+}
 
 HN_DEV f32x16 mfma3(const bf16x8& ah, const bf16x8& al, const bf16x8& bh, const bf16x8& bl,
                     f32x16 acc) {

@@ -731,8 +731,11 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void k_conv_pipe(
 // barrier per stage.  For the HBM-heavy stride-2 layers this keeps ~UNITS*32 B per
 // workgroup in flight instead of one unit per K-step.
 // ------------------------------------------------------------------------------------
+#ifndef HN_PST_KY
+#define HN_PST_KY 2
+#endif
 template <int CIN, int COUT, int HIN, int S, int NP, int TR, int WM, int WN, bool STEM = false, int PX = 80,
-          bool CST = false>
+          bool CST = false, bool PST = false>
 struct WsCfg : ConvCfg<CIN, COUT, HIN, S, NP, TR, WM, WN, PX> {
   using B = ConvCfg<CIN, COUT, HIN, S, NP, TR, WM, WN, PX>;
   static constexpr int NWC = WM * WN, NWP = 4, NTHR = (NWC + NWP) * 64, PTHR = NWP * 64;
@@ -742,10 +745,16 @@ struct WsCfg : ConvCfg<CIN, COUT, HIN, S, NP, TR, WM, WN, PX> {
   static constexpr int PBUF = 34 * 34 * 4;  // one private normalised patch per producer wave
   static constexpr int SROW = 36;                   // CST: floats per pixel row of the scratch
   static constexpr int SCR = 32 * SROW * 4;          // CST: one 32 x 32 tile per MFMA wave
-  static constexpr int SMEM = 2 * BUF + (STEM ? NWP * PBUF : 0) + (CST ? NWC * SCR : 0);
+  static constexpr int SMEM = 2 * BUF + (STEM ? NWP * PBUF : 0) + (CST ? NWC * SCR : 0) + (PST ? COUT * 4 : 0);
   static constexpr bool DEEP = !STEM && UPT <= 6;  // two stages of loads in flight
   static_assert(SMEM <= 160 * 1024, "LDS");
   static_assert(!(STEM && CST), "the CST epilogue scratch starts where the STEM buffers live");
+  // PST: a tile's outputs are staged in the window buffer its last stage has just consumed and
+  // stored by the producer waves (whole 512-byte pixel rows per 32 lanes)
+  static constexpr int OSTR = COUT * 4 + 16;    // bytes per staged output pixel (+16: conflict-free writes)
+  static constexpr int OCH = B::BM * COUT / 4;  // 16-byte output chunks per tile
+  static constexpr int OPT = OCH / PTHR;
+  static_assert(!PST || (!STEM && !CST && !DEEP && OCH % PTHR == 0 && B::BM * OSTR <= BUF), "PST");
 };
 
 // STEM (conv1 only): the producers load the raw patch, reduce mean/std per wave, write the
@@ -756,12 +765,12 @@ struct WsCfg : ConvCfg<CIN, COUT, HIN, S, NP, TR, WM, WN, PX> {
 // so that every store instruction writes 8 whole 128-byte pixel rows (8 lanes per row) instead
 // of 32 pixels x 32 bytes.
 template <int CIN, int COUT, int HIN, int S, int NP, int TR, int WM, int WN, bool STEM, int ABL = 0,
-          int PX = 80, bool CST = false>
+          int PX = 80, bool CST = false, bool PST = false>
 __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_ws(
     const float* __restrict__ in, float* __restrict__ out, const uint4* __restrict__ wp,
     const float* __restrict__ bias, int P, const float* __restrict__ stem_w,
     const float* __restrict__ stem_b, float eps, float relu_lo) {
-  using C = WsCfg<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM, PX, CST>;
+  using C = WsCfg<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM, PX, CST, PST>;
   static_assert(PX == 80 || !STEM, "the stem producer writes the 80-byte layout");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -827,6 +836,33 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_ws(
         *reinterpret_cast<uint4*>(dst + C::PLANE + off) = lo;
       }
     }
+  };
+
+  // PST: after the stage barrier that ends a tile, wait for the MFMA waves to stage the outputs in
+  // that stage's buffer (B_x), read them, release the buffer (B_y: the MFMA waves pass it KY K-steps
+  // into the next stage, the producers refill the buffer only after it), then store whole pixel rows
+  auto pstore = [&](int s, const char* src) {
+    int p0, y0;
+    tile_of(s, p0, y0);
+    // the tile's valid patches only (NP > 1: the batch's last tile may be half empty)
+    const int vp = NP == 1 ? 1 : min(NP, P - p0);
+    const __amdgpu_buffer_rsrc_t orsrc =
+        make_rsrc(out + (size_t)(p0 * C::HOUT + y0) * C::WOUT * COUT, (unsigned)vp * TR * C::WOUT * COUT * 4);
+    __syncthreads();  // B_x
+    constexpr int G = 8;  // chunks read per batch (the next stage's loads are in flight in pf)
+    static_assert(!PST || C::OPT % G == 0, "batches");
+#pragma unroll
+    for (int k0 = 0; k0 < C::OPT; k0 += G) {
+      uint4 rv[G];
+#pragma unroll
+      for (int k = 0; k < G; ++k) {
+        const int c = ptid + (k0 + k) * C::PTHR, m = c / (COUT / 4), j = c % (COUT / 4);
+        rv[k] = *reinterpret_cast<const uint4*>(src + m * C::OSTR + 16 * j);
+      }
+#pragma unroll
+      for (int k = 0; k < G; ++k) buf_store16(orsrc, rv[k], (unsigned)(ptid * 16), (unsigned)((k0 + k) * C::PTHR * 16));
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // B_y
   };
 
   // ---- stem producer (STEM only) ----
@@ -932,6 +968,8 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_ws(
       produce_write(buf0, pf);
       if (NS > 1) produce_loads(1, pf);
     }
+  } else if constexpr (PST) {
+    for (int i = tid; i < COUT; i += C::NWC * 64) reinterpret_cast<float*>(smem + 2 * C::BUF)[i] = bias[i];
   }
   __syncthreads();
 
@@ -957,6 +995,8 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_ws(
           if (s + 2 < NS) produce_loads(s + 2, pf);
         }
         __syncthreads();
+        if constexpr (PST)
+          if (s % C::NCC == C::NCC - 1) pstore(s, (s & 1) ? buf1 : buf0);
       }
     } else {
       // stage s + 2's loads are issued before stage s + 1 is written, so each load has two
@@ -977,6 +1017,9 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_ws(
 
   // ---- compute side ----
   const int wm = wave / WN, wn = wave % WN;
+  // PST: the bias in LDS (read right after the tile's last stage barrier, where a global load's
+  // latency would hold up every wave)
+  float* const sbias = reinterpret_cast<float*>(smem + 2 * C::BUF);
   int abase[C::MT], ylr[C::MT];
 #pragma unroll
   for (int mt = 0; mt < C::MT; ++mt) {
@@ -996,7 +1039,6 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_ws(
     for (int nt = 0; nt < C::NT; ++nt) acc[mt][nt] = f32x16{};
 
   constexpr int NKS = 18;
-  static_assert(NKS % 3 == 0, "the weight ring runs on across stages");
   // weight fragments of K-step k of channel chunk cc; a stage's first two K-steps are
   // fetched during the previous stage's last two, i.e. before its epilogue stores, which
   // would otherwise sit in front of them in the in-order vmcnt queue
@@ -1009,9 +1051,11 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_ws(
       dst[nt][1] = buf_load16(wr_, wvoff, k + 64 * 16);
     }
   };
-  uint4 bq[3][C::NT][2];
-  load_b(0, 0, bq[0]);
-  load_b(0, 1, bq[1]);
+  constexpr int WD = 3;  // weight ring depth: K-step fragments loaded WD - 1 steps ahead
+  static_assert(NKS % WD == 0, "the weight ring runs on across stages");
+  uint4 bq[WD][C::NT][2];
+#pragma unroll
+  for (int k = 0; k + 1 < WD; ++k) load_b(0, k, bq[k]);
 #pragma unroll 1
   for (int s = 0; s < NS; ++s) {
     const char* cur = (s & 1) ? buf1 : buf0;
@@ -1031,12 +1075,16 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_ws(
     load_a(0, aq[0]);
 #pragma unroll
     for (int ksx = 0; ksx < NKS; ++ksx) {
-      if (ksx + 2 < NKS)
-        load_b(cc, ksx + 2, bq[(ksx + 2) % 3]);
+      if (ksx + WD - 1 < NKS)
+        load_b(cc, ksx + WD - 1, bq[(ksx + WD - 1) % WD]);
       else if (s + 1 < NS)
-        load_b(ccn, ksx + 2 - NKS, bq[(ksx + 2) % 3]);
+        load_b(ccn, ksx + WD - 1 - NKS, bq[(ksx + WD - 1) % WD]);
       if (ksx + 1 < NKS) load_a(ksx + 1, aq[(ksx + 1) & 1]);
       __builtin_amdgcn_sched_barrier(0);
+      if constexpr (PST) {
+        constexpr int KY = HN_PST_KY;  // B_y of the previous tile (see pstore)
+        if (ksx == KY && cc == 0 && s > 0) __builtin_amdgcn_s_barrier();
+      }
 #pragma unroll
       for (int mt = 0; mt < C::MT; ++mt) {
         const bf16x8 xh = as_bf16x8(aq[ksx & 1][mt][0]), xl = as_bf16x8(aq[ksx & 1][mt][1]);
@@ -1044,13 +1092,40 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_ws(
         for (int nt = 0; nt < C::NT; ++nt) {
           if constexpr (ABL & 16)  // timing only: no MFMA, operands kept live
             acc[mt][nt][0] += __builtin_bit_cast(float, aq[ksx & 1][mt][0].x ^ aq[ksx & 1][mt][1].y ^
-                                                           bq[ksx % 3][nt][0].z ^ bq[ksx % 3][nt][1].w);
+                                                           bq[ksx % WD][nt][0].z ^ bq[ksx % WD][nt][1].w);
           else
-            acc[mt][nt] = mfma3(as_bf16x8(bq[ksx % 3][nt][0]), as_bf16x8(bq[ksx % 3][nt][1]), xh,
+            acc[mt][nt] = mfma3(as_bf16x8(bq[ksx % WD][nt][0]), as_bf16x8(bq[ksx % WD][nt][1]), xh,
                                 xl, acc[mt][nt]);
         }
       }
       __builtin_amdgcn_sched_barrier(0);
+    }
+    if (PST && cc == C::NCC - 1) {
+      __syncthreads();  // B_s: the stage's buffer is free
+      char* stg = const_cast<char*>(cur);
+#pragma unroll
+      for (int nt = 0; nt < C::NT; ++nt) {
+        float4 bv[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          bv[q] = *reinterpret_cast<const float4*>(sbias + (wn * C::NT + nt) * 32 + 8 * q + 4 * h);
+#pragma unroll
+        for (int mt = 0; mt < C::MT; ++mt) {
+          char* o = stg + ((wm * C::MT + mt) * 32 + r) * C::OSTR + ((wn * C::NT + nt) * 32 + 4 * h) * 4;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            float4 v;
+            v.x = fmaxf(acc[mt][nt][4 * q + 0] + bv[q].x, relu_lo);
+            v.y = fmaxf(acc[mt][nt][4 * q + 1] + bv[q].y, relu_lo);
+            v.z = fmaxf(acc[mt][nt][4 * q + 2] + bv[q].z, relu_lo);
+            v.w = fmaxf(acc[mt][nt][4 * q + 3] + bv[q].w, relu_lo);
+            *reinterpret_cast<float4*>(o + 32 * q) = v;
+          }
+          acc[mt][nt] = f32x16{};
+        }
+      }
+      __syncthreads();  // B_x
+      continue;
     }
     if (cc == C::NCC - 1) {
       int p0, y0;
@@ -1103,6 +1178,7 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_ws(
     }
     if constexpr (!(ABL & 32)) __syncthreads();
   }
+  if constexpr (PST) __builtin_amdgcn_s_barrier();  // B_y of the last tile
 }
 
 // ------------------------------------------------------------------------------------
@@ -1524,20 +1600,22 @@ HN_PIPE_C(pipe5_cst, false, 128, 128, 8, 1, 2, 8, 1, 4, 0, true)  // HN_VARIANT 
 #define HN_WS_S(NAME, STEM, CIN, COUT, HIN, S, NP, TR, WM, WN) HN_WS_A(NAME, STEM, CIN, COUT, HIN, S, NP, TR, WM, WN, 0)
 #define HN_WS_A(NAME, STEM, CIN, COUT, HIN, S, NP, TR, WM, WN, ABL) HN_WS_X(NAME, STEM, CIN, COUT, HIN, S, NP, TR, WM, WN, ABL, 80)
 #define HN_WS_X(NAME, STEM, CIN, COUT, HIN, S, NP, TR, WM, WN, ABL, PX) HN_WS_C(NAME, STEM, CIN, COUT, HIN, S, NP, TR, WM, WN, ABL, PX, false)
-#define HN_WS_C(NAME, STEM, CIN, COUT, HIN, S, NP, TR, WM, WN, ABL, PX, CST)             \
-  using NAME##_cfg = WsCfg<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM, PX, CST>;                   \
+#define HN_WS_C(NAME, STEM, CIN, COUT, HIN, S, NP, TR, WM, WN, ABL, PX, CST) \
+  HN_WS_P(NAME, STEM, CIN, COUT, HIN, S, NP, TR, WM, WN, ABL, PX, CST, false)
+#define HN_WS_P(NAME, STEM, CIN, COUT, HIN, S, NP, TR, WM, WN, ABL, PX, CST, PST)        \
+  using NAME##_cfg = WsCfg<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM, PX, CST, PST>;              \
   static hipError_t NAME##_lo(const float* in, float* out, const void* wp, const float* bias,\
                          int P, const float* sw, const float* sb, float eps, hipStream_t st, \
                          float lo) {                                                       \
     constexpr int lds = NAME##_cfg::SMEM;                                                  \
     const void* fn =                                                                       \
-        reinterpret_cast<const void*>(&k_conv_ws<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM, ABL, PX, CST>); \
+        reinterpret_cast<const void*>(&k_conv_ws<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM, ABL, PX, CST, PST>); \
     int resident = 0;                                                                      \
     const hipError_t e = hn_resident_blocks(fn, NAME##_cfg::NTHR, lds, &resident);         \
     if (e != hipSuccess) return e;                                                         \
     const int tiles = (P + NP - 1) / NP * NAME##_cfg::RT;                                  \
     const int grid = std::min(tiles, resident);                                            \
-    hipLaunchKernelGGL((k_conv_ws<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM, ABL, PX, CST>), dim3(grid), \
+    hipLaunchKernelGGL((k_conv_ws<CIN, COUT, HIN, S, NP, TR, WM, WN, STEM, ABL, PX, CST, PST>), dim3(grid), \
                        dim3(NAME##_cfg::NTHR), lds, st, in, out,                           \
                        static_cast<const uint4*>(wp), bias, P, sw, sb, eps, lo);               \
     return hipGetLastError();                                                              \
@@ -1564,6 +1642,8 @@ HN_WS_X(ws4_np2s, false, 64, 128, 16, 2, 2, 8, 1, 4, 0, 64)
 HN_WS_X(ws4_s, false, 64, 128, 16, 2, 1, 8, 1, 4, 0, 64)
 #endif
 HN_WS_X(ws4_np2s22, false, 64, 128, 16, 2, 2, 8, 2, 2, 0, 64)  // digit f: 2 x 2 waves
+// digit i: the same with the outputs stored by the producer waves (PST)
+HN_WS_P(ws4_pst, false, 64, 128, 16, 2, 2, 8, 2, 2, 0, 64, false, true)
 // conv3 with the epilogue transposed through LDS for whole-row stores (CST): HN_VARIANT digit g
 // (the default, conv3 12.8 -> 12.1 ms).  The same on conv4's one-patch tiling (8.49 -> 8.35 ms)
 // and conv5's k_conv_ws form (13.0 -> 12.6) stays behind their defaults; conv5's k_conv_pipe
@@ -1615,7 +1695,7 @@ bool hn_hardnet_variant_ok(int layer, int v) {
   if (v == 7) return layer >= 3;
   if (v == 1 || v == 2 || v == 3) return true;
 #endif
-  if (v == 15) return layer == 4;
+  if (v == 15 || v == 18) return layer == 4;
   if (v == 16) return layer == 3 || layer == 5;
   if (v == 0 || v == 5 || v == 6) return true;  // (layer 1 always runs conv1_launch)
   return false;
@@ -1636,9 +1716,9 @@ hipError_t hn_launch_hardnet_conv(int layer, int variant, const HardnetDev& d, c
     return hipErrorInvalidValue;
   }
 #endif
-  if (variant == 15) {  // conv4, 64-byte swizzled window, two patches per stage
+  if (variant == 15 || variant == 18) {  // conv4, 64-byte swizzled window, two patches per stage
     if (layer != 4) return hipErrorInvalidValue;
-    return ws4_np2s22(in, out, d.wpack[4], d.bias[4], P, nullptr, nullptr, 0.f, st);
+    return (variant == 18 ? ws4_pst : ws4_np2s22)(in, out, d.wpack[4], d.bias[4], P, nullptr, nullptr, 0.f, st);
   }
 #ifdef HN_EXPERIMENTS
   if (variant == 13 || variant == 14) {  // conv4, 64-byte swizzled window (2 / 1 patches per stage)

@@ -452,7 +452,6 @@ __global__ __launch_bounds__(NW * 64) void k_pairdist_ring(
   static_assert(G * NW * 1024 == 2 * PLANE, "tile split");
   __shared__ __attribute__((aligned(16))) char sb0[BUF], sb1[BUF], sb2[BUF];
   __shared__ float2 cred[3][NW][TN];
-  __shared__ __attribute__((aligned(16))) float ainit[NW][32];
   __shared__ float xms[NW][16][64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
@@ -471,10 +470,16 @@ __global__ __launch_bounds__(NW * 64) void k_pairdist_ring(
       al[ks] = as_bf16x8(lo);
     }
   }
-  if (lane < 32) ainit[wave][lane] = i0 + lane < NA ? -0.5f * asq[i0 + lane] : -INFINITY;
   // row minima of the unmasked entries in registers; those of the masked entries (rare: only the
   // masked sub-tiles touch them) in LDS, each lane its own 16 slots, so that the common epilogue
   // path and the masked one leave the same registers live (no per-sub-tile copies at the join)
+  // -|a_i|^2 / 2 of this lane's 16 accumulator rows: every chain starts from it
+  f32x16 areg;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int ia = i0 + (i & 3) + 8 * (i >> 2) + 4 * h;
+    areg[i] = ia < NA ? -0.5f * asq[ia] : -INFINITY;
+  }
   float xu[16];
   float* xm = &xms[wave][0][lane];
 #pragma unroll
@@ -552,15 +557,7 @@ __global__ __launch_bounds__(NW * 64) void k_pairdist_ring(
   };
   // one 32-column sub-tile's bf16x3 chain (K = 128) with the previous sub-tile's epilogue woven in
   auto chain_epi = [&](const char* cur, int nt, f32x16 accp, float pj, int dsel, int cslot) {
-    f32x16 acc;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float4 v = *reinterpret_cast<const float4*>(&ainit[wave][8 * q + 4 * h]);
-      acc[4 * q] = v.x;
-      acc[4 * q + 1] = v.y;
-      acc[4 * q + 2] = v.z;
-      acc[4 * q + 3] = v.w;
-    }
+    f32x16 acc = areg;
     float lm = INFINITY;
     const int row = nt * 32 + r, sw = row & 15;
     const char* base = cur + row * ROWB;
@@ -612,7 +609,7 @@ __global__ __launch_bounds__(NW * 64) void k_pairdist_ring(
   f32x16 accp{};
   float pjp = INFINITY;
   int dselp = -1000, cslotp = wave * TN + 32;
-  // prologue: tiles 0 and 1 in flight, wait for tile 0 (ainit, written above, is read after it)
+  // prologue: tiles 0 and 1 in flight, wait for tile 0
   issue(sb0, 0);
   if (ntile > 1) issue(sb1, TN);
   sync_tile(ntile > 1);

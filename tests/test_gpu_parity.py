@@ -82,7 +82,7 @@ def test_chunked_forward_equals_unchunked(name, cuda_device, monkeypatch):
 
 
 @pytest.mark.parametrize("variant", ["000000", "005555", "006666", "505000", "605000", "6050f0", "605g0g",
-                                     "505gfg", "605gfg", "6056f6"])
+                                     "505gfg", "605gfg", "6056f6", "605gig"])
 def test_tiling_variants_match_reference(variant, cuda_device, monkeypatch):
     from hardnetnas_amd._native import NativeModel
     m, fx, _ = build_module("hardnet")
@@ -91,6 +91,22 @@ def test_tiling_variants_match_reference(variant, cuda_device, monkeypatch):
     x = torch.from_numpy(golden_inputs(fx)).to(cuda_device)
     y = NativeModel.from_module(m, cuda_device)(x).cpu().numpy()
     assert np.abs(y - fx["y"]).max() <= TOL["hardnet"]
+
+
+def test_conv4_producer_stores_are_bit_identical(cuda_device, monkeypatch):
+    """conv4 with its outputs staged in LDS and stored by the producer waves (HN_VARIANT digit i)
+    against the MFMA waves' own stores (digit f): same arithmetic, so identical bits, including
+    ragged batches whose last two-patch tile is half empty."""
+    from hardnetnas_amd._native import NativeModel
+    m, fx, _ = build_module("hardnet")
+    x = torch.from_numpy(golden_inputs(fx)).to(cuda_device)
+    out = {}
+    for v in ("605gfg", "605gig"):
+        monkeypatch.setenv("HN_VARIANT", v)
+        nm = NativeModel.from_module(m, cuda_device)
+        out[v] = [nm(x[:b]) for b in (1, 3, 255, x.shape[0])]
+    for a, b in zip(out["605gfg"], out["605gig"]):
+        assert torch.equal(a, b)
 
 
 def test_fused_c12_is_default_and_matches_layerwise(cuda_device, monkeypatch):
