@@ -745,16 +745,18 @@ struct WsCfg : ConvCfg<CIN, COUT, HIN, S, NP, TR, WM, WN, PX> {
   static constexpr int PBUF = 34 * 34 * 4;  // one private normalised patch per producer wave
   static constexpr int SROW = 36;                   // CST: floats per pixel row of the scratch
   static constexpr int SCR = 32 * SROW * 4;          // CST: one 32 x 32 tile per MFMA wave
-  static constexpr int SMEM = 2 * BUF + (STEM ? NWP * PBUF : 0) + (CST ? NWC * SCR : 0) + (PST ? COUT * 4 : 0);
-  static constexpr bool DEEP = !STEM && UPT <= 6;  // two stages of loads in flight
-  static_assert(SMEM <= 160 * 1024, "LDS");
-  static_assert(!(STEM && CST), "the CST epilogue scratch starts where the STEM buffers live");
-  // PST: a tile's outputs are staged in the window buffer its last stage has just consumed and
-  // stored by the producer waves (whole 512-byte pixel rows per 32 lanes)
+  // PST: a tile's outputs are staged in the window buffer its last stage has just consumed (pixels
+  // below MB) and an extra region (the rest), then stored by the producer waves as whole pixel rows
   static constexpr int OSTR = COUT * 4 + 16;    // bytes per staged output pixel (+16: conflict-free writes)
   static constexpr int OCH = B::BM * COUT / 4;  // 16-byte output chunks per tile
   static constexpr int OPT = OCH / PTHR;
-  static_assert(!PST || (!STEM && !CST && !DEEP && OCH % PTHR == 0 && B::BM * OSTR <= BUF), "PST");
+  static constexpr int MB = PST ? (B::BM < BUF / OSTR ? B::BM : BUF / OSTR) : 0;
+  static constexpr int XST = PST ? (B::BM - MB) * OSTR : 0;
+  static constexpr int SMEM = 2 * BUF + (STEM ? NWP * PBUF : 0) + (CST ? NWC * SCR : 0) + (PST ? COUT * 4 + XST : 0);
+  static constexpr bool DEEP = !STEM && UPT <= 6;  // two stages of loads in flight
+  static_assert(SMEM <= 160 * 1024, "LDS");
+  static_assert(!(STEM && CST), "the CST epilogue scratch starts where the STEM buffers live");
+  static_assert(!PST || (!STEM && !CST && OCH % PTHR == 0), "PST");
 };
 
 // STEM (conv1 only): the producers load the raw patch, reduce mean/std per wave, write the
@@ -789,6 +791,10 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_ws(
   if (NS == 0) return;
   char* const buf0 = smem;
   char* const buf1 = smem + C::BUF;
+  // PST staging slot of output pixel m of the tile whose last stage read buffer `b`
+  auto stage_at = [&](const char* b, int m) -> char* {
+    return m < C::MB ? const_cast<char*>(b) + m * C::OSTR : smem + 2 * C::BUF + COUT * 4 + (m - C::MB) * C::OSTR;
+  };
 
   auto tile_of = [&](int s, int& p0, int& y0) {
     const int t = STEM ? t_begin + s / C::NCC : rb + (s / C::NCC) * nwg;
@@ -857,7 +863,7 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_ws(
 #pragma unroll
       for (int k = 0; k < G; ++k) {
         const int c = ptid + (k0 + k) * C::PTHR, m = c / (COUT / 4), j = c % (COUT / 4);
-        rv[k] = *reinterpret_cast<const uint4*>(src + m * C::OSTR + 16 * j);
+        rv[k] = *reinterpret_cast<const uint4*>(stage_at(src, m) + 16 * j);
       }
 #pragma unroll
       for (int k = 0; k < G; ++k) buf_store16(orsrc, rv[k], (unsigned)(ptid * 16), (unsigned)((k0 + k) * C::PTHR * 16));
@@ -1006,10 +1012,14 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_ws(
         if (s + 2 < NS) produce_loads(s + 2, pf2);
         if (s + 1 < NS) produce_write(buf1, pf);
         __syncthreads();
+        if constexpr (PST)
+          if (s % C::NCC == C::NCC - 1) pstore(s, buf0);
         if (s + 1 >= NS) break;
         if (s + 3 < NS) produce_loads(s + 3, pf);
         if (s + 2 < NS) produce_write(buf0, pf2);
         __syncthreads();
+        if constexpr (PST)
+          if ((s + 1) % C::NCC == C::NCC - 1) pstore(s + 1, buf1);
       }
     }
     return;
@@ -1111,7 +1121,7 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_ws(
           bv[q] = *reinterpret_cast<const float4*>(sbias + (wn * C::NT + nt) * 32 + 8 * q + 4 * h);
 #pragma unroll
         for (int mt = 0; mt < C::MT; ++mt) {
-          char* o = stg + ((wm * C::MT + mt) * 32 + r) * C::OSTR + ((wn * C::NT + nt) * 32 + 4 * h) * 4;
+          char* o = stage_at(stg, (wm * C::MT + mt) * 32 + r) + ((wn * C::NT + nt) * 32 + 4 * h) * 4;
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             float4 v;
@@ -1649,6 +1659,12 @@ HN_WS_P(ws4_pst, false, 64, 128, 16, 2, 2, 8, 2, 2, 0, 64, false, true)
 // and conv5's k_conv_ws form (13.0 -> 12.6) stays behind their defaults; conv5's k_conv_pipe
 // gets the half-tile form (pipe5_cst, 11.9 -> 11.5 ms, the default).
 HN_WS_C(ws3_cst, false, 64, 64, 16, 1, 1, 16, 2, 2, 0, 80, true)
+#ifdef HN_EXPERIMENTS
+// conv3 with the outputs stored by the producer waves (PST, HN_VARIANT digit i): 12.8 vs 12.1 ms
+// for the CST form (same-box A/B; the DEEP producers' two extra barriers per tile cost more than
+// the MFMA waves' whole-row stores)
+HN_WS_P(ws3_pst, false, 64, 64, 16, 1, 1, 16, 2, 2, 0, 80, false, true)
+#endif
 
 // wider N tiles (fewer A-fragment reads, weights shared through L1)
 #ifdef HN_EXPERIMENTS  // superseded tiling (experiments library only)
@@ -1689,13 +1705,14 @@ bool hn_hardnet_variant_ok(int layer, int v) {
   // kernels (17) and the timing-only ablations (4, 8, 9) exist only with -DHN_EXPERIMENTS.
   if (layer < 0 || layer > 5) return false;
 #ifdef HN_EXPERIMENTS
+  if (v == 18 && layer == 3) return true;
   if (v == 4 || v == 8 || v == 9) return layer >= 3;
   if (v == 13 || v == 14) return layer == 4;
   if (v == 17) return layer == 3 || layer == 5;  // Winograd F(2x2,3x3), hn_wino.hip
   if (v == 7) return layer >= 3;
   if (v == 1 || v == 2 || v == 3) return true;
 #endif
-  if (v == 15 || v == 18) return layer == 4;
+  if (v == 15 || v == 18) return layer == 4;  // 18: outputs stored by the producer waves
   if (v == 16) return layer == 3 || layer == 5;
   if (v == 0 || v == 5 || v == 6) return true;  // (layer 1 always runs conv1_launch)
   return false;
@@ -1716,10 +1733,13 @@ hipError_t hn_launch_hardnet_conv(int layer, int variant, const HardnetDev& d, c
     return hipErrorInvalidValue;
   }
 #endif
-  if (variant == 15 || variant == 18) {  // conv4, 64-byte swizzled window, two patches per stage
+  if (variant == 15 || (variant == 18 && layer == 4)) {  // conv4, 64-byte swizzled window, two patches per stage
     if (layer != 4) return hipErrorInvalidValue;
     return (variant == 18 ? ws4_pst : ws4_np2s22)(in, out, d.wpack[4], d.bias[4], P, nullptr, nullptr, 0.f, st);
   }
+#ifdef HN_EXPERIMENTS
+  if (variant == 18 && layer == 3) return ws3_pst(in, out, d.wpack[3], d.bias[3], P, nullptr, nullptr, 0.f, st);
+#endif
 #ifdef HN_EXPERIMENTS
   if (variant == 13 || variant == 14) {  // conv4, 64-byte swizzled window (2 / 1 patches per stage)
     if (layer != 4) return hipErrorInvalidValue;
