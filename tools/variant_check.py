@@ -6,7 +6,8 @@ import sys
 import numpy as np
 import torch
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tests"))
+_root = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+sys.path[:0] = [_root, os.path.join(_root, "tests")]
 from fixtures import build_module, golden_inputs  # noqa: E402
 from hardnetnas_amd._native import NativeModel  # noqa: E402
 
