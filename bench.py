@@ -522,12 +522,12 @@ def run(opts, world, rank, local, dev, on_gpu, backend):
             achieved = flop / (pair_ms * 1e-3) / 1e12
             pmc = read_pmc("c5") or {}
             tr = pmc.get("pairdist") if pmc.get("pairs") == pairs and world == 1 else None
-            roof = {"bound": "mfma", "kernel": "pair step (k_pairdist_rows + k_sq/k_pos/k_loss)",
+            roof = {"bound": "mfma", "kernel": "pair step (k_pairdist_ring + k_split_planes/k_sq/k_pos/k_loss)",
                     "achieved": round(achieved, 2), "peak": round(PEAK_BF16X3, 1), "unit": "TFLOP/s",
                     "frac": round(achieved / PEAK_BF16X3, 4),
                     "traffic": int(tr["bytes_per_launch"]) if tr else None,
                     "traffic_source": "profiles/pmc_c5.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, separate "
-                                      "passes, k_pairdist_rows at this batch)" if tr else None,
+                                      "passes, k_pairdist_ring at this batch)" if tr else None,
                     "avg_launch_ms": round(pair_ms, 4), "launches": opts.steps,
                     "pairs_per_launch": int(pairs),
                     "peak_basis": "bf16 MFMA dense 2.5 PFLOP/s / 3 (bf16x3 split-precision distance "
