@@ -413,6 +413,14 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void k_conv_pipe(
   const int my_tiles = rb < ntiles ? (ntiles - 1 - rb) / nwg + 1 : 0;
   const int NS = my_tiles * C::NCC;
   if (NS == 0) return;
+  // this wave's bias channels, loaded once (an epilogue global load waits behind the next stage's
+  // staging loads in vmcnt)
+  float4 bvr[C::NT][4];
+#pragma unroll
+  for (int nt = 0; nt < C::NT; ++nt)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      bvr[nt][q] = *reinterpret_cast<const float4*>(bias + (wn * C::NT + nt) * 32 + 8 * q + 4 * h);
 
   int abase[C::MT];
 #pragma unroll
@@ -669,10 +677,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void k_conv_pipe(
                      wn * C::NT * 32 + 4 * h;
 #pragma unroll
       for (int nt = 0; nt < C::NT; ++nt) {
-        float4 bv[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          bv[q] = *reinterpret_cast<const float4*>(bias + (wn * C::NT + nt) * 32 + 8 * q + 4 * h);
+        const float4* bv = bvr[nt];
 #pragma unroll
         for (int mt = 0; mt < C::MT; ++mt) {
           const bool ok = NP == 1 || p0 + ((wm * C::MT + mt) * 32) / (TR * C::WOUT) < P;
@@ -752,7 +757,10 @@ struct WsCfg : ConvCfg<CIN, COUT, HIN, S, NP, TR, WM, WN, PX> {
   static constexpr int OPT = OCH / PTHR;
   static constexpr int MB = PST ? (B::BM < BUF / OSTR ? B::BM : BUF / OSTR) : 0;
   static constexpr int XST = PST ? (B::BM - MB) * OSTR : 0;
-  static constexpr int SMEM = 2 * BUF + (STEM ? NWP * PBUF : 0) + (CST ? NWC * SCR : 0) + (PST ? COUT * 4 + XST : 0);
+  // the bias (read by the epilogue from LDS: a global load there queues behind the next stage's
+  // weight prefetch in the in-order vmcnt) after the STEM / CST regions, then PST's extra staging
+  static constexpr int BIAS_OFF = 2 * BUF + (STEM ? NWP * PBUF : 0) + (CST ? NWC * SCR : 0);
+  static constexpr int SMEM = BIAS_OFF + COUT * 4 + XST;
   static constexpr bool DEEP = !STEM && UPT <= 6;  // two stages of loads in flight
   static_assert(SMEM <= 160 * 1024, "LDS");
   static_assert(!(STEM && CST), "the CST epilogue scratch starts where the STEM buffers live");
@@ -793,7 +801,7 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_ws(
   char* const buf1 = smem + C::BUF;
   // PST staging slot of output pixel m of the tile whose last stage read buffer `b`
   auto stage_at = [&](const char* b, int m) -> char* {
-    return m < C::MB ? const_cast<char*>(b) + m * C::OSTR : smem + 2 * C::BUF + COUT * 4 + (m - C::MB) * C::OSTR;
+    return m < C::MB ? const_cast<char*>(b) + m * C::OSTR : smem + C::BIAS_OFF + COUT * 4 + (m - C::MB) * C::OSTR;
   };
 
   auto tile_of = [&](int s, int& p0, int& y0) {
@@ -974,8 +982,8 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_ws(
       produce_write(buf0, pf);
       if (NS > 1) produce_loads(1, pf);
     }
-  } else if constexpr (PST) {
-    for (int i = tid; i < COUT; i += C::NWC * 64) reinterpret_cast<float*>(smem + 2 * C::BUF)[i] = bias[i];
+  } else {
+    for (int i = tid; i < COUT; i += C::NWC * 64) reinterpret_cast<float*>(smem + C::BIAS_OFF)[i] = bias[i];
   }
   __syncthreads();
 
@@ -1027,9 +1035,9 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_ws(
 
   // ---- compute side ----
   const int wm = wave / WN, wn = wave % WN;
-  // PST: the bias in LDS (read right after the tile's last stage barrier, where a global load's
-  // latency would hold up every wave)
-  float* const sbias = reinterpret_cast<float*>(smem + 2 * C::BUF);
+  // the bias from LDS (a global load in the epilogue would wait for the weight prefetch ahead of it
+  // in vmcnt; with PST it would hold up every wave after the tile's last stage barrier)
+  const float* const sbias = reinterpret_cast<const float*>(smem + C::BIAS_OFF);
   int abase[C::MT], ylr[C::MT];
 #pragma unroll
   for (int mt = 0; mt < C::MT; ++mt) {
@@ -1147,7 +1155,7 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_ws(
         float4 bv[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-          bv[q] = *reinterpret_cast<const float4*>(bias + (wn * C::NT + nt) * 32 + 8 * q + 4 * h);
+          bv[q] = *reinterpret_cast<const float4*>(sbias + (wn * C::NT + nt) * 32 + 8 * q + 4 * h);
 #pragma unroll
         for (int mt = 0; mt < C::MT; ++mt) {
           const bool ok = NP == 1 || p0 + ((wm * C::MT + mt) * 32) / (TR * C::WOUT) < P;
