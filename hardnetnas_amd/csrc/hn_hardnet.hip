@@ -736,9 +736,6 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void k_conv_pipe(
 // barrier per stage.  For the HBM-heavy stride-2 layers this keeps ~UNITS*32 B per
 // workgroup in flight instead of one unit per K-step.
 // ------------------------------------------------------------------------------------
-#ifndef HN_PST_KY
-#define HN_PST_KY 2
-#endif
 template <int CIN, int COUT, int HIN, int S, int NP, int TR, int WM, int WN, bool STEM = false, int PX = 80,
           bool CST = false, bool PST = false>
 struct WsCfg : ConvCfg<CIN, COUT, HIN, S, NP, TR, WM, WN, PX> {
@@ -1100,8 +1097,9 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_ws(
       if (ksx + 1 < NKS) load_a(ksx + 1, aq[(ksx + 1) & 1]);
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (PST) {
-        constexpr int KY = HN_PST_KY;  // B_y of the previous tile (see pstore)
-        if (ksx == KY && cc == 0 && s > 0) __builtin_amdgcn_s_barrier();
+        // B_y of the previous tile (see pstore), at the first K-step: same-box conv4 6.93 ms there,
+        // 6.95 at K-step 1, 7.02 at 2, 7.09 at 4; the producers' window writes wait for it
+        if (ksx == 0 && cc == 0 && s > 0) __builtin_amdgcn_s_barrier();
       }
 #pragma unroll
       for (int mt = 0; mt < C::MT; ++mt) {
