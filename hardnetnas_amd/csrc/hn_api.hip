@@ -38,6 +38,7 @@ void hn_read_knobs(HnKnobs* k) {
   k->pairdist_valu = std::getenv("HN_PAIRDIST_VALU") != nullptr;
   k->pairdist_reg = env_int("HN_PAIRDIST_REG", 0) != 0;
   k->front_fold = env_int("HN_FRONT_FOLD", 0) != 0;
+  k->front_k5 = env_int("HN_FRONT_K5", 0) & 3;
   k->train_splitk = std::max(32, env_int("HN_TRAIN_SPLITK", 1024)) / 32 * 32;
   k->train_f32 = env_int("HN_TRAIN_F32", 1) & 255;
 #ifdef HN_EXPERIMENTS
@@ -784,6 +785,8 @@ extern "C" int hn_create(const hn_arch_desc* desc, const float* host_params, siz
       else if (*c >= 'a' && *c <= 'z') m->variant[i++] = 10 + (*c - 'a');
   }
   hn_read_knobs(&m->knobs);
+  // k_head4 takes 256 patches per workgroup: chunks of 65,536 keep every CU busy in the head
+  if (m->knobs.head == 4 && !std::getenv("HN_CHUNK")) m->chunk = 65536;
   for (int l = 0; l < 6; ++l)
     if (!hn_hardnet_variant_ok(l, m->variant[l])) {
       const std::string msg = "HN_VARIANT: tiling " + std::to_string(m->variant[l]) +
@@ -795,9 +798,9 @@ extern "C" int hn_create(const hn_arch_desc* desc, const float* host_params, siz
     delete m;
     return fail(HN_ERR_ARG, "HN_C12_CFG / HN_C12_ABL: no such k_c12 build in this library");
   }
-  if (m->knobs.head < 1 || m->knobs.head > 3) {
+  if (m->knobs.head < 1 || m->knobs.head > 4) {
     delete m;
-    return fail(HN_ERR_ARG, "HN_HEAD: head GEMM form must be 1, 2 or 3");
+    return fail(HN_ERR_ARG, "HN_HEAD: head GEMM form must be 1, 2, 3 or 4");
   }
   (void)hipGetDevice(&m->device);
   Cursor cur{host_params, n_params};

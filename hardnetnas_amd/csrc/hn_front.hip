@@ -62,7 +62,7 @@ __constant__ unsigned char kDwLane[64] = {
 // 1 / 4 KiB of HBM per patch and no intermediate fp32 tensor exists.  (PIL mode stays unfused:
 // its 12 prefetched byte registers took the k3 front from three workgroups per CU to two, wang2
 // front 5.7 -> 7.2 ms, against 0.46 ms for the separate hn_preprocess.)
-template <int K, int MID, int MODE, bool NORM, bool NF, int U8 = -1>
+template <int K, int MID, int MODE, bool NORM, bool NF, int U8 = -1, int DY5 = 1>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRONT_IRF && K == 3 && MID == 32 ? 3 : 1))) void k_front(const void* __restrict__ in_,
                                                float* __restrict__ out,
                                                const uint4* __restrict__ spack,  // stem A operand
@@ -88,7 +88,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRO
   constexpr bool LEAN = MODE == FRONT_IRF && K == 3 && MID == 32;
   constexpr int NT = LEAN ? 2 : (IR + 3) / 4;  // row tiles per wave (at most)
   constexpr int OC = 32;  // layer-0 output channels (SEARCH_SPACE2[0] = (32, 32, 2))
-  constexpr int DYU = KK == 3 ? 3 : 1;  // k5: rolled dy loop keeps VGPRs (and occupancy) in check
+  constexpr int DYU = KK == 3 ? 3 : DY5;  // k5: rolled dy loop keeps VGPRs (and occupancy) in check
   constexpr bool RING = MID == 32;
   constexpr bool SPLIT = MODE == FRONT_IRF;                  // even/odd column split
   constexpr int HALF = (PC + 1) / 2;                         // first odd-column position
@@ -456,14 +456,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRO
   }
 }
 
-template <int K, int MID, int MODE, bool NORM, bool NF, int U8 = -1>
+template <int K, int MID, int MODE, bool NORM, bool NF, int U8 = -1, int DY5 = 1>
 hipError_t front_launch_nf(const HnFrontArgs& a, int P, float eps, hipStream_t st, const HnU8In* u8 = nullptr) {
   int resident = 0;  // persistent grid: every workgroup resident at once
   const hipError_t e =
-      hn_resident_blocks(reinterpret_cast<const void*>(&k_front<K, MID, MODE, NORM, NF, U8>), 256, 0, &resident);
+      hn_resident_blocks(reinterpret_cast<const void*>(&k_front<K, MID, MODE, NORM, NF, U8, DY5>), 256, 0, &resident);
   if (e != hipSuccess) return e;
   const void* src = u8 ? static_cast<const void*>(u8->in) : static_cast<const void*>(a.in);
-  hipLaunchKernelGGL((k_front<K, MID, MODE, NORM, NF, U8>), dim3(std::min(P, resident)), dim3(256), 0, st, src,
+  hipLaunchKernelGGL((k_front<K, MID, MODE, NORM, NF, U8, DY5>), dim3(std::min(P, resident)), dim3(256), 0, st, src,
                      a.out, a.spack, a.stem_b, a.apack, a.pw_b, a.dw_w, a.dw_b, a.pwl_a, a.pwl_b, a.pwl_a16, P,
                      eps, u8 ? u8->mean : 0.f, u8 ? u8->stdv : 1.f, u8 ? u8->normalize : 0);
   return hipGetLastError();
@@ -491,6 +491,13 @@ hipError_t front_launch_t(const HnFrontArgs& a, int P, float eps, hipStream_t st
           return front_launch_nf<K, MID, MODE, false, NFD, HN_RESIZE_CV2_LINEAR>(a, P, eps, st, u8);
       }
       return hipErrorInvalidValue;
+    }
+  }
+  if constexpr (K == 5 && MID == 32 && MODE == FRONT_IRF) {  // HN_FRONT_K5 (A/B): 1 dy unrolled, 2 no fold, 3 both
+    switch (hn_knobs().front_k5) {
+      case 1: return front_launch_nf<K, MID, MODE, NORM, false, -1, 5>(a, P, eps, st);
+      case 2: return front_launch_nf<K, MID, MODE, NORM, true, -1, 1>(a, P, eps, st);
+      case 3: return front_launch_nf<K, MID, MODE, NORM, true, -1, 5>(a, P, eps, st);
     }
   }
   if (nf) return front_launch_nf<K, MID, MODE, NORM, true>(a, P, eps, st);

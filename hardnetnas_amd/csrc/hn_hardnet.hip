@@ -1521,6 +1521,149 @@ __global__ __launch_bounds__(512) void k_head3(const float* __restrict__ a, floa
 }
 
 // ------------------------------------------------------------------------------------
+// k_head4: k_head3 at 256 patches per workgroup.  The head is bound by what one CU can pull
+// through LDS-DMA (~12 B/clk: per 128-patch k_head3 chunk 16 KB of activations + 16 KB of weights
+// arrive in ~2,700 cycles against ~770 MFMA cycles per SIMD), and half of those bytes are the
+// weights, re-streamed by every workgroup.  256 patches per workgroup carry the same 16 KB of
+// weights per chunk for twice the activations: 48 KB per 256 patches instead of 64 KB.  Each of
+// the 8 waves owns 32 patches x all 128 columns (4 accumulator tiles), so every activation
+// fragment is split once (k_head3 splits each twice, once per column half).  Rings: A DA x 32 KB,
+// B DB x 16 KB.  The DMA schedule, the K-chunk accumulation order and the L2 norm's summation
+// order (two 64-column half sums, then + l2eps) are k_head3's: bit-identical results.
+// ------------------------------------------------------------------------------------
+template <int K, bool F16, int DA, int DB>
+__global__ __launch_bounds__(512) void k_head4(const float* __restrict__ a, float* __restrict__ out,
+                                               const uint4* __restrict__ wp,
+                                               const float* __restrict__ bias, int P, float l2eps) {
+  constexpr int KC = 32, NCH = K / KC, M = 256;
+  constexpr int ABYTES = M * KC * 4;           // 32 KB per A chunk: 4 DMA instructions per wave
+  constexpr int BBYTES = 2 * 4 * 2 * 64 * 16;  // 16 KB per B chunk: 2 per wave
+  constexpr int NA = 4, NB = 2;
+  static_assert(DA >= 2 && DB >= 2 && NCH >= DA && NCH >= DB && DA * 32 + DB * 16 <= 152, "rings");
+  typedef __attribute__((address_space(3))) void* lds_ptr_t;
+  __shared__ __attribute__((aligned(16))) char sa[DA * ABYTES];
+  __shared__ __attribute__((aligned(16))) char sbw[DB * BBYTES];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, h = lane >> 5;
+  const int pbase = blockIdx.x * M;
+
+  const float* asrc[NA];
+  const uint4* bsrc[NB];
+  unsigned adst[NA], bdst[NB];
+#pragma unroll
+  for (int k = 0; k < NA; ++k) {
+    const int gi = NA * wave + k, s = gi * 64 + lane, row = s >> 3, c = (s & 7) ^ ((row >> 1) & 7);
+    asrc[k] = a + (size_t)min(pbase + row, P - 1) * K + c * 4;
+    adst[k] = (unsigned)(uintptr_t)(lds_ptr_t)(sa + gi * 1024);
+  }
+#pragma unroll
+  for (int k = 0; k < NB; ++k) {
+    const int gi = NB * wave + k;
+    bsrc[k] = wp + gi * 64 + lane;
+    bdst[k] = (unsigned)(uintptr_t)(lds_ptr_t)(sbw + gi * 1024);
+  }
+  auto dma = [](const void* src, unsigned dst) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
+  };
+  auto live = [](int chunk) { return chunk >= 0 && chunk < NCH; };
+  constexpr int J0 = 1 - (DA > DB ? DA : DB);  // first (prologue) iteration
+  auto issue = [&](int j) {  // iteration j's DMA: B(j + DB - 1), then A(j + DA - 1)
+    const int cb = j + DB - 1, ca = j + DA - 1;
+    if (live(cb)) {
+      const unsigned so = (unsigned)(cb % DB) * BBYTES;
+#pragma unroll
+      for (int k = 0; k < NB; ++k) dma(bsrc[k] + (size_t)cb * 1024, bdst[k] + so);
+    }
+    if (live(ca)) {
+      const unsigned so = (unsigned)(ca % DA) * ABYTES;
+#pragma unroll
+      for (int k = 0; k < NA; ++k) dma(asrc[k] + (size_t)ca * KC, adst[k] + so);
+    }
+  };
+  // this wave's DMA instructions issued after the latest one of A(c) / B(c): walk the issue
+  // sequence back from iteration c - 1 to the first group belonging to chunk c
+  auto after = [&](int c) {
+    int n = 0;
+    for (int i = c - 1; i >= J0; --i) {
+      if (live(i + DA - 1)) {
+        if (i + DA - 1 == c) return n;
+        n += NA;
+      }
+      if (live(i + DB - 1)) {
+        if (i + DB - 1 == c) return n;
+        n += NB;
+      }
+    }
+    return 0;
+  };
+  const int arow = 32 * wave + r, asw = (arow >> 1) & 7;
+  f32x16 acc[4] = {f32x16{}, f32x16{}, f32x16{}, f32x16{}};
+  for (int j = J0; j < 0; ++j) issue(j);
+#pragma unroll 1
+  for (int c = 0; c < NCH; ++c) {
+    switch (after(c)) {
+      case 0: head_wait_vm<0>(); break;
+      case 2: head_wait_vm<2>(); break;
+      case 4: head_wait_vm<4>(); break;
+      case 6: head_wait_vm<6>(); break;
+      case 8: head_wait_vm<8>(); break;
+      case 10: head_wait_vm<10>(); break;
+      case 12: head_wait_vm<12>(); break;
+      case 14: head_wait_vm<14>(); break;
+      case 16: head_wait_vm<16>(); break;
+      case 18: head_wait_vm<18>(); break;
+      case 20: head_wait_vm<20>(); break;
+      case 22: head_wait_vm<22>(); break;
+      default: head_wait_vm<0>(); break;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    issue(c);
+    const char* ast = sa + (c % DA) * ABYTES + arow * (KC * 4);
+    const char* bst = sbw + (c % DB) * BBYTES;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int p0 = 4 * ks + 2 * h;
+      const float4 x0 = *reinterpret_cast<const float4*>(ast + ((p0 ^ asw) << 4));
+      const float4 x1 = *reinterpret_cast<const float4*>(ast + (((p0 + 1) ^ asw) << 4));
+      uint4 ah, al;
+      if (F16) split8_f16(x0, x1, ah, al);
+      else split8(x0, x1, ah, al);
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const char* bp = bst + ((((ks * 4 + nt) * 2) * 64 + lane) << 4);
+        const uint4 bh = *reinterpret_cast<const uint4*>(bp);
+        const uint4 bl = *reinterpret_cast<const uint4*>(bp + 1024);
+        if (F16)
+          acc[nt] = mfma3_f16(as_f16x8(ah), as_f16x8(al), as_f16x8(bh), as_f16x8(bl), acc[nt]);
+        else
+          acc[nt] = mfma3(as_bf16x8(ah), as_bf16x8(al), as_bf16x8(bh), as_bf16x8(bl), acc[nt]);
+      }
+    }
+  }
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) {
+    const float b = bias[32 * nt + r];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[nt][i] += b;
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    // k_head3's order: each 64-column half summed over its lanes, then the halves + l2eps
+    const float s01 = half_sum(acc[0][i] * acc[0][i] + acc[1][i] * acc[1][i]);
+    const float s23 = half_sum(acc[2][i] * acc[2][i] + acc[3][i] * acc[3][i]);
+    const float norm = sqrtf(s01 + s23 + l2eps);
+    const int p = pbase + 32 * wave + (i & 3) + 8 * (i >> 2) + 4 * h;
+    if (p < P) {
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) out[(size_t)p * 128 + 32 * nt + r] = acc[nt][i] / norm;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
 // host launchers
 // ------------------------------------------------------------------------------------
 // stem-fused kernels carry the normalised patch (34x34 fp32) + 8 reduction floats
@@ -1836,7 +1979,7 @@ hipError_t hn_launch_conv_raw(int layer, const void* wp, const float* zero_bias,
 hipError_t hn_launch_head(const float* a, float* out, const void* wp, const float* bias, int P,
                           int K, float l2eps, hipStream_t st, bool f16) {
   const int grid = (P + 63) / 64;
-  const int form = hn_knobs().head;  // HN_HEAD: 1 k_head, 2 k_head2, 3 k_head3 (default)
+  const int form = hn_knobs().head;  // HN_HEAD: 1 k_head, 2 k_head2, 3 k_head3 (default), 4 k_head4
   const uint4* w = static_cast<const uint4*>(wp);
 #define HN_HEAD3(KK, F, DA, DB)                                                                              \
   if (K == KK && f16 == F) {                                                                                 \
@@ -1846,10 +1989,21 @@ hipError_t hn_launch_head(const float* a, float* out, const void* wp, const floa
   }
   // both rings 4 deep (128 KB): same-box A/B of the HardNet head at A / B depths 4 / 4, 5 / 3, 5 / 4,
   // 4 / 5 = 2.11, 2.29, 2.33, 2.31 ms (k_head2 2.33)
-  if (form == 3) {
+  // k_head4 (256 patches per workgroup) when the launch still gives most CUs a workgroup
+#define HN_HEAD4(KK, F, DA, DB)                                                                              \
+  if (K == KK && f16 == F) {                                                                                 \
+    hipLaunchKernelGGL((k_head4<KK, F, DA, DB>), dim3((P + 255) / 256), dim3(512), 0, st, a, out, w, bias, P, \
+                       l2eps);                                                                               \
+    return hipGetLastError();                                                                                \
+  }
+  if (form == 4 && P >= 240 * 256) {
+    HN_HEAD4(8192, false, 3, 3) HN_HEAD4(2048, true, 3, 3)
+  }
+  if (form >= 3) {
     HN_HEAD3(8192, false, 4, 4) HN_HEAD3(2048, true, 4, 4)
   }
 #undef HN_HEAD3
+#undef HN_HEAD4
   if (K == 8192 && !f16 && form == 1)
     hipLaunchKernelGGL(k_head<8192>, dim3(grid), dim3(256), 0, st, a, out, w, bias, P, l2eps);
   else if (K == 8192 && !f16)

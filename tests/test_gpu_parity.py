@@ -413,6 +413,26 @@ def test_head_forms_are_bit_identical(name, cuda_device, monkeypatch):
     assert np.abs(y.cpu().numpy() - fx["y"]).max() <= _tol(name)
 
 
+@pytest.mark.parametrize("name", ["hardnet", "wang2"])
+def test_head4_is_bit_identical(name, cuda_device, monkeypatch):
+    """k_head4 (HN_HEAD=4: 256-patch workgroups, every wave all 128 columns, chunks of 65,536) keeps
+    k_head3's K-chunk order and L2 summation order: bit-identical descriptors at a ragged batch above
+    its 61,440-patch launch threshold (partial last workgroup), and at a small one (k_head3 runs)."""
+    from hardnetnas_amd._native import NativeModel
+    m, fx, _ = build_module(name)
+    g = golden_inputs(fx)
+    xb = torch.from_numpy(np.concatenate([g] * (61_517 // len(g) + 1))[:61_517]).to(cuda_device)
+    xs = torch.from_numpy(g[:37]).to(cuda_device)
+    nm = NativeModel.from_module(m, cuda_device)
+    yb, ys = nm(xb), nm(xs)
+    monkeypatch.setenv("HN_HEAD", "4")
+    nm4 = NativeModel.from_module(m, cuda_device)
+    nm4.set_profiling(True)
+    assert torch.equal(yb, nm4(xb))
+    assert torch.equal(ys, nm4(xs))
+    assert np.abs(yb[: len(g)].cpu().numpy() - fx["y"]).max() <= _tol(name)
+
+
 @pytest.mark.parametrize("name", ["wang2", "wang4"])
 def test_two_block_kernel_is_bit_identical(name, cuda_device, monkeypatch):
     """k_irf2 (layers 1+2 / 3+4 in one kernel, the activation between them in LDS) computes exactly
