@@ -30,7 +30,7 @@ static int env_int(const char* name, int dflt) {
 void hn_read_knobs(HnKnobs* k) {
   *k = HnKnobs{};
   k->c12_cfg = env_int("HN_C12_CFG", 12);
-  k->head = std::getenv("HN_HEAD_V1") ? 1 : env_int("HN_HEAD", 3);
+  k->head = std::getenv("HN_HEAD_V1") ? 1 : env_int("HN_HEAD", 4);
   k->fdl_valu = std::getenv("HN_FDL_VALU") != nullptr;
   k->naive_pw = std::getenv("HN_NAIVE_PW") != nullptr;
   k->naive_dw = std::getenv("HN_NAIVE_DW") != nullptr;
@@ -38,7 +38,7 @@ void hn_read_knobs(HnKnobs* k) {
   k->pairdist_valu = std::getenv("HN_PAIRDIST_VALU") != nullptr;
   k->pairdist_reg = env_int("HN_PAIRDIST_REG", 0) != 0;
   k->front_fold = env_int("HN_FRONT_FOLD", 0) != 0;
-  k->front_k5 = env_int("HN_FRONT_K5", 0) & 3;
+  k->front_k5 = env_int("HN_FRONT_K5", 0) & 7;
   k->train_splitk = std::max(32, env_int("HN_TRAIN_SPLITK", 1024)) / 32 * 32;
   k->train_f32 = env_int("HN_TRAIN_F32", 1) & 255;
 #ifdef HN_EXPERIMENTS

@@ -41,33 +41,11 @@ HN_DEV bf16x8 as_bf16x8(const uint4& v) { return __builtin_bit_cast(bf16x8, v); 
 // NAS front: no input_norm, ReLU outputs of O(1)); same MFMA rate as bf16.
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 // (v_fma_mix{lo,hi}_f16 for the lo half -- one instruction per value -- measured slower on
-// gfx950: k_irf 12.3 -> 13.7 ms)
-#ifdef HN_SPLIT_MIX
-// x - f32(h) in one v_fma_mix_f32 (h an fp16 half of a packed register), exact
-HN_DEV float mix_rem_lo(float x, unsigned hp) {
-  float r;
-  asm("v_fma_mix_f32 %0, %1, 1.0, -%2 op_sel:[0,0,0] op_sel_hi:[0,0,1]" : "=v"(r) : "v"(x), "v"(hp));
-  return r;
-}
-HN_DEV float mix_rem_hi(float x, unsigned hp) {
-  float r;
-  asm("v_fma_mix_f32 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "=v"(r) : "v"(x), "v"(hp));
-  return r;
-}
-#endif
+// gfx950: k_irf 12.3 -> 13.7 ms; so did v_fma_mix_f32 for x - f32(hi), two
+// instructions per value instead of three: wang2 17.6 -> 16.8, wang4 20.0 -> 19.4 Mpatches/s)
 HN_DEV void split8_f16(const float4& a, const float4& b, uint4& hi, uint4& lo) {
   const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
   f16x8 h, l;
-#ifdef HN_SPLIT_MIX
-#pragma unroll
-  for (int j = 0; j < 8; ++j) h[j] = (_Float16)v[j];
-  hi = __builtin_bit_cast(uint4, h);
-  const unsigned hw[4] = {hi.x, hi.y, hi.z, hi.w};
-#pragma unroll
-  for (int j = 0; j < 8; ++j) l[j] = (_Float16)((j & 1) ? mix_rem_hi(v[j], hw[j >> 1]) : mix_rem_lo(v[j], hw[j >> 1]));
-  lo = __builtin_bit_cast(uint4, l);
-  return;
-#endif
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     h[j] = (_Float16)v[j];

@@ -62,7 +62,7 @@ __constant__ unsigned char kDwLane[64] = {
 // 1 / 4 KiB of HBM per patch and no intermediate fp32 tensor exists.  (PIL mode stays unfused:
 // its 12 prefetched byte registers took the k3 front from three workgroups per CU to two, wang2
 // front 5.7 -> 7.2 ms, against 0.46 ms for the separate hn_preprocess.)
-template <int K, int MID, int MODE, bool NORM, bool NF, int U8 = -1, int DY5 = 1>
+template <int K, int MID, int MODE, bool NORM, bool NF, int U8 = -1, int DY5 = 1, bool P5 = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRONT_IRF && K == 3 && MID == 32 ? 3 : 1))) void k_front(const void* __restrict__ in_,
                                                float* __restrict__ out,
                                                const uint4* __restrict__ spack,  // stem A operand
@@ -86,7 +86,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRO
   // round trips on the row's latency chain cost more than they free (k5: register-bound at two
   // workgroups either way; maxpool: LDS-bound at three).
   constexpr bool LEAN = MODE == FRONT_IRF && K == 3 && MID == 32;
-  constexpr int NT = LEAN ? 2 : (IR + 3) / 4;  // row tiles per wave (at most)
+  // PAIR5 (k5, MID = 32): the k3 form's two-rows-per-gather stem on the k5 ring (8 new rows per
+  // band; band 0 has a ninth real row, which wave 0 computes alone as tile 2); biases stay in
+  // registers (the k5 front is LDS-bound at two workgroups per CU, not register-bound)
+  constexpr bool PAIR5 = P5 && MODE == FRONT_IRF && K == 5 && MID == 32;
+  constexpr bool RL = LEAN || PAIR5;  // the waves take only the band's real rows
+  constexpr int NT = LEAN ? 2 : PAIR5 ? 3 : (IR + 3) / 4;  // row tiles per wave (at most)
   constexpr int OC = 32;  // layer-0 output channels (SEARCH_SPACE2[0] = (32, 32, 2))
   constexpr int DYU = KK == 3 ? 3 : DY5;  // k5: rolled dy loop keeps VGPRs (and occupancy) in check
   constexpr bool RING = MID == 32;
@@ -124,7 +129,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRO
   // the 4 x 3 input window of the two rows (K slot 3 dy + dx, dy = 0..3; slots 12..15 carry any valid
   // input against zero weights), with the row-y taps in K slots 0..8 (spack op 0) and the row-(y + 1)
   // taps in slots 3..11 (op 1): one gather and one hi / lo split per two rows
-  constexpr bool PAIR = LEAN && NF;
+  constexpr bool PAIR = (LEAN && NF) || PAIR5;
   f16x8 sah2{}, sal2{};
   int toff[8] = {};  // PAIR: this lane's s_in offsets of its 8 K slots, from (row y0, column px)
   if constexpr (PAIR) {
@@ -227,8 +232,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRO
       const int ybeg = (RING && band > 0) ? ylast - 7 : 2 * r0 - PAD;
       // LEAN: the real rows yr0 .. go to the waves round-robin and the padding rows are
       // zero-filled apart; otherwise all rows ybeg .. ylast round-robin
-      const int yr0 = LEAN ? max(ybeg, 0) : ybeg;
-      const int nreal = LEAN ? min(ylast, 31) + 1 - yr0 : ylast + 1 - ybeg;
+      const int yr0 = RL ? max(ybeg, 0) : ybeg;
+      const int nreal = RL ? min(ylast, 31) + 1 - yr0 : ylast + 1 - ybeg;
 
       // ---- phase A: stem rows on the MFMA ------------------------------------------------
       // A = stem weights [32 ch][16 = 9 taps + 0], B = im2col of one image row (lane: pixel
@@ -238,15 +243,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRO
         float4* d = reinterpret_cast<float4*>(s_pw + slot_of(y) * RS);
         for (int j = lane; j < RS / 4; j += 64) d[j] = make_float4(0.f, 0.f, 0.f, 0.f);
       };
-      if constexpr (LEAN)
+      if constexpr (RL)
         for (int y = ybeg + w; y <= ylast; y += 4)
           if (y < 0 || y >= 32) zero_row(y);
       uint4 bh[NT][2], bl[NT][2];
-      // row tile i of this wave: band row 2w + i (PAIR) or w + 4i
-      auto row_of = [&](int i) { return PAIR ? 2 * w + i : w + 4 * i; };
+      // row tile i of this wave: band row 2w + i (PAIR; PAIR5's tile 2: band row 8) or w + 4i
+      // (PAIR5: the window base row y5 = min(y0, 30) keeps the 4-row window inside s_in; a wave
+      // whose y0 is 31 takes row 31 as op 1 of the window at 30, and drops tile 0 = row 30)
+      const int y5 = min(yr0 + 2 * w, 30);
+      auto row_of = [&](int i) { return PAIR5 ? (i < 2 ? y5 - yr0 + i : 8) : PAIR ? 2 * w + i : w + 4 * i; };
+      auto tile_on = [&](int i) {  // PAIR5: tile i holds a real row this wave owns
+        const int ri = row_of(i);
+        return i < 2 ? (ri >= 2 * w && ri < nreal) : (w == 0 && nreal > 8);
+      };
       if constexpr (PAIR) {
-        static_assert(!PAIR || NT == 2, "two rows per wave");
-        const int y0 = yr0 + 2 * w;  // rows y0, y0 + 1: real (LEAN bands hold 8 real rows)
+        static_assert(!PAIR || NT == 2 || PAIR5, "two rows per wave");
+        const int y0 = PAIR5 ? y5 : yr0 + 2 * w;  // rows y0, y0 + 1 (LEAN bands hold 8 real rows)
         const float* sb = s_in + y0 * 34 + px;
         float tp[8];
 #pragma unroll
@@ -255,8 +267,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRO
         split8_f16(make_float4(tp[0], tp[1], tp[2], tp[3]), make_float4(tp[4], tp[5], tp[6], tp[7]), xh, xl);
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-          const f32x16 c = i == 0 ? mfma3_f16(sah, sal, as_f16x8(xh), as_f16x8(xl), bias16(s_sb))
-                                  : mfma3_f16(sah2, sal2, as_f16x8(xh), as_f16x8(xl), bias16(s_sb));
+          const f32x16 c = i == 0 ? mfma3_f16(sah, sal, as_f16x8(xh), as_f16x8(xl), LDSB ? bias16(s_sb) : sbr)
+                                  : mfma3_f16(sah2, sal2, as_f16x8(xh), as_f16x8(xl), LDSB ? bias16(s_sb) : sbr);
           float4 o[4];
 #pragma unroll
           for (int q = 0; q < 4; ++q)
@@ -267,9 +279,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRO
         }
       }
 #pragma unroll
-      for (int i = 0; i < (PAIR ? 0 : NT); ++i) {
+      for (int i = (PAIR5 ? 2 : 0); i < (PAIR && !PAIR5 ? 0 : NT); ++i) {
         const int ri = row_of(i), y = yr0 + ri;
-        if (ri >= nreal) continue;  // wave-uniform; such tiles are never read
+        if (PAIR5 ? !tile_on(i) : ri >= nreal) continue;  // wave-uniform; such tiles are never read
         if (!LEAN && (y < 0 || y >= 32)) {
           zero_row(y);
           continue;
@@ -350,7 +362,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRO
 #pragma unroll
         for (int i = 0; i < NT; ++i) {
           const int ri = row_of(i), y = yr0 + ri;
-          if (ri >= nreal || y < 0 || y >= 32) continue;
+          if (PAIR5 ? !tile_on(i) : (ri >= nreal || y < 0 || y >= 32)) continue;
           if constexpr (LDSB) bias = bias16(s_pwb);
           f32x16 acc = mfma3_f16(ah0, al0, as_f16x8(bh[i][0]), as_f16x8(bl[i][0]), bias);
           acc = mfma3_f16(ah1, al1, as_f16x8(bh[i][1]), as_f16x8(bl[i][1]), acc);
@@ -456,14 +468,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRO
   }
 }
 
-template <int K, int MID, int MODE, bool NORM, bool NF, int U8 = -1, int DY5 = 1>
+template <int K, int MID, int MODE, bool NORM, bool NF, int U8 = -1, int DY5 = 1, bool P5 = false>
 hipError_t front_launch_nf(const HnFrontArgs& a, int P, float eps, hipStream_t st, const HnU8In* u8 = nullptr) {
   int resident = 0;  // persistent grid: every workgroup resident at once
   const hipError_t e =
-      hn_resident_blocks(reinterpret_cast<const void*>(&k_front<K, MID, MODE, NORM, NF, U8, DY5>), 256, 0, &resident);
+      hn_resident_blocks(reinterpret_cast<const void*>(&k_front<K, MID, MODE, NORM, NF, U8, DY5, P5>), 256, 0, &resident);
   if (e != hipSuccess) return e;
   const void* src = u8 ? static_cast<const void*>(u8->in) : static_cast<const void*>(a.in);
-  hipLaunchKernelGGL((k_front<K, MID, MODE, NORM, NF, U8, DY5>), dim3(std::min(P, resident)), dim3(256), 0, st, src,
+  hipLaunchKernelGGL((k_front<K, MID, MODE, NORM, NF, U8, DY5, P5>), dim3(std::min(P, resident)), dim3(256), 0, st, src,
                      a.out, a.spack, a.stem_b, a.apack, a.pw_b, a.dw_w, a.dw_b, a.pwl_a, a.pwl_b, a.pwl_a16, P,
                      eps, u8 ? u8->mean : 0.f, u8 ? u8->stdv : 1.f, u8 ? u8->normalize : 0);
   return hipGetLastError();
@@ -494,10 +506,14 @@ hipError_t front_launch_t(const HnFrontArgs& a, int P, float eps, hipStream_t st
     }
   }
   if constexpr (K == 5 && MID == 32 && MODE == FRONT_IRF) {  // HN_FRONT_K5 (A/B): 1 dy unrolled, 2 no fold, 3 both
-    switch (hn_knobs().front_k5) {
+    switch (hn_knobs().front_k5) {  // bit 0: dy unrolled, bit 1: no fold, bit 2: paired stem rows
       case 1: return front_launch_nf<K, MID, MODE, NORM, false, -1, 5>(a, P, eps, st);
       case 2: return front_launch_nf<K, MID, MODE, NORM, true, -1, 1>(a, P, eps, st);
       case 3: return front_launch_nf<K, MID, MODE, NORM, true, -1, 5>(a, P, eps, st);
+      case 4: return front_launch_nf<K, MID, MODE, NORM, false, -1, 1, true>(a, P, eps, st);
+      case 5: return front_launch_nf<K, MID, MODE, NORM, false, -1, 5, true>(a, P, eps, st);
+      case 6: return front_launch_nf<K, MID, MODE, NORM, true, -1, 1, true>(a, P, eps, st);
+      case 7: return front_launch_nf<K, MID, MODE, NORM, true, -1, 5, true>(a, P, eps, st);
     }
   }
   if (nf) return front_launch_nf<K, MID, MODE, NORM, true>(a, P, eps, st);

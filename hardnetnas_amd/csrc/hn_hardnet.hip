@@ -1979,7 +1979,7 @@ hipError_t hn_launch_conv_raw(int layer, const void* wp, const float* zero_bias,
 hipError_t hn_launch_head(const float* a, float* out, const void* wp, const float* bias, int P,
                           int K, float l2eps, hipStream_t st, bool f16) {
   const int grid = (P + 63) / 64;
-  const int form = hn_knobs().head;  // HN_HEAD: 1 k_head, 2 k_head2, 3 k_head3 (default), 4 k_head4
+  const int form = hn_knobs().head;  // HN_HEAD: 1 k_head, 2 k_head2, 3 k_head3, 4 k_head4 (default; k_head3 below 61,440 patches)
   const uint4* w = static_cast<const uint4*>(wp);
 #define HN_HEAD3(KK, F, DA, DB)                                                                              \
   if (K == KK && f16 == F) {                                                                                 \

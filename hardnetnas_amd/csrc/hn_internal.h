@@ -11,7 +11,7 @@
 // dbg: timing-only builds with wrong results) exist only in the HN_EXPERIMENTS library.
 struct HnKnobs {
   int c12_cfg = 12;            // HN_C12_CFG: k_c12 configuration (0..12, all exact)
-  int head = 3;                // HN_HEAD: head GEMM form (1 k_head, 2 k_head2, 3 k_head3 LDS-DMA rings, 4 k_head4)
+  int head = 4;                // HN_HEAD: head GEMM form (1 k_head, 2 k_head2, 3 k_head3 LDS-DMA rings, 4 k_head4 256-patch rings)
   bool fdl_valu = false;       // HN_FDL_VALU: FDLNet front as fp32 VALU
   bool naive_pw = false;       // HN_NAIVE_PW: untiled 1x1 conv kernel
   bool naive_dw = false;       // HN_NAIVE_DW: untiled depthwise kernel
@@ -19,7 +19,7 @@ struct HnKnobs {
   bool pairdist_valu = false;  // HN_PAIRDIST_VALU: fp32 VALU pair-distance kernel
   bool pairdist_reg = false;   // HN_PAIRDIST_REG: register-staged positives instead of the LDS-DMA ring
   bool front_fold = false;     // HN_FRONT_FOLD: the NAS front's pwl with the LDS partial-sum fold
-  int front_k5 = 0;            // HN_FRONT_K5 (A/B): k5 MID-32 front, 1 dy loop unrolled, 2 no fold, 3 both
+  int front_k5 = 0;            // HN_FRONT_K5 (A/B): k5 MID-32 front, bit 0 dy loop unrolled, bit 1 no fold, bit 2 paired stem rows
   int train_splitk = 1024;     // HN_TRAIN_SPLITK: K per split-K slice of the train GEMMs
   int train_f32 = 1;           // HN_TRAIN_F32: bit 0 train forward convs, bit 1 stride-1 dgrads as f32-MFMA
                                // GEMMs (else the bf16x3 conv kernels); default 1 = every product f32;
