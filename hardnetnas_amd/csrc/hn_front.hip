@@ -62,7 +62,7 @@ __constant__ unsigned char kDwLane[64] = {
 // 1 / 4 KiB of HBM per patch and no intermediate fp32 tensor exists.  (PIL mode stays unfused:
 // its 12 prefetched byte registers took the k3 front from three workgroups per CU to two, wang2
 // front 5.7 -> 7.2 ms, against 0.46 ms for the separate hn_preprocess.)
-template <int K, int MID, int MODE, bool NORM, bool NF, int U8 = -1, int DY5 = 1, bool P5 = false>
+template <int K, int MID, int MODE, bool NORM, bool NF, int U8 = -1, bool P5 = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRONT_IRF && K == 3 && MID == 32 ? 3 : 1))) void k_front(const void* __restrict__ in_,
                                                float* __restrict__ out,
                                                const uint4* __restrict__ spack,  // stem A operand
@@ -93,7 +93,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRO
   constexpr bool RL = LEAN || PAIR5;  // the waves take only the band's real rows
   constexpr int NT = LEAN ? 2 : PAIR5 ? 3 : (IR + 3) / 4;  // row tiles per wave (at most)
   constexpr int OC = 32;  // layer-0 output channels (SEARCH_SPACE2[0] = (32, 32, 2))
-  constexpr int DYU = KK == 3 ? 3 : DY5;  // k5: rolled dy loop keeps VGPRs (and occupancy) in check
+  constexpr int DYU = KK == 3 ? 3 : 1;  // k5: rolled dy loop keeps VGPRs (and occupancy) in check
   constexpr bool RING = MID == 32;
   constexpr bool SPLIT = MODE == FRONT_IRF;                  // even/odd column split
   constexpr int HALF = (PC + 1) / 2;                         // first odd-column position
@@ -468,55 +468,49 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRO
   }
 }
 
-template <int K, int MID, int MODE, bool NORM, bool NF, int U8 = -1, int DY5 = 1, bool P5 = false>
+template <int K, int MID, int MODE, bool NORM, bool NF, int U8 = -1, bool P5 = false>
 hipError_t front_launch_nf(const HnFrontArgs& a, int P, float eps, hipStream_t st, const HnU8In* u8 = nullptr) {
   int resident = 0;  // persistent grid: every workgroup resident at once
   const hipError_t e =
-      hn_resident_blocks(reinterpret_cast<const void*>(&k_front<K, MID, MODE, NORM, NF, U8, DY5, P5>), 256, 0, &resident);
+      hn_resident_blocks(reinterpret_cast<const void*>(&k_front<K, MID, MODE, NORM, NF, U8, P5>), 256, 0, &resident);
   if (e != hipSuccess) return e;
   const void* src = u8 ? static_cast<const void*>(u8->in) : static_cast<const void*>(a.in);
-  hipLaunchKernelGGL((k_front<K, MID, MODE, NORM, NF, U8, DY5, P5>), dim3(std::min(P, resident)), dim3(256), 0, st, src,
+  hipLaunchKernelGGL((k_front<K, MID, MODE, NORM, NF, U8, P5>), dim3(std::min(P, resident)), dim3(256), 0, st, src,
                      a.out, a.spack, a.stem_b, a.apack, a.pw_b, a.dw_w, a.dw_b, a.pwl_a, a.pwl_b, a.pwl_a16, P,
                      eps, u8 ? u8->mean : 0.f, u8 ? u8->stdv : 1.f, u8 ? u8->normalize : 0);
   return hipGetLastError();
 }
 
-// the production form of (K, MODE): the no-fold pwl for k3 IRF fronts
-template <int K, int MODE>
-constexpr bool front_nf() { return MODE == FRONT_IRF && K == 3; }
+// the production form of (K, MID, MODE): the no-fold pwl for the k3 IRF fronts and the k5 MID-32 one,
+// the latter with paired stem rows (same-box A/B, wang3 front ms per step: fold form 8.94, + dy loop
+// unrolled 8.56, no fold 9.19, no fold + dy unrolled 8.54, paired rows with the fold 8.16, paired rows
+// without it 8.13 (the default), both + dy unrolled 8.0-8.4)
+template <int K, int MID, int MODE>
+constexpr bool front_nf() { return MODE == FRONT_IRF && (K == 3 || (K == 5 && MID == 32)); }
+template <int K, int MID, int MODE>
+constexpr bool front_p5() { return MODE == FRONT_IRF && K == 5 && MID == 32; }
 
 template <int K, int MID, int MODE, bool NORM>
 hipError_t front_launch_t(const HnFrontArgs& a, int P, float eps, hipStream_t st, const HnU8In* u8) {
-  // HN_FRONT_FOLD=1: the 32x32x16 pwl with the partial-sum fold through LDS (the round-2 form)
-  // (k3 only: the k5 form measured 6 % slower without the fold -- its rolled dy loop keeps more live
-  // registers in the no-fold mapping; wang2 front k3 6.12 -> 5.59 ms, wang3 front k5 8.77 -> 9.30 ms)
-  const bool nf = MODE == FRONT_IRF && K == 3 && !hn_knobs().front_fold && a.pwl_a16;
+  // HN_FRONT_FOLD=1: the 32x32x16 pwl with the partial-sum fold through LDS (the round-2 form;
+  // wang2 front k3 6.12 -> 5.59 ms without it; the k5 front without the fold alone was 6 % slower, with
+  // the paired stem rows 9 % faster than the fold form)
+  const bool nf = front_nf<K, MID, MODE>() && !hn_knobs().front_fold && a.pwl_a16;
   if (u8) {  // uint8 loads (NONE / CV2): the production form without input_norm only (hn_api.hip u8_fused)
     if constexpr (NORM) {
       return hipErrorInvalidValue;
     } else {
-      if (nf != front_nf<K, MODE>()) return hipErrorInvalidValue;
-      constexpr bool NFD = front_nf<K, MODE>();
+      if (nf != front_nf<K, MID, MODE>()) return hipErrorInvalidValue;
+      constexpr bool NFD = front_nf<K, MID, MODE>(), P5D = front_p5<K, MID, MODE>();
       switch (u8->resize) {
-        case HN_RESIZE_NONE: return front_launch_nf<K, MID, MODE, false, NFD, HN_RESIZE_NONE>(a, P, eps, st, u8);
+        case HN_RESIZE_NONE: return front_launch_nf<K, MID, MODE, false, NFD, HN_RESIZE_NONE, P5D>(a, P, eps, st, u8);
         case HN_RESIZE_CV2_LINEAR:
-          return front_launch_nf<K, MID, MODE, false, NFD, HN_RESIZE_CV2_LINEAR>(a, P, eps, st, u8);
+          return front_launch_nf<K, MID, MODE, false, NFD, HN_RESIZE_CV2_LINEAR, P5D>(a, P, eps, st, u8);
       }
       return hipErrorInvalidValue;
     }
   }
-  if constexpr (K == 5 && MID == 32 && MODE == FRONT_IRF) {  // HN_FRONT_K5 (A/B): 1 dy unrolled, 2 no fold, 3 both
-    switch (hn_knobs().front_k5) {  // bit 0: dy unrolled, bit 1: no fold, bit 2: paired stem rows
-      case 1: return front_launch_nf<K, MID, MODE, NORM, false, -1, 5>(a, P, eps, st);
-      case 2: return front_launch_nf<K, MID, MODE, NORM, true, -1, 1>(a, P, eps, st);
-      case 3: return front_launch_nf<K, MID, MODE, NORM, true, -1, 5>(a, P, eps, st);
-      case 4: return front_launch_nf<K, MID, MODE, NORM, false, -1, 1, true>(a, P, eps, st);
-      case 5: return front_launch_nf<K, MID, MODE, NORM, false, -1, 5, true>(a, P, eps, st);
-      case 6: return front_launch_nf<K, MID, MODE, NORM, true, -1, 1, true>(a, P, eps, st);
-      case 7: return front_launch_nf<K, MID, MODE, NORM, true, -1, 5, true>(a, P, eps, st);
-    }
-  }
-  if (nf) return front_launch_nf<K, MID, MODE, NORM, true>(a, P, eps, st);
+  if (nf) return front_launch_nf<K, MID, MODE, NORM, true, -1, front_p5<K, MID, MODE>()>(a, P, eps, st);
   return front_launch_nf<K, MID, MODE, NORM, false>(a, P, eps, st);
 }
 

@@ -19,7 +19,6 @@ struct HnKnobs {
   bool pairdist_valu = false;  // HN_PAIRDIST_VALU: fp32 VALU pair-distance kernel
   bool pairdist_reg = false;   // HN_PAIRDIST_REG: register-staged positives instead of the LDS-DMA ring
   bool front_fold = false;     // HN_FRONT_FOLD: the NAS front's pwl with the LDS partial-sum fold
-  int front_k5 = 0;            // HN_FRONT_K5 (A/B): k5 MID-32 front, bit 0 dy loop unrolled, bit 1 no fold, bit 2 paired stem rows
   int train_splitk = 1024;     // HN_TRAIN_SPLITK: K per split-K slice of the train GEMMs
   int train_f32 = 1;           // HN_TRAIN_F32: bit 0 train forward convs, bit 1 stride-1 dgrads as f32-MFMA
                                // GEMMs (else the bf16x3 conv kernels); default 1 = every product f32;

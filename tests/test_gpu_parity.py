@@ -557,12 +557,13 @@ def test_nas_fused_skip_s2_matches_unfused(name, cuda_device, monkeypatch):
     assert "maxpool" in lw.stage_times() and "skip" not in lw.stage_times()
 
 
-@pytest.mark.parametrize("name", ["wang2", "cov_a", "cov_b", "cov_c"])
+@pytest.mark.parametrize("name", ["wang2", "wang3", "cov_a", "cov_b", "cov_c"])
 def test_front_pwl_forms_match_reference(name, cuda_device, monkeypatch):
     """The NAS front's two pwl forms -- the default 16x16x32 one (wave = band row, no partial-sum
-    fold) and the round-2 32x32x16 one with the fold through LDS (HN_FRONT_FOLD=1) -- both against
-    the reference vectors (MID 32 / 96 / 128, with and without groups and SE), and close to each
-    other (they differ only in the pwl's summation order)."""
+    fold; for k3 and the k5 MID-32 front (wang3) with two stem rows per gathered window) and the
+    round-2 32x32x16 one with the fold through LDS (HN_FRONT_FOLD=1) -- both against the reference
+    vectors (MID 32 / 96 / 128, k3 / k5, with and without groups and SE), and close to each other
+    (they differ only in summation orders)."""
     from hardnetnas_amd._native import NativeModel
     m, fx, _ = build_module(name)
     x = torch.from_numpy(golden_inputs(fx)).to(cuda_device)

@@ -2,13 +2,13 @@
 # Per-stage PMC passes (tools/pmc_groups_stage.txt: FETCH_SIZE, WRITE_SIZE, then the SQ instruction
 # / busy counters; one rocprofv3 --pmc pass each, --kernel-trace only) for each model, then
 # tools/pmc_stage.py -> gpurun_out/pmc_<model>.json (copy to profiles/ for bench.py's roofline).
-# hardnet / NAS: batch 32,768 x (1 warmup + 1 timed step) = 65,536 patches; c5: the config-5 pair
+# hardnet / NAS: batch 65,536 (k_head4 runs) x (1 warmup + 1 timed step) = 131,072 patches; c5: the config-5 pair
 # step at 65,536 pairs x 2 launches.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 for M in ${MODELS:-hardnet wang2 wang3 wang4 c5}; do
   rm -rf gpurun_out/pmc_$M; mkdir -p gpurun_out/pmc_$M
-  if [ "$M" = c5 ]; then ARGS="--config 5 --batch 65536"; UNITS=131072; else ARGS="--model $M --batch 32768"; UNITS=65536; fi
+  if [ "$M" = c5 ]; then ARGS="--config 5 --batch 65536"; UNITS=131072; else ARGS="--model $M --batch 65536"; UNITS=131072; fi
   i=0
   while IFS= read -r group; do
     [ -z "$group" ] && continue

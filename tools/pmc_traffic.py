@@ -26,7 +26,7 @@ def stage_of(name: str):
         key = (int(m.group(1)), int(m.group(2)), int(m.group(3)), int(m.group(4) == "true"))
         return HARDNET.get(key)
     for k, st in (("k_c12<", "stem+conv1+conv2"), ("k_front<", "front"), ("k_irf<", "irf"),
-                  ("k_head<", "head"), ("k_head2<", "head"), ("k_head3<", "head")):
+                  ("k_head<", "head"), ("k_head2<", "head"), ("k_head3<", "head"), ("k_head4<", "head")):
         if k in name:
             return st
     if "k_stem<" in name:
