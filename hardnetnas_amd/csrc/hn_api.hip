@@ -785,7 +785,7 @@ extern "C" int hn_create(const hn_arch_desc* desc, const float* host_params, siz
   }
   hn_read_knobs(&m->knobs);
   // k_head4 takes 256 patches per workgroup: chunks of 65,536 keep every CU busy in the head
-  if (m->knobs.head >= 4 && !std::getenv("HN_CHUNK")) m->chunk = m->knobs.head == 5 ? 131072 : 65536;
+  if (m->knobs.head == 4 && !std::getenv("HN_CHUNK")) m->chunk = 65536;
   for (int l = 0; l < 6; ++l)
     if (!hn_hardnet_variant_ok(l, m->variant[l])) {
       const std::string msg = "HN_VARIANT: tiling " + std::to_string(m->variant[l]) +
@@ -797,9 +797,9 @@ extern "C" int hn_create(const hn_arch_desc* desc, const float* host_params, siz
     delete m;
     return fail(HN_ERR_ARG, "HN_C12_CFG / HN_C12_ABL: no such k_c12 build in this library");
   }
-  if (m->knobs.head < 1 || m->knobs.head > 5) {
+  if (m->knobs.head < 1 || m->knobs.head > 4) {
     delete m;
-    return fail(HN_ERR_ARG, "HN_HEAD: head GEMM form must be 1 .. 5");
+    return fail(HN_ERR_ARG, "HN_HEAD: head GEMM form must be 1, 2, 3 or 4");
   }
   (void)hipGetDevice(&m->device);
   Cursor cur{host_params, n_params};

@@ -1664,147 +1664,6 @@ __global__ __launch_bounds__(512) void k_head4(const float* __restrict__ a, floa
 }
 
 // ------------------------------------------------------------------------------------
-// k_head5: 512 patches per workgroup on 16-wide K-chunks (A 32 KB + B 8 KB per chunk: 40 KB per
-// 512 patches where k_head4 moves 48 KB per 256), 8 waves x 64 patches (two 32-patch M-tiles) x
-// all 128 columns -- every B fragment read from LDS feeds both M-tiles.  A rows are 64 B (four
-// 16-byte pieces), piece c of row j at c ^ ((j >> 2) & 3): conflict-free for the ds_read_b128 lane
-// groups of a fragment read.  Chunk c' = 2c + ks of k_head3 / k_head4, so the accumulation order and
-// the L2 summation are theirs: bit-identical results.
-// ------------------------------------------------------------------------------------
-HN_DEV void head_wait_vm_dyn(int n) {  // s_waitcnt vmcnt(n) for a wave-uniform n (0 if out of range)
-  switch (n) {
-#define HN_W(N) case N: head_wait_vm<N>(); break;
-    HN_W(1) HN_W(2) HN_W(3) HN_W(4) HN_W(5) HN_W(6) HN_W(7) HN_W(8) HN_W(9) HN_W(10) HN_W(11) HN_W(12)
-    HN_W(13) HN_W(14) HN_W(15) HN_W(16) HN_W(17) HN_W(18) HN_W(19) HN_W(20) HN_W(21) HN_W(22) HN_W(23) HN_W(24)
-#undef HN_W
-    default: head_wait_vm<0>(); break;
-  }
-}
-
-template <int K, bool F16, int DA, int DB>
-__global__ __launch_bounds__(512) void k_head5(const float* __restrict__ a, float* __restrict__ out,
-                                               const uint4* __restrict__ wp,
-                                               const float* __restrict__ bias, int P, float l2eps) {
-  constexpr int KC = 16, NCH = K / KC, M = 512;
-  constexpr int ABYTES = M * KC * 4;       // 32 KB per A chunk: 4 DMA instructions per wave
-  constexpr int BBYTES = 4 * 2 * 64 * 16;  // 8 KB per B chunk: 1 per wave
-  constexpr int NA = 4, NB = 1;
-  static_assert(DA >= 2 && DB >= 2 && NCH >= DA && NCH >= DB && DA * 32 + DB * 8 <= 152, "rings");
-  typedef __attribute__((address_space(3))) void* lds_ptr_t;
-  __shared__ __attribute__((aligned(16))) char sa[DA * ABYTES];
-  __shared__ __attribute__((aligned(16))) char sbw[DB * BBYTES];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int r = lane & 31, h = lane >> 5;
-  const int pbase = blockIdx.x * M;
-
-  const float* asrc[NA];
-  unsigned adst[NA];
-#pragma unroll
-  for (int k = 0; k < NA; ++k) {
-    const int gi = NA * wave + k, s = gi * 64 + lane, row = s >> 2, c = (s & 3) ^ ((row >> 2) & 3);
-    asrc[k] = a + (size_t)min(pbase + row, P - 1) * K + c * 4;
-    adst[k] = (unsigned)(uintptr_t)(lds_ptr_t)(sa + gi * 1024);
-  }
-  const uint4* bsrc = wp + wave * 64 + lane;
-  const unsigned bdst = (unsigned)(uintptr_t)(lds_ptr_t)(sbw + wave * 1024);
-  auto dma = [](const void* src, unsigned dst) {
-    unsigned keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
-  };
-  auto live = [](int chunk) { return chunk >= 0 && chunk < NCH; };
-  constexpr int J0 = 1 - (DA > DB ? DA : DB);
-  auto issue = [&](int j) {  // iteration j's DMA: B(j + DB - 1), then A(j + DA - 1)
-    const int cb = j + DB - 1, ca = j + DA - 1;
-    if (live(cb)) dma(bsrc + (size_t)cb * 512, bdst + (unsigned)(cb % DB) * BBYTES);
-    if (live(ca)) {
-      const unsigned so = (unsigned)(ca % DA) * ABYTES;
-#pragma unroll
-      for (int k = 0; k < NA; ++k) dma(asrc[k] + (size_t)ca * KC, adst[k] + so);
-    }
-  };
-  auto after = [&](int c) {  // as k_head4
-    int n = 0;
-    for (int i = c - 1; i >= J0; --i) {
-      if (live(i + DA - 1)) {
-        if (i + DA - 1 == c) return n;
-        n += NA;
-      }
-      if (live(i + DB - 1)) {
-        if (i + DB - 1 == c) return n;
-        n += NB;
-      }
-    }
-    return 0;
-  };
-  int arow[2], asw[2];
-#pragma unroll
-  for (int mt = 0; mt < 2; ++mt) {
-    arow[mt] = 64 * wave + 32 * mt + r;
-    asw[mt] = (arow[mt] >> 2) & 3;
-  }
-  f32x16 acc[2][4];
-#pragma unroll
-  for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = f32x16{};
-  for (int j = J0; j < 0; ++j) issue(j);
-#pragma unroll 1
-  for (int c = 0; c < NCH; ++c) {
-    head_wait_vm_dyn(after(c));
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    issue(c);
-    const char* abase = sa + (c % DA) * ABYTES;
-    const char* bst = sbw + (c % DB) * BBYTES;
-    uint4 bh[4], bl[4];
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-      const char* bp = bst + (((nt * 2) * 64 + lane) << 4);
-      bh[nt] = *reinterpret_cast<const uint4*>(bp);
-      bl[nt] = *reinterpret_cast<const uint4*>(bp + 1024);
-    }
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt) {
-      const char* ast = abase + arow[mt] * (KC * 4);
-      const float4 x0 = *reinterpret_cast<const float4*>(ast + (((2 * h) ^ asw[mt]) << 4));
-      const float4 x1 = *reinterpret_cast<const float4*>(ast + (((2 * h + 1) ^ asw[mt]) << 4));
-      uint4 ah, al;
-      if (F16) split8_f16(x0, x1, ah, al);
-      else split8(x0, x1, ah, al);
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        if (F16)
-          acc[mt][nt] = mfma3_f16(as_f16x8(ah), as_f16x8(al), as_f16x8(bh[nt]), as_f16x8(bl[nt]), acc[mt][nt]);
-        else
-          acc[mt][nt] = mfma3(as_bf16x8(ah), as_bf16x8(al), as_bf16x8(bh[nt]), as_bf16x8(bl[nt]), acc[mt][nt]);
-      }
-    }
-  }
-#pragma unroll
-  for (int nt = 0; nt < 4; ++nt) {
-    const float b = bias[32 * nt + r];
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) acc[mt][nt][i] += b;
-  }
-#pragma unroll
-  for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const float s01 = half_sum(acc[mt][0][i] * acc[mt][0][i] + acc[mt][1][i] * acc[mt][1][i]);
-      const float s23 = half_sum(acc[mt][2][i] * acc[mt][2][i] + acc[mt][3][i] * acc[mt][3][i]);
-      const float norm = sqrtf(s01 + s23 + l2eps);
-      const int p = pbase + 64 * wave + 32 * mt + (i & 3) + 8 * (i >> 2) + 4 * h;
-      if (p < P) {
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) out[(size_t)p * 128 + 32 * nt + r] = acc[mt][nt][i] / norm;
-      }
-    }
-}
-
-// ------------------------------------------------------------------------------------
 // host launchers
 // ------------------------------------------------------------------------------------
 // stem-fused kernels carry the normalised patch (34x34 fp32) + 8 reduction floats
@@ -2137,15 +1996,6 @@ hipError_t hn_launch_head(const float* a, float* out, const void* wp, const floa
                        l2eps);                                                                               \
     return hipGetLastError();                                                                                \
   }
-#define HN_HEAD5(KK, F, DA, DB)                                                                              \
-  if (K == KK && f16 == F) {                                                                                 \
-    hipLaunchKernelGGL((k_head5<KK, F, DA, DB>), dim3((P + 511) / 512), dim3(512), 0, st, a, out, w, bias, P, \
-                       l2eps);                                                                               \
-    return hipGetLastError();                                                                                \
-  }
-  if (form == 5 && P >= 240 * 512) {
-    HN_HEAD5(8192, false, 3, 3) HN_HEAD5(2048, true, 3, 3)
-  }
   if (form >= 4 && P >= 240 * 256) {
     HN_HEAD4(8192, false, 3, 3) HN_HEAD4(2048, true, 3, 3)
   }
@@ -2154,7 +2004,6 @@ hipError_t hn_launch_head(const float* a, float* out, const void* wp, const floa
   }
 #undef HN_HEAD3
 #undef HN_HEAD4
-#undef HN_HEAD5
   if (K == 8192 && !f16 && form == 1)
     hipLaunchKernelGGL(k_head<8192>, dim3(grid), dim3(256), 0, st, a, out, w, bias, P, l2eps);
   else if (K == 8192 && !f16)

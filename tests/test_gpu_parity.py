@@ -433,23 +433,6 @@ def test_head4_is_bit_identical(name, cuda_device, monkeypatch):
     assert np.abs(yb[: len(g)].cpu().numpy() - fx["y"]).max() <= _tol(name)
 
 
-@pytest.mark.parametrize("name", ["hardnet", "wang2"])
-def test_head5_is_bit_identical(name, cuda_device, monkeypatch):
-    """k_head5 (HN_HEAD=5: 512-patch workgroups on 16-wide K-chunks, chunks of 131,072) walks the K
-    chunks of k_head3 / k_head4 in the same order: bit-identical descriptors above its 122,880-patch
-    launch threshold (ragged last workgroup)."""
-    from hardnetnas_amd._native import NativeModel
-    m, fx, _ = build_module(name)
-    g = golden_inputs(fx)
-    xb = torch.from_numpy(np.concatenate([g] * (122_917 // len(g) + 1))[:122_917]).to(cuda_device)
-    y = NativeModel.from_module(m, cuda_device)(xb)
-    monkeypatch.setenv("HN_HEAD", "5")
-    nm5 = NativeModel.from_module(m, cuda_device)
-    nm5.set_profiling(True)
-    assert torch.equal(y, nm5(xb))
-    assert np.abs(y[: len(g)].cpu().numpy() - fx["y"]).max() <= _tol(name)
-
-
 @pytest.mark.parametrize("name", ["wang2", "wang4"])
 def test_two_block_kernel_is_bit_identical(name, cuda_device, monkeypatch):
     """k_irf2 (layers 1+2 / 3+4 in one kernel, the activation between them in LDS) computes exactly
