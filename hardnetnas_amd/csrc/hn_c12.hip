@@ -102,6 +102,13 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, WP
   constexpr int NSET = RB2 / 2, NCH2 = NW / NSET, G2 = 4 / NCH2;
   constexpr int G1 = 2, NCH1 = 2 / G1;  // conv1 output groups per wave / waves sharing a P2 unit
   static_assert(NSET * NCH2 == NW && G2 * NCH2 == 4, "P3 work split");
+  // XST (the 4-wave, 2-row-band form): P3's a2 tile leaves through an LDS staging buffer so that each
+  // store instruction writes 4 whole 256-byte pixel rows (1 KB contiguous) instead of 16 64-byte
+  // quarters; 16-byte chunk q of pixel x at slot q ^ (x & 7) (the P3 writes and the read-back are
+  // conflict-free).  The read-back + stores of band b run after the next band's P1 barrier (no extra
+  // barrier; the buffer is rewritten only after the following one).
+  constexpr bool XST = NW == 4 && NSET == 1 && G2 == 1 && (ABL & 192) == 0;
+  __shared__ __attribute__((aligned(16))) float s_st[XST ? 2 * 16 * 64 : 4];
 
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -226,6 +233,17 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, WP
     vnext = reinterpret_cast<const pxv*>(in + pb * 1024)[t];
   else
     rnext.load(in8 + pb * INB, py, px);
+  long pend_patch = -1;  // XST: the band whose a2 rows wait in s_st (patch, first row)
+  int pend_row = 0;
+  auto xst_flush = [&]() {  // wave w: row w >> 1, pixels 8 (w & 1) + (lane >> 4) + 4 j, chunk lane & 15
+    const int ry = w >> 1, q = lane & 15;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int x = 8 * (w & 1) + (lane >> 4) + 4 * j;
+      const f32x4v v = *reinterpret_cast<const f32x4v*>(s_st + ((ry * 16 + x) * 16 + (q ^ (x & 7))) * 4);
+      *reinterpret_cast<f32x4v*>(out + ((pend_patch * 16 + pend_row + ry) * 16 + x) * 64 + 4 * q) = v;
+    }
+  };
 #pragma unroll 1
   for (long patch = pb; patch < pe; ++patch) {
     if constexpr ((ABL & 192) != 0) patch_ts = pb + 2;
@@ -320,6 +338,9 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, WP
     if constexpr (PRIO != 0) __builtin_amdgcn_s_setprio(0);
     __syncthreads();
     HN_C12_TS(2);
+    if constexpr (XST) {  // the previous band's a2 rows (every wave's P3 staging writes are past the barrier)
+      if (pend_patch >= 0) xst_flush();
+    }
 
     // ---- P2: conv1 -> W1 ring (units: new a1 row, both 16-pixel halves; G1 groups) ----------
     // band b: a1 rows 2 RB2 b .. + 2 RB2 - 1 (+ row -1, conv2's zero padding, in band 0).  The two halves
@@ -541,6 +562,14 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, WP
         }
       }
       }
+      if constexpr (XST) {
+#pragma unroll
+        for (int ry = 0; ry < 2; ++ry)
+          *reinterpret_cast<f32x4v*>(s_st + ((ry * 16 + c16) * 16 + ((4 * cs2 + g16) ^ (c16 & 7))) * 4) =
+              __builtin_elementwise_max(acc[ry][0], f32x4v{});
+        pend_patch = patch;
+        pend_row = r0 + oy0;
+      } else {
 #pragma unroll
       for (int ry = 0; ry < 2; ++ry) {
         float* o = out + ((patch * 16 + r0 + oy0 + NSET * ry) * 16 + c16) * 64 + 4 * g16;
@@ -549,12 +578,17 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, WP
           *reinterpret_cast<f32x4v*>(o + 16 * (cs2 * G2 + g)) =
               __builtin_elementwise_max(acc[ry][g], f32x4v{});
       }
+      }
     }
     HN_C12_TS(5);
     // no barrier: the next band's P1 writes only W0, which P3 does not read; its first
     // barrier orders this P3's W1 reads before the next P2's W1 writes
   }  // band
   }  // patch
+  if constexpr (XST) {  // the last band's rows
+    __syncthreads();
+    xst_flush();
+  }
 }
 
 }  // namespace
