@@ -63,7 +63,7 @@ __constant__ unsigned char kDwLane[64] = {
 // its 12 prefetched byte registers took the k3 front from three workgroups per CU to two, wang2
 // front 5.7 -> 7.2 ms, against 0.46 ms for the separate hn_preprocess.)
 template <int K, int MID, int MODE, bool NORM, bool NF, int U8 = -1, bool P5 = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRONT_IRF && K == 3 && MID == 32 ? 3 : 1))) void k_front(const void* __restrict__ in_,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRONT_IRF && K == 3 && MID == 32 ? 3 : MODE == FRONT_IRF && K == 5 && MID == 32 ? 2 : 1))) void k_front(const void* __restrict__ in_,
                                                float* __restrict__ out,
                                                const uint4* __restrict__ spack,  // stem A operand
                                                const float* __restrict__ stem_b,  // [32]
@@ -430,6 +430,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRO
         __syncthreads();  // s_dw (and, without the ring, s_pw) is rewritten next
       }
       if constexpr (NF) {  // band row r0 + w, pixel lane & 15: 4 consecutive channels per tile
+        // (whole 128-byte rows per store after a DPP row rotation measured slower: wang2 front 5.07 -> 5.26 ms)
         float* dst = out + ((patch * 16 + r0 + w) * 16 + (lane & 15)) * OC + 4 * (lane >> 4);
 #pragma unroll
         for (int tt = 0; tt < 2; ++tt)
