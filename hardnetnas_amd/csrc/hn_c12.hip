@@ -297,7 +297,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, WP
     // PRIO & 3: wave priority raised over P1 -- a short serial latency chain that every wave of
     // the workgroup waits for at the next barrier -- so its VALU and MFMA issue ahead of the
     // other workgroup's waves on the same SIMD (MI355X_MICROARCH.md, two waves per SIMD, item 4);
-    // PRIO & 4: over P3 as well (P3 -> P1 -> barrier)
+    // PRIO >> 2: P3's level (P3 -> P1 -> barrier)
     if constexpr ((PRIO & 3) != 0) __builtin_amdgcn_s_setprio(PRIO & 3);
     // ---- P1: the band's new a0 rows -> W0 ring (slot (y + 1) % NA0) ------------------------
     // band 0: rows -1 .. 8 (row -1 is conv1's zero padding); band b: rows 8b+1 .. 8b+8
@@ -470,7 +470,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, WP
     __syncthreads();
     HN_C12_TS(4);
 
-    if constexpr ((PRIO & 4) != 0) __builtin_amdgcn_s_setprio(PRIO & 3);  // P3 too (P3 -> P1 -> barrier)
+    if constexpr ((PRIO >> 2) != 0) __builtin_amdgcn_s_setprio((PRIO >> 2) & 3);  // P3 too (P3 -> P1 -> barrier)
     // ---- P3: conv2 (stride 2) -> a2 in HBM (units: output rows oy and oy + 2 together; this
     // wave's G2 quarters) ----------------------------------------------------------------------
     {
@@ -599,13 +599,15 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, WP
 //   3 / 4: 0 with tap-interleaved P3, conv2 fragments 2 / 3 taps ahead;  5 / 6: the same for 2
 //   7 / 8: 2 / 5 with the tap-interleaved P2 (both halves' chains MFMA by MFMA);  9: 0 with it
 //   10 / 11: 7 with the P1 wave priority raised to 1 / 3;  12: 7 with P3 and P1 at priority 1
+//   13 / 14 / 15: 7 with (P1, P3) at priority (2, 1) / (1, 2) / (2, 2)
 #define HN_C12_CFGS(X)                                                                   \
   X(0, 8, 4, 2, false, 2, false, 0) X(1, 4, 4, 1, false, 2, false, 0) X(2, 4, 2, 2, false, 2, false, 0) \
   X(3, 8, 4, 2, true, 2, false, 0) X(4, 8, 4, 2, true, 3, false, 0) X(5, 4, 2, 2, true, 2, false, 0)     \
   X(6, 4, 2, 2, true, 3, false, 0) X(7, 4, 2, 2, false, 2, true, 0) X(8, 4, 2, 2, true, 2, true, 0)      \
   X(9, 8, 4, 2, false, 2, true, 0) X(10, 4, 2, 2, false, 2, true, 1) X(11, 4, 2, 2, false, 2, true, 3) \
-  X(12, 4, 2, 2, false, 2, true, 5)
-constexpr int kC12Cfgs = 13;
+  X(12, 4, 2, 2, false, 2, true, 5) X(13, 4, 2, 2, false, 2, true, 6) X(14, 4, 2, 2, false, 2, true, 9)         \
+  X(15, 4, 2, 2, false, 2, true, 10)
+constexpr int kC12Cfgs = 16;
 
 bool hn_c12_cfg_ok(int cfg, int abl) {
   if (cfg < 0 || cfg >= kC12Cfgs) return false;
