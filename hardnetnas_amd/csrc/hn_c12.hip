@@ -599,15 +599,13 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, WP
 //   3 / 4: 0 with tap-interleaved P3, conv2 fragments 2 / 3 taps ahead;  5 / 6: the same for 2
 //   7 / 8: 2 / 5 with the tap-interleaved P2 (both halves' chains MFMA by MFMA);  9: 0 with it
 //   10 / 11: 7 with the P1 wave priority raised to 1 / 3;  12: 7 with P3 and P1 at priority 1
-//   13 / 14 / 15: 7 with (P1, P3) at priority (2, 1) / (1, 2) / (2, 2)
 #define HN_C12_CFGS(X)                                                                   \
   X(0, 8, 4, 2, false, 2, false, 0) X(1, 4, 4, 1, false, 2, false, 0) X(2, 4, 2, 2, false, 2, false, 0) \
   X(3, 8, 4, 2, true, 2, false, 0) X(4, 8, 4, 2, true, 3, false, 0) X(5, 4, 2, 2, true, 2, false, 0)     \
   X(6, 4, 2, 2, true, 3, false, 0) X(7, 4, 2, 2, false, 2, true, 0) X(8, 4, 2, 2, true, 2, true, 0)      \
   X(9, 8, 4, 2, false, 2, true, 0) X(10, 4, 2, 2, false, 2, true, 1) X(11, 4, 2, 2, false, 2, true, 3) \
-  X(12, 4, 2, 2, false, 2, true, 5) X(13, 4, 2, 2, false, 2, true, 6) X(14, 4, 2, 2, false, 2, true, 9)         \
-  X(15, 4, 2, 2, false, 2, true, 10)
-constexpr int kC12Cfgs = 16;
+  X(12, 4, 2, 2, false, 2, true, 5)
+constexpr int kC12Cfgs = 13;  // (P1, P3) at priority (2, 1) / (1, 2) / (2, 2): within the box noise of 12, removed
 
 bool hn_c12_cfg_ok(int cfg, int abl) {
   if (cfg < 0 || cfg >= kC12Cfgs) return false;

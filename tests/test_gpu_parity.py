@@ -129,12 +129,11 @@ def test_fused_c12_is_default_and_matches_layerwise(cuda_device, monkeypatch):
         assert np.abs(nm(x[:b]).cpu().numpy() - lw(x[:b]).cpu().numpy()).max() <= 2e-5
 
 
-@pytest.mark.parametrize("cfg", ["0", "1", "2", "3", "5", "7", "8", "9", "10", "11", "13", "14", "15"])
+@pytest.mark.parametrize("cfg", ["0", "1", "2", "3", "5", "7", "8", "9", "10", "11"])
 def test_c12_variants_match(cuda_device, monkeypatch, cfg):
     """HN_C12_CFG=0: 8-wave workgroups with 4-row bands; 1: one wave per SIMD (512-register
     file); 2: 4-wave workgroups with 2-row bands, two per CU; 3 / 5: tap-interleaved P3; 7 / 8 / 9:
-    tap-interleaved P2; 10 / 11: raised P1 priority; 13-15: P1 / P3 at other priority levels -- against
-    the production build (12: 2 with
+    tap-interleaved P2; 10 / 11: raised P1 priority -- against the production build (12: 2 with
     the tap-interleaved P2 and P3 + P1 at raised wave priority).  Both agree with the default build to the split-precision level (the 4-wave builds sum
     input_norm's mean/std in a different order; the MFMA order per output is the same)."""
     from hardnetnas_amd._native import NativeModel
