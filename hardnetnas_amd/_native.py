@@ -53,7 +53,8 @@ EXPORTED = ["hn_param_count", "hn_create", "hn_workspace_bytes", "hn_forward",
             "hn_pairdist_rows", "hn_hardnet_loss", "hn_workspace_bytes_u8", "hn_forward_u8",
             "hn_hardnet_train_workspace_bytes", "hn_hardnet_train_forward", "hn_hardnet_train_backward",
             "hn_nas_train_tensor_count", "hn_nas_train_workspace_bytes", "hn_nas_train_forward",
-            "hn_nas_train_backward", "hn_fpr95_workspace_bytes",
+            "hn_nas_train_backward", "hn_hardnet_loss_train_workspace_bytes", "hn_hardnet_loss_train_forward",
+            "hn_hardnet_loss_backward", "hn_fpr95_workspace_bytes",
             "hn_fpr95", "hn_preprocess", "hn_set_profiling",
             "hn_stage_times", "hn_destroy", "hn_last_error", "hn_abi_version"]
 
@@ -99,6 +100,9 @@ def load_library():
         lib.hn_pairdist_rows_workspace_bytes.argtypes = [I64, I64, ctypes.POINTER(S)]
         lib.hn_pairdist_rows.argtypes = [P, I64, I64, P, I64, I32, P, P, P, P, S, P]
         lib.hn_hardnet_loss.argtypes = [P, P, P, I64, ctypes.c_float, I32, ctypes.c_float, P, P, P]
+        lib.hn_hardnet_loss_train_workspace_bytes.argtypes = [I64, ctypes.POINTER(S)]
+        lib.hn_hardnet_loss_train_forward.argtypes = [P, P, I64, I32, I32, ctypes.c_float, I32, P, P, S, P]
+        lib.hn_hardnet_loss_backward.argtypes = [P, P, I64, I32, I32, ctypes.c_float, I32, P, P, P, P, S, P]
         lib.hn_fpr95_workspace_bytes.argtypes = [I64, ctypes.POINTER(S)]
         lib.hn_fpr95.argtypes = [P, P, P, I64, I32, P, P, P, S, P]
         lib.hn_preprocess.argtypes = [P, I64, I32, I32, I32, ctypes.c_float, ctypes.c_float, P, P]
@@ -115,7 +119,8 @@ def load_library():
                      "hn_hardnet_loss", "hn_workspace_bytes_u8", "hn_forward_u8",
                      "hn_hardnet_train_workspace_bytes", "hn_hardnet_train_forward",
                      "hn_hardnet_train_backward", "hn_nas_train_tensor_count", "hn_nas_train_workspace_bytes",
-                     "hn_nas_train_forward", "hn_nas_train_backward"):
+                     "hn_nas_train_forward", "hn_nas_train_backward", "hn_hardnet_loss_train_workspace_bytes",
+                     "hn_hardnet_loss_train_forward", "hn_hardnet_loss_backward"):
             getattr(lib, name).restype = ctypes.c_int
         if lib.hn_abi_version() != ABI_VERSION:
             raise RuntimeError(f"{path}: ABI version {lib.hn_abi_version()}, expected {ABI_VERSION}; rebuild it")
@@ -156,10 +161,10 @@ def nas_desc(ops: List[str], layers=None, input_norm_eps: float = -1.0,
     return d
 
 
-def fdl_desc(variant: str = "NASNet") -> HnArchDesc:
+def fdl_desc(variant: str = "NASNet", input_norm_eps: float = A.FDL_INPUT_NORM_EPS) -> HnArchDesc:
     """FDLNet HardNetNeiMask (latency/NASNet{,_0.1}/model/des.py): the fixed front is implied
     by the kind; the three IRFBlocks are described like NAS layers."""
-    d = nas_desc(A.FDL_OPS, A.FDL_LAYERS, input_norm_eps=A.FDL_INPUT_NORM_EPS, l2_eps=0.0)
+    d = nas_desc(A.FDL_OPS, A.FDL_LAYERS, input_norm_eps=input_norm_eps, l2_eps=0.0)
     d.kind = HN_KIND_FDL_NASNET if variant == "NASNet" else HN_KIND_FDL_NASNET01
     return d
 
@@ -183,7 +188,7 @@ def desc_for_module(module) -> HnArchDesc:
     if isinstance(module, HardNet):
         return hardnet_desc(module.input_norm_eps, module.l2_eps)
     if isinstance(module, HardNetNeiMask):
-        return fdl_desc(module.variant)
+        return fdl_desc(module.variant, module.input_norm_eps)
     if isinstance(module, HardNetNAS):
         return nas_desc(module.arch_ops, module.layers)
     raise TypeError(type(module))
@@ -364,6 +369,46 @@ def pairdist_rows(anchor_rows: torch.Tensor, row0: int, positive: torch.Tensor, 
 
 
 LOSS_TYPES = {"triplet_margin": 0, "softmax": 1, "contrastive": 2}  # enum hn_loss_type
+
+
+class HardNetLossFunction(torch.autograd.Function):
+    """loss_HardNet with batch_reduce 'min' (hardnet/Losses.py:87-154) and its backward on the fused
+    kernels of hn_loss.hip: no B x B matrix, the gradient routed to each row's positive and its
+    selected hardest negative as autograd routes it through the reference formulation
+    (HardNet.py:408-423).  anchor / positive: [B,128] fp32 HIP tensors."""
+
+    @staticmethod
+    def forward(ctx, anchor, positive, anchor_swap, margin, loss_type):
+        lib = load_library()
+        a, p = anchor.detach().contiguous(), positive.detach().contiguous()
+        b = a.shape[0]
+        n = ctypes.c_size_t()
+        _check(lib.hn_hardnet_loss_train_workspace_bytes(b, ctypes.byref(n)), "hn_hardnet_loss_train_workspace_bytes")
+        saved = torch.empty(n.value, device=a.device, dtype=torch.uint8)
+        loss = torch.empty((), device=a.device, dtype=torch.float32)
+        stream = torch.cuda.current_stream(a.device).cuda_stream
+        with torch.cuda.device(a.device):
+            _check(lib.hn_hardnet_loss_train_forward(a.data_ptr(), p.data_ptr(), b, a.shape[1], int(bool(anchor_swap)),
+                                                     float(margin), LOSS_TYPES[loss_type], loss.data_ptr(),
+                                                     saved.data_ptr(), saved.numel(), stream),
+                   "hn_hardnet_loss_train_forward")
+        ctx.args = (bool(anchor_swap), float(margin), LOSS_TYPES[loss_type])
+        ctx.save_for_backward(a, p, saved)
+        return loss
+
+    @staticmethod
+    def backward(ctx, dloss):
+        lib = load_library()
+        a, p, saved = ctx.saved_tensors
+        swap, margin, lt = ctx.args
+        ga, gp = torch.empty_like(a), torch.empty_like(p)
+        dl = dloss.detach().to(device=a.device, dtype=torch.float32).contiguous().reshape(1)
+        stream = torch.cuda.current_stream(a.device).cuda_stream
+        with torch.cuda.device(a.device):
+            _check(lib.hn_hardnet_loss_backward(a.data_ptr(), p.data_ptr(), a.shape[0], a.shape[1], int(swap), margin,
+                                                lt, dl.data_ptr(), ga.data_ptr(), gp.data_ptr(), saved.data_ptr(),
+                                                saved.numel(), stream), "hn_hardnet_loss_backward")
+        return ga, gp, None, None, None
 
 
 def hardnet_loss(pos: torch.Tensor, row_min: torch.Tensor, col_min: Optional[torch.Tensor] = None,
@@ -575,6 +620,15 @@ class NasTrainFunction(torch.autograd.Function):
     def forward(ctx, x, soft, desc, tensors, momentum, *params):
         lib = load_library()
         b = x.shape[0]
+        nt = ctypes.c_size_t()
+        _check(lib.hn_nas_train_tensor_count(ctypes.byref(desc), ctypes.byref(nt)), "hn_nas_train_tensor_count")
+        if len(tensors) != nt.value:
+            raise ValueError(f"the module has {len(tensors)} float state_dict tensors, the descriptor walks {nt.value}")
+        if soft is not None:
+            n_layers = int(desc.n_layers)
+            if tuple(soft.shape) != (n_layers, 17) or soft.device != x.device or soft.dtype != torch.float32:
+                raise ValueError(f"soft must be fp32 [{n_layers}, 17] on {x.device}, got {soft.dtype} "
+                                 f"{tuple(soft.shape)} on {soft.device}")
         sv, sc = ctypes.c_size_t(), ctypes.c_size_t()
         _check(lib.hn_nas_train_workspace_bytes(ctypes.byref(desc), b, ctypes.byref(sv), ctypes.byref(sc)),
                "hn_nas_train_workspace_bytes")
@@ -590,7 +644,9 @@ class NasTrainFunction(torch.autograd.Function):
                                             stream), "hn_nas_train_forward")
         del scratch
         ctx.desc, ctx.tensors, ctx.b = desc, tensors, b
-        ctx.is_param = [t.requires_grad for t in tensors]
+        # per slot: 1 = a parameter whose gradient is returned, 2 = a frozen parameter (the kernels still
+        # write its gradient: it gets a throwaway buffer), 0 = a buffer (running statistics)
+        ctx.slot = [1 if t.requires_grad else 2 if isinstance(t, torch.nn.Parameter) else 0 for t in tensors]
         ctx.has_soft = soft is not None
         ctx.save_for_backward(saved, x, soft_c if soft_c is not None else x.new_empty(0), *params)
         return out
@@ -601,7 +657,8 @@ class NasTrainFunction(torch.autograd.Function):
         saved, x, soft_c, *params = ctx.saved_tensors
         grads = [torch.empty_like(p) for p in params]
         it = iter(grads)
-        gptrs = [next(it) if isp else None for isp in ctx.is_param]
+        gptrs = [next(it) if k == 1 else torch.empty_like(t) if k == 2 else None
+                 for k, t in zip(ctx.slot, ctx.tensors)]
         sv, sc = ctypes.c_size_t(), ctypes.c_size_t()
         _check(lib.hn_nas_train_workspace_bytes(ctypes.byref(ctx.desc), ctx.b, ctypes.byref(sv), ctypes.byref(sc)),
                "hn_nas_train_workspace_bytes")

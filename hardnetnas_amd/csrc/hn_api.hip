@@ -820,10 +820,21 @@ extern "C" int hn_create(const hn_arch_desc* desc, const float* host_params, siz
   return HN_OK;
 }
 
+// HardNet on k_c12: the conv stages run per sub-chunk, so only the head's input (a5, 32 KiB per
+// patch) spans the whole chunk; a2 / a3 (64 KiB per patch each) span one sub-chunk
+static bool hardnet_subchunked(const hn_model* m) {
+  return m->desc.kind == HN_KIND_HARDNET && m->c12 && !m->unfused_stem;
+}
+
 extern "C" int hn_workspace_bytes(const hn_model* m, int64_t batch, size_t* bytes_out) {
   if (!m || !bytes_out || batch < 0) return fail(HN_ERR_ARG, "bad argument");
   const int64_t p = batch < m->chunk ? batch : m->chunk;
-  *bytes_out = (size_t)p * m->ws_floats_per_patch * m->n_bufs * sizeof(float);
+  if (hardnet_subchunked(m)) {
+    const int64_t sub = std::max<int64_t>(1, std::min<int64_t>(p, m->subchunk));
+    *bytes_out = ((size_t)sub * 2 * 16384 + (size_t)p * 8192) * sizeof(float);
+  } else {
+    *bytes_out = (size_t)p * m->ws_floats_per_patch * m->n_bufs * sizeof(float);
+  }
   return HN_OK;
 }
 
@@ -852,12 +863,17 @@ static int forward_hardnet(hn_model* m, const float* in, int P, int pmax, float*
   float* a1 = ws + per;
   float* a2 = ws + 2 * per;
   const float ineps = m->desc.input_norm_eps;
-  if (m->c12 && !m->unfused_stem) {
+  if (hardnet_subchunked(m)) {
     // conv stages in sub-chunks (HN_SUBCHUNK, default 16384 patches): a sub-chunk's a2..a4
     // (1 GiB for a2) partly stays in the 256 MiB Infinity Cache between its kernels; the
     // head GEMM, which needs many patches per launch to fill the GPU, runs once per chunk
-    // over the a5 of all sub-chunks.
+    // over the a5 of all sub-chunks.  Workspace (hn_workspace_bytes): [a3: sub x 64 KiB]
+    // [a2 / a4: sub x 64 KiB] [a5: pmax x 32 KiB]
     const int sub = std::max(1, std::min(P, m->subchunk));
+    const size_t subper = (size_t)16384 * std::max(1, std::min(pmax, m->subchunk));
+    a0 = ws;
+    a2 = ws + subper;
+    a1 = ws + 2 * subper;
     for (int s0 = 0; s0 < P; s0 += sub) {
       const int n = std::min(sub, P - s0);
       float* a5 = a1 + (size_t)s0 * 8192;
@@ -1227,10 +1243,54 @@ extern "C" int hn_nas_train_backward(const hn_arch_desc* desc, const float* d_do
   if (rc) return rc;
   if (!d_dout || !d_in) return fail(HN_ERR_ARG, "NULL device pointer");
   if (!d_grads) return fail(HN_ERR_ARG, "NULL gradient pointer array");
+  if (const int slot = hn_nas_train_null_grad_slot(*desc, d_grads); slot >= 0) {
+    return fail(HN_ERR_ARG, "d_grads[" + std::to_string(slot) + "] is NULL: every weight slot needs a gradient buffer");
+  }
   if (desc->kind == HN_KIND_NAS_SUPERNET && !d_dsoft) return fail(HN_ERR_ARG, "the supernet needs d_dsoft");
   HIPCHK(hn_nas_train_backward_impl(*desc, d_dout, (long)batch, d_in, d_tensors, d_soft, d_grads, d_dsoft,
                                     static_cast<char*>(d_saved), static_cast<char*>(d_scratch),
                                     static_cast<hipStream_t>(hip_stream)));
+  return HN_OK;
+}
+
+extern "C" int hn_hardnet_loss_train_workspace_bytes(int64_t batch, size_t* bytes_out) {
+  if (!bytes_out || batch < 1 || batch > (1 << 22)) return fail(HN_ERR_ARG, "batch out of range");
+  *bytes_out = hn_loss_train_saved_bytes((long)batch);
+  return HN_OK;
+}
+
+static int loss_train_args(const float* a, const float* p, int64_t batch, int32_t dim, int32_t loss_type,
+                           void* saved, size_t saved_bytes) {
+  if (!a || !p || !saved) return fail(HN_ERR_ARG, "NULL device pointer");
+  if (batch < 1 || batch > (1 << 22)) return fail(HN_ERR_ARG, "batch out of range");
+  if (dim != 128) return fail(HN_ERR_ARG, "dim must be 128");
+  if (loss_type < 0 || loss_type > 2) return fail(HN_ERR_ARG, "unknown loss_type");
+  if ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(saved)) & 15)
+    return fail(HN_ERR_ARG, "device pointers must be 16-byte aligned");
+  if (saved_bytes < hn_loss_train_saved_bytes((long)batch)) return fail(HN_ERR_WORKSPACE, "saved workspace too small");
+  return HN_OK;
+}
+
+extern "C" int hn_hardnet_loss_train_forward(const float* d_anchor, const float* d_positive, int64_t batch,
+                                             int32_t dim, int32_t anchor_swap, float margin, int32_t loss_type,
+                                             float* d_loss, void* d_saved, size_t saved_bytes, void* hip_stream) {
+  if (int rc = loss_train_args(d_anchor, d_positive, batch, dim, loss_type, d_saved, saved_bytes)) return rc;
+  if (!d_loss) return fail(HN_ERR_ARG, "NULL device pointer");
+  HIPCHK(hn_launch_loss_train_fwd(d_anchor, d_positive, (int)batch, anchor_swap ? 1 : 0, margin, loss_type, d_loss,
+                                  d_saved, static_cast<hipStream_t>(hip_stream)));
+  return HN_OK;
+}
+
+extern "C" int hn_hardnet_loss_backward(const float* d_anchor, const float* d_positive, int64_t batch, int32_t dim,
+                                        int32_t anchor_swap, float margin, int32_t loss_type, const float* d_dloss,
+                                        float* d_grad_anchor, float* d_grad_positive, void* d_saved,
+                                        size_t saved_bytes, void* hip_stream) {
+  if (int rc = loss_train_args(d_anchor, d_positive, batch, dim, loss_type, d_saved, saved_bytes)) return rc;
+  if (!d_dloss || !d_grad_anchor || !d_grad_positive) return fail(HN_ERR_ARG, "NULL device pointer");
+  if ((reinterpret_cast<uintptr_t>(d_grad_anchor) | reinterpret_cast<uintptr_t>(d_grad_positive)) & 7)
+    return fail(HN_ERR_ARG, "gradient pointers must be 8-byte aligned");
+  HIPCHK(hn_launch_loss_train_bwd(d_anchor, d_positive, (int)batch, anchor_swap ? 1 : 0, margin, loss_type, d_dloss,
+                                  d_grad_anchor, d_grad_positive, d_saved, static_cast<hipStream_t>(hip_stream)));
   return HN_OK;
 }
 

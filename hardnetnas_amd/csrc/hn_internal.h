@@ -176,6 +176,7 @@ struct HnTrainWs {  // byte offsets into the train workspace's saved region (xn 
 HnTrainWs hn_train_layout(long B);
 // train-mode hardnetNAS (hn_nas_train.hip): tensors consumed, saved / scratch workspace bytes
 int hn_nas_train_plan(const hn_arch_desc& d, long B, size_t* n_tensors, size_t* saved, size_t* scratch);
+int hn_nas_train_null_grad_slot(const hn_arch_desc& d, float* const* grads);
 hipError_t hn_nas_train_forward_impl(const hn_arch_desc& d, const float* in, long B, float* const* tensors,
                                      float momentum, const float* soft, float* out, char* saved, char* scratch,
                                      hipStream_t st);
@@ -188,3 +189,10 @@ hipError_t hn_train_forward(const float* in, long B, const float* const* W, floa
 hipError_t hn_train_backward(const float* dout, long B, const float* const* W, float* const* dW, float* din,
                              float l2_eps, float drop_p, unsigned long long seed, char* saved, char* scratch,
                              hipStream_t st);
+
+// train-mode loss_HardNet 'min' reduce and its backward (hn_loss.hip)
+size_t hn_loss_train_saved_bytes(long B);
+hipError_t hn_launch_loss_train_fwd(const float* a, const float* p, int B, int swap, float margin, int type,
+                                    float* loss, void* saved, hipStream_t st);
+hipError_t hn_launch_loss_train_bwd(const float* a, const float* p, int B, int swap, float margin, int type,
+                                    const float* dloss, float* ga, float* gp, void* saved, hipStream_t st);

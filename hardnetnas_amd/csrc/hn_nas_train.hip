@@ -327,48 +327,47 @@ __global__ void k_dot_final(const double* __restrict__ part, int n, float* __res
 
 // SEModule (fbnet_builder.py:407-421): out = x * sigmoid(W2 relu(W1 avgpool(x) + b1) + b2)
 __global__ __launch_bounds__(256) void k_se_pool(const float* __restrict__ x, long CB, int HW, float* __restrict__ pooled) {
-  const long cb = (long)blockIdx.x * 256 + threadIdx.x;
-  if (cb >= CB) return;
-  const float* r = x + cb * HW;
-  float s = 0.f;
-  for (int i = 0; i < HW; ++i) s += r[i];
-  pooled[cb] = s / (float)HW;
+  for (long cb = (long)blockIdx.x * 256 + threadIdx.x; cb < CB; cb += (long)gridDim.x * 256) {
+    const float* r = x + cb * HW;
+    float s = 0.f;
+    for (int i = 0; i < HW; ++i) s += r[i];
+    pooled[cb] = s / (float)HW;
+  }
 }
 // v[r][j] = act(v[r][j] + bias[r]): act 1 = ReLU, 2 = sigmoid
 __global__ __launch_bounds__(256) void k_bias_act(float* __restrict__ v, int R, long N, const float* __restrict__ bias,
                                                   int act) {
-  const long e = (long)blockIdx.x * 256 + threadIdx.x;
-  if (e >= (long)R * N) return;
-  float t = v[e] + bias[e / N];
-  if (act == 1) t = fmaxf(t, 0.f);
-  if (act == 2) t = 1.f / (1.f + expf(-t));
-  v[e] = t;
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < (long)R * N; e += (long)gridDim.x * 256) {
+    float t = v[e] + bias[e / N];
+    if (act == 1) t = fmaxf(t, 0.f);
+    if (act == 2) t = 1.f / (1.f + expf(-t));
+    v[e] = t;
+  }
 }
 __global__ __launch_bounds__(256) void k_se_scale(const float* __restrict__ x, const float* __restrict__ s, long CB,
                                                   int HW, float* __restrict__ out) {
-  const long e = (long)blockIdx.x * 256 + threadIdx.x;
-  if (e < CB * HW) out[e] = x[e] * s[e / HW];
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < CB * HW; e += (long)gridDim.x * 256) out[e] = x[e] * s[e / HW];
 }
 // dq[cb] = (sum_hw dO x) s (1 - s)   (the gradient at the sigmoid's input)
 __global__ __launch_bounds__(256) void k_se_bwd_ds(const float* __restrict__ dO, const float* __restrict__ x,
                                                    const float* __restrict__ s, long CB, int HW, float* __restrict__ dq) {
-  const long cb = (long)blockIdx.x * 256 + threadIdx.x;
-  if (cb >= CB) return;
-  float acc = 0.f;
-  for (int i = 0; i < HW; ++i) acc = fmaf(dO[cb * HW + i], x[cb * HW + i], acc);
-  const float sv = s[cb];
-  dq[cb] = acc * sv * (1.f - sv);
+  for (long cb = (long)blockIdx.x * 256 + threadIdx.x; cb < CB; cb += (long)gridDim.x * 256) {
+    float acc = 0.f;
+    for (int i = 0; i < HW; ++i) acc = fmaf(dO[cb * HW + i], x[cb * HW + i], acc);
+    const float sv = s[cb];
+    dq[cb] = acc * sv * (1.f - sv);
+  }
 }
 __global__ __launch_bounds__(256) void k_relu_mask(float* __restrict__ d, const float* __restrict__ h, long n) {
-  const long e = (long)blockIdx.x * 256 + threadIdx.x;
-  if (e < n && !(h[e] > 0.f)) d[e] = 0.f;
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < n; e += (long)gridDim.x * 256)
+    if (!(h[e] > 0.f)) d[e] = 0.f;
 }
 // dx = dO s + dpooled / HW
 __global__ __launch_bounds__(256) void k_se_bwd_dx(const float* __restrict__ dO, const float* __restrict__ s,
                                                    const float* __restrict__ dpooled, long CB, int HW,
                                                    float* __restrict__ dx) {
-  const long e = (long)blockIdx.x * 256 + threadIdx.x;
-  if (e < CB * HW) dx[e] = fmaf(dO[e], s[e / HW], dpooled[e / HW] / (float)HW);
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < CB * HW; e += (long)gridDim.x * 256)
+    dx[e] = fmaf(dO[e], s[e / HW], dpooled[e / HW] / (float)HW);
 }
 // out[r] = sum_j x[r][j] (fp64), one workgroup per row
 __global__ __launch_bounds__(256) void k_rowsum(const float* __restrict__ x, long N, float* __restrict__ out) {
@@ -395,14 +394,15 @@ struct HeadBT {  // weight gradient: B(k = patch, j = column)
 // dcol [K = C * 16][B] -> dX [C][B][16]
 __global__ __launch_bounds__(256) void k_head_scatter(const float* __restrict__ dcol, int C, long B,
                                                       float* __restrict__ dx) {
-  const long e = (long)blockIdx.x * 256 + threadIdx.x;
-  if (e >= (long)C * B * 16) return;
-  const int yx = (int)(e & 15);
-  const long cb = e >> 4, b = cb % B;
-  const int c = (int)(cb / B);
-  dx[e] = dcol[((long)c * 16 + yx) * B + b];
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < (long)C * B * 16; e += (long)gridDim.x * 256) {
+    const int yx = (int)(e & 15);
+    const long cb = e >> 4, b = cb % B;
+    const int c = (int)(cb / B);
+    dx[e] = dcol[((long)c * 16 + yx) * B + b];
+  }
 }
 
+// every kernel launched on grid_of(n) walks its n elements in a grid-stride loop (the grid is capped)
 unsigned grid_of(long n) { return (unsigned)std::max<long>(1, std::min<long>((n + 255) / 256, 65536)); }
 
 #define HCK(x)                        \
@@ -453,6 +453,7 @@ struct Plan {
   int fdl = 0;  // FDLNet HardNetNeiMask front: 1 NASNet, 2 NASNet_0.1 (0: the NAS stem)
   float in_eps = 0.f;
   int nt = 0;  // tensors consumed
+  std::vector<int> gw;  // tensor slots whose gradient the backward always writes (every conv / SE weight and bias)
   int stem_w = -1, stem_bn = -1, head_w = -1, head_rm = -1;
   size_t x0z = 0, x0r = 0, x0a = 0;    // stem (FDL: conv0 output + bias; NASNet: its BN's z, in place)
   // FDL front: input_norm; NASNet: BN(affine=False) -> 1x1 s2 32->32 BN ReLU -> 1x1 s2 32->64 BN ReLU;
@@ -486,6 +487,7 @@ Plan make_plan(const hn_arch_desc& d, long B) {
   auto wg = [&](long M, long N, long K) { part = std::max(part, (size_t)(M * N * gemm_slices(M, N, K))); };
   int nt = 0;
   auto bn = [&]() { const int t = nt; nt += 4; return t; };
+  auto wt = [&]() { P.gw.push_back(nt); return nt++; };  // a weight slot: its gradient pointer must be valid
   P.fdl = d.kind == HN_KIND_FDL_NASNET ? 1 : d.kind == HN_KIND_FDL_NASNET01 ? 2 : 0;
   int hw = 32;
   if (P.fdl) {
@@ -495,15 +497,15 @@ Plan make_plan(const hn_arch_desc& d, long B) {
     P.in_eps = d.input_norm_eps;
     P.xn = take((size_t)B * 1024 * sizeof(float));
     P.xsd = take((size_t)B * sizeof(float));
-    P.stem_w = nt++;
-    P.stem_b = nt++;
+    P.stem_w = wt();
+    P.stem_b = wt();
     P.x0z = take(act(32, 32));
     if (P.fdl == 1) {
       P.f_bn0 = nt;
       nt += 2;
       P.x0r = take(32 * sizeof(float));
       P.f_xs1 = take(act(32, 16));
-      P.f_w1 = nt++;
+      P.f_w1 = wt();
       P.f_bn1 = bn();
       P.f_z1 = take(act(32, 16));
       P.f_r1 = take(32 * sizeof(float));
@@ -513,7 +515,7 @@ Plan make_plan(const hn_arch_desc& d, long B) {
       P.f_mp = take(act(32, 16));
     }
     P.f_xs2 = take(act(32, 8));
-    P.f_w2 = nt++;
+    P.f_w2 = wt();
     P.f_bn2 = bn();
     P.f_z2 = take(act(64, 8));
     P.f_r2 = take(64 * sizeof(float));
@@ -522,7 +524,7 @@ Plan make_plan(const hn_arch_desc& d, long B) {
     hw = 8;
   } else {
     // stem ConvBNRelu(1 -> 32, 3x3): conv.weight, bn.{weight, bias, running_mean, running_var}
-    P.stem_w = nt++;
+    P.stem_w = wt();
     P.stem_bn = bn();
     P.x0z = take(act(32, 32));
     P.x0r = take(32 * sizeof(float));
@@ -549,7 +551,7 @@ Plan make_plan(const hn_arch_desc& d, long B) {
           else o.out = take(act(o.cout, Lo));
         } else {
           o.kind = o.s == 1 ? SKIP_CONV : SKIP_MPCONV;
-          o.sk_w = nt++;
+          o.sk_w = wt();
           o.sk_bn = bn();
           if (o.kind == SKIP_MPCONV) o.mp = take(act(o.cin, Lo));
           o.z1 = take(act(o.cout, Lo));
@@ -565,11 +567,11 @@ Plan make_plan(const hn_arch_desc& d, long B) {
         o.se = sp.se;
         o.mid = o.cin * sp.e;
         o.res = o.s == 1 && o.cin == o.cout;
-        o.pw_w = nt++;
+        o.pw_w = wt();
         o.pw_bn = bn();
-        o.dw_w = nt++;
+        o.dw_w = wt();
         o.dw_bn = bn();
-        o.pwl_w = nt++;
+        o.pwl_w = wt();
         o.pwl_bn = bn();
         o.z1 = take(act(o.mid, Li));
         o.r1 = take(o.mid * sizeof(float));
@@ -582,10 +584,10 @@ Plan make_plan(const hn_arch_desc& d, long B) {
         o.o3 = take(act(o.cout, Lo));
         if (o.se) {
           o.semid = o.cout / 4 > 8 ? o.cout / 4 : 8;
-          o.se_w1 = nt++;
-          o.se_b1 = nt++;
-          o.se_w2 = nt++;
-          o.se_b2 = nt++;
+          o.se_w1 = wt();
+          o.se_b1 = wt();
+          o.se_w2 = wt();
+          o.se_b2 = wt();
           o.pooled = take((size_t)o.cout * B * sizeof(float));
           o.hh = take((size_t)o.semid * B * sizeof(float));
           o.sg = take((size_t)o.cout * B * sizeof(float));
@@ -608,7 +610,7 @@ Plan make_plan(const hn_arch_desc& d, long B) {
   }
   // head: conv_k1.weight [128][C][4][4], batchnorm.{running_mean, running_var}
   const int cl = d.c_out[d.n_layers - 1];
-  P.head_w = nt++;
+  P.head_w = wt();
   P.head_rm = nt;
   nt += 2;
   P.hz = take((size_t)128 * B * sizeof(float));
@@ -1040,6 +1042,15 @@ int hn_nas_train_plan(const hn_arch_desc& d, long B, size_t* n_tensors, size_t* 
   if (saved) *saved = P.saved;
   if (scratch) *scratch = P.scratch;
   return 0;
+}
+
+// the first weight slot whose gradient pointer is NULL, or -1 (frozen parameters still need a buffer:
+// the weight-gradient kernels write unconditionally; only the affine BN gradients may be NULL)
+int hn_nas_train_null_grad_slot(const hn_arch_desc& d, float* const* grads) {
+  const Plan P = make_plan(d, 2);
+  for (int i : P.gw)
+    if (!grads[i]) return i;
+  return -1;
 }
 
 hipError_t hn_nas_train_forward_impl(const hn_arch_desc& d, const float* in, long B, float* const* tensors,

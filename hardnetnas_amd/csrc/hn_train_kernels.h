@@ -487,8 +487,7 @@ __global__ __launch_bounds__(256) void k_input_norm(const float* __restrict__ in
 }
 
 __global__ __launch_bounds__(256) void k_scale_rows(float* __restrict__ g, long B, const float* __restrict__ s) {
-  const long e = (long)blockIdx.x * 256 + threadIdx.x;
-  if (e < B * 1024) g[e] *= s[e >> 10];
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < B * 1024; e += (long)gridDim.x * 256) g[e] *= s[e >> 10];
 }
 
 // L2Norm (Utils.py:15-22) of z6 [128][B] -> out [B][128]; one wave per patch

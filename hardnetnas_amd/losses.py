@@ -1,12 +1,12 @@
 """Differentiable ``loss_HardNet`` for training loops (hardnet/Losses.py:87-154, batch_reduce
 'min'), with ``distance_matrix_vector`` (Losses.py:5-13) in the reference's formulation.
 
-This is the autograd form the reference training loop calls (HardNet.py:392-397): the B x B
-distance matrix is materialised (1024 pairs = 1 M entries), so gradients flow to both inputs
-through the selected hardest negatives exactly as in the reference.  For inference-time mining
-at large B (65,536 pairs: a 17 GB matrix) use ``hardnetnas_amd._native.pairdist_rows`` /
-``hardnet_loss`` and ``hardnetnas_amd.distributed.sharded_hardnet_loss``, the fused MFMA kernel
-that never materialises it (forward only).
+The training loop calls it as HardNet.py:408-413.  With batch_reduce 'min' on HIP fp32 [B,128]
+descriptors it runs the fused kernels of hn_loss.hip (forward and backward, no B x B matrix); the
+autograd formulation below (the B x B matrix materialised, as in the reference) serves CPU / fp64
+tensors, the 'average' and 'random' reductions and ``fused=False``.  For inference-time mining at
+large B (65,536 pairs) ``hardnetnas_amd._native.pairdist_rows`` / ``hardnet_loss`` and
+``hardnetnas_amd.distributed.sharded_hardnet_loss`` run the bf16x3 MFMA pair kernel (forward only).
 """
 from __future__ import annotations
 
@@ -24,31 +24,55 @@ def distance_matrix_vector(anchor: torch.Tensor, positive: torch.Tensor) -> torc
 
 def loss_HardNet(anchor: torch.Tensor, positive: torch.Tensor, anchor_swap: bool = False,
                  anchor_ave: bool = False, margin: float = 1.0, batch_reduce: str = "min",
-                 loss_type: str = "triplet_margin") -> torch.Tensor:
-    """Hardest-in-batch margin loss (Losses.py:87-154); batch_reduce 'min' only (the reference
-    training default, HardNet.py:392-397); anchor_ave is accepted and unused, as there."""
+                 loss_type: str = "triplet_margin", fused: bool = True) -> torch.Tensor:
+    """Hardest-in-batch margin loss (Losses.py:87-154); anchor_ave is accepted and unused, as there.
+
+    batch_reduce 'min' (the training default, HardNet.py:74) on [B,128] fp32 HIP tensors runs the
+    fused kernels (``_native.HardNetLossFunction``: forward and backward without the B x B matrix);
+    ``fused=False``, CPU / fp64 tensors and the other reductions run the reference's autograd
+    formulation here.  'average' (:124-130) takes every masked entry as a negative, paired -- as in
+    the reference -- with the positive distance of its column; 'random' (:131-138) one negative per
+    row at torch.randperm(B) drawn from the CPU generator as the reference draws it."""
     if anchor.size() != positive.size() or anchor.dim() != 2:
         raise ValueError("anchor and positive must be 2-D tensors of the same shape")
-    if batch_reduce != "min":
-        raise ValueError(f"batch_reduce {batch_reduce!r} is not supported (only 'min')")
+    if batch_reduce not in ("min", "average", "random"):
+        raise ValueError(f"unknown batch_reduce {batch_reduce!r} (min, average or random)")
+    if loss_type not in ("triplet_margin", "softmax", "contrastive"):
+        raise ValueError(f"unknown loss_type {loss_type!r}")
+    if (fused and batch_reduce == "min" and anchor.is_cuda and positive.is_cuda
+            and anchor.dtype == torch.float32 and positive.dtype == torch.float32 and anchor.shape[1] == 128):
+        from . import _native
+        return _native.HardNetLossFunction.apply(anchor, positive, anchor_swap, margin, loss_type)
     eps = 1e-8
     d = distance_matrix_vector(anchor, positive) + eps
-    eye = torch.eye(d.size(1), device=d.device, dtype=d.dtype)
-    pos = torch.diagonal(d)
+    b = d.size(1)
+    eye = torch.eye(b, device=d.device, dtype=d.dtype)
+    pos1 = torch.diagonal(d)
     dn = d + 10.0 * eye
     dn = dn + 10.0 * (dn < 0.008).to(dn.dtype)  # near-duplicate "negatives" pushed out
-    min_neg = dn.min(dim=1)[0]
-    if anchor_swap:
-        min_neg = torch.minimum(min_neg, dn.min(dim=0)[0])
+    if batch_reduce == "min":
+        pos = pos1
+        min_neg = dn.min(dim=1)[0]
+        if anchor_swap:
+            min_neg = torch.minimum(min_neg, dn.min(dim=0)[0])
+    elif batch_reduce == "average":
+        pos = pos1.repeat(anchor.size(0))          # entry k pairs with pos1[k % B]
+        min_neg = dn.reshape(-1)                   # entry k = dn[k // B][k % B]
+        if anchor_swap:
+            min_neg = torch.minimum(min_neg, dn.t().contiguous().reshape(-1))
+    else:
+        idxs = torch.randperm(anchor.size(0)).long().to(d.device)
+        min_neg = dn.gather(1, idxs.view(-1, 1)).reshape(-1)
+        if anchor_swap:
+            min_neg = torch.minimum(min_neg, dn.t().gather(1, idxs.view(-1, 1)).reshape(-1))
+        pos = pos1
     if loss_type == "triplet_margin":
         loss = torch.clamp(margin + pos - min_neg, min=0.0)
     elif loss_type == "softmax":
         e_pos = torch.exp(2.0 - pos)
         loss = -torch.log(e_pos / (e_pos + torch.exp(2.0 - min_neg) + eps))
-    elif loss_type == "contrastive":
-        loss = torch.clamp(margin - min_neg, min=0.0) + pos
     else:
-        raise ValueError(f"unknown loss_type {loss_type!r}")
+        loss = torch.clamp(margin - min_neg, min=0.0) + pos
     return loss.mean()
 
 

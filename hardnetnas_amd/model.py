@@ -87,7 +87,8 @@ class _NativeMixin:
     @torch.compiler.disable
     def _native_handle(self, x: torch.Tensor) -> int:
         from . import _native
-        key = (x.device.index, self._native_key())
+        key = (x.device.index, getattr(self, "input_norm_eps", None), getattr(self, "l2_eps", None),
+               self._native_key())
         h = getattr(self, "_hn_handle", None)
         if h is None or self._hn_key != key:
             self._hn_handle = None  # release the old one first
@@ -186,7 +187,7 @@ class HardNet(_NativeMixin, nn.Module):
         ts = [self.features[i].weight for i in (0, 3, 6, 9, 12, 15, 19)]
         ts += [t for b in bns for t in (b.running_mean, b.running_var)]
         return (self.input_norm_eps == 1e-7 and self.l2_eps == 1e-10
-                and all(b.momentum is not None and b.track_running_stats and b.eps == 1e-5
+                and all(b.training and b.momentum is not None and b.track_running_stats and b.eps == 1e-5
                         and not b.affine and b.momentum == bns[0].momentum for b in bns)
                 and all(t is not None and t.dtype == torch.float32 and t.device == x.device for t in ts))
 
@@ -446,11 +447,21 @@ def _nas_train_native_eligible(module: nn.Module, x: torch.Tensor, layers, expec
             and list(layers) == list(expect)):
         return False
     bns = [m for m in module.modules() if isinstance(m, nn.BatchNorm2d)]
-    if not all(b.momentum is not None and b.track_running_stats and b.eps == 1e-5
-               and b.momentum == bns[0].momentum for b in bns):
+    # the kernels' BatchNorm forms: affine=False for the head's BN (and FDLNet NASNet's BN after
+    # conv0), affine for every other; all of them in train mode (batch statistics)
+    plain = {id(b) for b in _non_affine_bns(module)}
+    if not all(b.training and b.momentum is not None and b.track_running_stats and b.eps == 1e-5
+               and b.momentum == bns[0].momentum and b.affine == (id(b) not in plain) for b in bns):
         return False
     ts = list(module.parameters()) + [b for b in module.buffers() if b.dtype != torch.int64]
     return all(t.dtype == torch.float32 and t.device == x.device and t.is_contiguous() for t in ts)
+
+
+def _non_affine_bns(module: nn.Module):
+    if isinstance(module, HardNetNeiMask):
+        f = module.features
+        return [f[1], f[-1]] if module.variant == "NASNet" else [f[-1]]
+    return [module.last_stages.batchnorm]
 
 
 def _nas_train_native_forward(module: nn.Module, x: torch.Tensor, soft):

@@ -131,6 +131,27 @@ int hn_hardnet_loss(const float* d_pos, const float* d_row_min, const float* d_c
                     float margin, int32_t loss_type, float scale, float* d_min_neg, float* d_loss,
                     void* hip_stream);
 
+/* Train-mode loss_HardNet, batch_reduce 'min' (hardnet/Losses.py:87-154 as the training loop calls
+ * it, HardNet.py:408-413) and its backward (HardNet.py:421-423), without a B x B matrix.
+ *   forward : *d_loss = mean_i loss(pos_i, min_neg_i) over d_anchor / d_positive [B,128] fp32
+ *             (exact fp32 dot products; the hardest negatives and their argmins -- the first index
+ *             on a tie -- are kept in d_saved);
+ *   backward: d_dloss (one float on the device: d L / d loss) -> d_grad_anchor, d_grad_positive
+ *             [B,128] (overwritten), as autograd differentiates the reference formulation: the
+ *             gradient reaches each row's positive entry and its selected negative (the row
+ *             minimum's argmin, the column minimum's for anchor_swap; halves on a row / column
+ *             tie, as torch.minimum's backward).  Deterministic: no atomics in the backward.
+ * d_saved (hn_hardnet_loss_train_workspace_bytes) is written by the forward and read by the
+ * backward with the same anchors, positives and arguments; 1 <= batch <= 2^22. */
+int hn_hardnet_loss_train_workspace_bytes(int64_t batch, size_t* bytes_out);
+int hn_hardnet_loss_train_forward(const float* d_anchor, const float* d_positive, int64_t batch, int32_t dim,
+                                  int32_t anchor_swap, float margin, int32_t loss_type, float* d_loss,
+                                  void* d_saved, size_t saved_bytes, void* hip_stream);
+int hn_hardnet_loss_backward(const float* d_anchor, const float* d_positive, int64_t batch, int32_t dim,
+                             int32_t anchor_swap, float margin, int32_t loss_type, const float* d_dloss,
+                             float* d_grad_anchor, float* d_grad_positive, void* d_saved, size_t saved_bytes,
+                             void* hip_stream);
+
 /* FPR at 95 % recall of an evaluation batch of descriptor pairs (hardnet/HardNet.py:450-472
  * + hardnet/EvalMetrics.py:6-19): per-pair L2 distance, scores -> distances transform, sort,
  * first index reaching 95 % recall, FP / (FP + TN).
@@ -214,7 +235,8 @@ int hn_hardnet_train_backward(const float* d_dout, int64_t batch, const float* c
  * d_tensors: host array of hn_nas_train_tensor_count() device pointers, one per float tensor of the
  * module's state_dict in order (num_batches_tracked and the supernet's `thetas` left out): conv
  * weights, BN weight, bias, running_mean, running_var (updated in place), SE weights / biases.
- * d_grads: the same length; entries for running buffers are ignored (may be NULL).
+ * d_grads: the same length; entries for running buffers are ignored (may be NULL); every weight
+ * slot (conv / SE weights and biases) needs a buffer, frozen parameters included (HN_ERR_ARG if NULL).
  * Workspace: d_saved is written by the forward and read by its backward (one per forward call);
  * d_scratch is transient. */
 int hn_nas_train_tensor_count(const hn_arch_desc* desc, size_t* n_out);

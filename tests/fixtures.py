@@ -39,8 +39,16 @@ def params_for(module: torch.nn.Module, fx) -> dict:
 
 
 def golden_inputs(fx) -> np.ndarray:
+    """The fixture's test patches, regenerated from the splitmix64 stream and checked against the
+    SHA-256 that tests/golden/make_golden.py recorded for the reference run's input."""
     meta = fx["meta"]
-    return synth.synth_patches(meta["n_test"], meta["test_seed"])
+    x = synth.synth_patches(meta["n_test"], meta["test_seed"])
+    ref = load("hardnet")["meta"]  # the NAS / FDL fixtures were made on the same seeded patches
+    sha = meta.get("x_sha256") or (ref["x_sha256"] if (ref["n_test"], ref["test_seed"]) ==
+                                   (meta["n_test"], meta["test_seed"]) else None)
+    assert sha is not None, "fixture records no input hash"
+    assert synth.sha256_f32(x) == sha, "synthetic input drift"
+    return x
 
 
 def build_module(name: str):

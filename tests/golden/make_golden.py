@@ -302,6 +302,48 @@ def make_losses():
     print("losses", out["fpr_kat"], out["fpr"])
 
 
+def make_loss_modes():
+    """loss_modes.npz: the reference loss_HardNet's 'average' and 'random' batch reductions
+    (Losses.py:124-138; 'random' after torch.manual_seed(seed), so its randperm is reproducible),
+    and the gradients of the 'min' reduce w.r.t. anchors and positives (the training step's
+    backward, HardNet.py:421-423) in fp64 and fp32, for every loss type and anchor_swap."""
+    ns = _ns()
+    exec(_extract(os.path.join(REF, "hardnet/Losses.py"), ["distance_matrix_vector", "loss_HardNet"]), ns)
+    torch.Tensor.cuda = lambda self, *a, **k: self  # CPU-only fixture generation
+    rs = np.random.RandomState(17)
+    out = {}
+    b = 129
+    a = torch.from_numpy(rs.randn(b, 128).astype(np.float32))
+    a = a / a.norm(dim=1, keepdim=True)
+    p = a + 0.3 * torch.from_numpy(rs.randn(b, 128).astype(np.float32))
+    p = p / p.norm(dim=1, keepdim=True)
+    p[5] = a[40]   # a masked near-duplicate negative
+    p[9] = a[9]    # a zero positive distance
+    out["a"], out["p"] = a.numpy(), p.numpy()
+    for swap in (False, True):
+        for lt in ("triplet_margin", "softmax", "contrastive"):
+            tag = f"{int(swap)}_{lt}"
+            for br in ("average", "random"):
+                torch.manual_seed(23)
+                out[f"{br}_{tag}"] = np.float64(ns["loss_HardNet"](a.double(), p.double(), anchor_swap=swap,
+                                                                    batch_reduce=br, loss_type=lt).item())
+            g = {}
+            for dt, sfx in ((torch.float64, "64"), (torch.float32, "32")):
+                ag = a.to(dt).clone().requires_grad_(True)
+                pg = p.to(dt).clone().requires_grad_(True)
+                loss = ns["loss_HardNet"](ag, pg, anchor_swap=swap, loss_type=lt)
+                loss.backward()
+                out[f"min_{tag}_{sfx}"] = np.float64(loss.item())
+                g[sfx] = torch.cat([ag.grad, pg.grad]).double()
+            # fp64 gradients (stored fp32) and the reference's own fp32 error on them (L2-relative)
+            out[f"g_{tag}"] = g["64"].numpy().astype(np.float32)
+            out[f"g32err_{tag}"] = np.float64((g["32"] - g["64"]).norm() / g["64"].norm())
+    out["meta"] = json.dumps({"b": b, "random_seed": 23, "source": "hardnet/Losses.py loss_HardNet "
+                              "(AST-extracted, torch %s CPU)" % torch.__version__})
+    np.savez_compressed(os.path.join(HERE, "loss_modes.npz"), **out)
+    print("loss modes", {k: float(v) for k, v in out.items() if k.startswith("average_1")})
+
+
 NAS_FIXTURES = OrderedDict([
     ("wang2", A.MODEL_ARCH["wang2"]),
     ("wang3", A.MODEL_ARCH["wang3"]),
@@ -316,10 +358,16 @@ NAS_FIXTURES = OrderedDict([
 if __name__ == "__main__":
     if not os.path.isdir(REF):
         sys.exit(f"{REF} not found: fixtures can only be regenerated in the survey container")
+    if sys.argv[1:] == ["loss_modes"]:
+        make_loss_modes()
+        sys.exit(0)
+    if not os.path.isdir(REF):
+        sys.exit(f"{REF} not found: fixtures can only be regenerated in the survey container")
     torch.set_num_threads(8)
     make_hardnet()
     for name, ops in NAS_FIXTURES.items():
         make_nas(name, ops)
     make_losses()
+    make_loss_modes()
     for v in A.FDL_VARIANTS:
         make_fdl(v)

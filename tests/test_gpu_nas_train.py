@@ -147,3 +147,76 @@ def test_fdl_train_step_matches_reference(variant, cuda_device):
     glob, worst, where = nas_grad_check([(k, t.grad.cpu().numpy()) for k, t in m.named_parameters()], fx, pre)
     print(f"{variant}: gradients L2-rel (all) {glob:.2e}, worst tensor {worst:.2e} at {where}")
     assert glob <= 5e-3 and worst <= 2e-2, (glob, where, worst)
+
+
+def _native_vs_torch(m_factory, x, cuda_device, freeze=()):
+    """One loss_HardNet train step of a fresh module on the HIP train path and on its torch layers
+    (MIOpen): (descriptors, {name: grad}) for each."""
+    from hardnetnas_amd.losses import loss_HardNet
+    res = {}
+    h = x.shape[0] // 2
+    for native in (True, False):
+        m = m_factory().to(cuda_device).train()
+        m.native_train = native
+        for k, t in m.named_parameters():
+            if k in freeze:
+                t.requires_grad_(False)
+        y = m(x)
+        assert ("NasTrainFunction" in type(y.grad_fn).__name__) == native
+        loss_HardNet(y[:h], y[h:], anchor_swap=True).backward()
+        res[native] = (y.detach(), {k: (t.grad.detach().clone() if t.grad is not None else None)
+                                    for k, t in m.named_parameters()})
+    return res
+
+
+def _compare(res, bar=2e-2):
+    e = (res[True][0] - res[False][0]).abs().max().item()
+    assert e <= 1e-4, e
+    worst = 0.0
+    for k, g in res[False][1].items():
+        gn = res[True][1][k]
+        assert (g is None) == (gn is None), k
+        if g is None:
+            continue
+        n = g.norm().item()
+        if n > 1e-6:
+            r = (gn - g).norm().item() / n
+            worst = max(worst, r)
+            assert r <= bar, (k, r)
+    return e, worst
+
+
+def test_frozen_parameters_train_natively(cuda_device):
+    """Frozen parameters (requires_grad False: the stem conv and an SE conv of cov_b) keep the native
+    train path (their gradient slots get throwaway buffers: the kernels write every weight
+    gradient) and the other gradients match the torch layers; frozen ones stay None."""
+    from fixtures import build_module
+    from hardnetnas_amd import synth
+    x = torch.from_numpy(synth.synth_patches(64, seed=5)).to(cuda_device)
+    freeze = ("first.conv.weight", "stages.2.se4.op.1.weight", "stages.2.se4.op.1.bias")
+    res = _native_vs_torch(lambda: build_module("cov_b")[0], x, cuda_device, freeze)
+    for k in freeze:
+        assert res[True][1][k] is None
+    e, worst = _compare(res)
+    print(f"frozen: fwd {e:.2e}, worst grad L2-rel {worst:.2e}")
+
+
+@pytest.mark.parametrize("name,b", [("fdl_NASNet", 1024), ("cov_b", 4096)])
+def test_large_batch_train_matches_torch_layers(name, b, cuda_device):
+    """Batches whose elementwise kernels cover > 2^24 elements (FDL conv0 bias over 32 x B x 1024;
+    SE scale / pool over C x B x 256 at 16 x 16): grid-stride loops, so every element is touched."""
+    from fixtures import build_module
+    from hardnetnas_amd import synth
+    x = torch.from_numpy(synth.synth_patches(b, seed=9)).to(cuda_device)
+    e, worst = _compare(_native_vs_torch(lambda: build_module(name)[0], x, cuda_device))
+    print(f"{name} B={b}: fwd {e:.2e}, worst grad L2-rel {worst:.2e}")
+
+
+def test_bn_in_eval_inside_a_train_module_takes_torch_layers(cuda_device):
+    """A BatchNorm switched to eval() inside a train() module uses running statistics in the
+    reference's layers; the native train path (batch statistics everywhere) must not take it."""
+    m, fx, a, _ = nas_train_start("wang2")
+    m = m.to(cuda_device)
+    x = torch.from_numpy(a[:8]).to(cuda_device)
+    m.stages[1].pw.bn.eval()
+    assert "NasTrainFunction" not in type(m(x).grad_fn).__name__

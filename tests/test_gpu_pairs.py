@@ -2,6 +2,7 @@
 masked distance + hardest negative (hardnet/Losses.py:5-13, 87-154) against the fp64 oracle --
 row blocks of a sharded batch, descriptors that are not unit-norm (dm > 10, where the +10 mask
 must not win), the full 65,536-pair batch on a row sample, and the three margin losses."""
+import numpy as np
 import pytest
 import torch
 
@@ -120,3 +121,55 @@ def test_lds_dma_ring_equals_register_staged_form(tmp_path, cuda_device):
         for x, y in zip(res["ring"][k], res["reg"][k]):
             if x is not None:
                 assert torch.equal(x, y), k
+
+
+LOSS_TYPES = ["triplet_margin", "softmax", "contrastive"]
+
+
+@pytest.mark.parametrize("swap", [False, True])
+@pytest.mark.parametrize("loss_type", LOSS_TYPES)
+def test_fused_train_loss_matches_reference_backward(swap, loss_type, cuda_device):
+    """loss_HardNet 'min' on HIP tensors runs hn_hardnet_loss_train_forward / hn_hardnet_loss_backward
+    (no B x B matrix): loss and d loss / d (anchor, positive) against the reference's fp64 step
+    (tests/golden/loss_modes.npz: a masked near-duplicate and a zero positive distance included);
+    loss <= 1e-6, gradients L2-relative <= 1e-5 (or 3x the reference's own fp32 error).  Run twice:
+    bit-identical (no atomics in the backward)."""
+    from fixtures import load
+    from hardnetnas_amd.losses import loss_HardNet
+    fx = load("loss_modes")
+    tag = f"{int(swap)}_{loss_type}"
+    res = []
+    for _ in range(2):
+        a = torch.from_numpy(fx["a"]).to(cuda_device).requires_grad_(True)
+        p = torch.from_numpy(fx["p"]).to(cuda_device).requires_grad_(True)
+        loss = loss_HardNet(a, p, anchor_swap=swap, loss_type=loss_type)
+        assert "HardNetLossFunction" in type(loss.grad_fn).__name__
+        loss.backward()
+        res.append((loss.item(), torch.cat([a.grad, p.grad]).cpu().numpy()))
+    assert res[0][0] == res[1][0] and np.array_equal(res[0][1], res[1][1])
+    el = abs(res[0][0] - float(fx[f"min_{tag}_64"]))
+    ref = fx[f"g_{tag}"].astype(np.float64)
+    eg = np.linalg.norm(res[0][1] - ref) / np.linalg.norm(ref)
+    print(f"{tag}: loss {el:.2e}, grad L2-rel {eg:.2e} (reference fp32: {float(fx[f'g32err_{tag}']):.2e})")
+    assert el <= 1e-6
+    assert eg <= max(1e-5, 3 * float(fx[f"g32err_{tag}"]))
+
+
+@pytest.mark.parametrize("b", [512, 4096])
+def test_fused_train_loss_matches_autograd_on_gpu(b, cuda_device):
+    """The fused loss against the autograd formulation on the same GPU (fused=False) at the training
+    loop's batch (512, HardNet.py:98) and 4,096 pairs of unit descriptors, anchor_swap on."""
+    from hardnetnas_amd.losses import loss_HardNet
+    g = torch.Generator(device=cuda_device).manual_seed(b)
+    a0 = torch.nn.functional.normalize(torch.randn(b, 128, device=cuda_device, generator=g), dim=1)
+    p0 = torch.nn.functional.normalize(a0 + 0.4 * torch.randn(b, 128, device=cuda_device, generator=g), dim=1)
+    out = {}
+    for fused in (True, False):
+        a, p = a0.clone().requires_grad_(True), p0.clone().requires_grad_(True)
+        loss = loss_HardNet(a, p, anchor_swap=True, fused=fused)
+        loss.backward()
+        out[fused] = (loss.item(), torch.cat([a.grad, p.grad]))
+    el = abs(out[True][0] - out[False][0]) / abs(out[False][0])
+    eg = ((out[True][1] - out[False][1]).norm() / out[False][1].norm()).item()
+    print(f"B={b}: loss rel {el:.2e}, grad L2-rel {eg:.2e}")
+    assert el <= 1e-5 and eg <= 1e-4

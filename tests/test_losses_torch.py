@@ -38,4 +38,40 @@ def test_distance_matrix_and_errors():
     with pytest.raises(ValueError):
         loss_HardNet(a, a[:3])
     with pytest.raises(ValueError):
-        loss_HardNet(a, a, batch_reduce="average")
+        loss_HardNet(a, a, batch_reduce="L2Net")
+
+
+LT = ["triplet_margin", "softmax", "contrastive"]
+
+
+@pytest.mark.parametrize("swap", [False, True])
+@pytest.mark.parametrize("loss_type", LT)
+def test_average_and_random_reductions_match_reference(swap, loss_type):
+    """batch_reduce 'average' / 'random' (Losses.py:124-138) against the reference's own values
+    (tests/golden/loss_modes.npz; 'random' draws torch.randperm after torch.manual_seed(23))."""
+    from fixtures import load
+    fx = load("loss_modes")
+    a, p = torch.from_numpy(fx["a"]).double(), torch.from_numpy(fx["p"]).double()
+    tag = f"{int(swap)}_{loss_type}"
+    got = loss_HardNet(a, p, anchor_swap=swap, batch_reduce="average", loss_type=loss_type).item()
+    assert abs(got - float(fx[f"average_{tag}"])) <= 1e-12
+    torch.manual_seed(fx["meta"]["random_seed"])
+    got = loss_HardNet(a, p, anchor_swap=swap, batch_reduce="random", loss_type=loss_type).item()
+    assert abs(got - float(fx[f"random_{tag}"])) <= 1e-12
+
+
+@pytest.mark.parametrize("swap", [False, True])
+@pytest.mark.parametrize("loss_type", LT)
+def test_min_gradients_match_reference(swap, loss_type):
+    """The autograd formulation's gradients (the CPU path) against the reference's fp64 backward."""
+    from fixtures import load
+    fx = load("loss_modes")
+    a = torch.from_numpy(fx["a"]).double().requires_grad_(True)
+    p = torch.from_numpy(fx["p"]).double().requires_grad_(True)
+    tag = f"{int(swap)}_{loss_type}"
+    loss = loss_HardNet(a, p, anchor_swap=swap, loss_type=loss_type)
+    loss.backward()
+    assert abs(loss.item() - float(fx[f"min_{tag}_64"])) <= 1e-12
+    g = torch.cat([a.grad, p.grad]).numpy()
+    ref = fx[f"g_{tag}"].astype(np.float64)
+    assert np.linalg.norm(g - ref) / np.linalg.norm(ref) <= 1e-6
