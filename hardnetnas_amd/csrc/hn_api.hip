@@ -499,6 +499,37 @@ static std::vector<uint16_t> pack_c12(const std::vector<float>& w, int cout) {
   return a;
 }
 
+// stride-1 3x3 conv (BN folded) as 1-D Winograd F(2,3) along x (hn_wino1.hip): U_xi[ky] =
+// sum_kx G[xi][kx] W[ky][kx] in fp64 (U3 negated: it accumulates into the odd output column with a
+// minus sign), bf16 hi / lo A fragments [cin/32][xi][ky][ks][cout/32][plane][lane][8] in the
+// kernel's K-step order kx = 6 xi + 2 ky + ks
+static std::vector<uint16_t> pack_wino1(const std::vector<float>& w, int cin, int cout) {
+  static const double G[4][3] = {{1, 0, 0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0, 0, 1}};
+  const int ncc = cin / 32, ntot = cout / 32;
+  std::vector<uint16_t> out((size_t)ncc * 24 * ntot * 2 * 64 * 8);
+  size_t o = 0;
+  for (int cc = 0; cc < ncc; ++cc)
+    for (int kx = 0; kx < 24; ++kx)
+      for (int nt = 0; nt < ntot; ++nt) {
+        const int xi = kx / 6, ky = (kx % 6) / 2, ks = kx % 2;
+        uint16_t* hi = &out[o];
+        uint16_t* lo = &out[o + 64 * 8];
+        for (int lane = 0; lane < 64; ++lane)
+          for (int j = 0; j < 8; ++j) {
+            const int n = nt * 32 + (lane & 31);
+            const int c = cc * 32 + ks * 16 + (lane >> 5) * 8 + j;
+            double u = 0;
+            for (int t = 0; t < 3; ++t) u += G[xi][t] * (double)w[((size_t)n * cin + c) * 9 + ky * 3 + t];
+            const float v = (float)(xi == 3 ? -u : u);
+            const uint16_t hv = f2bf(v);
+            hi[lane * 8 + j] = hv;
+            lo[lane * 8 + j] = f2bf(v - bf2f(hv));
+          }
+        o += 2 * 64 * 8;
+      }
+  return out;
+}
+
 #ifdef HN_EXPERIMENTS
 // stride-1 3x3 conv (BN folded) as Winograd F(2x2,3x3) U = G g G^T (fp64, then bf16 hi/lo),
 // packed as the B operand of hn_wino.hip's 32x32x16 MFMAs: [cout/32][cin/16][xi 16][plane][lane
@@ -554,6 +585,11 @@ static int build_hardnet(hn_model* m, Cursor& cur) {
     if ((rc = m->upload(pk, &d))) return rc;
     m->hd.wpack[l] = d;
     if ((rc = m->upload(f.b, &m->hd.bias[l]))) return rc;
+    if (l == 3 || l == 5) {  // 1-D Winograd F(2,3) U fragments (hn_wino1.hip)
+      uint16_t* c = nullptr;
+      if ((rc = m->upload(pack_wino1(f.w, cin[l], cout[l]), &c))) return rc;
+      m->hd.wino1[l] = c;
+    }
 #ifdef HN_EXPERIMENTS
     if (l == 3 || l == 5) {  // Winograd U fragments (experiments library only)
       uint16_t* c = nullptr;

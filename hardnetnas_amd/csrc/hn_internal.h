@@ -50,6 +50,7 @@ struct HardnetDev {
   void* c12_w1 = nullptr;    // conv1 / conv2 as 16x16x32 A operands for the fused k_c12
   void* c12_w2 = nullptr;
   void* wino[7] = {};        // conv3 / conv5: Winograd F(2x2,3x3) U fragments (hn_wino.hip)
+  void* wino1[7] = {};       // conv3 / conv5: 1-D Winograd F(2,3) U fragments (hn_wino1.hip)
 };
 // uint8 patches for the fused preprocessing load (hn_forward_u8)
 struct HnU8In {
@@ -76,6 +77,9 @@ int hn_conv_lds_bytes(int layer);
 // in the pack_conv3x3 layout
 hipError_t hn_launch_conv_raw(int layer, const void* wp, const float* zero_bias, const float* in, float* out,
                               int P, hipStream_t st);
+// 1-D Winograd F(2,3) conv3 / conv5 (hn_wino1.hip; HN_VARIANT digit j)
+hipError_t hn_launch_wino1(int layer, const HardnetDev& d, const float* in, float* out, int P, hipStream_t st);
+int hn_wino1_lds_bytes(int layer);
 // Winograd F(2x2,3x3) conv3 / conv5 (hn_wino.hip; HN_VARIANT digit h)
 hipError_t hn_launch_wino(int layer, const HardnetDev& d, const float* in, float* out, int P, hipStream_t st);
 

@@ -132,7 +132,7 @@ def test_fused_train_loss_matches_reference_backward(swap, loss_type, cuda_devic
     """loss_HardNet 'min' on HIP tensors runs hn_hardnet_loss_train_forward / hn_hardnet_loss_backward
     (no B x B matrix): loss and d loss / d (anchor, positive) against the reference's fp64 step
     (tests/golden/loss_modes.npz: a masked near-duplicate and a zero positive distance included);
-    loss <= 1e-6, gradients L2-relative <= 1e-5 (or 3x the reference's own fp32 error).  Run twice:
+    loss <= 1e-6 and gradients L2-relative <= 1e-5 (or 3x the reference's own fp32 error on each).  Run twice:
     bit-identical (no atomics in the backward)."""
     from fixtures import load
     from hardnetnas_amd.losses import loss_HardNet
@@ -151,7 +151,8 @@ def test_fused_train_loss_matches_reference_backward(swap, loss_type, cuda_devic
     ref = fx[f"g_{tag}"].astype(np.float64)
     eg = np.linalg.norm(res[0][1] - ref) / np.linalg.norm(ref)
     print(f"{tag}: loss {el:.2e}, grad L2-rel {eg:.2e} (reference fp32: {float(fx[f'g32err_{tag}']):.2e})")
-    assert el <= 1e-6
+    # the reference's own fp32 loss is 2e-6 off its fp64 value for 'contrastive' (a mean of distances)
+    assert el <= max(1e-6, 3 * abs(float(fx[f"min_{tag}_32"]) - float(fx[f"min_{tag}_64"])))
     assert eg <= max(1e-5, 3 * float(fx[f"g32err_{tag}"]))
 
 

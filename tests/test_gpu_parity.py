@@ -93,6 +93,28 @@ def test_tiling_variants_match_reference(variant, cuda_device, monkeypatch):
     assert np.abs(y - fx["y"]).max() <= TOL["hardnet"]
 
 
+@pytest.mark.parametrize("variant", ["605jig", "605gij", "605jij"])
+def test_winograd_1d_conv3_conv5_match_reference(variant, cuda_device, monkeypatch):
+    """conv3 / conv5 as 1-D Winograd F(2,3) (hn_wino1.hip, HN_VARIANT digit j) against the
+    reference's fp32 and fp64 vectors (edge patches included) and against the direct kernels on
+    ragged batches whose last two-patch conv5 tile is half empty."""
+    from hardnetnas_amd._native import NativeModel
+    m, fx, _ = build_module("hardnet")
+    x = torch.from_numpy(golden_inputs(fx)).to(cuda_device)
+    xe = torch.from_numpy(fx["x_edge"]).to(cuda_device)
+    direct = NativeModel.from_module(m, cuda_device)
+    monkeypatch.setenv("HN_VARIANT", variant)
+    nm = NativeModel.from_module(m, cuda_device)
+    y = nm(x).cpu().numpy()
+    ye = nm(xe).cpu().numpy()
+    e32 = max(np.abs(y - fx["y"]).max(), np.abs(ye - fx["y_edge"]).max())
+    e64 = max(np.abs(y - fx["y64"]).max(), np.abs(ye - fx["y_edge64"]).max())
+    print(f"{variant}: max abs vs reference fp32 {e32:.2e}, fp64 {e64:.2e}")
+    assert e32 <= TOL["hardnet"] and e64 <= TOL["hardnet"]
+    for b in (1, 3, 255):
+        assert (nm(x[:b]) - direct(x[:b])).abs().max().item() <= 5e-5
+
+
 def test_conv4_producer_stores_are_bit_identical(cuda_device, monkeypatch):
     """conv4 with its outputs staged in LDS and stored by the producer waves (HN_VARIANT digit i)
     against the MFMA waves' own stores (digit f): same arithmetic, so identical bits, including
