@@ -953,7 +953,7 @@ static int forward_nas(hn_model* m, const float* in, int P, int pmax, float* out
   size_t first = 0;
   if (m->desc.kind != HN_KIND_NAS) {  // FDLNet front (des.py) -> 8x8x64
     const HnFdlFrontArgs fa{in, x, m->stem_w, m->stem_b, m->fdl_w1, m->fdl_b1, m->fdl_w2, m->fdl_b2};
-    STAGE("front", hn_launch_fdl_front(fa, P, m->desc.kind == HN_KIND_FDL_NASNET ? 0 : 1, ineps, st));
+    STAGE("front", hn_launch_fdl_front(fa, P, m->desc.kind == HN_KIND_FDL_NASNET ? 0 : 1, ineps, st, u8));
   } else if (m->front) {
     const NasLayer& L = m->layers[0];
     const bool mp = m->front == 2;
@@ -1067,11 +1067,12 @@ extern "C" int hn_forward(hn_model* m, const float* d_in, int64_t batch, float* 
   return HN_OK;
 }
 
-// uint8 input: the stock HardNet's fused k_c12 (every resize mode) and the NAS
-// models' fused front (NONE / CV2) preprocess in their patch loads; every other model / mode /
-// configuration (FDLNet, NAS PIL, HN_NO_FRONT, HN_FRONT_FOLD, the A/B configurations) runs
-// hn_preprocess into the workspace tail first.
+// uint8 input: the stock HardNet's fused k_c12 and FDLNet's MFMA front (every resize
+// mode) and the NAS models' fused front (NONE / CV2) preprocess in their patch loads; every other
+// model / mode / configuration (NAS PIL, HN_NO_FRONT, HN_FRONT_FOLD, HN_FDL_VALU, the A/B
+// configurations) runs hn_preprocess into the workspace tail first.
 static bool u8_fused(const hn_model* m, int resize) {
+  if (m->desc.kind == HN_KIND_FDL_NASNET || m->desc.kind == HN_KIND_FDL_NASNET01) return !m->knobs.fdl_valu;
   if (m->desc.kind == HN_KIND_NAS)  // the fused front's patch load (hn_front.hip): no input_norm, not PIL
     return resize != HN_RESIZE_PIL_BILINEAR && m->front && m->desc.input_norm_eps < 0.f && !m->knobs.front_fold;
   return m->desc.kind == HN_KIND_HARDNET && m->c12 && !m->unfused_stem && m->knobs.c12_cfg == 12 &&

@@ -18,6 +18,7 @@
 // folded into them on the host.  input_norm as des.py:40-47: (x - mean) / (std_unbiased + eps).
 #include "hn_common.h"
 #include "hn_internal.h"
+#include "hn_preproc.h"
 
 #include <algorithm>
 #include <cstdlib>
@@ -135,15 +136,17 @@ __global__ __launch_bounds__(256) void k_fdl_front(const float* __restrict__ in,
 //   stem: K = 9 taps + the bias in K slot 9 (B = 1.0 there), BN folded on the host (MODE 0).
 //   MODE 0: stem -> 1x1 32 -> 32 (+ReLU) -> 1x1 32 -> 64 (+ReLU), one stem pixel per output.
 //   MODE 1: max over the 3x3 window of stem pixels (invalid positions excluded) -> 1x1 -> 64.
-template <int MODE>
-__global__ __launch_bounds__(256) void k_fdl_front_mfma(const float* __restrict__ in, float* __restrict__ out,
+// U8: -1 = fp32 [P,1,32,32] input; HN_RESIZE_* = uint8 patches resized, /255'd and
+// Normalize'd in the patch load (hn_preproc.h, the arithmetic of hn_preprocess), one patch ahead
+template <int MODE, int U8 = -1>
+__global__ __launch_bounds__(256) void k_fdl_front_mfma(const void* __restrict__ in_, float* __restrict__ out,
                                                         const float* __restrict__ ws,  // [9][32]
                                                         const float* __restrict__ bs,  // [32]
                                                         const float* __restrict__ w1,  // [32][32] (cin, cout)
                                                         const float* __restrict__ b1,  // [32]
                                                         const float* __restrict__ w2,  // [32][64] (cin, cout)
                                                         const float* __restrict__ b2,  // [64]
-                                                        int P, float eps) {
+                                                        int P, float eps, float pmean, float pstd, int pnorm) {
   __shared__ float s_x[4][34 * 34];  // normalised patches with a zero border
   // per-wave 32-pixel x 32-channel output tile, transposed for stores of whole 128-byte rows
   __shared__ __attribute__((aligned(16))) float s_o[4][32 * 36];
@@ -205,24 +208,40 @@ __global__ __launch_bounds__(256) void k_fdl_front_mfma(const float* __restrict_
 
   const long stride = (long)gridDim.x * 4;
   long p = (long)blockIdx.x * 4 + w;
+  // the lane's pixels: 4 runs of 4, (y, x) = (px >> 5, px & 31), px = 4 (lane + 64 k)
+  const float* in = static_cast<const float*>(in_);
+  const uint8_t* in8 = static_cast<const uint8_t*>(in_);
+  constexpr int INB = U8 == HN_RESIZE_NONE ? 1024 : 4096;  // bytes per uint8 patch
   float4 vn[4];
-  if (p < P) {
-    const float4* src = reinterpret_cast<const float4*>(in + p * 1024);
+  hnpre::U8Px<U8 < 0 ? HN_RESIZE_NONE : U8, 4> rn[4];
+  auto fetch = [&](long pp) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) vn[k] = src[lane + 64 * k];
-  }
+    for (int k = 0; k < 4; ++k) {
+      if constexpr (U8 < 0) {
+        vn[k] = reinterpret_cast<const float4*>(in + pp * 1024)[lane + 64 * k];
+      } else {
+        const int px = 4 * (lane + 64 * k);
+        rn[k].load(in8 + pp * INB, px >> 5, px & 31);
+      }
+    }
+  };
+  if (p < P) fetch(p);
 #pragma unroll 1
   for (; p < P; p += stride) {  // wave-uniform
     float v[16];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      v[4 * k] = vn[k].x; v[4 * k + 1] = vn[k].y; v[4 * k + 2] = vn[k].z; v[4 * k + 3] = vn[k].w;
-    }
-    if (p + stride < P) {
-      const float4* src = reinterpret_cast<const float4*>(in + (p + stride) * 1024);
+      if constexpr (U8 < 0) {
+        v[4 * k] = vn[k].x; v[4 * k + 1] = vn[k].y; v[4 * k + 2] = vn[k].z; v[4 * k + 3] = vn[k].w;
+      } else {
+        const int px = 4 * (lane + 64 * k);
+        int q[4];
+        rn[k].resized(px >> 5, px & 31, q);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) vn[k] = src[lane + 64 * k];
+        for (int j = 0; j < 4; ++j) v[4 * k + j] = hnpre::to_input(q[j], pmean, pstd, pnorm);
+      }
     }
+    if (p + stride < P) fetch(p + stride);
     // input_norm as des.py:40-47: (x - mean) / (std_unbiased + eps)
     float a = 0.f;
 #pragma unroll
@@ -327,32 +346,46 @@ __global__ __launch_bounds__(256) void k_fdl_front_mfma(const float* __restrict_
 
 }  // namespace
 
-hipError_t hn_launch_fdl_front(const HnFdlFrontArgs& a, int P, int mode, float eps, hipStream_t st) {
+hipError_t hn_launch_fdl_front(const HnFdlFrontArgs& a, int P, int mode, float eps, hipStream_t st,
+                               const HnU8In* u8) {
   if (P <= 0) return hipSuccess;
+  if (mode != 0 && mode != 1) return hipErrorInvalidValue;
   if (!hn_knobs().fdl_valu) {  // HN_FDL_VALU=1: the fp32 VALU form (A/B)
-    int resident = 0;  // persistent grid
-    const hipError_t e =
-        hn_resident_blocks(reinterpret_cast<const void*>(&k_fdl_front_mfma<0>), 256, 0, &resident);
-    if (e != hipSuccess) return e;
-    const int grid = std::min((P + 3) / 4, resident);
-    if (mode == 0)
-      hipLaunchKernelGGL(k_fdl_front_mfma<0>, dim3(grid), dim3(256), 0, st, a.in, a.out, a.stem_w, a.stem_b,
-                         a.w1, a.b1, a.w2, a.b2, P, eps);
-    else if (mode == 1)
-      hipLaunchKernelGGL(k_fdl_front_mfma<1>, dim3(grid), dim3(256), 0, st, a.in, a.out, a.stem_w, a.stem_b,
-                         a.w1, a.b1, a.w2, a.b2, P, eps);
-    else
-      return hipErrorInvalidValue;
+    const void* src = u8 ? static_cast<const void*>(u8->in) : static_cast<const void*>(a.in);
+    const float pm = u8 ? u8->mean : 0.f, ps = u8 ? u8->stdv : 1.f;
+    const int pn = u8 ? u8->normalize : 0;
+    // persistent grid: the resident workgroups of the instantiation launched (the PIL loads hold more registers)
+#define HN_FDL_GO(M, ...)                                                                                          \
+  {                                                                                                                \
+    int resident = 0;                                                                                              \
+    const hipError_t e = hn_resident_blocks(reinterpret_cast<const void*>(&k_fdl_front_mfma<M, ##__VA_ARGS__>), 256, \
+                                            0, &resident);                                                         \
+    if (e != hipSuccess) return e;                                                                                 \
+    hipLaunchKernelGGL((k_fdl_front_mfma<M, ##__VA_ARGS__>), dim3(std::min((P + 3) / 4, resident)), dim3(256), 0, st, \
+                       src, a.out, a.stem_w, a.stem_b, a.w1, a.b1, a.w2, a.b2, P, eps, pm, ps, pn);                \
+  }
+#define HN_FDL_MODES(M)                                                          \
+  if (!u8) HN_FDL_GO(M)                                                          \
+  else if (u8->resize == HN_RESIZE_NONE) HN_FDL_GO(M, HN_RESIZE_NONE)            \
+  else if (u8->resize == HN_RESIZE_CV2_LINEAR) HN_FDL_GO(M, HN_RESIZE_CV2_LINEAR) \
+  else if (u8->resize == HN_RESIZE_PIL_BILINEAR) HN_FDL_GO(M, HN_RESIZE_PIL_BILINEAR) \
+  else return hipErrorInvalidValue;
+    if (mode == 0) {
+      HN_FDL_MODES(0)
+    } else {
+      HN_FDL_MODES(1)
+    }
+#undef HN_FDL_MODES
+#undef HN_FDL_GO
     return hipGetLastError();
   }
+  if (u8) return hipErrorInvalidValue;  // the VALU A/B form reads fp32 patches only
   const int grid = (P + 3) / 4;
   if (mode == 0)
     hipLaunchKernelGGL(k_fdl_front<0>, dim3(grid), dim3(256), 0, st, a.in, a.out, a.stem_w, a.stem_b,
                        a.w1, a.b1, a.w2, a.b2, P, eps);
-  else if (mode == 1)
+  else
     hipLaunchKernelGGL(k_fdl_front<1>, dim3(grid), dim3(256), 0, st, a.in, a.out, a.stem_w, a.stem_b,
                        a.w1, a.b1, a.w2, a.b2, P, eps);
-  else
-    return hipErrorInvalidValue;
   return hipGetLastError();
 }

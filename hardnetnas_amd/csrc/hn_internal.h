@@ -136,7 +136,9 @@ struct HnFdlFrontArgs {
   const float *w1, *b1;          // [32][32], [32] (mode 0)
   const float *w2, *b2;          // [32][64], [64]
 };
-hipError_t hn_launch_fdl_front(const HnFdlFrontArgs& a, int P, int mode, float eps, hipStream_t st);
+// u8: uint8 patches preprocessed in the patch load (hn_forward_u8), else a.in (fp32)
+hipError_t hn_launch_fdl_front(const HnFdlFrontArgs& a, int P, int mode, float eps, hipStream_t st,
+                               const HnU8In* u8 = nullptr);
 // fused IRF block (pw -> dw -> pwl [+ residual]) for layers 1..5, hn_irf.hip
 struct HnIrfArgs {
   const float* x;

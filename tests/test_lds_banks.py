@@ -291,3 +291,61 @@ def test_irf_weight_pad_slots_conflict_free():
                     a = (tap * 8 + q) * 144 + 128
                     addrs.setdefault((a // 16) % 16, set()).add(a)
                 assert all(len(v) == 1 for v in addrs.values()), (k, tap)
+
+
+# hn_wino1.hip (1-D Winograd F(2,3)): (CIN, COUT, H, NP, TR, WM, WN) of conv3 / conv5
+W1_CONFIGS = {"3": (64, 64, 16, 1, 16, 2, 2), "5": (128, 128, 8, 2, 8, 1, 4)}
+WRITE_GROUPS = [list(range(i, i + 8)) for i in range(0, 64, 8)]  # ds_write_b128: 8 x 8 contiguous
+
+
+def w1_geometry(cin, cout, h, np_, tr, wm, wn):
+    ntx = h // 2
+    rin = tr + 2
+    xrow = ntx * 64
+    rs = 4 * xrow
+    ps = rin * rs
+    bm = np_ * tr * ntx
+    return dict(ntx=ntx, rin=rin, xrow=xrow, rs=rs, ps=ps, mt=bm // wm // 32, units=np_ * rin * ntx * 4)
+
+
+@pytest.mark.parametrize("layer", sorted(W1_CONFIGS))
+def test_wino1_operand_reads_conflict_free(layer):
+    """Every 32x32x16 operand read of k_conv_w1 (lane: M index r = (row, column pair), channel half
+    h; chunk 2 ks + h of window row yl + ky at chunk ^ ((yl + ky) & 3))."""
+    cin, cout, h, np_, tr, wm, wn = W1_CONFIGS[layer]
+    g = w1_geometry(*W1_CONFIGS[layer])
+    for w in range(wm):
+        for mt in range(g["mt"]):
+            for kx in range(24):
+                xi, ky, ks = kx // 6, (kx % 6) // 2, kx % 2
+                addrs = []
+                for lane in range(64):
+                    r, hh = lane & 31, lane >> 5
+                    m = (w * g["mt"] + mt) * 32 + r
+                    npi, rem = divmod(m, tr * g["ntx"])
+                    yl, t = divmod(rem, g["ntx"])
+                    addrs.append(npi * g["ps"] + (yl + ky) * g["rs"] + xi * g["xrow"] + t * 64
+                                 + 16 * ((2 * ks + hh) ^ ((yl + ky) & 3)))
+                for grp in GROUPS:
+                    slots = {(addrs[l] // 16) % 16 for l in grp}
+                    assert len(slots) == 16, (layer, w, mt, kx, grp[0])
+
+
+@pytest.mark.parametrize("layer", sorted(W1_CONFIGS))
+def test_wino1_producer_writes_conflict_free(layer):
+    """The producers' ds_write_b128 of one transform position xi: unit u = ((patch, row), column
+    pair, 8-channel group) -> chunk g ^ (row & 3) of position t; each 8-lane group covers 128
+    distinct contiguous bytes."""
+    g = w1_geometry(*W1_CONFIGS[layer])
+    for k in range(-(-g["units"] // 256)):
+        for wave in range(4):
+            for xi in range(4):
+                addrs = []
+                for lane in range(64):
+                    u = wave * 64 + lane + k * 256
+                    gg, t, rest = u & 3, (u >> 2) % g["ntx"], (u >> 2) // g["ntx"]
+                    wr, npi = rest % g["rin"], rest // g["rin"]
+                    addrs.append(npi * g["ps"] + wr * g["rs"] + xi * g["xrow"] + t * 64 + 16 * (gg ^ (wr & 3)))
+                for grp in WRITE_GROUPS:
+                    slots = {(addrs[l] // 16) % 16 for l in grp}
+                    assert len(slots) == 8, (layer, k, wave, xi, grp[0])

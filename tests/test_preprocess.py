@@ -140,13 +140,14 @@ def _u8_batch(n, seed, hw=64):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["hardnet", "wang2", "wang3", "wang4", "fdl_NASNet"])
+@pytest.mark.parametrize("name", ["hardnet", "wang2", "wang3", "wang4", "fdl_NASNet", "fdl_NASNet_01"])
 @pytest.mark.parametrize("resize,normalize", [("pil", False), ("pil", True), ("cv2", True), ("none", True)])
 @pytest.mark.parametrize("n", [1, 37, 3001])
 def test_forward_u8_equals_preprocess_then_forward(name, resize, normalize, n, cuda_device):
     """hn_forward_u8 == hn_preprocess followed by hn_forward, bit for bit (HardNet: fused into
-    k_c12's patch load; NAS: fused into k_front's in NONE / CV2 mode -- wang2 the k3 no-fold form,
-    wang3 k5, wang4 the maxpool form; FDLNet and NAS PIL: preprocessed into the workspace); 3,001 patches run every
+    k_c12's patch load; FDLNet: into k_fdl_front_mfma's, every mode; NAS: into k_front's in NONE / CV2
+    mode -- wang2 the k3 no-fold form, wang3 k5, wang4 the maxpool form; NAS PIL: preprocessed into the
+    workspace); 3,001 patches run every
     persistent workgroup over several patches and end on a ragged one."""
     m, _, _ = build_module(name)
     nm = N.NativeModel.from_module(m, cuda_device)
@@ -156,7 +157,7 @@ def test_forward_u8_equals_preprocess_then_forward(name, resize, normalize, n, c
     nm.set_profiling(True)
     got = nm.forward_u8(u, resize=resize, normalize=normalize)
     st = nm.stage_times()
-    assert ("preprocess" in st) == (name.startswith("fdl") or (name != "hardnet" and resize == "pil"))
+    assert ("preprocess" in st) == (name in ("wang2", "wang3", "wang4") and resize == "pil")
     assert torch.equal(got, ref)
 
 
