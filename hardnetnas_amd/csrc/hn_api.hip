@@ -1075,7 +1075,7 @@ static bool u8_fused(const hn_model* m, int resize) {
   if (m->desc.kind == HN_KIND_FDL_NASNET || m->desc.kind == HN_KIND_FDL_NASNET01) return !m->knobs.fdl_valu;
   if (m->desc.kind == HN_KIND_NAS)  // the fused front's patch load (hn_front.hip): no input_norm, not PIL
     return resize != HN_RESIZE_PIL_BILINEAR && m->front && m->desc.input_norm_eps < 0.f && !m->knobs.front_fold;
-  return m->desc.kind == HN_KIND_HARDNET && m->c12 && !m->unfused_stem && m->knobs.c12_cfg == 12 &&
+  return m->desc.kind == HN_KIND_HARDNET && m->c12 && !m->unfused_stem && (m->knobs.c12_cfg == 12 || m->knobs.c12_cfg == 13) &&
          !m->knobs.c12_abl;
 }
 

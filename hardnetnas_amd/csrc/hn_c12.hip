@@ -591,6 +591,331 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, WP
   }
 }
 
+
+// ------------------------------------------------------------------------------------------
+// k_c12h: the same computation with the roles split per SIMD.  One workgroup per CU of 8 waves:
+// waves 0-3 (one per SIMD, 256-register budget) run only conv1 (P2) and conv2 (P3) of band g on
+// the MFMA; waves 4-7 (the SIMDs' second waves) run the stem (P1) of band g + 1, the next patch's
+// input_norm and the stores of band g - 1's a2 rows meanwhile.  In k_c12 every wave runs P1 -> P2
+// -> P3 in sequence and P1 (3 % of the MFMA work, a latency chain of LDS reads, split, 3 MFMAs,
+// split, LDS stores) costs ~17 % of each band on every SIMD; here it runs beside the MFMA stream.
+// Two barriers per band: X_g (W1 rows of band g complete) and E_g (band g's a2 tile staged, band
+// g + 1's W0 rows complete).  Rings: W0 12 rows (P1 of band g + 1 -- or of the next patch's band 0
+// -- writes while P2 of band g reads), W1 5 rows; conv1's A fragments in LDS (the 4 MFMA waves
+// read the same ones), conv2's quarter of each MFMA wave resident in its registers.
+// U8: as k_c12 (the patch load preprocesses uint8 patches; -1 = fp32).
+template <int U8 = -1>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_c12h(
+    const void* __restrict__ in_, float* __restrict__ out, const float* __restrict__ stem_w,
+    const float* __restrict__ stem_b, const uint4* __restrict__ w1p, const float* __restrict__ b1,
+    const uint4* __restrict__ w2p, const float* __restrict__ b2, int P, float eps, float pmean, float pstd,
+    int pnorm) {
+  constexpr int NA0 = 12, NA1 = 5;
+  __shared__ __attribute__((aligned(16))) char s_w0[NA0 * W0C * PXB];
+  __shared__ __attribute__((aligned(16))) char s_w1[NA1 * W1C * PXB];
+  __shared__ __attribute__((aligned(16))) uint4 s_a1w[9 * 2 * 2 * 64];  // conv1 A fragments [tap][g][plane][lane]
+  __shared__ __attribute__((aligned(16))) float s_in[2][34 * 34];      // normalised patch, by patch parity
+  __shared__ __attribute__((aligned(16))) uint4 s_stem[64][2];
+  __shared__ __attribute__((aligned(16))) float s_st[2 * 16 * 64];     // a2 staging (k_c12's XST)
+  __shared__ __attribute__((aligned(16))) float s_b1[32], s_b2[64];
+
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const bool mw = w < 4;  // MFMA wave (one per SIMD)
+  const int hw = w & 3;   // index within the role
+  const int r32 = lane & 31, h32 = lane >> 5;
+  const int c16 = lane & 15, g16 = lane >> 4;
+
+  const long per = ((long)P + gridDim.x - 1) / gridDim.x;
+  const long pb = (long)xcd_remap(blockIdx.x, gridDim.x) * per;
+  const long pe = min((long)P, pb + per);
+  if (pb >= pe) return;  // workgroup-uniform
+  const long G = (pe - pb) * 8;  // bands (2 conv2 rows each)
+
+  // ---- one-time init ----
+  for (int i = t; i < NA0 * W0C * PXB / 16; i += 512) reinterpret_cast<uint4*>(s_w0)[i] = make_uint4(0, 0, 0, 0);
+  for (int i = t; i < NA1 * W1C * PXB / 16; i += 512) reinterpret_cast<uint4*>(s_w1)[i] = make_uint4(0, 0, 0, 0);
+  for (int i = t; i < 2 * 34 * 34; i += 512) (&s_in[0][0])[i] = 0.f;
+  for (int i = t; i < 9 * 2 * 2 * 64; i += 512) s_a1w[i] = w1p[i];
+  if (t < 64) {
+    bf16x8 sah, sal;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {  // K slot 9 carries the bias (its B input is 1.0)
+      const int tap = 8 * h32 + j;
+      const float v = tap < 9 ? stem_w[tap * 32 + r32] : (tap == 9 ? stem_b[r32] : 0.f);
+      sah[j] = (__bf16)v;
+      sal[j] = (__bf16)(v - (float)sah[j]);
+    }
+    s_stem[lane][0] = __builtin_bit_cast(uint4, sah);
+    s_stem[lane][1] = __builtin_bit_cast(uint4, sal);
+  }
+  for (int i = t; i < 96; i += 512) {
+    if (i < 32) s_b1[i] = b1[i];
+    else s_b2[i - 32] = b2[i - 32];
+  }
+
+  // W0 slot of a0 row y (-1 .. 32) of the workgroup's patch pl; W1 slot of a1 row y (-1 .. 31)
+  auto w0row = [&](long pl, int y) { return s_w0 + (int)((pl * 34 + y + 1) % NA0) * W0C * PXB; };
+  auto w1row = [&](int y) { return s_w1 + ((y + 1) % NA1) * W1C * PXB; };
+
+  // ---- helper side: input_norm (wave 4), P1, a2 stores ----
+  const float* in = static_cast<const float*>(in_);
+  const uint8_t* in8 = static_cast<const uint8_t*>(in_);
+  constexpr int INB = U8 == HN_RESIZE_NONE ? 1024 : 4096;
+  float4 vn[4];
+  hnpre::U8Px<U8 < 0 ? HN_RESIZE_NONE : U8, 4> rn[4];
+  auto patch_fetch = [&](long p) {  // lane's 16 pixels: 4 runs of 4 at px = 4 (lane + 64 k)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if constexpr (U8 < 0) {
+        vn[k] = reinterpret_cast<const float4*>(in + p * 1024)[lane + 64 * k];
+      } else {
+        const int px = 4 * (lane + 64 * k);
+        rn[k].load(in8 + p * INB, px >> 5, px & 31);
+      }
+    }
+  };
+  auto patch_norm = [&](long p) {  // input_norm (HardNet.py:306-310) of the fetched patch -> s_in[p & 1]
+    float v[16];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if constexpr (U8 < 0) {
+        v[4 * k] = vn[k].x; v[4 * k + 1] = vn[k].y; v[4 * k + 2] = vn[k].z; v[4 * k + 3] = vn[k].w;
+      } else {
+        const int px = 4 * (lane + 64 * k);
+        int q[4];
+        rn[k].resized(px >> 5, px & 31, q);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[4 * k + j] = hnpre::to_input(q[j], pmean, pstd, pnorm);
+      }
+    }
+    float mean = 0.f, sd = 1.f;
+    if (eps >= 0.f) {
+      float a = 0.f;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) a += v[j];
+      mean = wave_sum(a) * (1.f / 1024.f);
+      float q = 0.f;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) q += (v[j] - mean) * (v[j] - mean);
+      sd = sqrtf(wave_sum(q) * (1.f / 1023.f)) + eps;
+    }
+    const float inv = 1.f / sd;  // as k_c12
+    float* si = s_in[p & 1];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int px = 4 * (lane + 64 * k), y = px >> 5, x = px & 31;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) si[(y + 1) * 34 + x + 1 + j] = (v[4 * k + j] - mean) * inv;
+    }
+  };
+  // P1: the new a0 rows of band g (helper wave hw: rows ri = hw, hw + 4)
+  auto p1_band = [&](long g) {
+    const long pl = g >> 3;
+    const int band = (int)(g & 7);
+    const float* si = s_in[(pb + pl) & 1];
+    const int ybeg = band == 0 ? -1 : 4 * band + 1, nrows = band == 0 ? 6 : 4;
+#pragma unroll 1
+    for (int ri = hw; ri < nrows; ri += 4) {
+      const int y = ybeg + ri;
+      char* rowp = w0row(pl, y);
+      if (y < 0 || y >= 32) {  // zero padding row (interior columns)
+        for (int i = lane; i < 32 * (PXB / 16); i += 64) reinterpret_cast<uint4*>(rowp + PXB)[i] = make_uint4(0, 0, 0, 0);
+        continue;
+      }
+      bf16x8 xh, xl;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int tap = 8 * h32 + j;
+        const float xv = tap < 9 ? si[(y + tap / 3) * 34 + r32 + tap % 3] : (tap == 9 ? 1.f : 0.f);
+        xh[j] = (__bf16)xv;
+        xl[j] = (__bf16)(xv - (float)xh[j]);
+      }
+      const f32x16 c0 = mfma3(as_bf16x8(s_stem[lane][0]), as_bf16x8(s_stem[lane][1]), xh, xl, f32x16{});
+      uint2 hi[4], lo[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        hi[q] = pack_bf16x4(fmaxf(c0[4 * q], 0.f), fmaxf(c0[4 * q + 1], 0.f), fmaxf(c0[4 * q + 2], 0.f),
+                            fmaxf(c0[4 * q + 3], 0.f), lo[q]);
+      char* o = rowp + (r32 + 1) * PXB + 16 * h32;
+#pragma unroll
+      for (int k = 0; k < 4; k += 2) {
+        auto sw = [](uint2& a, uint2& b) {
+          const auto rx = __builtin_amdgcn_permlane32_swap(a.x, b.x, false, false);
+          const auto ry = __builtin_amdgcn_permlane32_swap(a.y, b.y, false, false);
+          a.x = rx[0]; b.x = rx[1]; a.y = ry[0]; b.y = ry[1];
+        };
+        sw(hi[k], hi[k + 1]);
+        sw(lo[k], lo[k + 1]);
+        *reinterpret_cast<uint4*>(o + 16 * k) = make_uint4(hi[k].x, hi[k].y, hi[k + 1].x, hi[k + 1].y);
+        *reinterpret_cast<uint4*>(o + 64 + 16 * k) = make_uint4(lo[k].x, lo[k].y, lo[k + 1].x, lo[k + 1].y);
+      }
+    }
+  };
+  // a2 rows 2 band .. 2 band + 1 of band g from s_st (k_c12's xst_flush: 4 whole pixel rows per store)
+  auto flush = [&](long g) {
+    const long patch = pb + (g >> 3);
+    const int row0 = 2 * (int)(g & 7), ry = hw >> 1, q = lane & 15;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int x = 8 * (hw & 1) + (lane >> 4) + 4 * j;
+      const f32x4v v = *reinterpret_cast<const f32x4v*>(s_st + ((ry * 16 + x) * 16 + (q ^ (x & 7))) * 4);
+      *reinterpret_cast<f32x4v*>(out + ((patch * 16 + row0 + ry) * 16 + x) * 64 + 4 * q) = v;
+    }
+  };
+
+  if (!mw) {
+    if (hw == 0) {
+      patch_fetch(pb);
+      patch_norm(pb);
+    }
+    __syncthreads();  // B0: s_in of the first patch
+    p1_band(0);
+    if (hw == 0 && pb + 1 < pe) patch_fetch(pb + 1);
+    __syncthreads();  // B1: band 0's W0 rows
+#pragma unroll 1
+    for (long g = 0; g < G; ++g) {
+      // part 1, beside P2(g): band g - 1's a2 rows, P1 of band g + 1
+      if (g > 0) flush(g - 1);
+      if (g + 1 < G) p1_band(g + 1);
+      __syncthreads();  // X_g
+      // part 2, beside P3(g): the next patch's input_norm (band 0), its pixels fetched a band ahead
+      if (hw == 0 && (g & 7) == 0) {
+        const long pn = pb + (g >> 3) + 1;
+        if (pn < pe) patch_norm(pn);
+        if (pn + 1 < pe) patch_fetch(pn + 1);
+      }
+      __syncthreads();  // E_g
+    }
+    flush(G - 1);
+    return;
+  }
+
+  // ---- MFMA side: P2 (conv1) and P3 (conv2) of every band ----
+  uint4 w2r[9][2];  // this wave's conv2 quarter (hw), both planes, resident
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+    for (int pl = 0; pl < 2; ++pl) w2r[tap][pl] = w2p[((tap * 4 + hw) * 2 + pl) * 64 + lane];
+  __syncthreads();  // B0
+  __syncthreads();  // B1
+#pragma unroll 1
+  for (long g = 0; g < G; ++g) {
+    const long pl = g >> 3;
+    const int band = (int)(g & 7);
+    // ---- P2: a1 row y1 = 4 band + hw, both 16-pixel halves, both 16-channel groups ----
+    {
+      const int y1 = 4 * band + hw;
+      if (band == 0 && hw == 0) {  // a1 row -1 (conv2's zero padding), every channel
+        char* zrow = w1row(-1);
+        for (int i = lane; i < W1C * (PXB / 16); i += 64) reinterpret_cast<uint4*>(zrow)[i] = make_uint4(0, 0, 0, 0);
+      }
+      f32x4v acc[2][2];
+#pragma unroll
+      for (int gg = 0; gg < 2; ++gg)
+        acc[0][gg] = acc[1][gg] = *reinterpret_cast<const f32x4v*>(s_b1 + 16 * gg + 4 * g16);
+      const char* srow[3];
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy) srow[dy] = w0row(pl, y1 - 1 + dy) + c16 * PXB + 16 * g16;
+      uint4 bq[2][2][2], aq[2][2][2];  // [buffer][half | group][plane]
+      auto fetch = [&](int tn, uint4 (&b)[2][2], uint4 (&a)[2][2]) {
+#pragma unroll
+        for (int hn = 0; hn < 2; ++hn) {
+          const char* p = srow[tn / 3] + (tn % 3 + 16 * hn) * PXB;
+          b[hn][0] = *reinterpret_cast<const uint4*>(p);
+          b[hn][1] = *reinterpret_cast<const uint4*>(p + 64);
+        }
+#pragma unroll
+        for (int gg = 0; gg < 2; ++gg)
+#pragma unroll
+          for (int pln = 0; pln < 2; ++pln) a[gg][pln] = s_a1w[((tn * 2 + gg) * 2 + pln) * 64 + lane];
+      };
+      fetch(0, bq[0], aq[0]);
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        if (tap + 1 < 9) fetch(tap + 1, bq[(tap + 1) & 1], aq[(tap + 1) & 1]);
+        __builtin_amdgcn_sched_barrier(0);
+        const uint4(&b)[2][2] = bq[tap & 1];
+        const uint4(&a)[2][2] = aq[tap & 1];
+#pragma unroll
+        for (int gg = 0; gg < 2; ++gg)
+#pragma unroll
+          for (int hx = 0; hx < 2; ++hx) acc[hx][gg] = mfma16(a[gg][1], b[hx][0], acc[hx][gg]);
+#pragma unroll
+        for (int gg = 0; gg < 2; ++gg)
+#pragma unroll
+          for (int hx = 0; hx < 2; ++hx) acc[hx][gg] = mfma16(a[gg][0], b[hx][1], acc[hx][gg]);
+#pragma unroll
+        for (int gg = 0; gg < 2; ++gg)
+#pragma unroll
+          for (int hx = 0; hx < 2; ++hx) acc[hx][gg] = mfma16(a[gg][0], b[hx][0], acc[hx][gg]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      char* prow = w1row(y1);
+#pragma unroll
+      for (int hx = 0; hx < 2; ++hx) {
+        char* pix = prow + w1_slot(16 * hx + c16) * PXB;
+#pragma unroll
+        for (int gg = 0; gg < 2; ++gg) {
+          const f32x4v r = __builtin_elementwise_max(acc[hx][gg], f32x4v{});
+          uint2 lo;
+          uint2 hi = pack_bf16x4(r[0], r[1], r[2], r[3], lo);
+          const auto rx = __builtin_amdgcn_permlane16_swap(hi.x, lo.x, false, false);
+          const auto ry = __builtin_amdgcn_permlane16_swap(hi.y, lo.y, false, false);
+          hi.x = rx[0]; lo.x = rx[1]; hi.y = ry[0]; lo.y = ry[1];
+          char* d16 = pix + 32 * gg + 16 * (g16 >> 1) + 64 * (g16 & 1);
+          *reinterpret_cast<uint4*>(d16) = make_uint4(hi.x, hi.y, lo.x, lo.y);
+        }
+      }
+    }
+    __syncthreads();  // X_g
+    // ---- P3: conv2 rows 2 band, 2 band + 1, this wave's 16-channel quarter ----
+    {
+      f32x4v acc[2];
+      acc[0] = acc[1] = *reinterpret_cast<const f32x4v*>(s_b2 + 16 * hw + 4 * g16);
+      const char* srow[2][3];
+#pragma unroll
+      for (int ry = 0; ry < 2; ++ry)
+#pragma unroll
+        for (int dy = 0; dy < 3; ++dy) srow[ry][dy] = w1row(2 * (2 * band + ry) - 1 + dy) + c16 * PXB + 16 * g16;
+      auto bptr = [&](int tn, int rn) {
+        const int dx = tn % 3;
+        return srow[rn][tn / 3] + (dx == 1 ? 17 : (dx >> 1)) * PXB;
+      };
+      uint4 bf[2][2][2];  // [buffer][row][plane]
+#pragma unroll
+      for (int rn = 0; rn < 2; ++rn) {
+        bf[0][rn][0] = *reinterpret_cast<const uint4*>(bptr(0, rn));
+        bf[0][rn][1] = *reinterpret_cast<const uint4*>(bptr(0, rn) + 64);
+      }
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        if (tap + 1 < 9) {
+#pragma unroll
+          for (int rn = 0; rn < 2; ++rn) {
+            bf[(tap + 1) & 1][rn][0] = *reinterpret_cast<const uint4*>(bptr(tap + 1, rn));
+            bf[(tap + 1) & 1][rn][1] = *reinterpret_cast<const uint4*>(bptr(tap + 1, rn) + 64);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        const uint4(&b)[2][2] = bf[tap & 1];
+        acc[0] = mfma16(w2r[tap][1], b[0][0], acc[0]);
+        acc[1] = mfma16(w2r[tap][1], b[1][0], acc[1]);
+        acc[0] = mfma16(w2r[tap][0], b[0][1], acc[0]);
+        acc[1] = mfma16(w2r[tap][0], b[1][1], acc[1]);
+        acc[0] = mfma16(w2r[tap][0], b[0][0], acc[0]);
+        acc[1] = mfma16(w2r[tap][0], b[1][0], acc[1]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int ry = 0; ry < 2; ++ry)
+        *reinterpret_cast<f32x4v*>(s_st + ((ry * 16 + c16) * 16 + ((4 * hw + g16) ^ (c16 & 7))) * 4) =
+            __builtin_elementwise_max(acc[ry], f32x4v{});
+    }
+    __syncthreads();  // E_g
+  }
+}
+
 }  // namespace
 
 // HN_C12_CFG variants (A/B and ablation builds; 12 is production):
@@ -605,7 +930,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, WP
   X(6, 4, 2, 2, true, 3, false, 0) X(7, 4, 2, 2, false, 2, true, 0) X(8, 4, 2, 2, true, 2, true, 0)      \
   X(9, 8, 4, 2, false, 2, true, 0) X(10, 4, 2, 2, false, 2, true, 1) X(11, 4, 2, 2, false, 2, true, 3) \
   X(12, 4, 2, 2, false, 2, true, 5)
-constexpr int kC12Cfgs = 13;  // (P1, P3) at priority (2, 1) / (1, 2) / (2, 2): within the box noise of 12, removed
+constexpr int kC12Cfgs = 14;  // 13: k_c12h (MFMA / helper waves split per SIMD), not in HN_C12_CFGS  // (P1, P3) at priority (2, 1) / (1, 2) / (2, 2): within the box noise of 12, removed
 
 bool hn_c12_cfg_ok(int cfg, int abl) {
   if (cfg < 0 || cfg >= kC12Cfgs) return false;
@@ -627,17 +952,17 @@ hipError_t hn_launch_c12(const float* in, float* out, const HardnetDev& d, int P
   const int cfg = hn_knobs().c12_cfg;  // same-box A/Bs: 12 2-4 % < 7 1.5 % < 2 4.5 % < 0
   const int abl = hn_knobs().c12_abl;
   if (!hn_c12_cfg_ok(cfg, abl)) return hipErrorInvalidValue;
-  if (u8 && (cfg != 12 || abl)) return hipErrorInvalidValue;  // the uint8 loads: production build only
+  if (u8 && ((cfg != 12 && cfg != 13) || abl)) return hipErrorInvalidValue;  // the uint8 loads: production builds only
   static const void* const fns[kC12Cfgs] = {
 #define HN_C12_FN(C, W, R, E, I, A, Q, PR) reinterpret_cast<const void*>(&k_c12<0, W, R, E, I, A, Q, PR>),
       HN_C12_CFGS(HN_C12_FN)
 #undef HN_C12_FN
-  };
+      reinterpret_cast<const void*>(&k_c12h<-1>)};
   static const int nws[kC12Cfgs] = {
 #define HN_C12_NWS(C, W, R, E, I, A, Q, PR) W,
       HN_C12_CFGS(HN_C12_NWS)
 #undef HN_C12_NWS
-  };
+      8};
   const int nw = nws[cfg];
   int resident = 0;
   const hipError_t e = hn_resident_blocks(fns[cfg], nw * 64, 0, &resident);
@@ -650,6 +975,19 @@ hipError_t hn_launch_c12(const float* in, float* out, const HardnetDev& d, int P
   hipLaunchKernelGGL((k_c12<A, W, R, E, I, WA, Q, PR, ##__VA_ARGS__>), dim3(grid), dim3(W * 64), 0, st, src, \
                      out, d.stem_w, d.stem_b, static_cast<const uint4*>(d.c12_w1), d.bias[1],   \
                      static_cast<const uint4*>(d.c12_w2), d.bias[2], P, eps, pm, ps, pn)
+#define HN_C12H_GO(U)                                                                                        \
+  hipLaunchKernelGGL((k_c12h<U>), dim3(grid), dim3(512), 0, st, src, out, d.stem_w, d.stem_b,               \
+                     static_cast<const uint4*>(d.c12_w1), d.bias[1], static_cast<const uint4*>(d.c12_w2),   \
+                     d.bias[2], P, eps, pm, ps, pn)
+  if (cfg == 13) {
+    if (!u8) HN_C12H_GO(-1);
+    else if (u8->resize == HN_RESIZE_NONE) HN_C12H_GO(HN_RESIZE_NONE);
+    else if (u8->resize == HN_RESIZE_CV2_LINEAR) HN_C12H_GO(HN_RESIZE_CV2_LINEAR);
+    else if (u8->resize == HN_RESIZE_PIL_BILINEAR) HN_C12H_GO(HN_RESIZE_PIL_BILINEAR);
+    else return hipErrorInvalidValue;
+#undef HN_C12H_GO
+    return hipGetLastError();
+  }
   if (u8) {
     switch (u8->resize) {
       case HN_RESIZE_NONE: HN_C12_GO(0, 4, 2, 2, false, 2, true, 5, HN_RESIZE_NONE); break;

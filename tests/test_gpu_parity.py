@@ -151,12 +151,12 @@ def test_fused_c12_is_default_and_matches_layerwise(cuda_device, monkeypatch):
         assert np.abs(nm(x[:b]).cpu().numpy() - lw(x[:b]).cpu().numpy()).max() <= 2e-5
 
 
-@pytest.mark.parametrize("cfg", ["0", "1", "2", "3", "5", "7", "8", "9", "10", "11"])
+@pytest.mark.parametrize("cfg", ["0", "1", "2", "3", "5", "7", "8", "9", "10", "11", "12", "13"])
 def test_c12_variants_match(cuda_device, monkeypatch, cfg):
     """HN_C12_CFG=0: 8-wave workgroups with 4-row bands; 1: one wave per SIMD (512-register
     file); 2: 4-wave workgroups with 2-row bands, two per CU; 3 / 5: tap-interleaved P3; 7 / 8 / 9:
-    tap-interleaved P2; 10 / 11: raised P1 priority -- against the production build (12: 2 with
-    the tap-interleaved P2 and P3 + P1 at raised wave priority).  Both agree with the default build to the split-precision level (the 4-wave builds sum
+    tap-interleaved P2; 10 / 11: raised P1 priority; 12: 2 with the tap-interleaved P2 and P3 + P1 at
+    raised wave priority; 13: k_c12h (MFMA and helper waves split per SIMD) -- against the default build.  Both agree with the default build to the split-precision level (the 4-wave builds sum
     input_norm's mean/std in a different order; the MFMA order per output is the same)."""
     from hardnetnas_amd._native import NativeModel
     m, fx, _ = build_module("hardnet")
@@ -171,6 +171,9 @@ def test_c12_variants_match(cuda_device, monkeypatch, cfg):
     assert np.abs(nm(xe).cpu().numpy() - fx["y_edge"]).max() <= TOL["hardnet"]
     for b in (1, 3, 130):
         assert np.abs(nm(x[:b]).cpu().numpy() - y0[:b]).max() <= 2e-5
+    # several patches per persistent workgroup, a ragged last range
+    xr = x.repeat(12, 1, 1, 1)[:3001]
+    assert np.abs(nm(xr).cpu().numpy() - np.tile(y0, (12, 1))[:3001]).max() <= 2e-5
 
 
 def test_unfused_stem_matches(cuda_device, monkeypatch):
