@@ -27,57 +27,60 @@
 
 namespace {
 
-template <int CIN, int COUT, int H, int NP, int TR, int WM, int WN>
+// Work tile = NP whole patches (every window row above / below the patch is padding, so the image
+// holds the H real rows of each patch and ONE zero row per plane that the padding reads point at).
+// CST: the epilogue goes through a per-wave LDS scratch so that each store writes 8 whole 128-byte
+// pixel slices (k_conv_ws's CST), one output column parity at a time.
+template <int CIN, int COUT, int H, int NP, int WM, int WN, bool CST>
 struct W1Cfg {
+  static constexpr int TR = H;              // output rows per work tile (whole patches)
   static constexpr int NTX = H / 2;         // output column pairs per row
-  static constexpr int RIN = TR + 2;        // window rows
-  static constexpr int RT = H / TR;         // row tiles per patch
   static constexpr int BM = NP * TR * NTX;  // GEMM M (output row x column pair) per work tile
   static constexpr int MT = BM / WM / 32, NT = COUT / WN / 32;
   static constexpr int NTOT = COUT / 32, NCC = CIN / 32;
   static constexpr int XROW = NTX * 64;  // bytes of one (row, xi) run of positions per plane
-  static constexpr int RS = 4 * XROW;    // bytes per window row per plane
-  static constexpr int PS = RIN * RS;    // per patch per plane
-  static constexpr int PLANE = NP * PS;
+  static constexpr int RS = 4 * XROW;    // bytes per image row per plane
+  static constexpr int PS = TR * RS;     // per patch per plane
+  static constexpr int ZROW = NP * PS;   // the zero row (offset within a plane)
+  static constexpr int PLANE = ZROW + RS;
   static constexpr int BUF = 2 * PLANE;
   static constexpr int NWC = WM * WN, NWP = 4, NTHR = (NWC + NWP) * 64, PTHR = NWP * 64;
-  static constexpr int UNITS = NP * RIN * NTX * 4;  // (patch, row, column pair, 8-channel group)
-  static_assert(64 % (4 * NTX) == 0 && PTHR % (4 * NTX) == 0, "a window row's units share one wave");
+  static constexpr int UNITS = NP * TR * NTX * 4;  // (patch, row, column pair, 8-channel group)
+  static_assert(64 % (4 * NTX) == 0 && PTHR % (4 * NTX) == 0, "a row's units share one wave");
   static constexpr int UPT = (UNITS + PTHR - 1) / PTHR;
   static constexpr bool DEEP = UPT <= 2;  // two stages of loads in flight
-  static constexpr int BIAS_OFF = 2 * BUF;
+  static constexpr int SROW = 36;                       // CST: floats per pixel slice of the scratch
+  static constexpr int SCR_OFF = 2 * BUF;
+  static constexpr int SCR = CST ? 32 * SROW * 4 : 0;   // CST: one 32-pixel x 32-channel tile per MFMA wave
+  static constexpr int BIAS_OFF = SCR_OFF + NWC * SCR;
   static constexpr int SMEM = BIAS_OFF + COUT * 4;
   static constexpr int NKS = 24;  // K-steps per stage: 4 xi x 3 ky x 2 halves of 16 channels
   static constexpr unsigned CHUNK_BYTES = NKS * NTOT * 2 * 64 * 16;
   static_assert(SMEM <= 160 * 1024, "LDS");
   static_assert(MT >= 1 && NT >= 1 && MT * WM * 32 == BM && NT * WN * 32 == COUT, "tiling");
   static_assert((TR * NTX) % 32 == 0 && 32 % NTX == 0, "an M tile = 32 / NTX whole rows of one patch");
-  static_assert(RS % 256 == 0, "window rows on 256-byte boundaries (the bank-conflict argument)");
-  static_assert(NP == 1 || TR == H, "multi-patch tiles cover whole patches");
+  static_assert(RS % 256 == 0, "image rows on 256-byte boundaries (the bank-conflict argument)");
 };
 
-template <int CIN, int COUT, int H, int NP, int TR, int WM, int WN>
+template <int CIN, int COUT, int H, int NP, int WM, int WN, bool CST>
 __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_w1(const float* __restrict__ in, float* __restrict__ out,
                                                                 const uint4* __restrict__ wp,
                                                                 const float* __restrict__ bias, int P) {
-  using C = W1Cfg<CIN, COUT, H, NP, TR, WM, WN>;
+  using C = W1Cfg<CIN, COUT, H, NP, WM, WN, CST>;
+  constexpr int TR = C::TR;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const bool producer = wave >= C::NWC;
   const int r = lane & 31, h = lane >> 5;
   const int nwg = gridDim.x, rb = xcd_remap(blockIdx.x, nwg);
-  const int ntiles = (P + NP - 1) / NP * C::RT;
+  const int ntiles = (P + NP - 1) / NP;
   const int my_tiles = rb < ntiles ? (ntiles - 1 - rb) / nwg + 1 : 0;
   const int NS = my_tiles * C::NCC;
   if (NS == 0) return;
   char* const buf0 = smem;
   char* const buf1 = smem + C::BUF;
-  auto tile_of = [&](int s, int& p0, int& y0) {
-    const int t = rb + (s / C::NCC) * nwg;
-    p0 = (t / C::RT) * NP;
-    y0 = (t % C::RT) * TR;
-  };
+  auto tile_of = [&](int s) { return (rb + (s / C::NCC) * nwg) * NP; };  // first patch of stage s's tile
 
   // ---- producer side ----
   // A unit (patch, window row, column pair t, 8-channel group) loads input columns 2t - 1 and 2t (the
@@ -86,16 +89,14 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_w1(const float* __r
   const int ptid = tid - C::NWC * 64;
   float4 pf[C::UPT][6], pf2[C::UPT][6];
   auto produce_loads = [&](int s, float4 (&d)[C::UPT][6]) {
-    int p0, y0;
-    tile_of(s, p0, y0);
+    const int p0 = tile_of(s);
     const int cc = s % C::NCC;
 #pragma unroll
     for (int k = 0; k < C::UPT; ++k) {
       const int u = ptid + k * C::PTHR;
       const int g = u & 3, t = (u >> 2) % C::NTX, rest = (u >> 2) / C::NTX;
-      const int wr = rest % C::RIN, np = rest / C::RIN;
-      const int y = y0 - 1 + wr;
-      const bool rowok = u < C::UNITS && (NP == 1 || p0 + np < P) && (unsigned)y < (unsigned)H;
+      const int y = rest % TR, np = rest / TR;
+      const bool rowok = u < C::UNITS && (NP == 1 || p0 + np < P);
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
         const int x = 2 * t - 1 + j;
@@ -118,7 +119,7 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_w1(const float* __r
     for (int k = 0; k < C::UPT; ++k) {
       const int u = ptid + k * C::PTHR;
       const int g = u & 3, t = (u >> 2) % C::NTX, rest = (u >> 2) / C::NTX;
-      const int wr = rest % C::RIN, np = rest / C::RIN;
+      const int y = rest % TR, np = rest / TR;
       const bool last = t == C::NTX - 1;
       const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
       float4 dd[4][2];  // d0..d3, channels 0-3 / 4-7
@@ -131,7 +132,7 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_w1(const float* __r
         dd[3][i] = last ? z : n1;
       }
       if (u < C::UNITS) {
-        const int off = np * C::PS + wr * C::RS + t * 64 + 16 * (g ^ (wr & 3));
+        const int off = np * C::PS + y * C::RS + t * 64 + 16 * (g ^ ((y + 1) & 3));  // window row y + 1
 #pragma unroll
         for (int xi = 0; xi < 4; ++xi) {
           float4 v[2];
@@ -152,6 +153,11 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_w1(const float* __r
     }
   };
 
+  // the zero rows (both buffers, both planes): what every padding-row operand read returns
+  for (int i = tid; i < 4 * C::RS / 16; i += C::NTHR) {
+    const int q = i / (C::RS / 16), o = (i % (C::RS / 16)) * 16;
+    *reinterpret_cast<uint4*>(smem + (q >> 1) * C::BUF + (q & 1) * C::PLANE + C::ZROW + o) = make_uint4(0, 0, 0, 0);
+  }
   // the two roles split here and share no value: each matches the other's barriers one for one
   if (producer) {
     produce_loads(0, pf);
@@ -196,11 +202,13 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_w1(const float* __r
     const int m = (wm * C::MT + mt) * 32 + r;
     const int np = m / (TR * C::NTX), rem = m % (TR * C::NTX);
     ylr[mt] = rem / C::NTX;
-    const int ab = np * C::PS + ylr[mt] * C::RS + (rem % C::NTX) * 64;
 #pragma unroll
-    for (int ky = 0; ky < 3; ++ky)
+    for (int ky = 0; ky < 3; ++ky) {
+      const int wr = ylr[mt] + ky;  // window row: input row wr - 1; rows -1 and TR read the zero row
+      const int rowb = (wr >= 1 && wr <= TR) ? np * C::PS + (wr - 1) * C::RS : C::ZROW;
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) vo[mt][ky][ks] = ab + 16 * ((2 * ks + h) ^ ((ylr[mt] + ky) & 3));
+      for (int ks = 0; ks < 2; ++ks) vo[mt][ky][ks] = rowb + (rem % C::NTX) * 64 + 16 * ((2 * ks + h) ^ (wr & 3));
+    }
   }
   const __amdgpu_buffer_rsrc_t wr_ = make_rsrc(wp, C::NCC * C::CHUNK_BYTES);
   const unsigned wvoff = (wn * C::NT * 2 * 64 + lane) * 16;
@@ -233,8 +241,8 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_w1(const float* __r
 #pragma unroll
       for (int mt = 0; mt < C::MT; ++mt) {
         const char* pa = cur + vo[mt][ky][ks];
-        dst[mt][0] = *reinterpret_cast<const uint4*>(pa + (ky * C::RS + xi * C::XROW));
-        dst[mt][1] = *reinterpret_cast<const uint4*>(pa + (C::PLANE + ky * C::RS + xi * C::XROW));
+        dst[mt][0] = *reinterpret_cast<const uint4*>(pa + xi * C::XROW);
+        dst[mt][1] = *reinterpret_cast<const uint4*>(pa + (C::PLANE + xi * C::XROW));
       }
     };
     load_a(0, aq[0]);
@@ -281,8 +289,7 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_w1(const float* __r
         y1a[mt][nt] -= ma[mt][nt];
       }
     if (cc == C::NCC - 1) {
-      int p0, y0;
-      tile_of(s, p0, y0);
+      const int p0 = tile_of(s);
 #pragma unroll
       for (int nt = 0; nt < C::NT; ++nt) {
         float4 bv[4];
@@ -291,23 +298,40 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_w1(const float* __r
           bv[q] = *reinterpret_cast<const float4*>(sbias + (wn * C::NT + nt) * 32 + 8 * q + 4 * h);
 #pragma unroll
         for (int mt = 0; mt < C::MT; ++mt) {
-          const int m = (wm * C::MT + mt) * 32 + r;
-          const int np = m / (TR * C::NTX), t = (m % (TR * C::NTX)) % C::NTX;
+          const int m0 = (wm * C::MT + mt) * 32;  // the M tile: 32 / NTX whole rows of patch np
+          const int np = m0 / (TR * C::NTX), yb = (m0 % (TR * C::NTX)) / C::NTX;
           if (NP == 1 || p0 + np < P) {
-            float* o = out + ((((size_t)p0 + np) * H + y0 + ylr[mt]) * H + 2 * t) * COUT + (wn * C::NT + nt) * 32 + 4 * h;
+            // pixel (row yb + m / NTX, column 2 (m % NTX) + par) of M index m = m0 + m
+            float* const ob = out + (((size_t)p0 + np) * H + yb) * H * COUT + (wn * C::NT + nt) * 32;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              float4 v0, v1;
-              v0.x = fmaxf(y0a[mt][nt][4 * q + 0] + bv[q].x, 0.f);
-              v0.y = fmaxf(y0a[mt][nt][4 * q + 1] + bv[q].y, 0.f);
-              v0.z = fmaxf(y0a[mt][nt][4 * q + 2] + bv[q].z, 0.f);
-              v0.w = fmaxf(y0a[mt][nt][4 * q + 3] + bv[q].w, 0.f);
-              v1.x = fmaxf(y1a[mt][nt][4 * q + 0] + bv[q].x, 0.f);
-              v1.y = fmaxf(y1a[mt][nt][4 * q + 1] + bv[q].y, 0.f);
-              v1.z = fmaxf(y1a[mt][nt][4 * q + 2] + bv[q].z, 0.f);
-              v1.w = fmaxf(y1a[mt][nt][4 * q + 3] + bv[q].w, 0.f);
-              *reinterpret_cast<float4*>(o + 8 * q) = v0;
-              *reinterpret_cast<float4*>(o + COUT + 8 * q) = v1;
+            for (int par = 0; par < 2; ++par) {
+              const f32x16& yv = par ? y1a[mt][nt] : y0a[mt][nt];
+              float4 v[4];
+#pragma unroll
+              for (int q = 0; q < 4; ++q)
+                v[q] = make_float4(fmaxf(yv[4 * q + 0] + bv[q].x, 0.f), fmaxf(yv[4 * q + 1] + bv[q].y, 0.f),
+                                   fmaxf(yv[4 * q + 2] + bv[q].z, 0.f), fmaxf(yv[4 * q + 3] + bv[q].w, 0.f));
+              if constexpr (CST) {
+                float* scr = reinterpret_cast<float*>(smem + C::SCR_OFF) + wave * (C::SCR / 4);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) *reinterpret_cast<float4*>(scr + r * C::SROW + 8 * q + 4 * h) = v[q];
+                __builtin_amdgcn_wave_barrier();  // same wave: its LDS accesses execute in order
+                asm volatile("" ::: "memory");
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                  const int ml = 8 * k + (lane >> 3), c4 = lane & 7;
+                  const int px = (ml / C::NTX) * H + 2 * (ml % C::NTX) + par;
+                  *reinterpret_cast<float4*>(ob + (size_t)px * COUT + 4 * c4) =
+                      *reinterpret_cast<const float4*>(scr + ml * C::SROW + 4 * c4);
+                }
+                __builtin_amdgcn_wave_barrier();
+                asm volatile("" ::: "memory");
+              } else {
+                const int px = (r / C::NTX) * H + 2 * (r % C::NTX) + par;
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                  *reinterpret_cast<float4*>(ob + (size_t)px * COUT + 8 * q + 4 * h) = v[q];
+              }
             }
           }
           y0a[mt][nt] = y1a[mt][nt] = f32x16{};
@@ -318,30 +342,33 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_w1(const float* __r
   }
 }
 
-template <int CIN, int COUT, int H, int NP, int TR, int WM, int WN>
+template <int CIN, int COUT, int H, int NP, int WM, int WN, bool CST>
 hipError_t launch_w1(const float* in, float* out, const void* wp, const float* bias, int P, hipStream_t st) {
-  using C = W1Cfg<CIN, COUT, H, NP, TR, WM, WN>;
-  const void* fn = reinterpret_cast<const void*>(&k_conv_w1<CIN, COUT, H, NP, TR, WM, WN>);
+  using C = W1Cfg<CIN, COUT, H, NP, WM, WN, CST>;
+  const void* fn = reinterpret_cast<const void*>(&k_conv_w1<CIN, COUT, H, NP, WM, WN, CST>);
   int resident = 0;
   const hipError_t e = hn_resident_blocks(fn, C::NTHR, C::SMEM, &resident);
   if (e != hipSuccess) return e;
-  const int tiles = (P + NP - 1) / NP * C::RT;
+  const int tiles = (P + NP - 1) / NP;
   const int grid = std::min(tiles, resident);
   if (grid <= 0) return hipSuccess;
-  hipLaunchKernelGGL((k_conv_w1<CIN, COUT, H, NP, TR, WM, WN>), dim3(grid), dim3(C::NTHR), C::SMEM, st, in, out,
+  hipLaunchKernelGGL((k_conv_w1<CIN, COUT, H, NP, WM, WN, CST>), dim3(grid), dim3(C::NTHR), C::SMEM, st, in, out,
                      static_cast<const uint4*>(wp), bias, P);
   return hipGetLastError();
 }
 
+using W1Conv3 = W1Cfg<64, 64, 16, 1, 2, 2, true>;
+using W1Conv5 = W1Cfg<128, 128, 8, 2, 1, 4, true>;
+
 }  // namespace
 
-// conv3: whole patches (16 rows) per work tile, 2 x 2 MFMA waves of 2 M tiles; conv5: two patches
+// conv3: one patch per work tile, 2 x 2 MFMA waves of 2 M tiles; conv5: two patches, 1 x 4 waves
 hipError_t hn_launch_wino1(int layer, const HardnetDev& d, const float* in, float* out, int P, hipStream_t st) {
   if (P <= 0) return hipSuccess;
   if (!d.wino1[layer]) return hipErrorInvalidValue;
   switch (layer) {
-    case 3: return launch_w1<64, 64, 16, 1, 16, 2, 2>(in, out, d.wino1[3], d.bias[3], P, st);
-    case 5: return launch_w1<128, 128, 8, 2, 8, 1, 4>(in, out, d.wino1[5], d.bias[5], P, st);
+    case 3: return launch_w1<64, 64, 16, 1, 2, 2, true>(in, out, d.wino1[3], d.bias[3], P, st);
+    case 5: return launch_w1<128, 128, 8, 2, 1, 4, true>(in, out, d.wino1[5], d.bias[5], P, st);
   }
   return hipErrorInvalidValue;
 }
@@ -349,8 +376,8 @@ hipError_t hn_launch_wino1(int layer, const HardnetDev& d, const float* in, floa
 // LDS bytes of the layer's configuration (tests / DESIGN.md)
 int hn_wino1_lds_bytes(int layer) {
   switch (layer) {
-    case 3: return W1Cfg<64, 64, 16, 1, 16, 2, 2>::SMEM;
-    case 5: return W1Cfg<128, 128, 8, 2, 8, 1, 4>::SMEM;
+    case 3: return W1Conv3::SMEM;
+    case 5: return W1Conv5::SMEM;
   }
   return -1;
 }
