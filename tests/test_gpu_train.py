@@ -263,7 +263,8 @@ def test_train_kernel_alternatives(knobs, cuda_device):
 def test_reference_train_step(init, cuda_device):
     """hardnet/HardNet.py:392-423 exactly: out_a = model(data_a); out_p = model(data_p) (two
     HardNetTrainFunction nodes, two BN batch statistics, two running-stat updates, both saved
-    workspaces alive until the backward), loss_HardNet(anchor_swap=True), backward -- against
+    workspaces alive until the backward), loss_HardNet(anchor_swap=True) on the fused loss kernels
+    (forward and backward, no B x B matrix), backward -- against
     tests/golden/train_hardnet.npz, which the reference's own module and loss produced
     (tests/golden/make_train_golden.py).  Bars: outputs 1e-4 max abs (north_star), running stats
     1e-5 relative, num_batches_tracked 2, loss 1e-5, gradients L2-relative 5e-3 vs the fp64 step."""
@@ -276,6 +277,7 @@ def test_reference_train_step(init, cuda_device):
     for y in (out_a, out_p):
         assert "HardNetTrainFunction" in type(y.grad_fn).__name__
     loss = loss_HardNet(out_a, out_p, anchor_swap=True)
+    assert "HardNetLossFunction" in type(loss.grad_fn).__name__  # the fused loss and its backward (hn_loss.hip)
     loss.backward()
     pre = f"{init}/"
     ea = np.abs(out_a.detach().cpu().numpy() - fx[pre + "out_a_32"]).max()
