@@ -592,6 +592,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, WP
 }
 
 
+#ifdef HN_EXPERIMENTS  // measured slower than k_c12 cfg 12 (24.2 vs 20.4 ms per step, same box): experiments library only
 // ------------------------------------------------------------------------------------------
 // k_c12h: the same computation with the roles split per SIMD.  One workgroup per CU of 8 waves:
 // waves 0-3 (one per SIMD, 256-register budget) run only conv1 (P2) and conv2 (P3) of band g on
@@ -915,6 +916,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     __syncthreads();  // E_g
   }
 }
+#endif  // HN_EXPERIMENTS
 
 }  // namespace
 
@@ -930,7 +932,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   X(6, 4, 2, 2, true, 3, false, 0) X(7, 4, 2, 2, false, 2, true, 0) X(8, 4, 2, 2, true, 2, true, 0)      \
   X(9, 8, 4, 2, false, 2, true, 0) X(10, 4, 2, 2, false, 2, true, 1) X(11, 4, 2, 2, false, 2, true, 3) \
   X(12, 4, 2, 2, false, 2, true, 5)
-constexpr int kC12Cfgs = 14;  // 13: k_c12h (MFMA / helper waves split per SIMD), not in HN_C12_CFGS  // (P1, P3) at priority (2, 1) / (1, 2) / (2, 2): within the box noise of 12, removed
+#ifdef HN_EXPERIMENTS
+constexpr int kC12Cfgs = 14;  // 13: k_c12h (MFMA / helper waves split per SIMD), not in HN_C12_CFGS
+#else
+constexpr int kC12Cfgs = 13;
+#endif  // (P1, P3) at priority (2, 1) / (1, 2) / (2, 2): within the box noise of 12, removed
 
 bool hn_c12_cfg_ok(int cfg, int abl) {
   if (cfg < 0 || cfg >= kC12Cfgs) return false;
@@ -957,12 +963,18 @@ hipError_t hn_launch_c12(const float* in, float* out, const HardnetDev& d, int P
 #define HN_C12_FN(C, W, R, E, I, A, Q, PR) reinterpret_cast<const void*>(&k_c12<0, W, R, E, I, A, Q, PR>),
       HN_C12_CFGS(HN_C12_FN)
 #undef HN_C12_FN
-      reinterpret_cast<const void*>(&k_c12h<-1>)};
+#ifdef HN_EXPERIMENTS
+      reinterpret_cast<const void*>(&k_c12h<-1>)
+#endif
+  };
   static const int nws[kC12Cfgs] = {
 #define HN_C12_NWS(C, W, R, E, I, A, Q, PR) W,
       HN_C12_CFGS(HN_C12_NWS)
 #undef HN_C12_NWS
-      8};
+#ifdef HN_EXPERIMENTS
+      8
+#endif
+  };
   const int nw = nws[cfg];
   int resident = 0;
   const hipError_t e = hn_resident_blocks(fns[cfg], nw * 64, 0, &resident);
@@ -975,6 +987,7 @@ hipError_t hn_launch_c12(const float* in, float* out, const HardnetDev& d, int P
   hipLaunchKernelGGL((k_c12<A, W, R, E, I, WA, Q, PR, ##__VA_ARGS__>), dim3(grid), dim3(W * 64), 0, st, src, \
                      out, d.stem_w, d.stem_b, static_cast<const uint4*>(d.c12_w1), d.bias[1],   \
                      static_cast<const uint4*>(d.c12_w2), d.bias[2], P, eps, pm, ps, pn)
+#ifdef HN_EXPERIMENTS
 #define HN_C12H_GO(U)                                                                                        \
   hipLaunchKernelGGL((k_c12h<U>), dim3(grid), dim3(512), 0, st, src, out, d.stem_w, d.stem_b,               \
                      static_cast<const uint4*>(d.c12_w1), d.bias[1], static_cast<const uint4*>(d.c12_w2),   \
@@ -988,6 +1001,7 @@ hipError_t hn_launch_c12(const float* in, float* out, const HardnetDev& d, int P
 #undef HN_C12H_GO
     return hipGetLastError();
   }
+#endif
   if (u8) {
     switch (u8->resize) {
       case HN_RESIZE_NONE: HN_C12_GO(0, 4, 2, 2, false, 2, true, 5, HN_RESIZE_NONE); break;

@@ -142,12 +142,13 @@ def test_product_library_has_no_ablation_builds():
 
 def test_product_library_has_one_tiling_per_layer_plus_fallbacks():
     """Measured-and-rejected kernels live only in the HN_EXPERIMENTS library:
-    no Winograd kernel (hn_wino.hip), and of k_conv_pipe only conv5's production instantiation
+    no 2-D Winograd kernel (hn_wino.hip), and of k_conv_pipe only conv5's production instantiation
     (the store-through-LDS form, CST = last template argument true)."""
     import subprocess
     out = subprocess.run(["nm", "-C", "--defined-only", N.lib_path()], capture_output=True,
                          text=True, check=True).stdout
-    assert "k_wino" not in out
+    assert "k_wino<" not in out and "hn_launch_wino(" not in out  # the 2-D F(2x2,3x3) form
+    assert "k_conv_w1<" in out  # the 1-D F(2,3) conv3 / conv5 (hn_wino1.hip), the default
     pipe = _kernel_template_args("k_conv_pipe")
     assert pipe and all(a[-1].strip() == "true" for a in pipe), pipe
 

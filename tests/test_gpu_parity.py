@@ -97,11 +97,12 @@ def test_tiling_variants_match_reference(variant, cuda_device, monkeypatch):
 def test_winograd_1d_conv3_conv5_match_reference(variant, cuda_device, monkeypatch):
     """conv3 / conv5 as 1-D Winograd F(2,3) (hn_wino1.hip, HN_VARIANT digit j) against the
     reference's fp32 and fp64 vectors (edge patches included) and against the direct kernels on
-    ragged batches whose last two-patch conv5 tile is half empty."""
+    ragged batches whose last two-patch conv5 tile is half empty.  605jij is the default."""
     from hardnetnas_amd._native import NativeModel
     m, fx, _ = build_module("hardnet")
     x = torch.from_numpy(golden_inputs(fx)).to(cuda_device)
     xe = torch.from_numpy(fx["x_edge"]).to(cuda_device)
+    monkeypatch.setenv("HN_VARIANT", "605gig")  # the direct conv3 / conv5 kernels
     direct = NativeModel.from_module(m, cuda_device)
     monkeypatch.setenv("HN_VARIANT", variant)
     nm = NativeModel.from_module(m, cuda_device)
@@ -151,12 +152,12 @@ def test_fused_c12_is_default_and_matches_layerwise(cuda_device, monkeypatch):
         assert np.abs(nm(x[:b]).cpu().numpy() - lw(x[:b]).cpu().numpy()).max() <= 2e-5
 
 
-@pytest.mark.parametrize("cfg", ["0", "1", "2", "3", "5", "7", "8", "9", "10", "11", "12", "13"])
+@pytest.mark.parametrize("cfg", ["0", "1", "2", "3", "5", "7", "8", "9", "10", "11", "12"])
 def test_c12_variants_match(cuda_device, monkeypatch, cfg):
     """HN_C12_CFG=0: 8-wave workgroups with 4-row bands; 1: one wave per SIMD (512-register
     file); 2: 4-wave workgroups with 2-row bands, two per CU; 3 / 5: tap-interleaved P3; 7 / 8 / 9:
     tap-interleaved P2; 10 / 11: raised P1 priority; 12: 2 with the tap-interleaved P2 and P3 + P1 at
-    raised wave priority; 13: k_c12h (MFMA and helper waves split per SIMD) -- against the default build.  Both agree with the default build to the split-precision level (the 4-wave builds sum
+    raised wave priority (the default) -- against the default build.  Both agree with the default build to the split-precision level (the 4-wave builds sum
     input_norm's mean/std in a different order; the MFMA order per output is the same)."""
     from hardnetnas_amd._native import NativeModel
     m, fx, _ = build_module("hardnet")
