@@ -1862,7 +1862,10 @@ bool hn_hardnet_variant_ok(int layer, int v) {
   if (v == 1 || v == 2 || v == 3) return true;
 #endif
   if (v == 15 || v == 18) return layer == 4;  // 18: outputs stored by the producer waves
-  if (v == 19) return layer == 3 || layer == 5;  // 1-D Winograd F(2,3) (hn_wino1.hip)
+  if (v >= 19 && v <= 21) return layer == 3 || layer == 5;  // 1-D Winograd F(2,3) (hn_wino1.hip), weight ring 3 / 4 / 6
+#ifdef HN_EXPERIMENTS
+  if (v >= 22 && v <= 25) return layer == 3 || layer == 5;  // its timing-only ablations (ABL 1 / 2 / 4 / 8)
+#endif
   if (v == 16) return layer == 3 || layer == 5;
   if (v == 0 || v == 5 || v == 6) return true;  // (layer 1 always runs conv1_launch)
   return false;
@@ -1905,7 +1908,10 @@ hipError_t hn_launch_hardnet_conv(int layer, int variant, const HardnetDev& d, c
     return hipErrorInvalidValue;
   }
 #endif
-  if (variant == 19) return hn_launch_wino1(layer, d, in, out, P, st);
+  if (variant >= 19 && variant <= 21) return hn_launch_wino1(layer, variant == 19 ? 3 : variant == 20 ? 4 : 6, d, in, out, P, st);
+#ifdef HN_EXPERIMENTS
+  if (variant >= 22 && variant <= 25) return hn_launch_wino1(layer, 100 + (1 << (variant - 22)), d, in, out, P, st);
+#endif
   if (variant == 16) {  // coalesced epilogue stores
     switch (layer) {
       case 3: return ws3_cst(in, out, d.wpack[3], d.bias[3], P, nullptr, nullptr, 0.f, st);

@@ -78,7 +78,8 @@ int hn_conv_lds_bytes(int layer);
 hipError_t hn_launch_conv_raw(int layer, const void* wp, const float* zero_bias, const float* in, float* out,
                               int P, hipStream_t st);
 // 1-D Winograd F(2,3) conv3 / conv5 (hn_wino1.hip; HN_VARIANT digit j)
-hipError_t hn_launch_wino1(int layer, const HardnetDev& d, const float* in, float* out, int P, hipStream_t st);
+hipError_t hn_launch_wino1(int layer, int wd, const HardnetDev& d, const float* in, float* out, int P,
+                           hipStream_t st);
 int hn_wino1_lds_bytes(int layer);
 // Winograd F(2x2,3x3) conv3 / conv5 (hn_wino.hip; HN_VARIANT digit h)
 hipError_t hn_launch_wino(int layer, const HardnetDev& d, const float* in, float* out, int P, hipStream_t st);

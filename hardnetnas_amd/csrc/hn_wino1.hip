@@ -62,7 +62,10 @@ struct W1Cfg {
   static_assert(RS % 256 == 0, "image rows on 256-byte boundaries (the bank-conflict argument)");
 };
 
-template <int CIN, int COUT, int H, int NP, int WM, int WN, bool CST>
+// ABL (timing-only ablation builds, HN_EXPERIMENTS library only; wrong results): bit 0 idle producers
+// (barriers only), bit 1 no MFMAs (operands still loaded), bit 2 no weight loads (K-step 0's fragments
+// reused), bit 3 no epilogue stores
+template <int CIN, int COUT, int H, int NP, int WM, int WN, bool CST, int WD = 3, int ABL = 0>
 __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_w1(const float* __restrict__ in, float* __restrict__ out,
                                                                 const uint4* __restrict__ wp,
                                                                 const float* __restrict__ bias, int P) {
@@ -160,6 +163,11 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_w1(const float* __r
   }
   // the two roles split here and share no value: each matches the other's barriers one for one
   if (producer) {
+    if constexpr ((ABL & 1) != 0) {  // timing only: idle producers
+#pragma unroll 1
+      for (int s = 0; s <= NS; ++s) __syncthreads();
+      return;
+    }
     produce_loads(0, pf);
     produce_write(buf0, pf);
     if (NS > 1) produce_loads(1, pf);
@@ -207,7 +215,10 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_w1(const float* __r
       const int wr = ylr[mt] + ky;  // window row: input row wr - 1; rows -1 and TR read the zero row
       const int rowb = (wr >= 1 && wr <= TR) ? np * C::PS + (wr - 1) * C::RS : C::ZROW;
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) vo[mt][ky][ks] = rowb + (rem % C::NTX) * 64 + 16 * ((2 * ks + h) ^ (wr & 3));
+      for (int ks = 0; ks < 2; ++ks) {
+        vo[mt][ky][ks] = rowb + (rem % C::NTX) * 64 + 16 * ((2 * ks + h) ^ (wr & 3));
+        asm volatile("" : "+v"(vo[mt][ky][ks]));  // one opaque register each (no re-split sums in the K-loop)
+      }
     }
   }
   const __amdgpu_buffer_rsrc_t wr_ = make_rsrc(wp, C::NCC * C::CHUNK_BYTES);
@@ -221,12 +232,13 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_w1(const float* __r
   auto load_b = [&](int cc, int kx, uint4 (&dst)[C::NT][2]) {
 #pragma unroll
     for (int nt = 0; nt < C::NT; ++nt) {
-      const unsigned k = cc * C::CHUNK_BYTES + (kx * C::NTOT + nt) * 2 * 64 * 16;
+      const unsigned k = cc * C::CHUNK_BYTES + (((ABL & 4) ? 0 : kx) * C::NTOT + nt) * 2 * 64 * 16;
       dst[nt][0] = buf_load16(wr_, wvoff, k);
       dst[nt][1] = buf_load16(wr_, wvoff, k + 64 * 16);
     }
   };
-  constexpr int WD = 3;  // weight ring depth: K-step fragments loaded WD - 1 steps ahead
+  // WD: weight ring depth, K-step fragments loaded WD - 1 steps ahead (a K-step is 6 MFMAs here, half
+  // the direct kernel's, so the same depth covers half the L2 latency)
   static_assert(C::NKS % WD == 0, "the weight ring runs on across stages");
   uint4 bq[WD][C::NT][2];
 #pragma unroll
@@ -270,7 +282,10 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_w1(const float* __r
 #pragma unroll
         for (int nt = 0; nt < C::NT; ++nt) {
           const bf16x8 wh = as_bf16x8(bq[kx % WD][nt][0]), wl = as_bf16x8(bq[kx % WD][nt][1]);
-          if (xi == 0)
+          if constexpr ((ABL & 2) != 0)  // timing only: no MFMA, operands kept live
+            y0a[mt][nt][0] += __builtin_bit_cast(float, aq[kx & 1][mt][0].x ^ aq[kx & 1][mt][1].y ^
+                                                            bq[kx % WD][nt][0].z ^ bq[kx % WD][nt][1].w);
+          else if (xi == 0)
             y0a[mt][nt] = mfma3(wh, wl, xh, xl, y0a[mt][nt]);
           else if (xi == 3)
             y1a[mt][nt] = mfma3(wh, wl, xh, xl, y1a[mt][nt]);
@@ -300,7 +315,7 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_w1(const float* __r
         for (int mt = 0; mt < C::MT; ++mt) {
           const int m0 = (wm * C::MT + mt) * 32;  // the M tile: 32 / NTX whole rows of patch np
           const int np = m0 / (TR * C::NTX), yb = (m0 % (TR * C::NTX)) / C::NTX;
-          if (NP == 1 || p0 + np < P) {
+          if ((NP == 1 || p0 + np < P) && ((ABL & 8) == 0 || y0a[mt][nt][0] == 1234.5f)) {  // ABL 8: timing only
             // pixel (row yb + m / NTX, column 2 (m % NTX) + par) of M index m = m0 + m
             float* const ob = out + (((size_t)p0 + np) * H + yb) * H * COUT + (wn * C::NT + nt) * 32;
 #pragma unroll
@@ -342,17 +357,17 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_w1(const float* __r
   }
 }
 
-template <int CIN, int COUT, int H, int NP, int WM, int WN, bool CST>
+template <int CIN, int COUT, int H, int NP, int WM, int WN, bool CST, int WD, int ABL = 0>
 hipError_t launch_w1(const float* in, float* out, const void* wp, const float* bias, int P, hipStream_t st) {
   using C = W1Cfg<CIN, COUT, H, NP, WM, WN, CST>;
-  const void* fn = reinterpret_cast<const void*>(&k_conv_w1<CIN, COUT, H, NP, WM, WN, CST>);
+  const void* fn = reinterpret_cast<const void*>(&k_conv_w1<CIN, COUT, H, NP, WM, WN, CST, WD, ABL>);
   int resident = 0;
   const hipError_t e = hn_resident_blocks(fn, C::NTHR, C::SMEM, &resident);
   if (e != hipSuccess) return e;
   const int tiles = (P + NP - 1) / NP;
   const int grid = std::min(tiles, resident);
   if (grid <= 0) return hipSuccess;
-  hipLaunchKernelGGL((k_conv_w1<CIN, COUT, H, NP, WM, WN, CST>), dim3(grid), dim3(C::NTHR), C::SMEM, st, in, out,
+  hipLaunchKernelGGL((k_conv_w1<CIN, COUT, H, NP, WM, WN, CST, WD, ABL>), dim3(grid), dim3(C::NTHR), C::SMEM, st, in, out,
                      static_cast<const uint4*>(wp), bias, P);
   return hipGetLastError();
 }
@@ -362,14 +377,32 @@ using W1Conv5 = W1Cfg<128, 128, 8, 2, 1, 4, true>;
 
 }  // namespace
 
-// conv3: one patch per work tile, 2 x 2 MFMA waves of 2 M tiles; conv5: two patches, 1 x 4 waves
-hipError_t hn_launch_wino1(int layer, const HardnetDev& d, const float* in, float* out, int P, hipStream_t st) {
+// conv3: one patch per work tile, 2 x 2 MFMA waves of 2 M tiles; conv5: two patches, 1 x 4 waves.
+// wd: the weight ring depth (HN_VARIANT digit j = 3, k = 4, l = 6)
+hipError_t hn_launch_wino1(int layer, int wd, const HardnetDev& d, const float* in, float* out, int P,
+                           hipStream_t st) {
   if (P <= 0) return hipSuccess;
   if (!d.wino1[layer]) return hipErrorInvalidValue;
-  switch (layer) {
-    case 3: return launch_w1<64, 64, 16, 1, 2, 2, true>(in, out, d.wino1[3], d.bias[3], P, st);
-    case 5: return launch_w1<128, 128, 8, 2, 1, 4, true>(in, out, d.wino1[5], d.bias[5], P, st);
+#ifdef HN_EXPERIMENTS  // wd = 100 + ABL: the timing-only ablations (WD 3)
+#define HN_W1_ABL(CI, CO, HH, NPP, WMM, WNN, L)                                                              \
+  if (wd == 101) return launch_w1<CI, CO, HH, NPP, WMM, WNN, true, 3, 1>(in, out, d.wino1[L], d.bias[L], P, st); \
+  if (wd == 102) return launch_w1<CI, CO, HH, NPP, WMM, WNN, true, 3, 2>(in, out, d.wino1[L], d.bias[L], P, st); \
+  if (wd == 104) return launch_w1<CI, CO, HH, NPP, WMM, WNN, true, 3, 4>(in, out, d.wino1[L], d.bias[L], P, st); \
+  if (wd == 108) return launch_w1<CI, CO, HH, NPP, WMM, WNN, true, 3, 8>(in, out, d.wino1[L], d.bias[L], P, st);
+#else
+#define HN_W1_ABL(CI, CO, HH, NPP, WMM, WNN, L)
+#endif
+#define HN_W1(L, CI, CO, HH, NPP, WMM, WNN)                                                                      \
+  if (layer == L) {                                                                                             \
+    if (wd == 3) return launch_w1<CI, CO, HH, NPP, WMM, WNN, true, 3>(in, out, d.wino1[L], d.bias[L], P, st); \
+    if (wd == 4) return launch_w1<CI, CO, HH, NPP, WMM, WNN, true, 4>(in, out, d.wino1[L], d.bias[L], P, st); \
+    if (wd == 6) return launch_w1<CI, CO, HH, NPP, WMM, WNN, true, 6>(in, out, d.wino1[L], d.bias[L], P, st); \
+    HN_W1_ABL(CI, CO, HH, NPP, WMM, WNN, L)                                                                     \
   }
+  HN_W1(3, 64, 64, 16, 1, 2, 2)
+  HN_W1(5, 128, 128, 8, 2, 1, 4)
+#undef HN_W1
+#undef HN_W1_ABL
   return hipErrorInvalidValue;
 }
 
