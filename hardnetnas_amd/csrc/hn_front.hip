@@ -171,6 +171,39 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRO
       reinterpret_cast<float4*>(s_dw)[i] = wv;
     }
   }
+  // INV (MID = 32: one chunk): the chunk's pw / pwl operands and biases are loop-invariant.  They
+  // are loaded here and consumed by an empty asm before the patch loop, so that no load from
+  // outside the loops is still pending at the band loop: otherwise the compiler flushes vmcnt to
+  // zero in front of the band loop (a loop with stores, no loads and operands loaded outside it),
+  // which also waited for the next patch's prefetch issued just before -- an exposed HBM latency
+  // per patch.
+  constexpr bool INV = MID == 32 && MODE == FRONT_IRF;
+  f16x8 iah0{}, ial0{}, iah1{}, ial1{};
+  f16x8 ilp[4] = {};
+  f32x16 ipwb = {};
+  f32x4_t ib16[2] = {};
+  if constexpr (INV) {
+    iah0 = as_f16x8(apack[lane]);
+    ial0 = as_f16x8(apack[64 + lane]);
+    iah1 = as_f16x8(apack[128 + lane]);
+    ial1 = as_f16x8(apack[192 + lane]);
+    asm volatile("" ::"v"(iah0), "v"(ial0), "v"(iah1), "v"(ial1));
+    if constexpr (NF) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) ilp[k] = as_f16x8(pwl_a16[64 * k + lane]);
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt) {
+        const float4 b = *reinterpret_cast<const float4*>(pwl_b + 16 * tt + 4 * (lane >> 4));
+        ib16[tt] = f32x4_t{b.x, b.y, b.z, b.w};
+      }
+      asm volatile("" ::"v"(ilp[0]), "v"(ilp[1]), "v"(ilp[2]), "v"(ilp[3]), "v"(ib16[0]), "v"(ib16[1]));
+    }
+    if constexpr (!LDSB) {
+      ipwb = bias16(pw_b);
+      asm volatile("" ::"v"(ipwb));
+    }
+    if constexpr (!LDSB) asm volatile("" ::"v"(sbr));
+  }
   const float* in = static_cast<const float*>(in_);
   const uint8_t* in8 = static_cast<const uint8_t*>(in_);
   constexpr int INB = U8 == HN_RESIZE_NONE ? 1024 : 4096;  // bytes per uint8 patch
@@ -338,8 +371,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRO
       if constexpr (NF) {
 #pragma unroll
         for (int tt = 0; tt < 2; ++tt) {
-          const float4 b = *reinterpret_cast<const float4*>(pwl_b + 16 * tt + 4 * (lane >> 4));
-          o16[tt] = f32x4_t{b.x, b.y, b.z, b.w};
+          if constexpr (INV) {
+            o16[tt] = ib16[tt];
+          } else {
+            const float4 b = *reinterpret_cast<const float4*>(pwl_b + 16 * tt + 4 * (lane >> 4));
+            o16[tt] = f32x4_t{b.x, b.y, b.z, b.w};
+          }
         }
       }
 #pragma unroll 1
@@ -355,10 +392,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRO
           reinterpret_cast<float4*>(s_dw)[i] = wv;
         }
         const uint4* ap = apack + (size_t)m * 4 * 64 + lane;
-        const f16x8 ah0 = as_f16x8(ap[0]), al0 = as_f16x8(ap[64]);
-        const f16x8 ah1 = as_f16x8(ap[128]), al1 = as_f16x8(ap[192]);
+        const f16x8 ah0 = INV ? iah0 : as_f16x8(ap[0]), al0 = INV ? ial0 : as_f16x8(ap[64]);
+        const f16x8 ah1 = INV ? iah1 : as_f16x8(ap[128]), al1 = INV ? ial1 : as_f16x8(ap[192]);
         f32x16 bias;  // pw bias as the initial accumulator (LDSB: read per row from LDS)
-        if constexpr (!LDSB) bias = bias16(pw_b + 32 * m);
+        if constexpr (!LDSB) bias = INV ? ipwb : bias16(pw_b + 32 * m);
 #pragma unroll
         for (int i = 0; i < NT; ++i) {
           const int ri = row_of(i), y = yr0 + ri;
@@ -395,8 +432,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRO
           const uint4* lp = pwl_a16 + (size_t)m * 4 * 64 + lane;
 #pragma unroll
           for (int tt = 0; tt < 2; ++tt)
-            o16[tt] = mfma3_f16_16(as_f16x8(lp[128 * tt]), as_f16x8(lp[128 * tt + 64]), as_f16x8(xh), as_f16x8(xl),
-                                   o16[tt]);
+            o16[tt] = mfma3_f16_16(INV ? ilp[2 * tt] : as_f16x8(lp[128 * tt]), INV ? ilp[2 * tt + 1] : as_f16x8(lp[128 * tt + 64]),
+                                   as_f16x8(xh), as_f16x8(xl), o16[tt]);
           __syncthreads();  // s_dw (and, without the ring, s_pw) is rewritten next
           continue;
         }

@@ -91,25 +91,31 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_w1(const float* __r
   // row's units are 4 NTX consecutive lanes of one wave) -- no pixel is loaded twice
   const int ptid = tid - C::NWC * 64;
   float4 pf[C::UPT][6], pf2[C::UPT][6];
+  // Loads are buffer loads over the stage's tile: a padding column, an absent third column or a patch
+  // past P gets an offset beyond the resource and reads zero in hardware. No branch, so the compiler's
+  // vmcnt accounting stays exact and stage s + 1's write waits only for stage s + 1's loads (with
+  // if-guarded global loads it waited vmcnt(0), i.e. also for the stage s + 2 loads just issued).
+  constexpr unsigned PATCH_BYTES = (unsigned)H * H * CIN * 4, OOB = 0x80000000u;
   auto produce_loads = [&](int s, float4 (&d)[C::UPT][6]) {
-    const int p0 = tile_of(s);
+    // a stage past the last one (the loops below issue it unconditionally) gets an empty resource
+    const bool live = s < NS;
+    const int p0 = live ? tile_of(s) : 0;
     const int cc = s % C::NCC;
+    const int nval = !live ? 0 : P - p0 < NP ? P - p0 : NP;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(in + (size_t)p0 * H * H * CIN, (unsigned)nval * PATCH_BYTES);
 #pragma unroll
     for (int k = 0; k < C::UPT; ++k) {
       const int u = ptid + k * C::PTHR;
       const int g = u & 3, t = (u >> 2) % C::NTX, rest = (u >> 2) / C::NTX;
       const int y = rest % TR, np = rest / TR;
-      const bool rowok = u < C::UNITS && (NP == 1 || p0 + np < P);
+      const bool rowok = C::UNITS % C::PTHR == 0 || u < C::UNITS;
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
         const int x = 2 * t - 1 + j;
-        d[k][2 * j] = d[k][2 * j + 1] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (rowok && (j < 2 || t == C::NTX - 1) && (unsigned)x < (unsigned)H) {
-          const float4* src = reinterpret_cast<const float4*>(
-              in + ((((size_t)p0 + np) * H + y) * H + x) * CIN + cc * 32 + g * 8);
-          d[k][2 * j] = src[0];
-          d[k][2 * j + 1] = src[1];
-        }
+        const bool ok = rowok && (j < 2 || t == C::NTX - 1) && (unsigned)x < (unsigned)H;
+        const unsigned vo = ok ? (unsigned)(((np * H + y) * H + x) * CIN + cc * 32 + g * 8) * 4u : OOB;
+        d[k][2 * j] = __builtin_bit_cast(float4, buf_load16(rs, vo, 0));
+        d[k][2 * j + 1] = __builtin_bit_cast(float4, buf_load16(rs, vo, 16));
       }
     }
   };
@@ -134,7 +140,7 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_w1(const float* __r
         dd[2][i] = last ? d[k][4 + i] : n0;
         dd[3][i] = last ? z : n1;
       }
-      if (u < C::UNITS) {
+      if (C::UNITS % C::PTHR == 0 || u < C::UNITS) {  // compile-time true for conv3 / conv5: no branch
         const int off = np * C::PS + y * C::RS + t * 64 + 16 * (g ^ ((y + 1) & 3));  // window row y + 1
 #pragma unroll
         for (int xi = 0; xi < 4; ++xi) {
@@ -168,29 +174,30 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_w1(const float* __r
       for (int s = 0; s <= NS; ++s) __syncthreads();
       return;
     }
+    // Loads and writes are unconditional (a stage past NS loads zeros from an empty resource and is
+    // written into the buffer nobody reads again): any branch around them makes the compiler's vmcnt
+    // merge conservative, and a vmcnt(0) here also waits for the loads issued one stage ahead.
     produce_loads(0, pf);
     produce_write(buf0, pf);
-    if (NS > 1) produce_loads(1, pf);
+    produce_loads(1, pf);
     __syncthreads();
     if constexpr (!C::DEEP) {
 #pragma unroll 1
       for (int s = 0; s < NS; ++s) {
-        if (s + 1 < NS) {
-          produce_write((s & 1) ? buf0 : buf1, pf);
-          if (s + 2 < NS) produce_loads(s + 2, pf);
-        }
+        produce_write((s & 1) ? buf0 : buf1, pf);
+        produce_loads(s + 2, pf);
         __syncthreads();
       }
     } else {
       // stage s + 2's loads are issued before stage s + 1 is written: two stages of MFMA work to land
 #pragma unroll 1
       for (int s = 0; s < NS; s += 2) {
-        if (s + 2 < NS) produce_loads(s + 2, pf2);
-        if (s + 1 < NS) produce_write(buf1, pf);
+        produce_loads(s + 2, pf2);
+        produce_write(buf1, pf);
         __syncthreads();
         if (s + 1 >= NS) break;
-        if (s + 3 < NS) produce_loads(s + 3, pf);
-        if (s + 2 < NS) produce_write(buf0, pf2);
+        produce_loads(s + 3, pf);
+        produce_write(buf0, pf2);
         __syncthreads();
       }
     }
