@@ -1098,7 +1098,8 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_ws(
     for (int ksx = 0; ksx < NKS; ++ksx) {
       if (ksx + WD - 1 < NKS)
         load_b(cc, ksx + WD - 1, bq[(ksx + WD - 1) % WD]);
-      else if (s + 1 < NS)
+      else  // the next stage's first fragments, unconditionally (valid weights even after the last
+            // stage): a branch here made the compiler's vmcnt merge wait vmcnt(0) at the stage's end
         load_b(ccn, ksx + WD - 1 - NKS, bq[(ksx + WD - 1) % WD]);
       if (ksx + 1 < NKS) load_a(ksx + 1, aq[(ksx + 1) & 1]);
       __builtin_amdgcn_sched_barrier(0);

@@ -269,7 +269,8 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_w1(const float* __r
     for (int kx = 0; kx < C::NKS; ++kx) {
       if (kx + WD - 1 < C::NKS)
         load_b(cc, kx + WD - 1, bq[(kx + WD - 1) % WD]);
-      else if (s + 1 < NS)
+      else  // the next stage's first fragments, unconditionally (valid weights even after the last
+            // stage): a branch here made the compiler's vmcnt merge wait vmcnt(0) at the stage's end
         load_b(ccn, kx + WD - 1 - C::NKS, bq[(kx + WD - 1) % WD]);
       if (kx + 1 < C::NKS) load_a(kx + 1, aq[(kx + 1) & 1]);
       __builtin_amdgcn_sched_barrier(0);
