@@ -7,7 +7,7 @@ L=abl/libhardnet_mi355x.so
 H=abl/head/libhardnet_mi355x.so
 timeout -k 10 500 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/ab3_pytest.log 2>&1 || { tail -30 gpurun_out/ab3_pytest.log; exit 1; }
 tail -1 gpurun_out/ab3_pytest.log
-REPS=${REPS:-2} ENVS="${ENVS:-HN_LIB=$H;-;HN_VARIANT=605jik;HN_LIB=$L HN_VARIANT=605mim;HN_LIB=$L HN_VARIANT=605nin}" bash tools/ab_env.sh || exit 1
+REPS=${REPS:-2} ENVS="${ENVS:-HN_LIB=$H;-;HN_VARIANT=605jik;HN_VARIANT=605kik;HN_VARIANT=605kil;HN_VARIANT=605lil}" bash tools/ab_env.sh || exit 1
 for m in wang2 wang3; do
   MODEL=$m REPS=2 ENVS="HN_LIB=$H;-" bash tools/ab_env.sh || exit 1
 done
