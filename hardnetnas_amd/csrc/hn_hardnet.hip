@@ -809,20 +809,10 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_ws(
   // ---- producer side ----
   const int ptid = tid - C::NWC * 64;
   float4 pf[C::UPT][2], pf2[C::UPT][2];  // two stages in flight (non-STEM)
-  // Buffer loads over the stage's patches: a padding pixel, a unit past UNITS or a patch past P gets an
-  // offset beyond the resource and reads zero in hardware, and a stage past NS (issued unconditionally
-  // by the loops below) gets an empty resource.  No branch around a load, so the compiler's vmcnt
-  // accounting stays exact: with if-guarded global loads the write of stage s + 1 waited vmcnt(0),
-  // i.e. also for the stage s + 2 loads just issued (hn_wino1.hip has the same producers).
-  constexpr unsigned PATCH_BYTES = (unsigned)HIN * HIN * CIN * 4, OOB = 0x80000000u;
-  constexpr bool FULL = C::UNITS % C::PTHR == 0;  // every producer thread owns UPT real units
   auto produce_loads = [&](int s, float4 (&pf)[C::UPT][2]) {
-    const bool live = s < NS;
-    int p0 = 0, y0 = 0;
-    if (live) tile_of(s, p0, y0);
+    int p0, y0;
+    tile_of(s, p0, y0);
     const int cc = s % C::NCC;
-    const int nval = !live ? 0 : (NP == 1 || P - p0 >= NP) ? NP : P - p0;
-    const __amdgpu_buffer_rsrc_t rs = make_rsrc(in + (size_t)p0 * HIN * HIN * CIN, (unsigned)nval * PATCH_BYTES);
 #pragma unroll
     for (int k = 0; k < C::UPT; ++k) {
       const int u = ptid + k * C::PTHR;
@@ -830,17 +820,21 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_ws(
       const int wc = pix % C::NCOLS, t2 = pix / C::NCOLS;
       const int wr = t2 % C::RIN, np = t2 / C::RIN;
       const int y = y0 * S - 1 + wr, x = wc - 1;
-      const bool ok = (FULL || u < C::UNITS) && (unsigned)y < (unsigned)HIN && (unsigned)x < (unsigned)HIN;
-      const unsigned vo = ok ? (unsigned)(((np * HIN + y) * HIN + x) * CIN + cc * 32 + g * 8) * 4u : OOB;
-      pf[k][0] = __builtin_bit_cast(float4, buf_load16(rs, vo, 0));
-      pf[k][1] = __builtin_bit_cast(float4, buf_load16(rs, vo, 16));
+      pf[k][0] = pf[k][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (u < C::UNITS && (NP == 1 || p0 + np < P) && (unsigned)y < (unsigned)HIN &&
+          (unsigned)x < (unsigned)HIN) {
+        const float4* src = reinterpret_cast<const float4*>(
+            in + ((((size_t)p0 + np) * HIN + y) * HIN + x) * CIN + cc * 32 + g * 8);
+        pf[k][0] = src[0];
+        pf[k][1] = src[1];
+      }
     }
   };
   auto produce_write = [&](char* dst, const float4 (&pf)[C::UPT][2]) {
 #pragma unroll
     for (int k = 0; k < C::UPT; ++k) {
       const int u = ptid + k * C::PTHR;
-      if (FULL || u < C::UNITS) {
+      if (u < C::UNITS) {
         const int g = u & 3, pix = u >> 2;
         const int wc = pix % C::NCOLS, t2 = pix / C::NCOLS;
         const int wr = t2 % C::RIN, np = t2 / C::RIN;
@@ -983,7 +977,7 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_ws(
     } else {
       produce_loads(0, pf);
       produce_write(buf0, pf);
-      produce_loads(1, pf);
+      if (NS > 1) produce_loads(1, pf);
     }
   } else {
     for (int i = tid; i < COUT; i += C::NWC * 64) reinterpret_cast<float*>(smem + C::BIAS_OFF)[i] = bias[i];
@@ -1007,9 +1001,10 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_ws(
     } else if constexpr (!C::DEEP) {
 #pragma unroll 1
       for (int s = 0; s < NS; ++s) {
-        // unconditional (see produce_loads): past NS the write goes to a buffer nobody reads again
-        produce_write((s & 1) ? buf0 : buf1, pf);
-        produce_loads(s + 2, pf);
+        if (s + 1 < NS) {
+          produce_write((s & 1) ? buf0 : buf1, pf);
+          if (s + 2 < NS) produce_loads(s + 2, pf);
+        }
         __syncthreads();
         if constexpr (PST)
           if (s % C::NCC == C::NCC - 1) pstore(s, (s & 1) ? buf1 : buf0);
@@ -1019,15 +1014,14 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_ws(
       // stages of MFMA work to land in
 #pragma unroll 1
       for (int s = 0; s < NS; s += 2) {
-        // unconditional (see produce_loads): past NS the write goes to a buffer nobody reads again
-        produce_loads(s + 2, pf2);
-        produce_write(buf1, pf);
+        if (s + 2 < NS) produce_loads(s + 2, pf2);
+        if (s + 1 < NS) produce_write(buf1, pf);
         __syncthreads();
         if constexpr (PST)
           if (s % C::NCC == C::NCC - 1) pstore(s, buf0);
         if (s + 1 >= NS) break;
-        produce_loads(s + 3, pf);
-        produce_write(buf0, pf2);
+        if (s + 3 < NS) produce_loads(s + 3, pf);
+        if (s + 2 < NS) produce_write(buf0, pf2);
         __syncthreads();
         if constexpr (PST)
           if ((s + 1) % C::NCC == C::NCC - 1) pstore(s + 1, buf1);

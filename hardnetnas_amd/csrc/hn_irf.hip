@@ -101,15 +101,19 @@ HN_DEV void irf_core(const uint4 (&bh)[IrfShape<CIN, COUT, HIN, S, K, MID>::TI][
   }
 #pragma unroll 1
   for (int m = 0; m < MID / 32; ++m) {
-    // dw weights + bias of the chunk (float4 t of K*K*8 + 8): loaded with the pw's first operands and
-    // stored to LDS after the pw, so their L2 round trip hides behind the pw MFMAs (loaded and
-    // stored up front it was exposed once per chunk); the clamped index keeps the load unconditional
+    // dw weights + bias of the chunk (float4 t of K*K*8 + 8).  RING (the 64- and 128-channel blocks,
+    // KS >= 4): loaded with the pw's first operands and stored to LDS after the pw, so their L2 round
+    // trip hides behind the pw MFMAs (the clamped index keeps the load unconditional); the 32-channel
+    // blocks keep the up-front store (same-box A/B: the RING form cost wang3's irf 2.42 -> 2.59 ms)
     static_assert(K * K * 8 + 8 <= 256, "one dw weight float4 per thread");
     constexpr int NWQ = K * K * 8 + 8;
+    constexpr bool RING = KS >= 4;
     const int iw = t < NWQ ? t : NWQ - 1;
     const float* const wsrc =
         iw < K * K * 8 ? dw_w + (iw >> 3) * MID + 32 * m + 4 * (iw & 7) : dw_b + 32 * m + 4 * (iw - K * K * 8);
     float4 wv;
+    if constexpr (!RING)
+      if (t < NWQ) *reinterpret_cast<float4*>(wslot(t)) = *reinterpret_cast<const float4*>(wsrc);
     // ---- pw --------------------------------------------------------------------------
     {
       f32x16 bias;  // pw bias as the initial accumulator (epilogue: ReLU only)
@@ -121,25 +125,36 @@ HN_DEV void irf_core(const uint4 (&bh)[IrfShape<CIN, COUT, HIN, S, K, MID>::TI][
       f32x16 c[TI];
 #pragma unroll
       for (int i = 0; i < TI; ++i) c[i] = bias;
-      // the weight fragments one K-step ahead (ring of two): left to itself the scheduler reused one
-      // register pair for every K-step of the 64-channel blocks, i.e. load -> vmcnt(0) -> MFMA, one L2
-      // round trip per K-step
-      uint4 fa[2][2];
       auto pw_frag = [&](int s, uint4 (&d)[2]) {
         const uint4* ap = pw_a + ((size_t)(m * KS + s) * 2) * 64 + lane;
         d[0] = ap[0];
         d[1] = ap[64];
       };
-      pw_frag(0, fa[0]);
-      wv = *reinterpret_cast<const float4*>(wsrc);
+      if constexpr (RING) {
+        // the weight fragments one K-step ahead (ring of two): left to itself the scheduler reused one
+        // register pair for every K-step of the 64-channel blocks, i.e. load -> vmcnt(0) -> MFMA, one L2
+        // round trip per K-step (same-box A/B: wang2 irf2 9.26 -> 8.40 ms)
+        uint4 fa[2][2];
+        pw_frag(0, fa[0]);
+        wv = *reinterpret_cast<const float4*>(wsrc);
 #pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        if (s + 1 < KS) pw_frag(s + 1, fa[(s + 1) & 1]);
-        __builtin_amdgcn_sched_barrier(0);
-        const f16x8 ah = as_f16x8(fa[s & 1][0]), al = as_f16x8(fa[s & 1][1]);
+        for (int s = 0; s < KS; ++s) {
+          if (s + 1 < KS) pw_frag(s + 1, fa[(s + 1) & 1]);
+          __builtin_amdgcn_sched_barrier(0);
+          const f16x8 ah = as_f16x8(fa[s & 1][0]), al = as_f16x8(fa[s & 1][1]);
 #pragma unroll
-        for (int i = 0; i < TI; ++i) c[i] = mfma3_f16(ah, al, as_f16x8(bh[i][s]), as_f16x8(bl[i][s]), c[i]);
-        __builtin_amdgcn_sched_barrier(0);
+          for (int i = 0; i < TI; ++i) c[i] = mfma3_f16(ah, al, as_f16x8(bh[i][s]), as_f16x8(bl[i][s]), c[i]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      } else {
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+          uint4 f[2];
+          pw_frag(s, f);
+          const f16x8 ah = as_f16x8(f[0]), al = as_f16x8(f[1]);
+#pragma unroll
+          for (int i = 0; i < TI; ++i) c[i] = mfma3_f16(ah, al, as_f16x8(bh[i][s]), as_f16x8(bl[i][s]), c[i]);
+        }
       }
 #pragma unroll
       for (int i = 0; i < TI; ++i) {
@@ -150,7 +165,8 @@ HN_DEV void irf_core(const uint4 (&bh)[IrfShape<CIN, COUT, HIN, S, K, MID>::TI][
                                      fmaxf(c[i][4 * q + 2], 0.f), fmaxf(c[i][4 * q + 3], 0.f));
       }
     }
-    if (t < NWQ) *reinterpret_cast<float4*>(wslot(t)) = wv;
+    if constexpr (RING)
+      if (t < NWQ) *reinterpret_cast<float4*>(wslot(t)) = wv;
     __syncthreads();
     // ---- dw: thread item = (run of R output pixels in one row, channel quad q) -----------
     // (BAND: item k of the thread is band k, computed and consumed by the pwl in turn)
