@@ -240,11 +240,12 @@ struct hn_model {
   bool no_irf2 = false;   // HN_NO_IRF2=1: one k_irf launch per block (no two-block fusion)
   // conv tiling per layer (index 0 = stem+conv1, 2..5 = conv2..5); defaults are the best
   // measured on MI355X (tools/tune_variants.py); HN_VARIANT="003303" style override
-  // 19 / 20 / 21 = 1-D Winograd F(2,3) (hn_wino1.hip; conv3 / conv5) with a weight ring of depth 3 / 4 / 6
-  // (21 the default: same-box HardNet 5.25 -> 5.40 Mpatches/s over 19); conv4: 18 = two patches per stage
-  // on the 64-byte swizzled window (15) with the outputs stored by the producer waves; 16 = the direct
-  // conv3 / conv5 with epilogue stores through LDS (the forms before 19)
-  int variant[6] = {6, 0, 5, 21, 18, 21};
+  // 19 / 20 / 21 / 26 = 1-D Winograd F(2,3) (hn_wino1.hip; conv3 / conv5) with a weight ring of depth
+  // 3 / 4 / 6 / 8 (same-box HardNet 5.25 Mpatches/s at 3 / 3, 5.40 at 6 / 6; conv3 at 8: 10.2 -> 9.9 ms,
+  // conv5 flat past 6); conv4: 18 = two patches per stage on the 64-byte swizzled window (15) with the
+  // outputs stored by the producer waves; 16 = the direct conv3 / conv5 with epilogue stores through LDS
+  // (the forms before 19)
+  int variant[6] = {6, 0, 5, 26, 18, 21};
   size_t ws_floats_per_patch = 0;  // per buffer
   int n_bufs = 0;
 

@@ -1864,6 +1864,7 @@ bool hn_hardnet_variant_ok(int layer, int v) {
 #endif
   if (v == 15 || v == 18) return layer == 4;  // 18: outputs stored by the producer waves
   if (v >= 19 && v <= 21) return layer == 3 || layer == 5;  // 1-D Winograd F(2,3) (hn_wino1.hip), weight ring 3 / 4 / 6
+  if (v == 26) return layer == 3 || layer == 5;              // the same, weight ring 8 (digit q)
 #ifdef HN_EXPERIMENTS
   if (v >= 22 && v <= 25) return layer == 3 || layer == 5;  // its timing-only ablations (ABL 1 / 2 / 4 / 8)
 #endif
@@ -1910,6 +1911,7 @@ hipError_t hn_launch_hardnet_conv(int layer, int variant, const HardnetDev& d, c
   }
 #endif
   if (variant >= 19 && variant <= 21) return hn_launch_wino1(layer, variant == 19 ? 3 : variant == 20 ? 4 : 6, d, in, out, P, st);
+  if (variant == 26) return hn_launch_wino1(layer, 8, d, in, out, P, st);
 #ifdef HN_EXPERIMENTS
   if (variant >= 22 && variant <= 25) return hn_launch_wino1(layer, 100 + (1 << (variant - 22)), d, in, out, P, st);
 #endif

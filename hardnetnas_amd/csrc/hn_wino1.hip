@@ -386,7 +386,7 @@ using W1Conv5 = W1Cfg<128, 128, 8, 2, 1, 4, true>;
 }  // namespace
 
 // conv3: one patch per work tile, 2 x 2 MFMA waves of 2 M tiles; conv5: two patches, 1 x 4 waves.
-// wd: the weight ring depth (HN_VARIANT digit j = 3, k = 4, l = 6)
+// wd: the weight ring depth (HN_VARIANT digit j = 3, k = 4, l = 6, q = 8)
 hipError_t hn_launch_wino1(int layer, int wd, const HardnetDev& d, const float* in, float* out, int P,
                            hipStream_t st) {
   if (P <= 0) return hipSuccess;
@@ -405,6 +405,7 @@ hipError_t hn_launch_wino1(int layer, int wd, const HardnetDev& d, const float* 
     if (wd == 3) return launch_w1<CI, CO, HH, NPP, WMM, WNN, true, 3>(in, out, d.wino1[L], d.bias[L], P, st); \
     if (wd == 4) return launch_w1<CI, CO, HH, NPP, WMM, WNN, true, 4>(in, out, d.wino1[L], d.bias[L], P, st); \
     if (wd == 6) return launch_w1<CI, CO, HH, NPP, WMM, WNN, true, 6>(in, out, d.wino1[L], d.bias[L], P, st); \
+    if (wd == 8) return launch_w1<CI, CO, HH, NPP, WMM, WNN, true, 8>(in, out, d.wino1[L], d.bias[L], P, st); \
     HN_W1_ABL(CI, CO, HH, NPP, WMM, WNN, L)                                                                     \
   }
   HN_W1(3, 64, 64, 16, 1, 2, 2)

@@ -93,12 +93,12 @@ def test_tiling_variants_match_reference(variant, cuda_device, monkeypatch):
     assert np.abs(y - fx["y"]).max() <= TOL["hardnet"]
 
 
-@pytest.mark.parametrize("variant", ["605jig", "605gij", "605jij", "605kik", "605lil"])
+@pytest.mark.parametrize("variant", ["605jig", "605gij", "605jij", "605kik", "605lil", "605qiq", "605qil"])
 def test_winograd_1d_conv3_conv5_match_reference(variant, cuda_device, monkeypatch):
-    """conv3 / conv5 as 1-D Winograd F(2,3) (hn_wino1.hip, HN_VARIANT digits j / k / l = weight ring
-    depth 3 / 4 / 6) against the reference's fp32 and fp64 vectors (edge patches included) and against
-    the direct kernels on ragged batches whose last two-patch conv5 tile is half empty.  605lil is the
-    default."""
+    """conv3 / conv5 as 1-D Winograd F(2,3) (hn_wino1.hip, HN_VARIANT digits j / k / l / q = weight
+    ring depth 3 / 4 / 6 / 8) against the reference's fp32 and fp64 vectors (edge patches included) and
+    against the direct kernels on ragged batches whose last two-patch conv5 tile is half empty.  605qil
+    is the default."""
     from hardnetnas_amd._native import NativeModel
     m, fx, _ = build_module("hardnet")
     x = torch.from_numpy(golden_inputs(fx)).to(cuda_device)
