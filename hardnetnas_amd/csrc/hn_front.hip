@@ -108,6 +108,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRO
 
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int px = lane & 31, h = lane >> 5;
+  // NF lane permutations (bank conflicts; tests/test_lds_banks.py::test_front_nf_*).  pxm: the image
+  // column that stem / pw MFMA column px stands for -- columns 0-15 take the pixels whose padded column
+  // PAD + pxm is even, 16-31 the odd ones, in order -- so each 8-lane group of the pw epilogue's
+  // ds_write_b128 covers 8 consecutive positions of one half of the even / odd-split pw row (2-way
+  // conflicted in column order).  dwx (below): the output column of 16x16 pwl column l & 15 -- columns
+  // {0-3, 12-15} the even ones, {4-11} the odd ones -- so the dw window reads of a ds_read_b128 lane group
+  // (mixing those two sets with channel offsets 8 apart) hit 16 distinct slots (2-way in order).
+  const int pxm = NF ? 2 * (px & 15) + (((px >> 4) & 1) ^ (PAD & 1)) : px;
+  const int l16 = lane & 15;
+  const int dwx = l16 < 4 ? 2 * l16 : l16 < 12 ? 2 * (l16 - 4) + 1 : 2 * (l16 - 8);
   // persistent: whole patches per workgroup, their 4 bands in order
   const long per = ((long)P + gridDim.x - 1) / gridDim.x;
   const long pb = (long)xcd_remap(blockIdx.x, gridDim.x) * per;
@@ -292,7 +302,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRO
       if constexpr (PAIR) {
         static_assert(!PAIR || NT == 2 || PAIR5, "two rows per wave");
         const int y0 = PAIR5 ? y5 : yr0 + 2 * w;  // rows y0, y0 + 1 (LEAN bands hold 8 real rows)
-        const float* sb = s_in + y0 * 34 + px;
+        const float* sb = s_in + y0 * 34 + pxm;
         float tp[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) tp[j] = sb[toff[j]];
@@ -323,7 +333,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRO
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int tap = 8 * h + j;  // h = 1 holds tap 8 and zeros
-          tp[j] = tap < 9 ? s_in[(y + tap / 3) * 34 + px + tap % 3] : 0.f;
+          tp[j] = tap < 9 ? s_in[(y + tap / 3) * 34 + pxm + tap % 3] : 0.f;
         }
         uint4 xh, xl;
         split8_f16(make_float4(tp[0], tp[1], tp[2], tp[3]), make_float4(tp[4], tp[5], tp[6], tp[7]), xh, xl);
@@ -403,7 +413,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRO
           if constexpr (LDSB) bias = bias16(s_pwb);
           f32x16 acc = mfma3_f16(ah0, al0, as_f16x8(bh[i][0]), as_f16x8(bl[i][0]), bias);
           acc = mfma3_f16(ah1, al1, as_f16x8(bh[i][1]), as_f16x8(bl[i][1]), acc);
-          float4* d = reinterpret_cast<float4*>(s_pw + slot_of(y) * RS + colpos(PAD + px) * PS);
+          float4* d = reinterpret_cast<float4*>(s_pw + slot_of(y) * RS + colpos(PAD + pxm) * PS);
 #pragma unroll
           for (int q = 0; q < 4; ++q)
             d[2 * q + h] = make_float4(fmaxf(acc[4 * q], 0.f), fmaxf(acc[4 * q + 1], 0.f),
@@ -411,7 +421,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRO
         }
         __syncthreads();
         if constexpr (NF) {  // dw of band row w, 8 channels of pixel lane & 15 -> 16x16x32 pwl
-          const int ox = lane & 15, c0 = 8 * (lane >> 4);
+          const int ox = dwx, c0 = 8 * (lane >> 4);
           f32x4 a0 = *reinterpret_cast<const f32x4*>(s_dw + KK * KK * 32 + c0);
           f32x4 a1 = *reinterpret_cast<const f32x4*>(s_dw + KK * KK * 32 + c0 + 4);
 #pragma unroll DYU
@@ -468,7 +478,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRO
       }
       if constexpr (NF) {  // band row r0 + w, pixel lane & 15: 4 consecutive channels per tile
         // (whole 128-byte rows per store after a DPP row rotation measured slower: wang2 front 5.07 -> 5.26 ms)
-        float* dst = out + ((patch * 16 + r0 + w) * 16 + (lane & 15)) * OC + 4 * (lane >> 4);
+        float* dst = out + ((patch * 16 + r0 + w) * 16 + dwx) * OC + 4 * (lane >> 4);
 #pragma unroll
         for (int tt = 0; tt < 2; ++tt)
           *reinterpret_cast<float4*>(dst + 16 * tt) = make_float4(o16[tt][0], o16[tt][1], o16[tt][2], o16[tt][3]);

@@ -174,6 +174,60 @@ def test_front_irf_dw_reads_conflict_free(kk):
                             assert len(slots) == 16, (kk, w, band, dy, dx, g[0])
 
 
+def _front_nf_maps(pad):
+    """hn_front.hip NF lane permutations: pxm (stem / pw MFMA column -> image column) and dwx
+    (16x16 pwl column -> output column)."""
+    pxm = [2 * (n & 15) + (((n >> 4) & 1) ^ (pad & 1)) for n in range(32)]
+    dwx = [2 * n if n < 4 else 2 * (n - 4) + 1 if n < 12 else 2 * (n - 8) for n in range(16)]
+    return pxm, dwx
+
+
+@pytest.mark.parametrize("kk", [3, 5])
+def test_front_nf_dw_reads_conflict_free(kk):
+    """NF dw window reads: lane l reads output column dwx[l & 15], channels 8 (l >> 4) (+4) at padded
+    input column 2 ox + dx of its wave's ring row (even / odd split positions, pixel stride 36
+    floats): every ds_read_b128 group hits 16 distinct 16-byte slots.  In column order (ox = l & 15)
+    the groups were 2-way conflicted -- the 35 % SQ_LDS_BANK_CONFLICT share of the k5 front."""
+    pad = kk // 2
+    half = (32 + 2 * pad + 1) // 2
+    _, dwx = _front_nf_maps(pad)
+    assert sorted(dwx) == list(range(16))
+    worst_identity = 0
+    for dx in range(kk):
+        for j in range(2):
+            for perm in (dwx, list(range(16))):
+                for g in GROUPS:
+                    slots = set()
+                    for lane in g:
+                        ox = perm[lane & 15]
+                        pos = half + ox + (dx >> 1) if dx & 1 else ox + (dx >> 1)
+                        slots.add(((pos * 36 + 8 * (lane >> 4) + 4 * j) * 4 // 16) % 16)
+                    if perm is dwx:
+                        assert len(slots) == 16, (kk, dx, j, g[0])
+                    else:
+                        worst_identity = max(worst_identity, 16 - len(slots))
+    assert worst_identity > 0  # the column-order map this replaced
+
+
+@pytest.mark.parametrize("kk", [3, 5])
+def test_front_nf_pw_writes_conflict_free(kk):
+    """NF pw epilogue: lane (n = l & 31, h) writes float4 2q + h of image column pxm[n] at position
+    colpos(PAD + pxm[n]) (pixel stride 36 floats); ds_write_b128 serves 8 groups of 8 consecutive
+    lanes, conflict-free when their addresses fall in 8 distinct 16-byte slots of 128 bytes."""
+    pad = kk // 2
+    half = (32 + 2 * pad + 1) // 2
+    pxm, _ = _front_nf_maps(pad)
+    assert sorted(pxm) == list(range(32))
+    for q in range(4):
+        for g0 in range(0, 64, 8):
+            slots = set()
+            for lane in range(g0, g0 + 8):
+                c = pad + pxm[lane & 31]
+                pos = half + c // 2 if c & 1 else c // 2
+                slots.add(((pos * 36 + 4 * (2 * q + (lane >> 5))) * 4 // 16) % 8)
+            assert len(slots) == 8, (kk, q, g0)
+
+
 @pytest.mark.parametrize("kk", [3, 5])
 def test_front_irf_fold_positions_are_interior(kk):
     """The pwl partial-sum fold uses the 16 interior even positions from 1 and the 16 interior
