@@ -7,7 +7,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out; export TMPDIR=/tmp
 H=abl/head/libhardnet_mi355x.so
 timeout -k 10 500 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/ab4_pytest.log 2>&1 || { tail -30 gpurun_out/ab4_pytest.log; exit 1; }
 tail -1 gpurun_out/ab4_pytest.log
-REPS=2 ENVS="HN_LIB=$H;-;HN_LIB=abl/ws1/libhardnet_mi355x.so;HN_LIB=abl/ws2/libhardnet_mi355x.so" bash tools/ab_env.sh || exit 1
-for m in wang2 wang3; do
+REPS=2 ENVS="HN_LIB=$H;-" bash tools/ab_env.sh || exit 1
+for m in wang2 wang3 wang4; do
   MODEL=$m REPS=2 ENVS="HN_LIB=$H;-" bash tools/ab_env.sh || exit 1
 done
