@@ -101,7 +101,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRO
   static_assert(IR >= 8, "ring holds a band's 8 new rows");
   __shared__ float s_in[34 * 34];
   __shared__ __attribute__((aligned(16))) float s_pw[IR * RS];
-  __shared__ __attribute__((aligned(16))) float s_dw[KK * KK * 32 + 32];
+  // XCH (the k5 front, MID = 32): the dw runs per channel group with its weights in SGPRs and crosses to
+  // the pwl's operand layout through s_x (see the dw phase); s_dw is not used
+  constexpr bool XCH = PAIR5 && NF;
+  __shared__ __attribute__((aligned(16))) float s_dw[XCH ? 4 : KK * KK * 32 + 32];
+  __shared__ uint4 s_x[XCH ? 2 * 4 * 16 * 4 : 1];  // [hi / lo][band row][column][16-byte chunk]
   __shared__ float red[8];
   // stem bias and (MID = 32: the single chunk's) pw bias, read where used (fewer live VGPRs)
   __shared__ __attribute__((aligned(16))) float s_sb[32], s_pwb[32];
@@ -171,7 +175,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRO
   auto slot_of = [](int y) { return (y + PAD + IR) % IR; };  // ring slot of pw row y
 
   constexpr bool DW_ONCE = NF && MID == 32 && MODE == FRONT_IRF;  // one chunk: its dw weights never change
-  if constexpr (DW_ONCE) {
+  if constexpr (DW_ONCE && !XCH) {
     for (int i = t; i < KK * KK * 8 + 8; i += 256) {
       float4 wv;
       if (i < KK * KK * 8)
@@ -420,31 +424,66 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRO
                                        fmaxf(acc[4 * q + 2], 0.f), fmaxf(acc[4 * q + 3], 0.f));
         }
         __syncthreads();
-        if constexpr (NF) {  // dw of band row w, 8 channels of pixel lane & 15 -> 16x16x32 pwl
-          const int ox = dwx, c0 = 8 * (lane >> 4);
-          f32x4 a0 = *reinterpret_cast<const f32x4*>(s_dw + KK * KK * 32 + c0);
-          f32x4 a1 = *reinterpret_cast<const f32x4*>(s_dw + KK * KK * 32 + c0 + 4);
-#pragma unroll DYU
-          for (int dy = 0; dy < KK; ++dy) {
-            const float* rp = s_pw + slot_of(2 * (r0 + w) - PAD + dy) * RS + c0;
-#pragma unroll
-            for (int dx = 0; dx < KK; ++dx) {
-              const float* wp = s_dw + (dy * KK + dx) * 32 + c0;
-              const float* ip = rp + ((dx & 1) ? HALF + ox + (dx >> 1) : ox + (dx >> 1)) * PS;
-              a0 = __builtin_elementwise_fma(*reinterpret_cast<const f32x4*>(wp), *reinterpret_cast<const f32x4*>(ip), a0);
-              a1 = __builtin_elementwise_fma(*reinterpret_cast<const f32x4*>(wp + 4), *reinterpret_cast<const f32x4*>(ip + 4), a1);
-            }
-          }
-          a0 = __builtin_elementwise_max(a0, f32x4{});
-          a1 = __builtin_elementwise_max(a1, f32x4{});
+        if constexpr (NF) {
           uint4 xh, xl;
-          split8_f16(make_float4(a0.x, a0.y, a0.z, a0.w), make_float4(a1.x, a1.y, a1.z, a1.w), xh, xl);
+          if constexpr (XCH) {
+            // wave w computes channel group w (8 channels) of all four band rows, lane (row lane >> 4, output
+            // column lane & 15): the dw weights are wave-uniform and come from SGPRs (scalar loads of dw_w /
+            // dw_b) instead of a broadcast ds_read_b128 per 4 channels and tap -- half the front's LDS
+            // reads.  The results cross to the pwl's (column, channel group) lane layout through s_x, chunk
+            // g of column c at g ^ ((c >> 1) & 3) (writes and reads conflict-free, tests/test_lds_banks.py).
+            const int cg = __builtin_amdgcn_readfirstlane(w), rr = lane >> 4, ox = lane & 15, c0 = 8 * cg;
+            const float* const wsrc = dw_w + 32 * m + c0;
+            f32x4 a0 = *reinterpret_cast<const f32x4*>(dw_b + 32 * m + c0);
+            f32x4 a1 = *reinterpret_cast<const f32x4*>(dw_b + 32 * m + c0 + 4);
+#pragma unroll DYU
+            for (int dy = 0; dy < KK; ++dy) {
+              const float* rp = s_pw + slot_of(2 * (r0 + rr) - PAD + dy) * RS + c0;
+#pragma unroll
+              for (int dx = 0; dx < KK; ++dx) {
+                const float* wp = wsrc + (dy * KK + dx) * MID;
+                const float* ip = rp + ((dx & 1) ? HALF + ox + (dx >> 1) : ox + (dx >> 1)) * PS;
+                a0 = __builtin_elementwise_fma(*reinterpret_cast<const f32x4*>(wp), *reinterpret_cast<const f32x4*>(ip), a0);
+                a1 = __builtin_elementwise_fma(*reinterpret_cast<const f32x4*>(wp + 4), *reinterpret_cast<const f32x4*>(ip + 4), a1);
+              }
+            }
+            a0 = __builtin_elementwise_max(a0, f32x4{});
+            a1 = __builtin_elementwise_max(a1, f32x4{});
+            split8_f16(make_float4(a0.x, a0.y, a0.z, a0.w), make_float4(a1.x, a1.y, a1.z, a1.w), xh, xl);
+            const int wc = cg ^ ((ox >> 1) & 3);
+            s_x[((0 * 4 + rr) * 16 + ox) * 4 + wc] = xh;
+            s_x[((1 * 4 + rr) * 16 + ox) * 4 + wc] = xl;
+            __syncthreads();  // every channel group of the band's pixels in s_x
+            const int kg = lane >> 4, rc = kg ^ ((l16 >> 1) & 3);
+            xh = s_x[((0 * 4 + w) * 16 + l16) * 4 + rc];
+            xl = s_x[((1 * 4 + w) * 16 + l16) * 4 + rc];
+          } else {  // dw of band row w, 8 channels of pixel dwx -> 16x16x32 pwl
+            const int ox = dwx, c0 = 8 * (lane >> 4);
+            f32x4 a0 = *reinterpret_cast<const f32x4*>(s_dw + KK * KK * 32 + c0);
+            f32x4 a1 = *reinterpret_cast<const f32x4*>(s_dw + KK * KK * 32 + c0 + 4);
+#pragma unroll DYU
+            for (int dy = 0; dy < KK; ++dy) {
+              const float* rp = s_pw + slot_of(2 * (r0 + w) - PAD + dy) * RS + c0;
+#pragma unroll
+              for (int dx = 0; dx < KK; ++dx) {
+                const float* wp = s_dw + (dy * KK + dx) * 32 + c0;
+                const float* ip = rp + ((dx & 1) ? HALF + ox + (dx >> 1) : ox + (dx >> 1)) * PS;
+                a0 = __builtin_elementwise_fma(*reinterpret_cast<const f32x4*>(wp), *reinterpret_cast<const f32x4*>(ip), a0);
+                a1 = __builtin_elementwise_fma(*reinterpret_cast<const f32x4*>(wp + 4), *reinterpret_cast<const f32x4*>(ip + 4), a1);
+              }
+            }
+            a0 = __builtin_elementwise_max(a0, f32x4{});
+            a1 = __builtin_elementwise_max(a1, f32x4{});
+            split8_f16(make_float4(a0.x, a0.y, a0.z, a0.w), make_float4(a1.x, a1.y, a1.z, a1.w), xh, xl);
+          }
           const uint4* lp = pwl_a16 + (size_t)m * 4 * 64 + lane;
 #pragma unroll
           for (int tt = 0; tt < 2; ++tt)
             o16[tt] = mfma3_f16_16(INV ? ilp[2 * tt] : as_f16x8(lp[128 * tt]), INV ? ilp[2 * tt + 1] : as_f16x8(lp[128 * tt + 64]),
                                    as_f16x8(xh), as_f16x8(xl), o16[tt]);
-          __syncthreads();  // s_dw (and, without the ring, s_pw) is rewritten next
+          // s_dw (and, without the ring, s_pw) is rewritten next; XCH: the next band's s_x writes come after
+          // its own first barrier, which every wave reaches only after these reads
+          if constexpr (!XCH) __syncthreads();
           continue;
         }
         // dw straight into the pwl B-operand layout: wave w owns band pixel tile (w & 1) and
@@ -478,7 +517,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRO
       }
       if constexpr (NF) {  // band row r0 + w, pixel lane & 15: 4 consecutive channels per tile
         // (whole 128-byte rows per store after a DPP row rotation measured slower: wang2 front 5.07 -> 5.26 ms)
-        float* dst = out + ((patch * 16 + r0 + w) * 16 + dwx) * OC + 4 * (lane >> 4);
+        float* dst = out + ((patch * 16 + r0 + w) * 16 + (XCH ? l16 : dwx)) * OC + 4 * (lane >> 4);
 #pragma unroll
         for (int tt = 0; tt < 2; ++tt)
           *reinterpret_cast<float4*>(dst + 16 * tt) = make_float4(o16[tt][0], o16[tt][1], o16[tt][2], o16[tt][3]);

@@ -228,6 +228,37 @@ def test_front_nf_pw_writes_conflict_free(kk):
             assert len(slots) == 8, (kk, q, g0)
 
 
+def test_front_xch_accesses_conflict_free():
+    """k5 front XCH form: wave w = channel group w of the band's four rows, lane (row l >> 4, column
+    l & 15) reads ring row 2 (r0 + row) - PAD + dy at split position pos(column, dx), channels
+    8 w (+4); then writes its hi / lo 16-byte chunk to s_x[plane][row][column][w ^ ((column >> 1) & 3)],
+    and wave w reads row w back as lane (column l & 15, channel group l >> 4).  Row stride RS is a
+    multiple of 64 floats, so the two rows a read group mixes share one slot pattern."""
+    kk, pad, ps = 5, 2, 36
+    pc = 32 + 2 * pad
+    half, rs, ir = (pc + 1) // 2, (pc * ps + 63) // 64 * 64, 2 * 3 + kk
+    for w in range(4):
+        for r0 in (0, 4, 8, 12):
+            for dy in range(kk):
+                for dx in range(kk):
+                    for j in range(2):
+                        for g in GROUPS:
+                            slots = set()
+                            for lane in g:
+                                rr, ox = lane >> 4, lane & 15
+                                slot = (2 * (r0 + rr) - pad + dy + pad + ir) % ir
+                                pos = half + ox + (dx >> 1) if dx & 1 else ox + (dx >> 1)
+                                slots.add(((slot * rs + pos * ps + 8 * w + 4 * j) * 4 // 16) % 16)
+                            assert len(slots) == 16, (w, r0, dy, dx, j, g[0])
+        for g0 in range(0, 64, 8):  # ds_write_b128: 8 groups of 8 lanes, slots of 128 bytes
+            slots = {((((l >> 4) * 16 + (l & 15)) * 4 + (w ^ (((l & 15) >> 1) & 3))) * 16 // 16) % 8
+                     for l in range(g0, g0 + 8)}
+            assert len(slots) == 8, (w, g0)
+        for g in GROUPS:
+            slots = {(((w * 16 + (l & 15)) * 4 + ((l >> 4) ^ (((l & 15) >> 1) & 3))) * 16 // 16) % 16 for l in g}
+            assert len(slots) == 16, (w, g[0])
+
+
 @pytest.mark.parametrize("kk", [3, 5])
 def test_front_irf_fold_positions_are_interior(kk):
     """The pwl partial-sum fold uses the 16 interior even positions from 1 and the 16 interior
