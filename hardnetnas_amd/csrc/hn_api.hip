@@ -38,6 +38,7 @@ void hn_read_knobs(HnKnobs* k) {
   k->pairdist_valu = std::getenv("HN_PAIRDIST_VALU") != nullptr;
   k->pairdist_reg = env_int("HN_PAIRDIST_REG", 0) != 0;
   k->front_fold = env_int("HN_FRONT_FOLD", 0) != 0;
+  k->front_xch3 = env_int("HN_FRONT_XCH3", 0) != 0;
   k->train_splitk = std::max(32, env_int("HN_TRAIN_SPLITK", 1024)) / 32 * 32;
   k->train_f32 = env_int("HN_TRAIN_F32", 1) & 255;
 #ifdef HN_EXPERIMENTS

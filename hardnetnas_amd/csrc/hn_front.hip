@@ -62,8 +62,8 @@ __constant__ unsigned char kDwLane[64] = {
 // 1 / 4 KiB of HBM per patch and no intermediate fp32 tensor exists.  (PIL mode stays unfused:
 // its 12 prefetched byte registers took the k3 front from three workgroups per CU to two, wang2
 // front 5.7 -> 7.2 ms, against 0.46 ms for the separate hn_preprocess.)
-template <int K, int MID, int MODE, bool NORM, bool NF, int U8 = -1, bool P5 = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRONT_IRF && K == 3 && MID == 32 ? 3 : MODE == FRONT_IRF && K == 5 && MID == 32 ? 2 : 1))) void k_front(const void* __restrict__ in_,
+template <int K, int MID, int MODE, bool NORM, bool NF, int U8 = -1, bool P5 = false, bool X3 = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRONT_IRF && K == 3 && MID == 32 && !X3 ? 3 : MODE == FRONT_IRF && MID == 32 ? 2 : 1))) void k_front(const void* __restrict__ in_,
                                                float* __restrict__ out,
                                                const uint4* __restrict__ spack,  // stem A operand
                                                const float* __restrict__ stem_b,  // [32]
@@ -103,7 +103,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRO
   __shared__ __attribute__((aligned(16))) float s_pw[IR * RS];
   // XCH (the k5 front, MID = 32): the dw runs per channel group with its weights in SGPRs and crosses to
   // the pwl's operand layout through s_x (see the dw phase); s_dw is not used
-  constexpr bool XCH = PAIR5 && NF;
+  // (X3, HN_FRONT_XCH3=1: the same for the k3 front, which then fits two workgroups per CU, not three)
+  constexpr bool XCH = NF && (PAIR5 || (X3 && K == 3 && MID == 32 && MODE == FRONT_IRF));
   __shared__ __attribute__((aligned(16))) float s_dw[XCH ? 4 : KK * KK * 32 + 32];
   __shared__ uint4 s_x[XCH ? 2 * 4 * 16 * 4 : 1];  // [hi / lo][band row][column][16-byte chunk]
   __shared__ float red[8];
@@ -555,14 +556,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRO
   }
 }
 
-template <int K, int MID, int MODE, bool NORM, bool NF, int U8 = -1, bool P5 = false>
+template <int K, int MID, int MODE, bool NORM, bool NF, int U8 = -1, bool P5 = false, bool X3 = false>
 hipError_t front_launch_nf(const HnFrontArgs& a, int P, float eps, hipStream_t st, const HnU8In* u8 = nullptr) {
   int resident = 0;  // persistent grid: every workgroup resident at once
   const hipError_t e =
-      hn_resident_blocks(reinterpret_cast<const void*>(&k_front<K, MID, MODE, NORM, NF, U8, P5>), 256, 0, &resident);
+      hn_resident_blocks(reinterpret_cast<const void*>(&k_front<K, MID, MODE, NORM, NF, U8, P5, X3>), 256, 0, &resident);
   if (e != hipSuccess) return e;
   const void* src = u8 ? static_cast<const void*>(u8->in) : static_cast<const void*>(a.in);
-  hipLaunchKernelGGL((k_front<K, MID, MODE, NORM, NF, U8, P5>), dim3(std::min(P, resident)), dim3(256), 0, st, src,
+  hipLaunchKernelGGL((k_front<K, MID, MODE, NORM, NF, U8, P5, X3>), dim3(std::min(P, resident)), dim3(256), 0, st, src,
                      a.out, a.spack, a.stem_b, a.apack, a.pw_b, a.dw_w, a.dw_b, a.pwl_a, a.pwl_b, a.pwl_a16, P,
                      eps, u8 ? u8->mean : 0.f, u8 ? u8->stdv : 1.f, u8 ? u8->normalize : 0);
   return hipGetLastError();
@@ -597,6 +598,8 @@ hipError_t front_launch_t(const HnFrontArgs& a, int P, float eps, hipStream_t st
       return hipErrorInvalidValue;
     }
   }
+  if constexpr (K == 3 && MID == 32 && MODE == FRONT_IRF)
+    if (nf && hn_knobs().front_xch3) return front_launch_nf<K, MID, MODE, NORM, true, -1, false, true>(a, P, eps, st);
   if (nf) return front_launch_nf<K, MID, MODE, NORM, true, -1, front_p5<K, MID, MODE>()>(a, P, eps, st);
   return front_launch_nf<K, MID, MODE, NORM, false>(a, P, eps, st);
 }

@@ -19,6 +19,8 @@ struct HnKnobs {
   bool pairdist_valu = false;  // HN_PAIRDIST_VALU: fp32 VALU pair-distance kernel
   bool pairdist_reg = false;   // HN_PAIRDIST_REG: register-staged positives instead of the LDS-DMA ring
   bool front_fold = false;     // HN_FRONT_FOLD: the NAS front's pwl with the LDS partial-sum fold
+  bool front_xch3 = false;     // HN_FRONT_XCH3: the k3 front's dw per channel group (SGPR weights, s_x; two
+                               // workgroups per CU instead of three: wang2 front 5.05 -> 5.57 ms, not the default)
   int train_splitk = 1024;     // HN_TRAIN_SPLITK: K per split-K slice of the train GEMMs
   int train_f32 = 1;           // HN_TRAIN_F32: bit 0 train forward convs, bit 1 stride-1 dgrads as f32-MFMA
                                // GEMMs (else the bf16x3 conv kernels); default 1 = every product f32;
