@@ -64,7 +64,7 @@ struct W1Cfg {
 
 // ABL (timing-only ablation builds, HN_EXPERIMENTS library only; wrong results): bit 0 idle producers
 // (barriers only), bit 1 no MFMAs (operands still loaded), bit 2 no weight loads (K-step 0's fragments
-// reused), bit 3 no epilogue stores
+// reused), bit 3 no epilogue stores, bit 4 idle MFMA waves
 template <int CIN, int COUT, int H, int NP, int WM, int WN, bool CST, int WD = 3, int ABL = 0>
 __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_w1(const float* __restrict__ in, float* __restrict__ out,
                                                                 const uint4* __restrict__ wp,
@@ -207,6 +207,11 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_w1(const float* __r
   // ---- MFMA side ----
   for (int i = tid; i < COUT; i += C::NWC * 64) reinterpret_cast<float*>(smem + C::BIAS_OFF)[i] = bias[i];
   __syncthreads();
+  if constexpr ((ABL & 16) != 0) {  // timing only: idle MFMA waves (the producers alone)
+#pragma unroll 1
+    for (int s = 0; s < NS; ++s) __syncthreads();
+    return;
+  }
   const int wm = wave / WN, wn = wave % WN;
   const float* const sbias = reinterpret_cast<const float*>(smem + C::BIAS_OFF);
   // per-lane part of an operand address: M tile mt's position + its swizzled chunk for (ky, ks); the
@@ -391,12 +396,13 @@ hipError_t hn_launch_wino1(int layer, int wd, const HardnetDev& d, const float* 
                            hipStream_t st) {
   if (P <= 0) return hipSuccess;
   if (!d.wino1[layer]) return hipErrorInvalidValue;
-#ifdef HN_EXPERIMENTS  // wd = 100 + ABL: the timing-only ablations (WD 3)
+#ifdef HN_EXPERIMENTS  // wd = 100 + ABL: the timing-only ablations (weight ring 8)
 #define HN_W1_ABL(CI, CO, HH, NPP, WMM, WNN, L)                                                              \
-  if (wd == 101) return launch_w1<CI, CO, HH, NPP, WMM, WNN, true, 3, 1>(in, out, d.wino1[L], d.bias[L], P, st); \
-  if (wd == 102) return launch_w1<CI, CO, HH, NPP, WMM, WNN, true, 3, 2>(in, out, d.wino1[L], d.bias[L], P, st); \
-  if (wd == 104) return launch_w1<CI, CO, HH, NPP, WMM, WNN, true, 3, 4>(in, out, d.wino1[L], d.bias[L], P, st); \
-  if (wd == 108) return launch_w1<CI, CO, HH, NPP, WMM, WNN, true, 3, 8>(in, out, d.wino1[L], d.bias[L], P, st);
+  if (wd == 101) return launch_w1<CI, CO, HH, NPP, WMM, WNN, true, 8, 1>(in, out, d.wino1[L], d.bias[L], P, st); \
+  if (wd == 102) return launch_w1<CI, CO, HH, NPP, WMM, WNN, true, 8, 2>(in, out, d.wino1[L], d.bias[L], P, st); \
+  if (wd == 104) return launch_w1<CI, CO, HH, NPP, WMM, WNN, true, 8, 4>(in, out, d.wino1[L], d.bias[L], P, st); \
+  if (wd == 108) return launch_w1<CI, CO, HH, NPP, WMM, WNN, true, 8, 8>(in, out, d.wino1[L], d.bias[L], P, st); \
+  if (wd == 116) return launch_w1<CI, CO, HH, NPP, WMM, WNN, true, 8, 16>(in, out, d.wino1[L], d.bias[L], P, st);
 #else
 #define HN_W1_ABL(CI, CO, HH, NPP, WMM, WNN, L)
 #endif
