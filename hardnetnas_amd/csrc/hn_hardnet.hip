@@ -1865,7 +1865,6 @@ bool hn_hardnet_variant_ok(int layer, int v) {
   if (v == 15 || v == 18) return layer == 4;  // 18: outputs stored by the producer waves
   if (v >= 19 && v <= 21) return layer == 3 || layer == 5;  // 1-D Winograd F(2,3) (hn_wino1.hip), weight ring 3 / 4 / 6
   if (v == 26) return layer == 3 || layer == 5;              // the same, weight ring 8 (digit q)
-  if (v == 27 || v == 28) return layer == 3 || layer == 5;   // ring 6 / 8 with the outputs stored by the producers (r / s)
 #ifdef HN_EXPERIMENTS
   if ((v >= 22 && v <= 25) || v == 29) return layer == 3 || layer == 5;  // its timing-only ablations (ABL 1 / 2 / 4 / 8; t: 16)
 #endif
@@ -1913,7 +1912,6 @@ hipError_t hn_launch_hardnet_conv(int layer, int variant, const HardnetDev& d, c
 #endif
   if (variant >= 19 && variant <= 21) return hn_launch_wino1(layer, variant == 19 ? 3 : variant == 20 ? 4 : 6, d, in, out, P, st);
   if (variant == 26) return hn_launch_wino1(layer, 8, d, in, out, P, st);
-  if (variant == 27 || variant == 28) return hn_launch_wino1(layer, variant == 27 ? 206 : 208, d, in, out, P, st);
 #ifdef HN_EXPERIMENTS
   if (variant >= 22 && variant <= 25) return hn_launch_wino1(layer, 100 + (1 << (variant - 22)), d, in, out, P, st);
   if (variant == 29) return hn_launch_wino1(layer, 116, d, in, out, P, st);

@@ -31,7 +31,7 @@ namespace {
 // holds the H real rows of each patch and ONE zero row per plane that the padding reads point at).
 // CST: the epilogue goes through a per-wave LDS scratch so that each store writes 8 whole 128-byte
 // pixel slices (k_conv_ws's CST), one output column parity at a time.
-template <int CIN, int COUT, int H, int NP, int WM, int WN, bool CST, bool PST = false>
+template <int CIN, int COUT, int H, int NP, int WM, int WN, bool CST>
 struct W1Cfg {
   static constexpr int TR = H;              // output rows per work tile (whole patches)
   static constexpr int NTX = H / 2;         // output column pairs per row
@@ -51,16 +51,9 @@ struct W1Cfg {
   static constexpr bool DEEP = UPT <= 2;  // two stages of loads in flight
   static constexpr int SROW = 36;                       // CST: floats per pixel slice of the scratch
   static constexpr int SCR_OFF = 2 * BUF;
-  static constexpr int SCR = CST && !PST ? 32 * SROW * 4 : 0;  // CST: one 32-pixel x 32-channel tile per MFMA wave
-  // PST: a tile's outputs ([pixel][COUT] fp32, 16-byte chunk ch of pixel p at ch ^ ((p >> 1) & 7)) are staged in
-  // LDS by the MFMA waves and stored by the producer waves -- in buf1, which the tile's last stage (always odd)
-  // has just consumed, where it fits (conv3), else in a region of their own (conv5)
-  static constexpr int OUTB = NP * H * H * COUT * 4, ROWB = COUT * 4;
-  static constexpr bool STG_BUF = PST && OUTB <= BUF;
-  static constexpr int STG_OFF = SCR_OFF + NWC * SCR;
-  static constexpr int BIAS_OFF = STG_OFF + (PST && !STG_BUF ? OUTB : 0);
+  static constexpr int SCR = CST ? 32 * SROW * 4 : 0;   // CST: one 32-pixel x 32-channel tile per MFMA wave
+  static constexpr int BIAS_OFF = SCR_OFF + NWC * SCR;
   static constexpr int SMEM = BIAS_OFF + COUT * 4;
-  static_assert(!PST || (NCC % 2 == 0 && (OUTB / 16) % (PTHR * 8) == 0), "PST: tiles end on odd stages, batches");
   static constexpr int NKS = 24;  // K-steps per stage: 4 xi x 3 ky x 2 halves of 16 channels
   static constexpr unsigned CHUNK_BYTES = NKS * NTOT * 2 * 64 * 16;
   static_assert(SMEM <= 160 * 1024, "LDS");
@@ -72,11 +65,11 @@ struct W1Cfg {
 // ABL (timing-only ablation builds, HN_EXPERIMENTS library only; wrong results): bit 0 idle producers
 // (barriers only), bit 1 no MFMAs (operands still loaded), bit 2 no weight loads (K-step 0's fragments
 // reused), bit 3 no epilogue stores, bit 4 idle MFMA waves
-template <int CIN, int COUT, int H, int NP, int WM, int WN, bool CST, int WD = 3, int ABL = 0, bool PST = false>
+template <int CIN, int COUT, int H, int NP, int WM, int WN, bool CST, int WD = 3, int ABL = 0>
 __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_w1(const float* __restrict__ in, float* __restrict__ out,
                                                                 const uint4* __restrict__ wp,
                                                                 const float* __restrict__ bias, int P) {
-  using C = W1Cfg<CIN, COUT, H, NP, WM, WN, CST, PST>;
+  using C = W1Cfg<CIN, COUT, H, NP, WM, WN, CST>;
   constexpr int TR = C::TR;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -174,28 +167,6 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_w1(const float* __r
     const int q = i / (C::RS / 16), o = (i % (C::RS / 16)) * 16;
     *reinterpret_cast<uint4*>(smem + (q >> 1) * C::BUF + (q & 1) * C::PLANE + C::ZROW + o) = make_uint4(0, 0, 0, 0);
   }
-  char* const stg = C::STG_BUF ? buf1 : smem + C::STG_OFF;  // PST staging
-  auto stg_at = [](int p, int ch) { return p * C::ROWB + 16 * (ch ^ ((p >> 1) & 7)); };
-  // PST, producer side: the tile whose last stage was s, from the staging buffer to HBM as whole 256 / 512-byte
-  // pixel rows (16-byte chunks, consecutive lanes on consecutive chunks); stores past P are dropped by the
-  // resource bound
-  auto pstore = [&](int s) {
-    const int p0 = tile_of(s);
-    const int nval = P - p0 < NP ? P - p0 : NP;
-    const __amdgpu_buffer_rsrc_t ors = make_rsrc(out + (size_t)p0 * H * H * COUT, (unsigned)nval * H * H * COUT * 4);
-    constexpr int CPP = COUT / 4, OPT = C::OUTB / 16 / C::PTHR, G = 8;
-#pragma unroll
-    for (int k0 = 0; k0 < OPT; k0 += G) {
-      uint4 rv[G];
-#pragma unroll
-      for (int k = 0; k < G; ++k) {
-        const int c = ptid + (k0 + k) * C::PTHR, p = c / CPP;
-        rv[k] = *reinterpret_cast<const uint4*>(stg + stg_at(p, c % CPP));
-      }
-#pragma unroll
-      for (int k = 0; k < G; ++k) buf_store16(ors, rv[k], (unsigned)(ptid * 16), (unsigned)((k0 + k) * C::PTHR * 16));
-    }
-  };
   // the two roles split here and share no value: each matches the other's barriers one for one
   if (producer) {
     if constexpr ((ABL & 1) != 0) {  // timing only: idle producers
@@ -221,13 +192,6 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_w1(const float* __r
       // stage s + 2's loads are issued before stage s + 1 is written: two stages of MFMA work to land
 #pragma unroll 1
       for (int s = 0; s < NS; s += 2) {
-        if constexpr (PST) {
-          if (s > 0 && (s - 1) % C::NCC == C::NCC - 1) {  // the tile that ended at stage s - 1
-            __syncthreads();  // B_x: its outputs are staged
-            pstore(s - 1);
-            if constexpr (C::STG_BUF) __syncthreads();  // B_y: staging (buf1) read, stage s + 1 may go in
-          }
-        }
         produce_loads(s + 2, pf2);
         produce_write(buf1, pf);
         __syncthreads();
@@ -235,10 +199,6 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_w1(const float* __r
         produce_loads(s + 3, pf);
         produce_write(buf0, pf2);
         __syncthreads();
-      }
-      if constexpr (PST) {
-        __syncthreads();  // B_x of the last tile
-        pstore(NS - 1);
       }
     }
     return;
@@ -295,45 +255,10 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_w1(const float* __r
   uint4 bq[WD][C::NT][2];
 #pragma unroll
   for (int k = 0; k + 1 < WD; ++k) load_b(0, k, bq[k]);
-  // PST, MFMA side: bias + ReLU, this wave's part of the tile's outputs into the staging buffer; resets the
-  // accumulators
-  auto stage_out = [&]() {
-#pragma unroll
-    for (int nt = 0; nt < C::NT; ++nt) {
-      float4 bv[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        bv[q] = *reinterpret_cast<const float4*>(sbias + (wn * C::NT + nt) * 32 + 8 * q + 4 * h);
-#pragma unroll
-      for (int mt = 0; mt < C::MT; ++mt) {
-        const int m = (wm * C::MT + mt) * 32 + r;  // this lane's column pair
-        const int np = m / (TR * C::NTX), rem = m % (TR * C::NTX);
-        const int pb = np * H * H + (rem / C::NTX) * H + 2 * (rem % C::NTX);
-#pragma unroll
-        for (int par = 0; par < 2; ++par) {
-          const f32x16& yv = par ? y1a[mt][nt] : y0a[mt][nt];
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-            *reinterpret_cast<float4*>(stg + stg_at(pb + par, (wn * C::NT + nt) * 8 + 2 * q + h)) =
-                make_float4(fmaxf(yv[4 * q + 0] + bv[q].x, 0.f), fmaxf(yv[4 * q + 1] + bv[q].y, 0.f),
-                            fmaxf(yv[4 * q + 2] + bv[q].z, 0.f), fmaxf(yv[4 * q + 3] + bv[q].w, 0.f));
-        }
-        y0a[mt][nt] = y1a[mt][nt] = f32x16{};
-      }
-    }
-  };
 #pragma unroll 1
   for (int s = 0; s < NS; ++s) {
     const char* cur = (s & 1) ? buf1 : buf0;
     const int cc = s % C::NCC, ccn = (s + 1) % C::NCC;
-    // PST: the previous tile's outputs go to the staging buffer once every wave is past its last stage
-    const bool tile_start = PST && s > 0 && cc == 0;
-    if constexpr (PST) {
-      if (tile_start) {
-        stage_out();
-        __syncthreads();  // B_x
-      }
-    }
     uint4 aq[2][C::MT][2];
     auto load_a = [&](int kx, uint4 (&dst)[C::MT][2]) {
       const int xi = kx / 6, ky = (kx % 6) >> 1, ks = kx & 1;
@@ -354,8 +279,6 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_w1(const float* __r
         load_b(ccn, kx + WD - 1 - C::NKS, bq[(kx + WD - 1) % WD]);
       if (kx + 1 < C::NKS) load_a(kx + 1, aq[(kx + 1) & 1]);
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (C::STG_BUF)
-        if (kx == 0 && tile_start) __syncthreads();  // B_y: the producers have read the staging (buf1)
       const int xi = kx / 6;
       if (kx == 12) {  // m1 complete: out[2t] += m1, out[2t+1] += m1
 #pragma unroll
@@ -393,7 +316,7 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_w1(const float* __r
         y0a[mt][nt] += ma[mt][nt];
         y1a[mt][nt] -= ma[mt][nt];
       }
-    if (!PST && cc == C::NCC - 1) {
+    if (cc == C::NCC - 1) {
       const int p0 = tile_of(s);
 #pragma unroll
       for (int nt = 0; nt < C::NT; ++nt) {
@@ -445,23 +368,19 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_w1(const float* __r
     }
     __syncthreads();
   }
-  if constexpr (PST) {  // the last tile
-    stage_out();
-    __syncthreads();  // B_x
-  }
 }
 
-template <int CIN, int COUT, int H, int NP, int WM, int WN, bool CST, int WD, int ABL = 0, bool PST = false>
+template <int CIN, int COUT, int H, int NP, int WM, int WN, bool CST, int WD, int ABL = 0>
 hipError_t launch_w1(const float* in, float* out, const void* wp, const float* bias, int P, hipStream_t st) {
-  using C = W1Cfg<CIN, COUT, H, NP, WM, WN, CST, PST>;
-  const void* fn = reinterpret_cast<const void*>(&k_conv_w1<CIN, COUT, H, NP, WM, WN, CST, WD, ABL, PST>);
+  using C = W1Cfg<CIN, COUT, H, NP, WM, WN, CST>;
+  const void* fn = reinterpret_cast<const void*>(&k_conv_w1<CIN, COUT, H, NP, WM, WN, CST, WD, ABL>);
   int resident = 0;
   const hipError_t e = hn_resident_blocks(fn, C::NTHR, C::SMEM, &resident);
   if (e != hipSuccess) return e;
   const int tiles = (P + NP - 1) / NP;
   const int grid = std::min(tiles, resident);
   if (grid <= 0) return hipSuccess;
-  hipLaunchKernelGGL((k_conv_w1<CIN, COUT, H, NP, WM, WN, CST, WD, ABL, PST>), dim3(grid), dim3(C::NTHR), C::SMEM, st, in, out,
+  hipLaunchKernelGGL((k_conv_w1<CIN, COUT, H, NP, WM, WN, CST, WD, ABL>), dim3(grid), dim3(C::NTHR), C::SMEM, st, in, out,
                      static_cast<const uint4*>(wp), bias, P);
   return hipGetLastError();
 }
@@ -493,8 +412,6 @@ hipError_t hn_launch_wino1(int layer, int wd, const HardnetDev& d, const float* 
     if (wd == 4) return launch_w1<CI, CO, HH, NPP, WMM, WNN, true, 4>(in, out, d.wino1[L], d.bias[L], P, st); \
     if (wd == 6) return launch_w1<CI, CO, HH, NPP, WMM, WNN, true, 6>(in, out, d.wino1[L], d.bias[L], P, st); \
     if (wd == 8) return launch_w1<CI, CO, HH, NPP, WMM, WNN, true, 8>(in, out, d.wino1[L], d.bias[L], P, st); \
-    if (wd == 206) return launch_w1<CI, CO, HH, NPP, WMM, WNN, true, 6, 0, true>(in, out, d.wino1[L], d.bias[L], P, st); \
-    if (wd == 208) return launch_w1<CI, CO, HH, NPP, WMM, WNN, true, 8, 0, true>(in, out, d.wino1[L], d.bias[L], P, st); \
     HN_W1_ABL(CI, CO, HH, NPP, WMM, WNN, L)                                                                     \
   }
   HN_W1(3, 64, 64, 16, 1, 2, 2)
