@@ -87,6 +87,29 @@ def irf2_pairs(ops) -> set:
     return out
 
 
+def irf_skip_layers(ops) -> dict:
+    """{i: n}: the IRF layer i (16x16 stride 2, 32 -> 64, no SE, not in a k_irf2 pair) whose output goes
+    -- past identity skips -- into the 8x8 64 -> 128 stride-2 skip of layer n, both in one k_irf_skip
+    (hn_api.hip::forward_nas), unless HN_NO_IRFSKIP / HN_NO_SKIPFUSE / HN_NO_IRF."""
+    if any(os.environ.get(k, "0") not in ("", "0") for k in ("HN_NO_IRFSKIP", "HN_NO_SKIPFUSE", "HN_NO_IRF")):
+        return {}
+    ops = A.arch_ops(ops)
+    pairs = irf2_pairs(ops)
+    out = {}
+    for i in range(1, len(ops)):
+        spec, (ci, co, s) = A.OP_SPECS[ops[i]], A.SEARCH_SPACE2[i]
+        if (spec.kind == "skip" or spec.se or i in pairs or i - 1 in pairs or (ci, co, s) != (32, 64, 2)
+                or A.ir_mid(ci, spec.expansion) not in (32, 96, 128)):
+            continue
+        n = i + 1
+        while n < len(ops) and A.OP_SPECS[ops[n]].kind == "skip" and A.SEARCH_SPACE2[n][2] == 1 and \
+                A.SEARCH_SPACE2[n][0] == A.SEARCH_SPACE2[n][1]:
+            n += 1
+        if n < len(ops) and A.OP_SPECS[ops[n]].kind == "skip" and A.SEARCH_SPACE2[n] == (64, 128, 2):
+            out[i] = n
+    return out
+
+
 def nas_stage_bytes(ops) -> dict:
     """Algorithmic HBM bytes per patch of each NAS stage class, summed over its launches in
     one forward (fp32 NHWC in + out (+ residual read)), mirroring hn_api.hip::forward_nas
@@ -95,12 +118,21 @@ def nas_stage_bytes(ops) -> dict:
     front = os.environ.get("HN_NO_FRONT", "0") in ("", "0")
     irf = os.environ.get("HN_NO_IRF", "0") in ("", "0")
     out = {"stem": 0 if front else 4096 + 32 * 32 * 32 * 4, "front": 0, "irf": 0, "irf2": 0, "skip": 0, "pw": 0,
-           "dw": 0, "pwl": 0, "maxpool": 0, "se": 0, "head": 0}
+           "dw": 0, "pwl": 0, "maxpool": 0, "se": 0, "head": 0, "irf+skip": 0}
     pairs = irf2_pairs(ops)
+    fused_skip = irf_skip_layers(ops)
+    skipped = {n for n in fused_skip.values()}
     hw = 32
     for i, (op, (ci, co, s)) in enumerate(zip(A.arch_ops(ops), A.SEARCH_SPACE2)):
         spec = A.OP_SPECS[op]
         ho = hw // s
+        if i in fused_skip:  # k_irf_skip: the block's input in, the skip's 4x4x128 output out
+            out["irf+skip"] += 4 * ci * hw * hw + 4 * 128 * 4 * 4
+            hw = ho
+            continue
+        if i in skipped:
+            hw = ho
+            continue
         if i in pairs:  # k_irf2: this block's input in, the next block's output out
             _, co2, s2 = A.SEARCH_SPACE2[i + 1]
             out["irf2"] += 4 * ci * hw * hw + 4 * co2 * (hw // s2) ** 2
@@ -288,7 +320,7 @@ def cpu_baseline(name: str, model, seconds: float = 12.0, x_timed=None, y_timed=
 def nas_stage_flop(name: str) -> dict:
     """Algorithmic FLOP per patch of each NAS / FDL stage class (summed over its launches in one
     forward), mirroring hn_api.hip::forward_nas (fused front = stem + layer 0; "irf" = every
-    fused IRF block; "skip" = the fused maxpool + 1x1 ConvBNRelu; head = 4x4 conv)."""
+    fused IRF block; "skip" = the fused maxpool + 1x1 ConvBNRelu; "irf+skip" = k_irf_skip; head = 4x4 conv)."""
     if name in FDL_MODELS:
         v = FDL_MODELS[name]
         front = 9 * 32 * 32 * 32 + (32 * 32 * 16 * 16 + 32 * 64 * 64 if v == "NASNet" else 32 * 64 * 64)
@@ -298,12 +330,16 @@ def nas_stage_flop(name: str) -> dict:
             hw //= st
         return {"front": 2 * front, "irf": 2 * irf, "head": 2 * 128 * 128 * 16}
     ops = A.arch_ops(name)
-    out = {"front": 0, "irf": 0, "irf2": 0, "skip": 0, "head": 2 * A.SEARCH_SPACE2[-1][1] * 128 * 16}
+    out = {"front": 0, "irf": 0, "irf2": 0, "skip": 0, "irf+skip": 0, "head": 2 * A.SEARCH_SPACE2[-1][1] * 128 * 16}
     pairs = irf2_pairs(ops)
+    fused_skip = irf_skip_layers(ops)
+    skipped = set(fused_skip.values())
     hw = 32
     for i, (op, (ci, co, st)) in enumerate(zip(ops, A.SEARCH_SPACE2)):
         macs = A.layer_macs(ci, co, st, op, hw)
-        if i in pairs or i - 1 in pairs:
+        if i in fused_skip or i in skipped:
+            out["irf+skip"] += 2 * macs
+        elif i in pairs or i - 1 in pairs:
             out["irf2"] += 2 * macs
         elif i == 0:
             out["front"] += 2 * (9 * 32 * 32 * 32 + macs)

@@ -35,6 +35,7 @@ void hn_read_knobs(HnKnobs* k) {
   k->naive_pw = std::getenv("HN_NAIVE_PW") != nullptr;
   k->naive_dw = std::getenv("HN_NAIVE_DW") != nullptr;
   k->no_skipfuse = std::getenv("HN_NO_SKIPFUSE") != nullptr;
+  k->no_irfskip = std::getenv("HN_NO_IRFSKIP") != nullptr;
   k->pairdist_valu = std::getenv("HN_PAIRDIST_VALU") != nullptr;
   k->pairdist_reg = env_int("HN_PAIRDIST_REG", 0) != 0;
   k->front_fold = env_int("HN_FRONT_FOLD", 0) != 0;
@@ -1014,6 +1015,23 @@ static int forward_nas(hn_model* m, const float* in, int P, int pmax, float* out
         std::swap(x, y);
         ++li;
         continue;
+      }
+    }
+    if (L.irf_pwl_a && !L.se && !m->knobs.no_skipfuse && !m->knobs.no_irfskip &&
+        hn_irf_skip_supported(L.cin, L.cout, L.hin, L.stride, L.k, L.mid)) {
+      // the 8x8 stride-2 skip after this block (past identity skips) in the same kernel (k_irf_skip)
+      size_t ni = li + 1;
+      while (ni < m->layers.size() && m->layers[ni].skip && !m->layers[ni].skip_conv && m->layers[ni].stride == 1) ++ni;
+      if (ni < m->layers.size()) {
+        const NasLayer& N = m->layers[ni];
+        if (N.skip && N.skip_conv && N.stride == 2 && N.hin == L.hout && N.cin == L.cout && N.cout == 128) {
+          const HnIrfArgs ia{x, y, reinterpret_cast<const uint4*>(L.irf_pw_a), L.irf_pw_b, L.dw_w, L.dw_b,
+                             reinterpret_cast<const uint4*>(L.irf_pwl_a), L.pwl_b};
+          STAGE("irf+skip", hn_launch_irf_skip(ia, N.pw_w, N.pw_b, P, L.k, L.mid, st));
+          std::swap(x, y);
+          li = ni;
+          continue;
+        }
       }
     }
     if (L.irf_pwl_a) {

@@ -15,7 +15,8 @@ struct HnKnobs {
   bool fdl_valu = false;       // HN_FDL_VALU: FDLNet front as fp32 VALU
   bool naive_pw = false;       // HN_NAIVE_PW: untiled 1x1 conv kernel
   bool naive_dw = false;       // HN_NAIVE_DW: untiled depthwise kernel
-  bool no_skipfuse = false;    // HN_NO_SKIPFUSE: maxpool + pw instead of k_skip_s2
+  bool no_skipfuse = false;    // HN_NO_SKIPFUSE: maxpool + pw instead of k_skip_s2 (and no k_irf_skip)
+  bool no_irfskip = false;     // HN_NO_IRFSKIP: k_irf + k_skip_s2 instead of k_irf_skip
   bool pairdist_valu = false;  // HN_PAIRDIST_VALU: fp32 VALU pair-distance kernel
   bool pairdist_reg = false;   // HN_PAIRDIST_REG: register-staged positives instead of the LDS-DMA ring
   bool front_fold = false;     // HN_FRONT_FOLD: the NAS front's pwl with the LDS partial-sum fold
@@ -160,6 +161,11 @@ hipError_t hn_launch_irf2(const HnIrfArgs& a, const HnIrfArgs& b, int P, int ca,
                           int kb, int mb, hipStream_t st);
 hipError_t hn_launch_irf(const HnIrfArgs& a, int P, int cin, int cout, int hin, int s, int k, int mid,
                          hipStream_t st);
+// a 16x16 stride-2 32 -> 64 block and the 8x8 64 -> 128 stride-2 skip that follows it (after identity
+// skips) in one kernel (hn_irf.hip k_irf_skip); a.y receives the skip's [P,4,4,128] output
+bool hn_irf_skip_supported(int cin, int cout, int hin, int s, int k, int mid);
+hipError_t hn_launch_irf_skip(const HnIrfArgs& a, const float* skip_w, const float* skip_b, int P, int k, int mid,
+                              hipStream_t st);
 hipError_t hn_launch_preprocess(const uint8_t* in, int64_t n, int resize, int norm, float mean,
                                 float stdv, float* out, hipStream_t st);
 hipError_t hn_launch_fpr95(const float* a, const float* p, const int* labels, int64_t n, int dim,

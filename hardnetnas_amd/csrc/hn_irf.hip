@@ -455,6 +455,123 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
   }
 }
 
+// A 16x16 stride-2 block (32 -> 64, SEARCH_SPACE2 layer 2) followed -- after any identity skips -- by the
+// channel-changing stride-2 "skip" op at 8x8 (layer 4: MaxPool2d(3, 2, 1) then ConvBNRelu 1x1 64 -> 128,
+// fbnet_builder.py:202-228; wang3's layers 2-4, fbnet_modeldef.py:30-95): the block's 8x8x64 output
+// stays in LDS and the pooled 1x1 conv runs in the same workgroup, so the 16 KB / patch layer-2 output
+// never reaches HBM (write + read back by k_skip_s2).  The skip arithmetic is k_skip_s2's (hn_nas.hip)
+// step for step -- pooling max over the clamped 3x3 window, fp16 hi / lo split of the pooled value and of
+// the weights, the same 32x32x16 fp16x3 K-loop from the bias -- so the result is bit-identical to the
+// unfused pair (tests/test_gpu_parity.py).  One patch per workgroup (NPB = 1): wave w computes output
+// channels 32 w .. + 31 of the 16 pooled pixels (MFMA columns 16 .. 31 repeat them and are not stored).
+template <int K, int MID>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_irf_skip(
+    const float* __restrict__ x, float* __restrict__ y, HnIrfArgs A, const float* __restrict__ swt,  // [64][128]
+    const float* __restrict__ sbias,  // [128]
+    int P) {
+  constexpr int CIN = 32, COUT = 64, HIN = 16, S = 2;
+  using Sh = IrfShape<CIN, COUT, HIN, S, K, MID>;
+  constexpr int TI = Sh::TI, KS = Sh::KS, TW = Sh::TW, MODE = irf_mode<CIN, S>();
+  constexpr int SMEM = irf_smem_floats<CIN, COUT, HIN, S, K, MID>();
+  static_assert(Sh::NPB == 1 && TW == 1 && Sh::NOT == 2 && Sh::NCT == 2, "one 8x8x64 patch per workgroup");
+  constexpr int XS = COUT + 4;             // block output in LDS: [64 pixels][68 floats]
+  constexpr int SC = 128, SKS = COUT / 16;  // skip output channels, K-steps
+  constexpr int LY = 64 * XS, LB = SKS * 2 * 64 * 4, LO = 4 * 32 * 36;
+  static_assert(LY + LB + LO <= SMEM, "the skip's buffers fit in the block's LDS");
+  static_assert(3 * SMEM * 4 <= 160 * 1024, "three workgroups per CU");
+  __shared__ __attribute__((aligned(16))) float smem[SMEM];
+  const int tile = (int)blockIdx.x;  // = patch
+  if (tile >= P) return;             // workgroup-uniform
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, px = lane & 31, h = lane >> 5;
+  f32x16 acc[TW];
+  {
+    float4 pa[TI][KS], pb[TI][KS];
+    irf_load<CIN, COUT, HIN, S, K, MID>(&pa[0][0], &pb[0][0], x, tile, P);
+    uint4 bh[TI][KS], bl[TI][KS];
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int s = 0; s < KS; ++s) split8_f16(pa[i][s], pb[i][s], bh[i][s], bl[i][s]);
+    irf_core<CIN, COUT, HIN, S, K, MID, MODE>(bh, bl, acc, A.pw_a, A.pw_b, A.dw_w, A.dw_b, A.pwl_a, A.pwl_b, smem,
+                                             smem + Sh::LDS_PW, smem + Sh::LDS_PW + Sh::LDS_DW);
+  }
+  // the skip's weights (k_skip_s2's A operand: row = output channel 32 w + px, K-step ks = input channels
+  // 16 ks + 8 h + j) are loaded now, consumed after the pooling
+  float wv[SKS][8];
+#pragma unroll
+  for (int ks = 0; ks < SKS; ++ks)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) wv[ks][j] = swt[(16 * ks + 8 * h + j) * SC + 32 * w + px];
+  float* s_y = smem;
+  uint4* s_b = reinterpret_cast<uint4*>(smem + LY);  // [ks][plane][lane]
+  float* s_o = smem + LY + LB + w * 32 * 36;         // per-wave output staging
+  {  // block output tile (pixel tile pt, channel tile ct) -> s_y; lane (px, h): channels 8q + 4h .. + 3
+    const int pt = w % Sh::NOT, ct = w / Sh::NOT;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      *reinterpret_cast<float4*>(s_y + (pt * 32 + px) * XS + 32 * ct + 8 * q + 4 * h) =
+          make_float4(acc[0][4 * q], acc[0][4 * q + 1], acc[0][4 * q + 2], acc[0][4 * q + 3]);
+  }
+  __syncthreads();
+  {  // pool: thread = (pooled pixel o, channel quad c4); the padding row / column -1 is replaced by 0
+    const int o = t >> 4, c4 = t & 15, oy = o >> 2, ox = o & 3;
+    float4 m = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+      const int yy = max(2 * oy - 1 + ky, 0);
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        const int xx = max(2 * ox - 1 + kx, 0);
+        const float4 a = *reinterpret_cast<const float4*>(s_y + (yy * 8 + xx) * XS + 4 * c4);
+        m.x = fmaxf(m.x, a.x); m.y = fmaxf(m.y, a.y); m.z = fmaxf(m.z, a.z); m.w = fmaxf(m.w, a.w);
+      }
+    }
+    typedef _Float16 f16x4_t __attribute__((ext_vector_type(4)));
+    f16x4_t hi, lo;
+    hi[0] = (_Float16)m.x; lo[0] = (_Float16)(m.x - (float)hi[0]);
+    hi[1] = (_Float16)m.y; lo[1] = (_Float16)(m.y - (float)hi[1]);
+    hi[2] = (_Float16)m.z; lo[2] = (_Float16)(m.z - (float)hi[2]);
+    hi[3] = (_Float16)m.w; lo[3] = (_Float16)(m.w - (float)hi[3]);
+    const int ks = c4 >> 2, ln = ((c4 >> 1) & 1) * 32 + o, half = c4 & 1;
+#pragma unroll
+    for (int d = 0; d < 2; ++d) {  // MFMA columns o and o + 16 (the latter never stored)
+      reinterpret_cast<uint2*>(&s_b[(ks * 2 + 0) * 64 + ln + 16 * d])[half] = __builtin_bit_cast(uint2, hi);
+      reinterpret_cast<uint2*>(&s_b[(ks * 2 + 1) * 64 + ln + 16 * d])[half] = __builtin_bit_cast(uint2, lo);
+    }
+  }
+  f16x8 ah[SKS], al[SKS];
+#pragma unroll
+  for (int ks = 0; ks < SKS; ++ks)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      ah[ks][j] = (_Float16)wv[ks][j];
+      al[ks][j] = (_Float16)(wv[ks][j] - (float)ah[ks][j]);
+    }
+  f32x16 c;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float4 b = *reinterpret_cast<const float4*>(sbias + 32 * w + 8 * q + 4 * h);
+    c[4 * q] = b.x; c[4 * q + 1] = b.y; c[4 * q + 2] = b.z; c[4 * q + 3] = b.w;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int ks = 0; ks < SKS; ++ks)
+    c = mfma3_f16(ah[ks], al[ks], as_f16x8(s_b[(ks * 2) * 64 + lane]), as_f16x8(s_b[(ks * 2 + 1) * 64 + lane]), c);
+  // bias + ReLU -> per-wave staging -> 16 pixels x 128-byte rows of channels 32 w .. + 31
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    *reinterpret_cast<float4*>(s_o + px * 36 + 8 * q + 4 * h) =
+        make_float4(fmaxf(c[4 * q], 0.f), fmaxf(c[4 * q + 1], 0.f), fmaxf(c[4 * q + 2], 0.f), fmaxf(c[4 * q + 3], 0.f));
+  __builtin_amdgcn_wave_barrier();  // (one wave: its LDS accesses execute in order)
+  asm volatile("" ::: "memory");
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int pl = 8 * k + (lane >> 3), c4 = lane & 7;
+    *reinterpret_cast<float4*>(y + ((long)tile * 16 + pl) * SC + 32 * w + 4 * c4) =
+        *reinterpret_cast<const float4*>(s_o + pl * 36 + 4 * c4);
+  }
+}
+
 template <int CIN, int COUT, int HIN, int S, int K, int MID>
 hipError_t irf_launch(const HnIrfArgs& a, int P, hipStream_t st) {
   constexpr int NPB = IrfTile<CIN, HIN, MID>::NPB;
@@ -495,6 +612,24 @@ hipError_t hn_launch_irf2(const HnIrfArgs& a, const HnIrfArgs& b, int P, int ca,
     return irf2_launch<CA, HI, KA, MA, CB, KB, MB>(a, b, P, st);
   HN_IRF2_SHAPES(HN_IRF2_GO)
 #undef HN_IRF2_GO
+  return hipErrorInvalidValue;
+}
+
+// layer 2 (32 -> 64, 16x16, stride 2; e1 / e3 / e4, k3 / k5) + the 8x8 64 -> 128 skip (k_irf_skip)
+bool hn_irf_skip_supported(int cin, int cout, int hin, int s, int k, int mid) {
+  return cin == 32 && cout == 64 && hin == 16 && s == 2 && (k == 3 || k == 5) && (mid == 32 || mid == 96 || mid == 128);
+}
+
+hipError_t hn_launch_irf_skip(const HnIrfArgs& a, const float* skip_w, const float* skip_b, int P, int k, int mid,
+                              hipStream_t st) {
+  if (P <= 0) return hipSuccess;
+#define HN_IRFSK_GO(KK, MM)                                                                               \
+  if (k == KK && mid == MM) {                                                                             \
+    hipLaunchKernelGGL((k_irf_skip<KK, MM>), dim3(P), dim3(256), 0, st, a.x, a.y, a, skip_w, skip_b, P); \
+    return hipGetLastError();                                                                             \
+  }
+  HN_IRFSK_GO(3, 32) HN_IRFSK_GO(3, 96) HN_IRFSK_GO(3, 128) HN_IRFSK_GO(5, 32) HN_IRFSK_GO(5, 96) HN_IRFSK_GO(5, 128)
+#undef HN_IRFSK_GO
   return hipErrorInvalidValue;
 }
 

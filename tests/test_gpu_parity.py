@@ -574,7 +574,8 @@ def test_nas_fused_skip_s2_matches_unfused(name, cuda_device, monkeypatch):
     nm.set_profiling(True)
     y = nm(x).cpu().numpy()
     st = nm.stage_times()
-    assert "skip" in st and "maxpool" not in st
+    # (wang3's skip runs inside k_irf_skip with the layer-2 block, stage "irf+skip")
+    assert ("skip" in st or "irf+skip" in st) and "maxpool" not in st
     assert np.abs(y - fx["y"]).max() <= NAS_TOL
     monkeypatch.setenv("HN_NO_SKIPFUSE", "1")
     lw = NativeModel.from_module(m, cuda_device)
@@ -582,6 +583,40 @@ def test_nas_fused_skip_s2_matches_unfused(name, cuda_device, monkeypatch):
     for b in (1, 3, 37, 256):
         assert np.abs(lw(x[:b]).cpu().numpy() - y[:b]).max() <= NAS_TOL
     assert "maxpool" in lw.stage_times() and "skip" not in lw.stage_times()
+
+
+@pytest.mark.parametrize("op", ["ir_k3_e1", "ir_k3_e3", "ir_k3_s4", "ir_k5_e1", "ir_k5_e3", "ir_k5_s4", "ir_k5_s2",
+                                "wang3"])
+def test_irf_skip_kernel_is_bit_identical(op, cuda_device, monkeypatch):
+    """k_irf_skip: the 16x16 stride-2 block of layer 2 and the 8x8 64 -> 128 stride-2 skip after the
+    identity skip of layer 3 (wang3's layers 2-4) in one kernel, the block's output kept in LDS.  It
+    repeats k_skip_s2's arithmetic step for step, so its descriptors equal the two-kernel path
+    (HN_NO_IRFSKIP=1) bit for bit -- every MID (e1 / e3 / e4 + groups) and kernel size, ragged batches --
+    and match the reference restatement (wang3: the golden vectors)."""
+    from hardnetnas_amd import synth
+    from hardnetnas_amd._native import NativeModel
+    if op == "wang3":
+        m, fx, _ = build_module("wang3")
+        x = torch.from_numpy(golden_inputs(fx))
+        ref = fx["y"]
+    else:
+        ops = ["ir_k3_e1", "skip", op, "skip", "skip", "skip"]
+        m, p = _synth_nas(ops, seed=13)
+        x = torch.from_numpy(synth.synth_patches(301, seed=17))
+        ref = O.nas_forward(p, ops, x).numpy()
+    nm = NativeModel.from_module(m, cuda_device)
+    nm.set_profiling(True)
+    y = nm(x.to(cuda_device))
+    st = nm.stage_times()
+    assert "irf+skip" in st and "skip" not in st and "irf" not in st, st
+    assert np.abs(y.cpu().numpy() - ref).max() <= NAS_TOL
+    monkeypatch.setenv("HN_NO_IRFSKIP", "1")
+    n2 = NativeModel.from_module(m, cuda_device)
+    n2.set_profiling(True)
+    assert torch.equal(y, n2(x.to(cuda_device)))
+    assert "irf+skip" not in n2.stage_times() and "skip" in n2.stage_times()
+    for b in (1, 37):
+        assert torch.equal(nm(x[:b].to(cuda_device)), n2(x[:b].to(cuda_device)))
 
 
 @pytest.mark.parametrize("name", ["wang2", "wang3", "cov_a", "cov_b", "cov_c"])

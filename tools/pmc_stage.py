@@ -26,6 +26,8 @@ def stage(name: str):
         return "pairdist"
     if "k_irf2<" in name:
         return "irf2"
+    if "k_irf_skip<" in name:
+        return "irf+skip"
     if "k_skip_s2<" in name or "k_skip_s2(" in name:
         return "skip"
     if "k_fdl_front" in name:
