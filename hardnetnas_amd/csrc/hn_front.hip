@@ -63,7 +63,7 @@ __constant__ unsigned char kDwLane[64] = {
 // its 12 prefetched byte registers took the k3 front from three workgroups per CU to two, wang2
 // front 5.7 -> 7.2 ms, against 0.46 ms for the separate hn_preprocess.)
 template <int K, int MID, int MODE, bool NORM, bool NF, int U8 = -1, bool P5 = false, bool X3 = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRONT_IRF && K == 3 && MID == 32 && !X3 ? 3 : MODE == FRONT_IRF && MID == 32 ? 2 : 1))) void k_front(const void* __restrict__ in_,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRONT_IRF && K == 3 && MID == 32 ? 3 : MODE == FRONT_IRF && MID == 32 ? 2 : 1))) void k_front(const void* __restrict__ in_,
                                                float* __restrict__ out,
                                                const uint4* __restrict__ spack,  // stem A operand
                                                const float* __restrict__ stem_b,  // [32]
@@ -97,14 +97,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRO
   constexpr bool RING = MID == 32;
   constexpr bool SPLIT = MODE == FRONT_IRF;                  // even/odd column split
   constexpr int HALF = (PC + 1) / 2;                         // first odd-column position
-  constexpr int RS = SPLIT ? (PC * PS + 63) / 64 * 64 : PC * PS;  // row stride (floats)
+  // XCH (the k5 front, MID = 32): the dw runs per channel group with its weights in SGPRs and crosses to
+  // the pwl's operand layout through s_x (see the dw phase); s_dw is not used
+  // (X3, HN_FRONT_XCH3=1: the same for the k3 front)
+  constexpr bool XCH = NF && (PAIR5 || (X3 && K == 3 && MID == 32 && MODE == FRONT_IRF));
+  // SW (X3): 32-float pw pixels (no pad floats) with the 16-byte channel chunk c of ring position pos
+  // stored at c ^ swz(pos) -- the XCH dw reads and the pw epilogue writes stay conflict-free
+  // (tests/test_lds_banks.py::test_front_x3_swizzle_conflict_free) and the ring shrinks by 1/9, so
+  // the k3 XCH front fits three workgroups per CU (52 KB)
+  constexpr bool SW = XCH && K == 3;
+  constexpr int PSX = SW ? 32 : PS;
+  auto swz = [](int pos) { return SW ? (pos + 3 * (pos >> 1)) & 7 : 0; };
+  constexpr int RS = SPLIT ? (PC * PSX + 63) / 64 * 64 : PC * PSX;  // row stride (floats)
   static_assert(IR >= 8, "ring holds a band's 8 new rows");
   __shared__ float s_in[34 * 34];
   __shared__ __attribute__((aligned(16))) float s_pw[IR * RS];
-  // XCH (the k5 front, MID = 32): the dw runs per channel group with its weights in SGPRs and crosses to
-  // the pwl's operand layout through s_x (see the dw phase); s_dw is not used
-  // (X3, HN_FRONT_XCH3=1: the same for the k3 front, which then fits two workgroups per CU, not three)
-  constexpr bool XCH = NF && (PAIR5 || (X3 && K == 3 && MID == 32 && MODE == FRONT_IRF));
   __shared__ __attribute__((aligned(16))) float s_dw[XCH ? 4 : KK * KK * 32 + 32];
   __shared__ uint4 s_x[XCH ? 2 * 4 * 16 * 4 : 1];  // [hi / lo][band row][column][16-byte chunk]
   __shared__ float red[8];
@@ -133,9 +140,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRO
   auto colpos = [](int c) { return SPLIT ? ((c & 1) ? HALF + (c >> 1) : c >> 1) : c; };
   // ---- one-time init: zero s_in (its frame stays zero) and the pw pad columns ---------------
   for (int i = t; i < 34 * 34; i += 256) s_in[i] = 0.f;
-  for (int i = t; i < IR * 2 * PAD * (PS / 4); i += 256) {  // left/right pad columns
-    const int ri = i / (2 * PAD * (PS / 4)), rem = i % (2 * PAD * (PS / 4)), c = rem / (PS / 4);
-    reinterpret_cast<float4*>(s_pw)[(ri * RS + colpos(c < PAD ? c : 32 + c) * PS) / 4 + rem % (PS / 4)] =
+  for (int i = t; i < IR * 2 * PAD * (PSX / 4); i += 256) {  // left/right pad columns
+    const int ri = i / (2 * PAD * (PSX / 4)), rem = i % (2 * PAD * (PSX / 4)), c = rem / (PSX / 4);
+    reinterpret_cast<float4*>(s_pw)[(ri * RS + colpos(c < PAD ? c : 32 + c) * PSX) / 4 + rem % (PSX / 4)] =
         make_float4(0.f, 0.f, 0.f, 0.f);
   }
   const f16x8 sah = as_f16x8(spack[lane]), sal = as_f16x8(spack[64 + lane]);
@@ -418,10 +425,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRO
           if constexpr (LDSB) bias = bias16(s_pwb);
           f32x16 acc = mfma3_f16(ah0, al0, as_f16x8(bh[i][0]), as_f16x8(bl[i][0]), bias);
           acc = mfma3_f16(ah1, al1, as_f16x8(bh[i][1]), as_f16x8(bl[i][1]), acc);
-          float4* d = reinterpret_cast<float4*>(s_pw + slot_of(y) * RS + colpos(PAD + pxm) * PS);
+          const int pos = colpos(PAD + pxm);
+          float4* d = reinterpret_cast<float4*>(s_pw + slot_of(y) * RS + pos * PSX);
 #pragma unroll
           for (int q = 0; q < 4; ++q)
-            d[2 * q + h] = make_float4(fmaxf(acc[4 * q], 0.f), fmaxf(acc[4 * q + 1], 0.f),
+            d[(2 * q + h) ^ swz(pos)] = make_float4(fmaxf(acc[4 * q], 0.f), fmaxf(acc[4 * q + 1], 0.f),
                                        fmaxf(acc[4 * q + 2], 0.f), fmaxf(acc[4 * q + 3], 0.f));
         }
         __syncthreads();
@@ -439,13 +447,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRO
             f32x4 a1 = *reinterpret_cast<const f32x4*>(dw_b + 32 * m + c0 + 4);
 #pragma unroll DYU
             for (int dy = 0; dy < KK; ++dy) {
-              const float* rp = s_pw + slot_of(2 * (r0 + rr) - PAD + dy) * RS + c0;
+              const float* rp = s_pw + slot_of(2 * (r0 + rr) - PAD + dy) * RS;
 #pragma unroll
               for (int dx = 0; dx < KK; ++dx) {
                 const float* wp = wsrc + (dy * KK + dx) * MID;
-                const float* ip = rp + ((dx & 1) ? HALF + ox + (dx >> 1) : ox + (dx >> 1)) * PS;
-                a0 = __builtin_elementwise_fma(*reinterpret_cast<const f32x4*>(wp), *reinterpret_cast<const f32x4*>(ip), a0);
-                a1 = __builtin_elementwise_fma(*reinterpret_cast<const f32x4*>(wp + 4), *reinterpret_cast<const f32x4*>(ip + 4), a1);
+                const int pos = (dx & 1) ? HALF + ox + (dx >> 1) : ox + (dx >> 1);
+                const float* ip = rp + pos * PSX;
+                const int sz = swz(pos);
+                a0 = __builtin_elementwise_fma(*reinterpret_cast<const f32x4*>(wp),
+                                               *reinterpret_cast<const f32x4*>(ip + 4 * ((2 * cg) ^ sz)), a0);
+                a1 = __builtin_elementwise_fma(*reinterpret_cast<const f32x4*>(wp + 4),
+                                               *reinterpret_cast<const f32x4*>(ip + 4 * ((2 * cg + 1) ^ sz)), a1);
               }
             }
             a0 = __builtin_elementwise_max(a0, f32x4{});

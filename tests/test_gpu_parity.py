@@ -619,6 +619,25 @@ def test_irf_skip_kernel_is_bit_identical(op, cuda_device, monkeypatch):
         assert torch.equal(nm(x[:b].to(cuda_device)), n2(x[:b].to(cuda_device)))
 
 
+@pytest.mark.parametrize("name", ["wang2", "cov_c"])
+def test_front_k3_xch_form_is_bit_identical(name, cuda_device, monkeypatch):
+    """The k3 MID-32 front in the XCH form (HN_FRONT_XCH3=1: dw per channel group with SGPR weights,
+    results crossed to the pwl layout through s_x, 32-float ring pixels with the swizzled chunks) runs
+    the same fp32 FMAs in the same order as the default form: bit-identical descriptors (wang2's k3
+    front; cov_c's layer 0 is a k5 front, so there the knob changes nothing), ragged batches included."""
+    from hardnetnas_amd._native import NativeModel
+    m, fx, _ = build_module(name)
+    x = torch.from_numpy(golden_inputs(fx)).to(cuda_device)
+    nm = NativeModel.from_module(m, cuda_device)
+    y = nm(x)
+    monkeypatch.setenv("HN_FRONT_XCH3", "1")
+    n3 = NativeModel.from_module(m, cuda_device)
+    assert torch.equal(y, n3(x))
+    for b in (1, 37):
+        assert torch.equal(nm(x[:b]), n3(x[:b]))
+    assert np.abs(y.cpu().numpy() - fx["y"]).max() <= NAS_TOL
+
+
 @pytest.mark.parametrize("name", ["wang2", "wang3", "cov_a", "cov_b", "cov_c"])
 def test_front_pwl_forms_match_reference(name, cuda_device, monkeypatch):
     """The NAS front's two pwl forms -- the default 16x16x32 one (wave = band row, no partial-sum

@@ -259,6 +259,40 @@ def test_front_xch_accesses_conflict_free():
             assert len(slots) == 16, (w, g[0])
 
 
+def test_front_x3_swizzle_conflict_free():
+    """k3 front XCH form (HN_FRONT_XCH3, SW in hn_front.hip): ring pixels of 32 floats, 16-byte channel
+    chunk c of position pos at c ^ swz(pos), swz(pos) = (pos + 3 (pos >> 1)) & 7.  The dw reads (lane
+    (row l >> 4, column l & 15), chunks 2 w, 2 w + 1 at position pos(column, dx)) hit 16 distinct slots
+    per ds_read_b128 group and the pw epilogue writes (lane (n, h): chunk 2 q + h of image column pxm[n])
+    8 distinct slots per 8-lane ds_write_b128 group; without the swizzle both conflict."""
+    kk, pad, ps = 3, 1, 32
+    pc = 32 + 2 * pad
+    half, rs = (pc + 1) // 2, pc * ps
+    assert rs % 64 == 0  # the rows a read group mixes share one slot pattern
+    pxm, _ = _front_nf_maps(pad)
+    for swz, want in ((lambda p: (p + 3 * (p >> 1)) & 7, True), (lambda p: 0, False)):
+        ok = True
+        for w in range(4):
+            for dx in range(kk):
+                for j in range(2):
+                    for g in GROUPS:
+                        slots = set()
+                        for lane in g:
+                            ox = lane & 15
+                            pos = half + ox + (dx >> 1) if dx & 1 else ox + (dx >> 1)
+                            slots.add(((pos * ps + 4 * ((2 * w + j) ^ swz(pos))) * 4 // 16) % 16)
+                        ok &= len(slots) == 16
+        for q in range(4):
+            for g0 in range(0, 64, 8):
+                slots = set()
+                for lane in range(g0, g0 + 8):
+                    c = pad + pxm[lane & 31]
+                    pos = half + c // 2 if c & 1 else c // 2
+                    slots.add(((pos * ps + 4 * ((2 * q + (lane >> 5)) ^ swz(pos))) * 4 // 16) % 8)
+                ok &= len(slots) == 8
+        assert ok == want
+
+
 @pytest.mark.parametrize("kk", [3, 5])
 def test_front_irf_fold_positions_are_interior(kk):
     """The pwl partial-sum fold uses the 16 interior even positions from 1 and the 16 interior
