@@ -89,7 +89,7 @@ __global__ __launch_bounds__(256) void k_fdl_front(const float* __restrict__ in,
       float acc = b1[co];
 #pragma unroll
       for (int ci = 0; ci < 32; ++ci) acc = fmaf(w1[ci * 32 + co], s[ci], acc);
-      h[co] = fmaxf(acc, 0.f);
+      h[co] = relu0(acc);
     }
   } else {
 #pragma unroll
@@ -119,7 +119,7 @@ __global__ __launch_bounds__(256) void k_fdl_front(const float* __restrict__ in,
       float acc = b2[co];
 #pragma unroll
       for (int ci = 0; ci < 32; ++ci) acc = fmaf(w2[ci * 64 + co], h[ci], acc);
-      r[j] = fmaxf(acc, 0.f);
+      r[j] = relu0(acc);
     }
     reinterpret_cast<float4*>(dst)[c4] = make_float4(r[0], r[1], r[2], r[3]);
   }
@@ -286,7 +286,7 @@ __global__ __launch_bounds__(256) void k_fdl_front_mfma(const void* __restrict__
           c = mfma3_f16(ah1[ks], al1[ks], bh, bl, c);
         }
 #pragma unroll
-        for (int i = 0; i < 16; ++i) c[i] = fmaxf(c[i], 0.f);
+        for (int i = 0; i < 16; ++i) c[i] = relu0(c[i]);
         hmid[tt] = c;
       } else {
         f32x16 m;
@@ -319,15 +319,15 @@ __global__ __launch_bounds__(256) void k_fdl_front_mfma(const void* __restrict__
 #pragma unroll
           for (int qq = 0; qq < 4; ++qq)
             *reinterpret_cast<float4*>(dst + 8 * qq) =
-                make_float4(fmaxf(c[4 * qq], 0.f), fmaxf(c[4 * qq + 1], 0.f), fmaxf(c[4 * qq + 2], 0.f),
-                            fmaxf(c[4 * qq + 3], 0.f));
+                make_float4(relu0(c[4 * qq]), relu0(c[4 * qq + 1]), relu0(c[4 * qq + 2]),
+                            relu0(c[4 * qq + 3]));
           continue;
         }
 #pragma unroll
         for (int qq = 0; qq < 4; ++qq)
           *reinterpret_cast<float4*>(so + r * 36 + 8 * qq + 4 * h) =
-              make_float4(fmaxf(c[4 * qq], 0.f), fmaxf(c[4 * qq + 1], 0.f), fmaxf(c[4 * qq + 2], 0.f),
-                          fmaxf(c[4 * qq + 3], 0.f));
+              make_float4(relu0(c[4 * qq]), relu0(c[4 * qq + 1]), relu0(c[4 * qq + 2]),
+                          relu0(c[4 * qq + 3]));
         __builtin_amdgcn_wave_barrier();  // (one wave: its LDS accesses execute in order)
         asm volatile("" ::: "memory");
         float* dst = out + (p * 64 + 32 * tt) * 64 + 32 * nt;

@@ -327,8 +327,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRO
           float4 o[4];
 #pragma unroll
           for (int q = 0; q < 4; ++q)
-            o[q] = make_float4(fmaxf(c[4 * q], 0.f), fmaxf(c[4 * q + 1], 0.f), fmaxf(c[4 * q + 2], 0.f),
-                               fmaxf(c[4 * q + 3], 0.f));
+            o[q] = make_float4(relu0(c[4 * q]), relu0(c[4 * q + 1]), relu0(c[4 * q + 2]),
+                               relu0(c[4 * q + 3]));
           split8_f16(o[0], o[1], bh[i][0], bl[i][0]);
           split8_f16(o[2], o[3], bh[i][1], bl[i][1]);
         }
@@ -353,8 +353,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRO
         float4 o[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-          o[q] = make_float4(fmaxf(c[4 * q], 0.f), fmaxf(c[4 * q + 1], 0.f), fmaxf(c[4 * q + 2], 0.f),
-                             fmaxf(c[4 * q + 3], 0.f));
+          o[q] = make_float4(relu0(c[4 * q]), relu0(c[4 * q + 1]), relu0(c[4 * q + 2]),
+                             relu0(c[4 * q + 3]));
         if (MODE == FRONT_MAXPOOL) {
           float4* d = reinterpret_cast<float4*>(s_pw + slot_of(y) * RS + colpos(PAD + px) * PS);
 #pragma unroll
@@ -429,8 +429,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRO
           float4* d = reinterpret_cast<float4*>(s_pw + slot_of(y) * RS + pos * PSX);
 #pragma unroll
           for (int q = 0; q < 4; ++q)
-            d[(2 * q + h) ^ swz(pos)] = make_float4(fmaxf(acc[4 * q], 0.f), fmaxf(acc[4 * q + 1], 0.f),
-                                       fmaxf(acc[4 * q + 2], 0.f), fmaxf(acc[4 * q + 3], 0.f));
+            d[(2 * q + h) ^ swz(pos)] = make_float4(relu0(acc[4 * q]), relu0(acc[4 * q + 1]),
+                                       relu0(acc[4 * q + 2]), relu0(acc[4 * q + 3]));
         }
         __syncthreads();
         if constexpr (NF) {
@@ -460,8 +460,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRO
                                                *reinterpret_cast<const f32x4*>(ip + 4 * ((2 * cg + 1) ^ sz)), a1);
               }
             }
-            a0 = __builtin_elementwise_max(a0, f32x4{});
-            a1 = __builtin_elementwise_max(a1, f32x4{});
+            a0 = relu4(a0);
+            a1 = relu4(a1);
             split8_f16(make_float4(a0.x, a0.y, a0.z, a0.w), make_float4(a1.x, a1.y, a1.z, a1.w), xh, xl);
             const int wc = cg ^ ((ox >> 1) & 3);
             s_x[((0 * 4 + rr) * 16 + ox) * 4 + wc] = xh;
@@ -485,8 +485,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRO
                 a1 = __builtin_elementwise_fma(*reinterpret_cast<const f32x4*>(wp + 4), *reinterpret_cast<const f32x4*>(ip + 4), a1);
               }
             }
-            a0 = __builtin_elementwise_max(a0, f32x4{});
-            a1 = __builtin_elementwise_max(a1, f32x4{});
+            a0 = relu4(a0);
+            a1 = relu4(a1);
             split8_f16(make_float4(a0.x, a0.y, a0.z, a0.w), make_float4(a1.x, a1.y, a1.z, a1.w), xh, xl);
           }
           const uint4* lp = pwl_a16 + (size_t)m * 4 * 64 + lane;
@@ -519,8 +519,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRO
               a1 = __builtin_elementwise_fma(*reinterpret_cast<const f32x4*>(wp + 4), *reinterpret_cast<const f32x4*>(ip + 4), a1);
             }
           }
-          a0 = __builtin_elementwise_max(a0, f32x4{});
-          a1 = __builtin_elementwise_max(a1, f32x4{});
+          a0 = relu4(a0);
+          a1 = relu4(a1);
           uint4 xh, xl;
           split8_f16(make_float4(a0.x, a0.y, a0.z, a0.w), make_float4(a1.x, a1.y, a1.z, a1.w), xh, xl);
           const uint4* lp = pwl_a + ((size_t)(2 * m + (w >> 1)) * 2) * 64 + lane;

@@ -161,8 +161,8 @@ HN_DEV void irf_core(const uint4 (&bh)[IrfShape<CIN, COUT, HIN, S, K, MID>::TI][
         float4* d = reinterpret_cast<float4*>(s_pw + ((4 * i + w) * 32 + px) * PS);
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-          d[2 * q + h] = make_float4(fmaxf(c[i][4 * q], 0.f), fmaxf(c[i][4 * q + 1], 0.f),
-                                     fmaxf(c[i][4 * q + 2], 0.f), fmaxf(c[i][4 * q + 3], 0.f));
+          d[2 * q + h] = make_float4(relu0(c[i][4 * q]), relu0(c[i][4 * q + 1]),
+                                     relu0(c[i][4 * q + 2]), relu0(c[i][4 * q + 3]));
       }
     }
     if constexpr (RING)
@@ -201,7 +201,7 @@ HN_DEV void irf_core(const uint4 (&bh)[IrfShape<CIN, COUT, HIN, S, K, MID>::TI][
       }
 #pragma unroll
       for (int r = 0; r < R; ++r) {
-        const f32x4 v = __builtin_elementwise_max(o[r], f32x4{});
+        const f32x4 v = relu4(o[r]);
         if constexpr (BAND) {
           const int p = (o0 + r) & 127;  // band pixel
           *reinterpret_cast<f32x4*>(s_dw + p * 32 + 4 * (q ^ band_sw(p))) = v;
@@ -561,7 +561,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
 #pragma unroll
   for (int q = 0; q < 4; ++q)
     *reinterpret_cast<float4*>(s_o + px * 36 + 8 * q + 4 * h) =
-        make_float4(fmaxf(c[4 * q], 0.f), fmaxf(c[4 * q + 1], 0.f), fmaxf(c[4 * q + 2], 0.f), fmaxf(c[4 * q + 3], 0.f));
+        make_float4(relu0(c[4 * q]), relu0(c[4 * q + 1]), relu0(c[4 * q + 2]), relu0(c[4 * q + 3]));
   __builtin_amdgcn_wave_barrier();  // (one wave: its LDS accesses execute in order)
   asm volatile("" ::: "memory");
 #pragma unroll

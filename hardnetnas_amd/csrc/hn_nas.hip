@@ -42,8 +42,8 @@ __global__ __launch_bounds__(256) void k_pw(const float* __restrict__ in, float*
     }
   }
   if (relu) {
-    acc.x = fmaxf(acc.x, 0.f); acc.y = fmaxf(acc.y, 0.f);
-    acc.z = fmaxf(acc.z, 0.f); acc.w = fmaxf(acc.w, 0.f);
+    acc.x = relu0(acc.x); acc.y = relu0(acc.y);
+    acc.z = relu0(acc.z); acc.w = relu0(acc.w);
   }
   if (res) {
     const float4 rv = *reinterpret_cast<const float4*>(res + pix * cout + n);
@@ -128,7 +128,7 @@ __global__ __launch_bounds__(256) void k_pw_tiled(const float* __restrict__ in, 
     const int n = g * ng + nl;
     float4 v = make_float4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]);
     if (relu) {
-      v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+      v.x = relu0(v.x); v.y = relu0(v.y); v.z = relu0(v.z); v.w = relu0(v.w);
     }
     if (res) {
       const float4 rv = *reinterpret_cast<const float4*>(res + px * cout + n);
@@ -195,8 +195,8 @@ __global__ __launch_bounds__(256) void k_dw(const float* __restrict__ in, float*
       acc.w = fmaf(v.w, w.w, acc.w);
     }
   }
-  acc.x = fmaxf(acc.x, 0.f); acc.y = fmaxf(acc.y, 0.f);
-  acc.z = fmaxf(acc.z, 0.f); acc.w = fmaxf(acc.w, 0.f);
+  acc.x = relu0(acc.x); acc.y = relu0(acc.y);
+  acc.z = relu0(acc.z); acc.w = relu0(acc.w);
   *reinterpret_cast<float4*>(out + (((p * hout) + yo) * (long)hout + xo) * c + c4) = acc;
 }
 
@@ -254,8 +254,8 @@ __global__ __launch_bounds__(256) void k_dw_lds(const float* __restrict__ in, fl
         acc.z = fmaf(v.z, w.z, acc.z);
         acc.w = fmaf(v.w, w.w, acc.w);
       }
-    acc.x = fmaxf(acc.x, 0.f); acc.y = fmaxf(acc.y, 0.f);
-    acc.z = fmaxf(acc.z, 0.f); acc.w = fmaxf(acc.w, 0.f);
+    acc.x = relu0(acc.x); acc.y = relu0(acc.y);
+    acc.z = relu0(acc.z); acc.w = relu0(acc.w);
     *reinterpret_cast<float4*>(out + ((p * HOUT + y0 + yo) * (long)HOUT + xo) * c + cg * 32 + q * 4) = acc;
   }
 }
@@ -374,8 +374,8 @@ __global__ __launch_bounds__(256) void k_skip_s2(const float* __restrict__ in, f
 #pragma unroll
     for (int q = 0; q < 4; ++q)
       *reinterpret_cast<float4*>(so + r * 36 + 8 * q + 4 * h) =
-          make_float4(fmaxf(c[4 * q], 0.f), fmaxf(c[4 * q + 1], 0.f), fmaxf(c[4 * q + 2], 0.f),
-                      fmaxf(c[4 * q + 3], 0.f));
+          make_float4(relu0(c[4 * q]), relu0(c[4 * q + 1]), relu0(c[4 * q + 2]),
+                      relu0(c[4 * q + 3]));
     __builtin_amdgcn_wave_barrier();  // (one wave: its LDS accesses execute in order)
     asm volatile("" ::: "memory");
 #pragma unroll
@@ -408,7 +408,7 @@ __global__ __launch_bounds__(256) void k_se(float* __restrict__ y, const float* 
   if (t < mid) {
     float s = b1[t];
     for (int k = 0; k < c; ++k) s = fmaf(w1[t * c + k], avg[k], s);
-    s1[t] = fmaxf(s, 0.f);
+    s1[t] = relu0(s);
   }
   __syncthreads();
   if (t < c) {

@@ -337,8 +337,8 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_w1(const float* __r
               float4 v[4];
 #pragma unroll
               for (int q = 0; q < 4; ++q)
-                v[q] = make_float4(fmaxf(yv[4 * q + 0] + bv[q].x, 0.f), fmaxf(yv[4 * q + 1] + bv[q].y, 0.f),
-                                   fmaxf(yv[4 * q + 2] + bv[q].z, 0.f), fmaxf(yv[4 * q + 3] + bv[q].w, 0.f));
+                v[q] = make_float4(relu0(yv[4 * q + 0] + bv[q].x), relu0(yv[4 * q + 1] + bv[q].y),
+                                   relu0(yv[4 * q + 2] + bv[q].z), relu0(yv[4 * q + 3] + bv[q].w));
               if constexpr (CST) {
                 float* scr = reinterpret_cast<float*>(smem + C::SCR_OFF) + wave * (C::SCR / 4);
 #pragma unroll
