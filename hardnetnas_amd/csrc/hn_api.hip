@@ -128,6 +128,7 @@ struct NasLayer {
   uint16_t* front_pwl16 = nullptr;  // fused front: pwl as 16x16x32 A operands
   float* front_b = nullptr;
   uint16_t *irf_pw_a = nullptr, *irf_pwl_a = nullptr;  // fused IRF block (layers >= 1)
+  uint16_t* skip_a = nullptr;  // the 64 -> 128 skip's 1x1 weights as 32x32x16 fp16 hi / lo A fragments (k_irf_skip)
   float* irf_pw_b = nullptr;
 };
 
@@ -711,6 +712,9 @@ static int build_nas_layers(hn_model* m, Cursor& cur, int hw, size_t maxf) {
         if ((rc = take_cbr(m, cur, L.cout, L.cin, &f))) return rc;
         if ((rc = m->upload(transpose_pw(f.w, L.cout, L.cin), &L.pw_w))) return rc;
         if ((rc = m->upload(f.b, &L.pw_b))) return rc;
+        if (L.cin == 64 && L.cout == 128 &&
+            (rc = m->upload(pack_1x1_a(f.w, L.cout, L.cin, 1, [](int c) { return c; }), &L.skip_a)))
+          return rc;
       }
       maxf = std::max(maxf, (size_t)L.cin * L.hout * L.hout);
       maxf = std::max(maxf, (size_t)L.cout * L.hout * L.hout);
@@ -1024,10 +1028,10 @@ static int forward_nas(hn_model* m, const float* in, int P, int pmax, float* out
       while (ni < m->layers.size() && m->layers[ni].skip && !m->layers[ni].skip_conv && m->layers[ni].stride == 1) ++ni;
       if (ni < m->layers.size()) {
         const NasLayer& N = m->layers[ni];
-        if (N.skip && N.skip_conv && N.stride == 2 && N.hin == L.hout && N.cin == L.cout && N.cout == 128) {
+        if (N.skip && N.skip_conv && N.stride == 2 && N.hin == L.hout && N.cin == L.cout && N.cout == 128 && N.skip_a) {
           const HnIrfArgs ia{x, y, reinterpret_cast<const uint4*>(L.irf_pw_a), L.irf_pw_b, L.dw_w, L.dw_b,
                              reinterpret_cast<const uint4*>(L.irf_pwl_a), L.pwl_b};
-          STAGE("irf+skip", hn_launch_irf_skip(ia, N.pw_w, N.pw_b, P, L.k, L.mid, st));
+          STAGE("irf+skip", hn_launch_irf_skip(ia, reinterpret_cast<const uint4*>(N.skip_a), N.pw_b, P, L.k, L.mid, st));
           std::swap(x, y);
           li = ni;
           continue;

@@ -164,7 +164,7 @@ hipError_t hn_launch_irf(const HnIrfArgs& a, int P, int cin, int cout, int hin, 
 // a 16x16 stride-2 32 -> 64 block and the 8x8 64 -> 128 stride-2 skip that follows it (after identity
 // skips) in one kernel (hn_irf.hip k_irf_skip); a.y receives the skip's [P,4,4,128] output
 bool hn_irf_skip_supported(int cin, int cout, int hin, int s, int k, int mid);
-hipError_t hn_launch_irf_skip(const HnIrfArgs& a, const float* skip_w, const float* skip_b, int P, int k, int mid,
+hipError_t hn_launch_irf_skip(const HnIrfArgs& a, const uint4* skip_a, const float* skip_b, int P, int k, int mid,
                               hipStream_t st);
 hipError_t hn_launch_preprocess(const uint8_t* in, int64_t n, int resize, int norm, float mean,
                                 float stdv, float* out, hipStream_t st);

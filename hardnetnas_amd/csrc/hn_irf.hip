@@ -466,7 +466,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
 // channels 32 w .. + 31 of the 16 pooled pixels (MFMA columns 16 .. 31 repeat them and are not stored).
 template <int K, int MID>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_irf_skip(
-    const float* __restrict__ x, float* __restrict__ y, HnIrfArgs A, const float* __restrict__ swt,  // [64][128]
+    const float* __restrict__ x, float* __restrict__ y, HnIrfArgs A,
+    const uint4* __restrict__ sa,     // [128/32][64/16][plane 2][lane 64] x 8 fp16 (pack_1x1_a)
     const float* __restrict__ sbias,  // [128]
     int P) {
   constexpr int CIN = 32, COUT = 64, HIN = 16, S = 2;
@@ -495,13 +496,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
     irf_core<CIN, COUT, HIN, S, K, MID, MODE>(bh, bl, acc, A.pw_a, A.pw_b, A.dw_w, A.dw_b, A.pwl_a, A.pwl_b, smem,
                                              smem + Sh::LDS_PW, smem + Sh::LDS_PW + Sh::LDS_DW);
   }
-  // the skip's weights (k_skip_s2's A operand: row = output channel 32 w + px, K-step ks = input channels
-  // 16 ks + 8 h + j) are loaded now, consumed after the pooling
-  float wv[SKS][8];
+  // the skip's weights (k_skip_s2's A operand, split on the host the way k_skip_s2 splits it: row = output
+  // channel 32 w + px, K-step ks = input channels 16 ks + 8 h + j) are loaded now, consumed after the pooling
+  uint4 wa[SKS][2];
 #pragma unroll
-  for (int ks = 0; ks < SKS; ++ks)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) wv[ks][j] = swt[(16 * ks + 8 * h + j) * SC + 32 * w + px];
+  for (int ks = 0; ks < SKS; ++ks) {
+    wa[ks][0] = sa[((w * SKS + ks) * 2) * 64 + lane];
+    wa[ks][1] = sa[((w * SKS + ks) * 2 + 1) * 64 + lane];
+  }
   float* s_y = smem;
   uint4* s_b = reinterpret_cast<uint4*>(smem + LY);  // [ks][plane][lane]
   float* s_o = smem + LY + LB + w * 32 * 36;         // per-wave output staging
@@ -539,14 +541,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
       reinterpret_cast<uint2*>(&s_b[(ks * 2 + 1) * 64 + ln + 16 * d])[half] = __builtin_bit_cast(uint2, lo);
     }
   }
-  f16x8 ah[SKS], al[SKS];
-#pragma unroll
-  for (int ks = 0; ks < SKS; ++ks)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      ah[ks][j] = (_Float16)wv[ks][j];
-      al[ks][j] = (_Float16)(wv[ks][j] - (float)ah[ks][j]);
-    }
   f32x16 c;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -556,7 +550,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
   __syncthreads();
 #pragma unroll
   for (int ks = 0; ks < SKS; ++ks)
-    c = mfma3_f16(ah[ks], al[ks], as_f16x8(s_b[(ks * 2) * 64 + lane]), as_f16x8(s_b[(ks * 2 + 1) * 64 + lane]), c);
+    c = mfma3_f16(as_f16x8(wa[ks][0]), as_f16x8(wa[ks][1]), as_f16x8(s_b[(ks * 2) * 64 + lane]),
+                  as_f16x8(s_b[(ks * 2 + 1) * 64 + lane]), c);
   // bias + ReLU -> per-wave staging -> 16 pixels x 128-byte rows of channels 32 w .. + 31
 #pragma unroll
   for (int q = 0; q < 4; ++q)
@@ -620,12 +615,12 @@ bool hn_irf_skip_supported(int cin, int cout, int hin, int s, int k, int mid) {
   return cin == 32 && cout == 64 && hin == 16 && s == 2 && (k == 3 || k == 5) && (mid == 32 || mid == 96 || mid == 128);
 }
 
-hipError_t hn_launch_irf_skip(const HnIrfArgs& a, const float* skip_w, const float* skip_b, int P, int k, int mid,
+hipError_t hn_launch_irf_skip(const HnIrfArgs& a, const uint4* skip_a, const float* skip_b, int P, int k, int mid,
                               hipStream_t st) {
   if (P <= 0) return hipSuccess;
 #define HN_IRFSK_GO(KK, MM)                                                                               \
   if (k == KK && mid == MM) {                                                                             \
-    hipLaunchKernelGGL((k_irf_skip<KK, MM>), dim3(P), dim3(256), 0, st, a.x, a.y, a, skip_w, skip_b, P); \
+    hipLaunchKernelGGL((k_irf_skip<KK, MM>), dim3(P), dim3(256), 0, st, a.x, a.y, a, skip_a, skip_b, P); \
     return hipGetLastError();                                                                             \
   }
   HN_IRFSK_GO(3, 32) HN_IRFSK_GO(3, 96) HN_IRFSK_GO(3, 128) HN_IRFSK_GO(5, 32) HN_IRFSK_GO(5, 96) HN_IRFSK_GO(5, 128)
