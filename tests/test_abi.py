@@ -118,6 +118,27 @@ def test_bench_knows_every_hardnet_stage():
     assert names and names <= set(bench.HARDNET_STAGE_MAC) and names <= set(bench.HARDNET_STAGE_BYTES)
 
 
+def test_bench_knows_every_nas_stage(monkeypatch):
+    """bench.py's NAS byte / FLOP tables cover every stage name forward_nas records, and its mirror of the
+    dispatch puts wang3's layers 2-4 in k_irf_skip ("irf+skip": the block's input in, the skip's 4x4x128 out,
+    both layers' FLOP) unless HN_NO_IRFSKIP; the FLOP table sums to the architecture's total either way."""
+    import bench
+    from hardnetnas_amd import arch as A
+    src = open(os.path.join(ROOT, "hardnetnas_amd", "csrc", "hn_api.hip")).read()
+    fwd = src[src.index("static int forward_nas("):src.index('extern "C" int hn_forward(')]
+    names = set(re.findall(r'STAGE\("([^"]+)"', fwd))
+    assert "irf+skip" in names and names <= set(bench.nas_stage_bytes("wang2"))
+    assert bench.irf_skip_layers("wang3") == {2: 4} and bench.irf_skip_layers("wang2") == {}
+    assert bench.irf_skip_layers(["ir_k3_e1", "skip", "ir_k5_e3_se", "skip", "skip", "skip"]) == {}  # SE: unfused
+    b, f = bench.nas_stage_bytes("wang3"), bench.nas_stage_flop("wang3")
+    assert b["irf+skip"] == 4 * 32 * 16 * 16 + 4 * 128 * 4 * 4 and b["irf"] == b["skip"] == 0
+    assert sum(f.values()) == 2 * A.nas_macs("wang3")
+    monkeypatch.setenv("HN_NO_IRFSKIP", "1")
+    assert bench.irf_skip_layers("wang3") == {}
+    b, f = bench.nas_stage_bytes("wang3"), bench.nas_stage_flop("wang3")
+    assert b["irf+skip"] == 0 and b["irf"] > 0 and b["skip"] > 0 and sum(f.values()) == 2 * A.nas_macs("wang3")
+
+
 def _kernel_template_args(kernel: str):
     """Template argument lists of every `kernel<...>` symbol in the product library (nm -C)."""
     import subprocess
