@@ -44,6 +44,7 @@ void hn_read_knobs(HnKnobs* k) {
   k->train_f32 = env_int("HN_TRAIN_F32", 1) & 255;
 #ifdef HN_EXPERIMENTS
   k->c12_abl = env_int("HN_C12_ABL", 0) & 255;
+  k->c12w_pd = env_int("HN_C12W_PD", 11);
   k->dbg = env_int("HN_DEBUG", 0);
 #endif
 }
@@ -507,6 +508,31 @@ static std::vector<uint16_t> pack_c12(const std::vector<float>& w, int cout) {
   return a;
 }
 
+// conv1 (cin = cout = 32, BN folded) as 1-D Winograd F(4,3) along x for k_c12w (hn_c12w.hip):
+// Toom-Cook points 0, 1, -1, 1/2, -1/2, inf; U_xi[ky] = sum_kx G[xi][kx] W[ky][kx] in fp64, bf16
+// hi / lo 16x16x32 A fragments [xi 6][ky 3][group 2][plane][lane 64][8], lane (row = l & 15 ->
+// output channel 16 g + row, k-group l >> 4 -> input channels 8 (l >> 4) + j)
+static std::vector<uint16_t> pack_c12w(const std::vector<float>& w) {
+  static const double G[6][3] = {{4, 0, 0},           {2.0 / 3, 2.0 / 3, 2.0 / 3},   {2.0 / 3, -2.0 / 3, 2.0 / 3},
+                                 {-8.0 / 3, -4.0 / 3, -2.0 / 3}, {-8.0 / 3, 4.0 / 3, -2.0 / 3}, {0, 0, 1}};
+  std::vector<uint16_t> a((size_t)6 * 3 * 2 * 2 * 64 * 8);
+  for (int xi = 0; xi < 6; ++xi)
+    for (int ky = 0; ky < 3; ++ky)
+      for (int g = 0; g < 2; ++g)
+        for (int lane = 0; lane < 64; ++lane)
+          for (int j = 0; j < 8; ++j) {
+            const int oc = 16 * g + (lane & 15), ic = 8 * (lane >> 4) + j;
+            double u = 0;
+            for (int kx = 0; kx < 3; ++kx) u += G[xi][kx] * (double)w[((size_t)oc * 32 + ic) * 9 + ky * 3 + kx];
+            const float v = (float)u;
+            const uint16_t hv = f2bf(v);
+            const size_t o = ((((size_t)(xi * 3 + ky) * 2 + g) * 2) * 64 + lane) * 8 + j;
+            a[o] = hv;
+            a[o + 64 * 8] = f2bf(v - bf2f(hv));
+          }
+  return a;
+}
+
 // stride-1 3x3 conv (BN folded) as 1-D Winograd F(2,3) along x (hn_wino1.hip): U_xi[ky] =
 // sum_kx G[xi][kx] W[ky][kx] in fp64 (U3 negated: it accumulates into the odd output column with a
 // minus sign), bf16 hi / lo A fragments [cin/32][xi][ky][ks][cout/32][plane][lane][8] in the
@@ -609,6 +635,11 @@ static int build_hardnet(hn_model* m, Cursor& cur) {
       uint16_t* c = nullptr;
       if ((rc = m->upload(pack_c12(f.w, cout[l]), &c))) return rc;
       (l == 1 ? m->hd.c12_w1 : m->hd.c12_w2) = c;
+    }
+    if (l == 1) {
+      uint16_t* c = nullptr;
+      if ((rc = m->upload(pack_c12w(f.w), &c))) return rc;
+      m->hd.c12_w1w = c;
     }
   }
   m->ws_floats_per_patch = 32 * 32 * 32;
@@ -1103,7 +1134,7 @@ static bool u8_fused(const hn_model* m, int resize) {
   if (m->desc.kind == HN_KIND_FDL_NASNET || m->desc.kind == HN_KIND_FDL_NASNET01) return !m->knobs.fdl_valu;
   if (m->desc.kind == HN_KIND_NAS)  // the fused front's patch load (hn_front.hip): no input_norm, not PIL
     return resize != HN_RESIZE_PIL_BILINEAR && m->front && m->desc.input_norm_eps < 0.f && !m->knobs.front_fold;
-  return m->desc.kind == HN_KIND_HARDNET && m->c12 && !m->unfused_stem && (m->knobs.c12_cfg == 12 || m->knobs.c12_cfg == 13) &&
+  return m->desc.kind == HN_KIND_HARDNET && m->c12 && !m->unfused_stem && (m->knobs.c12_cfg == 12 || m->knobs.c12_cfg == 13 || m->knobs.c12_cfg == kC12Wino) &&
          !m->knobs.c12_abl;
 }
 

@@ -207,10 +207,10 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, WP
     }
   };
   // ABL bit 6 (timing only): per-wave s_memtime stamps at the phase boundaries of every band of
-  // the workgroup's third patch, written past the launch's a2 output (out + P * 16384 floats: the
-  // workspace buffer holds 32768 floats per patch); tools/c12_timeline.py
+  // the workgroup's third patch, written past the sub-chunk's a2 output and the head input that
+  // follows it (out + P * 24576 floats: tools/c12_timeline.py gives the workspace that much room)
   long long* const dbg =
-      reinterpret_cast<long long*>(out + (long)P * 16384) + ((long)blockIdx.x * NW + w) * 128;
+      reinterpret_cast<long long*>(out + (long)P * 24576) + ((long)blockIdx.x * NW + w) * 128;
   long patch_ts = -1;
 #define HN_C12_TS(K)                                                                        \
   if constexpr ((ABL & 192) != 0) {                                                          \
@@ -939,6 +939,13 @@ constexpr int kC12Cfgs = 13;
 #endif  // (P1, P3) at priority (2, 1) / (1, 2) / (2, 2): within the box noise of 12, removed
 
 bool hn_c12_cfg_ok(int cfg, int abl) {
+  if (cfg == kC12Wino) {  // k_c12w (hn_c12w.hip)
+#ifdef HN_EXPERIMENTS
+    return abl == 0 || abl == 1 || abl == 2 || abl == 4 || abl == 6 || abl == 64 || abl == 192;
+#else
+    return abl == 0;
+#endif
+  }
   if (cfg < 0 || cfg >= kC12Cfgs) return false;
   if (!abl) return true;
 #ifdef HN_EXPERIMENTS
@@ -958,6 +965,7 @@ hipError_t hn_launch_c12(const float* in, float* out, const HardnetDev& d, int P
   const int cfg = hn_knobs().c12_cfg;  // same-box A/Bs: 12 2-4 % < 7 1.5 % < 2 4.5 % < 0
   const int abl = hn_knobs().c12_abl;
   if (!hn_c12_cfg_ok(cfg, abl)) return hipErrorInvalidValue;
+  if (cfg == kC12Wino) return hn_launch_c12w(in, out, d, P, eps, st, u8, abl);
   if (u8 && ((cfg != 12 && cfg != 13) || abl)) return hipErrorInvalidValue;  // the uint8 loads: production builds only
   static const void* const fns[kC12Cfgs] = {
 #define HN_C12_FN(C, W, R, E, I, A, Q, PR) reinterpret_cast<const void*>(&k_c12<0, W, R, E, I, A, Q, PR>),

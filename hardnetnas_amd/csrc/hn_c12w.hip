@@ -1,0 +1,539 @@
+// k_c12w: HardNet input_norm + conv0 + conv1 + conv2 (hardnet/HardNet.py:281-289, 306-310) in one
+// kernel, as k_c12 (hn_c12.hip, production configuration 12: 4 waves, bands of 2 conv2 output rows,
+// two workgroups per CU), with conv1 as a 1-D Winograd F(4,3) along x.
+//
+// conv1 (9.4 of the kernel's 14.2 MMAC per patch) per output row and tile T of 4 columns
+// (4T .. 4T + 3) reads the 6 input columns d_i = a0[4T - 1 + i]; with the Toom-Cook points
+// 0, 1, -1, 1/2, -1/2, inf the 6 transformed inputs V = B^T d meet U_xi[ky] = sum_kx G[xi][kx]
+// W[ky][kx] (fp64 on the host, then bf16 hi / lo) in 6 x 3 GEMMs of K = 32 channels, and
+// y = A^T m: 18 multiplies per 4 outputs and input channel instead of 36, so conv1's MFMA work
+// halves (k_c12's drops by a third).  tests/precision/wino1d_precision.py: 1.7e-5 max abs from the
+// fp64 reference with conv1, conv3 and conv5 transformed (1.0e-5 all direct; the budget is 1e-4).
+//
+// Per band (P1 -> barrier -> P2 -> barrier -> P3, as k_c12):
+//   P1 stem: the band's new a0 rows (one per wave), 32x32x16 bf16x3 MFMA as k_c12, ReLU; the fp32
+//            row is staged in its own W0 ring slot (144-byte columns: the stores and the transform's
+//            reads are conflict-free), read back as lane (tile T, 4-channel chunk) = 6 columns,
+//            transformed (12 FMAs per channel), split to bf16 hi / lo and written over the staging
+//            as V records (xi, T): 128 B = 32 channels hi | lo, 16-byte chunk c at c ^ T.
+//   P2 conv1: wave (group g = w & 1 of 16 output channels, row pair rp = w >> 1): N = 16 = 8 tiles
+//            x 2 a1 rows, its 6 x 3 x 2 U fragments resident (144 VGPRs, as k_c12's direct
+//            weights); 18 (ky, xi) steps of 3 MFMAs; the output transform, bias (in m1, whose A^T
+//            column is all ones), ReLU, split -> ring W1 (unchanged layout: even / odd columns apart).
+//   P3 conv2: k_c12's (each wave a 16-channel quarter of the band's 2 x 16 output pixels), the a2
+//            tile staged through LDS and stored as whole 256-byte pixel rows after the next P1.
+// LDS 78.6 KB: W0 6 rows x 6 KB, W1 5 rows x 5,280 B, the normalised patch, the a2 staging.
+#include "hn_common.h"
+#include "hn_internal.h"
+#include "hn_preproc.h"
+
+#include <algorithm>
+
+namespace {
+
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+
+constexpr int NW = 4;                   // waves per workgroup
+constexpr int VROW = 6 * 8 * 128;       // W0 ring: bytes per a0 row (6 xi x 8 tiles x 128 B)
+constexpr int NA0 = 6, NA1 = 5;         // ring rows (a band's conv1 reads 6 a0 rows, conv2 5 a1 rows)
+constexpr int PXB = 160, W1C = 33;      // W1: bytes per pixel, column slots (x = -1 .. 31)
+constexpr int W1ROW = W1C * PXB;
+constexpr int IRS = 72, IPL = 35 * IRS; // normalised patch planes: bytes per row (36 bf16) / plane
+
+// The stem (conv0, 1 -> 32 channels, 3x3) as one 16x16x32 MFMA per channel half, the three bf16x3
+// products and the bias packed along K: K-group 0 = x_hi(tap j) . w_hi(tap j), 1 = x_lo . w_hi,
+// 2 = x_hi . w_lo (taps j = 0 .. 7), 3 = x_hi(8) w_hi(8), x_lo(8) w_hi(8), x_hi(8) w_lo(8), 1 . b_hi,
+// 1 . b_lo, 0, 0, 0 (the A side is built once into s_stem, the B side per view in P1).
+
+HN_DEV f32x4v mfma16(const uint4& a, const uint4& b, f32x4v c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a), as_bf16x8(b), c, 0, 0, 0);
+}
+
+HN_DEV uint2 pack_bf16x4(float a, float b, float c, float d, uint2& lo) {
+  bf16x4 h, l;
+  h[0] = (__bf16)a; l[0] = (__bf16)(a - (float)h[0]);
+  h[1] = (__bf16)b; l[1] = (__bf16)(b - (float)h[1]);
+  h[2] = (__bf16)c; l[2] = (__bf16)(c - (float)h[2]);
+  h[3] = (__bf16)d; l[3] = (__bf16)(d - (float)h[3]);
+  lo = __builtin_bit_cast(uint2, l);
+  return __builtin_bit_cast(uint2, h);
+}
+
+// lane (c, g16) holds 4 channels hi / lo; permlane16_swap (odd rows of vdst <-> even rows of src)
+// leaves the even 16-lane row with the hi halves of 8 channels and the odd row with their lo halves
+HN_DEV uint4 swap_hilo(uint2 hi, uint2 lo) {
+  const auto rx = __builtin_amdgcn_permlane16_swap(hi.x, lo.x, false, false);
+  const auto ry = __builtin_amdgcn_permlane16_swap(hi.y, lo.y, false, false);
+  return make_uint4(rx[0], ry[0], rx[1], ry[1]);
+}
+
+// W1 column slot of a1 column x (x = -1 .. 31): even (x + 1) -> (x + 1) / 2, odd -> 17 + x / 2
+HN_DEV int w1_slot(int x) { return ((x + 1) & 1) ? 17 + (x >> 1) : (x + 1) >> 1; }
+
+// U8: -1 = fp32 [P,1,32,32] input; HN_RESIZE_* = uint8 patches preprocessed in the load (hn_preproc.h)
+// ABL (timing builds of the experiments library only; 0 in production): bit 0 / 1 / 2 skip the stem /
+// conv1 / conv2 MFMAs, bit 6 stamps s_memtime at the phase boundaries of every band of each
+// workgroup's third patch (k_c12's layout, tools/c12_timeline.py), bit 7 also inside P1
+// PD2 / PD3: how many steps ahead P2 / P3 read their B fragments from LDS (rings of PD + 1)
+template <int U8 = -1, int ABL = 0, int PD2 = 1, int PD3 = 1>
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_c12w(
+    const void* __restrict__ in_, float* __restrict__ out, const float* __restrict__ stem_w,
+    const float* __restrict__ stem_b, const uint4* __restrict__ w1u, const float* __restrict__ b1,
+    const uint4* __restrict__ w2p, const float* __restrict__ b2, int P, float eps, float pmean,
+    float pstd, int pnorm) {
+  __shared__ __attribute__((aligned(16))) char s_w0[NA0 * VROW];
+  __shared__ __attribute__((aligned(16))) char s_w1[NA1 * W1ROW];
+  // the normalised patch as bf16 hi / lo planes: [plane][row -1 .. 33][column -2 .. 33], 72-byte rows
+  __shared__ __attribute__((aligned(16))) char s_in[2 * IPL];
+  __shared__ float red[2 * NW];
+  __shared__ __attribute__((aligned(16))) float s_st[2 * 16 * 64];  // a2 staging (k_c12's XST)
+  __shared__ __attribute__((aligned(16))) uint4 s_stem[2][64];        // K-packed stem A per channel half
+  __shared__ __attribute__((aligned(16))) float s_b1[32], s_b2[64];
+
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  // lane-derived addresses are recomputed in each phase from an opaque copy of the lane index (one
+  // or two VALU each) instead of being held in registers across the band loop
+  auto opaque_lane = [&]() {
+    int l = lane;
+    asm volatile("" : "+v"(l));
+    return l;
+  };
+
+  const long per = ((long)P + gridDim.x - 1) / gridDim.x;
+  const long pb = (long)xcd_remap(blockIdx.x, gridDim.x) * per;
+  const long pe = min((long)P, pb + per);
+  if (pb >= pe) return;  // workgroup-uniform
+
+  for (int i = t; i < NA0 * VROW / 16; i += NW * 64) reinterpret_cast<uint4*>(s_w0)[i] = make_uint4(0, 0, 0, 0);
+  for (int i = t; i < NA1 * W1ROW / 16; i += NW * 64) reinterpret_cast<uint4*>(s_w1)[i] = make_uint4(0, 0, 0, 0);
+  for (int i = t; i < 2 * IPL / 16; i += NW * 64) reinterpret_cast<uint4*>(s_in)[i] = make_uint4(0, 0, 0, 0);
+  if (t < 128) {  // stem A (16x16x32) of channel half t >> 6 with the bf16x3 products K-packed (stem_b1)
+    const int l = t & 63, ch = 16 * (t >> 6) + (l & 15), gk = l >> 4;
+    bf16x8 a;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float v = 0.f;
+      bool lo = false;
+      if (gk < 3) {
+        v = stem_w[j * 32 + ch];
+        lo = gk == 2;
+      } else if (j < 3) {
+        v = stem_w[8 * 32 + ch];
+        lo = j == 2;
+      } else if (j < 5) {
+        v = stem_b[ch];
+        lo = j == 4;
+      }
+      const __bf16 h = (__bf16)v;
+      a[j] = lo ? (__bf16)(v - (float)h) : h;
+    }
+    s_stem[t >> 6][l] = __builtin_bit_cast(uint4, a);
+  }
+  for (int i = t; i < 96; i += NW * 64) {
+    if (i < 32) s_b1[i] = b1[i];
+    else s_b2[i - 32] = b2[i - 32];
+  }
+  // conv1 U fragments resident: [xi][ky][plane] of this wave's 16-channel group
+  const int g1 = w & 1, rp = w >> 1;
+  uint4 uw[6][3][2];
+#pragma unroll
+  for (int xi = 0; xi < 6; ++xi)
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+      for (int pl = 0; pl < 2; ++pl) uw[xi][ky][pl] = w1u[(((xi * 3 + ky) * 2 + g1) * 2 + pl) * 64 + lane];
+  // conv2 A fragments of this wave's quarter, streamed from L2 two taps ahead
+  auto w2_frag = [&](int tap, int pl) {
+    int i = ((tap * 4 + w) * 2 + pl) * 64 + lane;
+    asm volatile("" : "+v"(i));  // keep the load here (not hoisted out of the patch loop)
+    return w2p[i];
+  };
+
+  constexpr int PPT = 1024 / (NW * 64);  // patch pixels per thread
+  typedef float pxv __attribute__((ext_vector_type(PPT)));
+  const float* in = static_cast<const float*>(in_);
+  const uint8_t* in8 = static_cast<const uint8_t*>(in_);
+  constexpr int INB = U8 == HN_RESIZE_NONE ? 1024 : 4096;
+  const int py = (PPT * t) >> 5, px = (PPT * t) & 31;
+  pxv vnext;
+  hnpre::U8Px<U8 < 0 ? HN_RESIZE_NONE : U8, PPT> rnext;
+  if constexpr (U8 < 0)
+    vnext = reinterpret_cast<const pxv*>(in + pb * 1024)[t];
+  else
+    rnext.load(in8 + pb * INB, py, px);
+  long pend_patch = -1;  // the band whose a2 rows wait in s_st
+  int pend_row = 0;
+  auto xst_flush = [&]() {  // wave w: row w >> 1, pixels 8 (w & 1) + (lane >> 4) + 4 j, chunk lane & 15
+    const int ry = w >> 1, q = lane & 15;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int x = 8 * (w & 1) + (lane >> 4) + 4 * j;
+      const f32x4v v = *reinterpret_cast<const f32x4v*>(s_st + ((ry * 16 + x) * 16 + (q ^ (x & 7))) * 4);
+      *reinterpret_cast<f32x4v*>(out + ((pend_patch * 16 + pend_row + ry) * 16 + x) * 64 + 4 * q) = v;
+    }
+  };
+  const int ph = w & 1, pr = w >> 1;  // P1: the wave's channel half and row pair
+  long long* const dbg =
+      reinterpret_cast<long long*>(out + (long)P * 24576) + ((long)blockIdx.x * NW + w) * 128;
+  long patch_ts = -1;
+#define HN_W_TS(K)                                                                                      \
+  if constexpr ((ABL & 192) != 0) {                                                                      \
+    if (patch == patch_ts && lane == 0) dbg[band * 6 + (K)] = (long long)__builtin_amdgcn_s_memtime(); \
+  }
+#define HN_W_TS2(K)                                                                                     \
+  if constexpr ((ABL & 128) != 0) {                                                                     \
+    if (patch == patch_ts && lane == 0 && q == pr) dbg[48 + band * 4 + (K)] = (long long)__builtin_amdgcn_s_memtime(); \
+  }
+
+#pragma unroll 1
+  for (long patch = pb; patch < pe; ++patch) {
+    if constexpr ((ABL & 192) != 0) patch_ts = pb + 2;
+    {
+      pxv v;
+      if constexpr (U8 < 0) {
+        v = vnext;
+        if (patch + 1 < pe) vnext = reinterpret_cast<const pxv*>(in + (patch + 1) * 1024)[t];
+      } else {
+        int q[PPT];
+        rnext.resized(py, px, q);
+#pragma unroll
+        for (int j = 0; j < PPT; ++j) v[j] = hnpre::to_input(q[j], pmean, pstd, pnorm);
+        if (patch + 1 < pe) rnext.load(in8 + (patch + 1) * INB, py, px);
+      }
+      float mean = 0.f, sd = 1.f;
+      if (eps >= 0.f) {  // input_norm: (x - mean) / (std_unbiased + eps), HardNet.py:306-310
+        float a = 0.f;
+#pragma unroll
+        for (int j = 0; j < PPT; ++j) a += v[j];
+        const float s = wave_sum(a);
+        if (lane == 0) red[w] = s;
+        __syncthreads();
+        a = 0.f;
+#pragma unroll
+        for (int i = 0; i < NW; ++i) a += red[i];
+        mean = a * (1.f / 1024.f);
+        float q = 0.f;
+#pragma unroll
+        for (int j = 0; j < PPT; ++j) q += (v[j] - mean) * (v[j] - mean);
+        q = wave_sum(q);
+        if (lane == 0) red[NW + w] = q;
+        __syncthreads();
+        a = 0.f;
+#pragma unroll
+        for (int i = 0; i < NW; ++i) a += red[NW + i];
+        sd = sqrtf(a * (1.f / 1023.f)) + eps;
+      } else {
+        __syncthreads();
+      }
+      const float inv = 1.f / sd;
+      const int q0 = PPT * t, y = q0 >> 5, x = q0 & 31;
+      static_assert(PPT == 4, "4 pixels per thread");
+      uint32_t hw[2], lw[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const float a = (v[2 * j] - mean) * inv, b = (v[2 * j + 1] - mean) * inv;
+        const __bf16 ha = (__bf16)a, hb = (__bf16)b;
+        const __bf16 la = (__bf16)(a - (float)ha), lb = (__bf16)(b - (float)hb);
+        hw[j] = (uint32_t)__builtin_bit_cast(uint16_t, ha) | ((uint32_t)__builtin_bit_cast(uint16_t, hb) << 16);
+        lw[j] = (uint32_t)__builtin_bit_cast(uint16_t, la) | ((uint32_t)__builtin_bit_cast(uint16_t, lb) << 16);
+      }
+      char* o = s_in + (y + 1) * IRS + (x + 2) * 2;
+      reinterpret_cast<uint32_t*>(o)[0] = hw[0];
+      reinterpret_cast<uint32_t*>(o)[1] = hw[1];
+      reinterpret_cast<uint32_t*>(o + IPL)[0] = lw[0];
+      reinterpret_cast<uint32_t*>(o + IPL)[1] = lw[1];
+      __syncthreads();
+    }
+#pragma unroll 1
+    for (int band = 0; band < 8; ++band) {
+      const int r0 = 2 * band;  // conv2 output rows r0, r0 + 1
+      HN_W_TS(0);
+      __builtin_amdgcn_s_setprio(1);
+      // ---- P1: the band's new a0 rows -> V records in W0 (row y in slot (y + 1) % 6) ---------------
+      // wave (pair pr, channel half ph); band 0: rows -1 (zero), 0 .. 4 (pairs 0, 2, 4; row 5 is not
+      // written), band b: pairs 4b + 1, 4b + 3 (row 32 is zeroed after its pair)
+      if (band == 0)
+        for (int i = t; i < VROW / 16; i += NW * 64) reinterpret_cast<uint4*>(s_w0)[i] = make_uint4(0, 0, 0, 0);
+      const int npair = band == 0 ? 3 : 2;
+#pragma unroll 1
+      for (int q = pr; q < npair; q += 2) {
+        const int y0 = band == 0 ? 2 * q : 4 * band + 1 + 2 * q;
+        // lane roles (16x16x32, N = 8 tiles x 2 a0 rows): tile pT, row pj of the pair; K-group g16
+        // reads the lo plane (1) or the hi plane (0, 2, 3)
+        const int ln = opaque_lane(), g16 = ln >> 4, pT = ln & 7, pj = (ln >> 3) & 1;
+        const bool pg3 = g16 == 3;
+        const int pbase = (g16 == 1 ? IPL : 0) + pj * IRS + 8 * pT;  // + (y0 + dy) * IRS: window row dy
+        const int lbase = IPL + pj * IRS + 8 * pT;                     // the lo plane (tap 8's x_lo)
+        const int pchunk = ((2 * ph + (g16 >> 1)) + 4 * (g16 & 1)) ^ pT;  // V chunk written after the swap
+        // window rows y - 1 .. y + 1 (y = y0 + pj), columns 4 pT - 2 .. 4 pT + 5, this lane's plane
+        uint32_t R[3][4], L[4];
+#pragma unroll
+        for (int dy = 0; dy < 3; ++dy) {
+          const uint2 a = *reinterpret_cast<const uint2*>(s_in + pbase + (y0 + dy) * IRS);
+          const uint2 b = *reinterpret_cast<const uint2*>(s_in + pbase + (y0 + dy) * IRS + 8);
+          R[dy][0] = a.x; R[dy][1] = a.y; R[dy][2] = b.x; R[dy][3] = b.y;
+        }
+        {
+          const uint2 a = *reinterpret_cast<const uint2*>(s_in + lbase + (y0 + 2) * IRS);
+          const uint2 b = *reinterpret_cast<const uint2*>(s_in + lbase + (y0 + 2) * IRS + 8);
+          L[0] = a.x; L[1] = a.y; L[2] = b.x; L[3] = b.y;
+        }
+        const uint4 sa = s_stem[ph][ln];
+        // pair (W(dy, c), W(dy, c + 1)) of window row dy
+        auto pair = [&](int dy, int c) -> uint32_t {
+          return (c & 1) ? __builtin_amdgcn_alignbit(R[dy][(c + 1) >> 1], R[dy][(c - 1) >> 1], 16) : R[dy][c >> 1];
+        };
+        f32x4v acc[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {  // view i: a0 column 4 pT - 1 + i
+          const int p = i & 1;
+          const uint32_t sel = p ? 0x07060302u : 0x05040100u;
+          uint4 b;
+          b.x = pair(0, i);
+          b.y = __builtin_amdgcn_perm(R[1][i >> 1], R[0][(i + 2) >> 1], sel);  // (W(0, i + 2), W(1, i))
+          b.z = pair(1, i + 1);
+          b.w = pair(2, i);
+          // K-group 3: (x_hi(8), x_lo(8)), (x_hi(8), 1), (1, 0), 0 with tap 8 = W(2, i + 2)
+          const uint32_t s0 = __builtin_amdgcn_perm(L[(i + 2) >> 1], R[2][(i + 2) >> 1], sel);
+          const uint32_t s1 = __builtin_amdgcn_perm(0x3F80u, R[2][(i + 2) >> 1], p ? 0x05040302u : 0x05040100u);
+          b.x = pg3 ? s0 : b.x;
+          b.y = pg3 ? s1 : b.y;
+          b.z = pg3 ? 0x3F80u : b.z;
+          b.w = pg3 ? 0u : b.w;
+          acc[i] = (ABL & 1) ? f32x4v{} : mfma16(sa, b, f32x4v{});
+        }
+        if constexpr ((ABL & 128) != 0) {  // sub-stamp a: the stem's results are available
+          float z = acc[0][0] + acc[5][3];
+          asm volatile("" : "+v"(z));
+          if (z == 1234.5f) dbg[127] = 0;
+          HN_W_TS2(0);
+        }
+        // V = B^T relu(d) (points 0, 1, -1, 1/2, -1/2, inf), channels 16 ph + 4 g16 + c; columns -1 (view 0
+        // of tile 0) and 32 (view 5 of tile 7) are conv1's zero padding, not the stem evaluated there:
+        // their coefficients (d0 only enters V0, d5 only V5) are zeroed per lane
+        const float k0 = pT == 0 ? 0.f : 0.25f, k5 = pT == 7 ? 0.f : 1.f;
+        float V[6][4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const float d0 = fmaxf(acc[0][c], 0.f), d1 = fmaxf(acc[1][c], 0.f), d2 = fmaxf(acc[2][c], 0.f);
+          const float d3 = fmaxf(acc[3][c], 0.f), d4 = fmaxf(acc[4][c], 0.f), d5 = fmaxf(acc[5][c], 0.f);
+          V[0][c] = fmaf(k0, d0, fmaf(-1.25f, d2, d4));
+          const float pa = fmaf(-0.25f, d2, d4), pb_ = fmaf(-0.25f, d1, d3);
+          V[1][c] = pa + pb_;
+          V[2][c] = pa - pb_;
+          const float pc = d4 - d2, pe_ = d3 - d1;
+          V[3][c] = fmaf(0.5f, pe_, pc);
+          V[4][c] = fmaf(-0.5f, pe_, pc);
+          V[5][c] = fmaf(k5, d5, fmaf(0.25f, d1, -1.25f * d3));
+        }
+        HN_W_TS2(1);
+        char* S = s_w0 + ((y0 + pj + 1) % NA0) * VROW + pT * 128 + 16 * pchunk;
+        const bool wr = !(band == 0 && q == 2 && pj == 1);  // band 0's row 5 belongs to band 1
+#pragma unroll
+        for (int xi = 0; xi < 6; ++xi) {
+          uint2 lo;
+          const uint2 hi = pack_bf16x4(V[xi][0], V[xi][1], V[xi][2], V[xi][3], lo);
+          const uint4 vv = swap_hilo(hi, lo);
+          if (wr) *reinterpret_cast<uint4*>(S + xi * 1024) = vv;
+        }
+        HN_W_TS2(2);  // sub-stamp c: V records issued (the stamp's wait drains the LDS stores)
+      }
+      if (band == 7 && pr == 1) {  // a0 row 32 (conv1's zero padding): this wave's channel half
+        char* S = s_w0 + (33 % NA0) * VROW;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          const int idx = k * 64 + lane, rec = idx >> 2, cc = idx & 3;
+          const int c = (cc & 1) + 2 * ph + 4 * (cc >> 1);
+          *reinterpret_cast<uint4*>(S + rec * 128 + 16 * (c ^ (rec & 7))) = make_uint4(0, 0, 0, 0);
+        }
+      }
+      HN_W_TS(1);
+      __builtin_amdgcn_s_setprio(0);
+      __syncthreads();
+      HN_W_TS(2);
+      if (pend_patch >= 0) xst_flush();  // the previous band's a2 rows
+
+      // ---- P2: conv1 (F(4,3)) -> W1 ring: a1 rows 4 band + 2 rp + j (j = lane bit 3), group g1 ------
+      if (band == 0 && rp == 0) {  // a1 row -1 (conv2's zero padding): this wave's channel group
+        const int c16 = lane & 15, g16 = lane >> 4;
+#pragma unroll
+        for (int hx = 0; hx < 2; ++hx) {
+          char* dst = s_w1 + w1_slot(16 * hx + c16) * PXB + 32 * g1 + 8 * g16;
+          *reinterpret_cast<uint2*>(dst) = make_uint2(0, 0);
+          *reinterpret_cast<uint2*>(dst + 64) = make_uint2(0, 0);
+        }
+      }
+      {
+        const int ln = opaque_lane(), g16 = ln >> 4, tj = (ln >> 3) & 1, tt = ln & 7;
+        f32x4v acc[6];
+#pragma unroll
+        for (int xi = 0; xi < 6; ++xi) acc[xi] = f32x4v{};
+        acc[1] = *reinterpret_cast<const f32x4v*>(s_b1 + 16 * g1 + 4 * g16);  // the bias rides in m1
+        const char* vrow[3];  // a0 row 4 band + 2 rp + tj - 1 + ky: ring slot (row + 1) % 6
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky) vrow[ky] = s_w0 + ((4 * band + 2 * rp + tj + ky) % NA0) * VROW + tt * 128;
+        const int ohi = 16 * (g16 ^ tt), olo = 16 * ((4 + g16) ^ tt);
+        constexpr int R2 = PD2 + 1;
+        uint4 bh[R2], bl[R2];
+        auto ld2 = [&](int s) {
+          bh[s % R2] = *reinterpret_cast<const uint4*>(vrow[s / 6] + (s % 6) * 1024 + ohi);
+          bl[s % R2] = *reinterpret_cast<const uint4*>(vrow[s / 6] + (s % 6) * 1024 + olo);
+        };
+#pragma unroll
+        for (int s = 0; s < PD2; ++s) ld2(s);
+#pragma unroll
+        for (int s = 0; s < 18; ++s) {
+          const int ky = s / 6, xi = s % 6;
+          if (s + PD2 < 18) ld2(s + PD2);
+          __builtin_amdgcn_sched_barrier(0);
+          if constexpr ((ABL & 2) != 0) {
+            acc[xi][0] += __builtin_bit_cast(float, bh[s % R2].x ^ bl[s % R2].y);
+            continue;
+          }
+          acc[xi] = mfma16(uw[xi][ky][1], bh[s % R2], acc[xi]);
+          acc[xi] = mfma16(uw[xi][ky][0], bl[s % R2], acc[xi]);
+          acc[xi] = mfma16(uw[xi][ky][0], bh[s % R2], acc[xi]);
+        }
+        // y = A^T m: lane (tile tt, row tj, channels 16 g1 + 4 g16 ..) -> columns 4 tt .. 4 tt + 3
+        f32x4v yv[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const float s12 = acc[1][c] + acc[2][c], d12 = acc[1][c] - acc[2][c];
+          const float s34 = acc[3][c] + acc[4][c], d34 = acc[3][c] - acc[4][c];
+          yv[0][c] = acc[0][c] + s12 + s34;
+          yv[1][c] = fmaf(0.5f, d34, d12);
+          yv[2][c] = fmaf(0.25f, s34, s12);
+          yv[3][c] = fmaf(0.125f, d34, d12) + acc[5][c];
+        }
+        char* prow = s_w1 + ((4 * band + 2 * rp + tj + 1) % NA1) * W1ROW + 32 * g1 + 16 * (g16 >> 1) + 64 * (g16 & 1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          uint2 lo;
+          const uint2 hi = pack_bf16x4(fmaxf(yv[i][0], 0.f), fmaxf(yv[i][1], 0.f), fmaxf(yv[i][2], 0.f),
+                                       fmaxf(yv[i][3], 0.f), lo);
+          *reinterpret_cast<uint4*>(prow + w1_slot(4 * tt + i) * PXB) = swap_hilo(hi, lo);
+        }
+      }
+      HN_W_TS(3);
+      uint4 wq[3][2];  // conv2 fragments, the first two taps in flight across the barrier
+#pragma unroll
+      for (int tap = 0; tap < 2; ++tap)
+#pragma unroll
+        for (int pl = 0; pl < 2; ++pl) wq[tap][pl] = w2_frag(tap, pl);
+      __syncthreads();
+      HN_W_TS(4);
+
+      __builtin_amdgcn_s_setprio(1);
+      // ---- P3: conv2 (stride 2), output rows r0, r0 + 1, this wave's 16-channel quarter ----------
+      {
+        const int ln = opaque_lane(), c16 = ln & 15, g16 = ln >> 4;
+        f32x4v acc[2];
+        acc[0] = acc[1] = *reinterpret_cast<const f32x4v*>(s_b2 + 16 * w + 4 * g16);
+        // output column c16 reads a1 column 2 c16 - 1 + dx: W1 slot c16 (dx 0), 17 + c16 (dx 1),
+        // c16 + 1 (dx 2); a1 rows 2 (r0 + ry) - 1 + dy sit in ring slots (2 (r0 + ry) + dy) % 5
+        const char* srow[2][3];
+#pragma unroll
+        for (int ry = 0; ry < 2; ++ry)
+#pragma unroll
+          for (int dy = 0; dy < 3; ++dy) srow[ry][dy] = s_w1 + (((2 * (r0 + ry) + dy) % NA1) * W1C + c16) * PXB + 16 * g16;
+        constexpr int R3 = PD3 + 1;
+        uint4 bh[R3], bl[R3];
+        auto ld3 = [&](int j) {
+          const int tn = j >> 1, rn = j & 1;
+          const int dy = tn / 3, dx = tn % 3;
+          const char* p = srow[rn][dy] + (dx == 1 ? 17 : (dx >> 1)) * PXB;
+          bh[j % R3] = *reinterpret_cast<const uint4*>(p);
+          bl[j % R3] = *reinterpret_cast<const uint4*>(p + 64);
+        };
+#pragma unroll
+        for (int j = 0; j < PD3; ++j) ld3(j);
+#pragma unroll
+        for (int j = 0; j < 18; ++j) {
+          const int tap = j >> 1, ry = j & 1;
+          if (ry == 0 && tap + 2 < 9) {
+#pragma unroll
+            for (int pl = 0; pl < 2; ++pl) wq[(tap + 2) % 3][pl] = w2_frag(tap + 2, pl);
+          }
+          if (j + PD3 < 18) ld3(j + PD3);
+          __builtin_amdgcn_sched_barrier(0);
+          const uint4* wc = wq[tap % 3];
+          if constexpr ((ABL & 4) != 0) {
+            acc[ry][0] += __builtin_bit_cast(float, bh[j % R3].x ^ bl[j % R3].y ^ wc[0].x);
+            continue;
+          }
+          acc[ry] = mfma16(wc[1], bh[j % R3], acc[ry]);
+          acc[ry] = mfma16(wc[0], bl[j % R3], acc[ry]);
+          acc[ry] = mfma16(wc[0], bh[j % R3], acc[ry]);
+        }
+#pragma unroll
+        for (int ry = 0; ry < 2; ++ry)
+          *reinterpret_cast<f32x4v*>(s_st + ((ry * 16 + c16) * 16 + ((4 * w + g16) ^ (c16 & 7))) * 4) =
+              __builtin_elementwise_max(acc[ry], f32x4v{});
+        pend_patch = patch;
+        pend_row = r0;
+      }
+      HN_W_TS(5);
+      // no barrier: the next band's P1 writes only W0, which P3 does not read; its barrier orders this
+      // P3's W1 reads before the next P2's W1 writes
+    }  // band
+  }  // patch
+  __syncthreads();
+  xst_flush();
+#undef HN_W_TS
+#undef HN_W_TS2
+}
+
+}  // namespace
+
+hipError_t hn_launch_c12w(const float* in, float* out, const HardnetDev& d, int P, float eps, hipStream_t st,
+                          const HnU8In* u8, int abl) {
+  if (P <= 0) return hipSuccess;
+  if (!d.c12_w1w) return hipErrorInvalidValue;
+  int resident = 0;
+  const hipError_t e = hn_resident_blocks(reinterpret_cast<const void*>(&k_c12w<-1>), NW * 64, 0, &resident);
+  if (e != hipSuccess) return e;
+  const int grid = (int)std::min<long>((long)P, resident);
+  const void* src = u8 ? u8->in : static_cast<const void*>(in);
+  const float pm = u8 ? u8->mean : 0.f, ps = u8 ? u8->stdv : 1.f;
+  const int pn = u8 ? u8->normalize : 0;
+#define HN_C12W_GO(U, ...)                                                                                \
+  hipLaunchKernelGGL((k_c12w<U, ##__VA_ARGS__>), dim3(grid), dim3(NW * 64), 0, st, src, out, d.stem_w, d.stem_b,        \
+                     static_cast<const uint4*>(d.c12_w1w), d.bias[1], static_cast<const uint4*>(d.c12_w2), \
+                     d.bias[2], P, eps, pm, ps, pn)
+  const int pd = hn_knobs().c12w_pd;
+  if (!u8 && !abl && pd != 11) {
+    switch (pd) {
+      case 21: HN_C12W_GO(-1, 0, 2, 1); break;
+      case 31: HN_C12W_GO(-1, 0, 3, 1); break;
+      case 12: HN_C12W_GO(-1, 0, 1, 2); break;
+      case 22: HN_C12W_GO(-1, 0, 2, 2); break;
+      case 32: HN_C12W_GO(-1, 0, 3, 2); break;
+      case 33: HN_C12W_GO(-1, 0, 3, 3); break;
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
+  if (abl) {
+#ifdef HN_EXPERIMENTS
+    if (u8) return hipErrorInvalidValue;
+    switch (abl) {
+      case 1: HN_C12W_GO(-1, 1); break;
+      case 2: HN_C12W_GO(-1, 2); break;
+      case 4: HN_C12W_GO(-1, 4); break;
+      case 6: HN_C12W_GO(-1, 6); break;
+      case 64: HN_C12W_GO(-1, 64); break;
+      case 192: HN_C12W_GO(-1, 192); break;
+      default: return hipErrorInvalidValue;
+    }
+#else
+    return hipErrorInvalidValue;
+#endif
+  } else if (!u8) HN_C12W_GO(-1);
+  else if (u8->resize == HN_RESIZE_NONE) HN_C12W_GO(HN_RESIZE_NONE);
+  else if (u8->resize == HN_RESIZE_CV2_LINEAR) HN_C12W_GO(HN_RESIZE_CV2_LINEAR);
+  else if (u8->resize == HN_RESIZE_PIL_BILINEAR) HN_C12W_GO(HN_RESIZE_PIL_BILINEAR);
+  else return hipErrorInvalidValue;
+#undef HN_C12W_GO
+  return hipGetLastError();
+}

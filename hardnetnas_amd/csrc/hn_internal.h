@@ -33,6 +33,7 @@ struct HnKnobs {
                                // k_fwd0 / k_wgrad0); bit 7: swaps the one-ring-per-wave and the
                                // shared-ring-per-patch forms (default shared: conv3 / conv5 k_fwd3s,
                                // conv4 k_dgrad2; per wave: conv2 / conv4 k_fwd2)
+  int c12w_pd = 11;            // HN_C12W_PD: k_c12w's P2 / P3 B-fragment prefetch distances (tens / units)
   int c12_abl = 0;             // HN_C12_ABL (HN_EXPERIMENTS only)
   int dbg = 0;                 // HN_DEBUG (HN_EXPERIMENTS only)
 };
@@ -52,6 +53,7 @@ struct HardnetDev {
   float* bias[7] = {};       // folded BN bias per conv
   void* c12_w1 = nullptr;    // conv1 / conv2 as 16x16x32 A operands for the fused k_c12
   void* c12_w2 = nullptr;
+  void* c12_w1w = nullptr;   // conv1 as 1-D Winograd F(4,3) U fragments for k_c12w
   void* wino[7] = {};        // conv3 / conv5: Winograd F(2x2,3x3) U fragments (hn_wino.hip)
   void* wino1[7] = {};       // conv3 / conv5: 1-D Winograd F(2,3) U fragments (hn_wino1.hip)
 };
@@ -71,6 +73,10 @@ hipError_t hn_launch_stem(const float* in, float* out, const float* w, const flo
                           bool norm, float eps, hipStream_t st);
 bool hn_hardnet_variant_ok(int layer, int variant);
 bool hn_c12_cfg_ok(int cfg, int abl);
+// HN_C12_CFG 14: k_c12w (hn_c12w.hip), conv1 as a 1-D Winograd F(4,3)
+constexpr int kC12Wino = 14;
+hipError_t hn_launch_c12w(const float* in, float* out, const HardnetDev& d, int P, float eps, hipStream_t st,
+                          const HnU8In* u8, int abl);
 hipError_t hn_launch_hardnet_conv(int layer, int variant, const HardnetDev& d, const float* in,
                                   float* out, int P, float eps, hipStream_t st);
 hipError_t hn_launch_head(const float* a, float* out, const void* wp, const float* bias, int P,

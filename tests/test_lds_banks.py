@@ -473,3 +473,60 @@ def test_wino1_producer_writes_conflict_free(layer):
                 for grp in WRITE_GROUPS:
                     slots = {(addrs[l] // 16) % 16 for l in grp}
                     assert len(slots) == 8, (layer, k, wave, xi, grp[0])
+
+
+# ---- k_c12w (hn_c12w.hip): conv1 as a 1-D Winograd F(4,3) inside the fused stem+conv1+conv2 kernel ----
+C12W_VROW = 6 * 8 * 128  # W0 ring bytes per a0 row: V records (xi, tile T), 128 B, chunk c at c ^ T
+
+
+def test_c12w_conv1_operand_reads_conflict_free():
+    """P2's ds_read_b128 of V_xi (lane n = T + 8 j: tile T of a0 row y0 + j - 1 + ky; K-group g16 = hi chunk
+    g16 / lo chunk 4 + g16) for every ring slot pair, ky and xi."""
+    for slot0 in range(6):
+        for ky in range(3):
+            for xi in range(6):
+                for plane in range(2):
+                    addrs = []
+                    for lane in range(64):
+                        n, g16 = lane & 15, lane >> 4
+                        t, j = n & 7, n >> 3
+                        slot = (slot0 + j + ky) % 6
+                        c = g16 + 4 * plane
+                        addrs.append(slot * C12W_VROW + (xi * 8 + t) * 128 + 16 * (c ^ t))
+                    for grp in GROUPS:
+                        assert len({(addrs[l] // 16) % 16 for l in grp}) == 16, (slot0, ky, xi, plane, grp[0])
+
+
+def test_c12w_transform_writes_conflict_free():
+    """P1's ds_write_b128 of the V records after the hi / lo swap: lane (tile T = l & 7, row j = (l >> 3) & 1,
+    K-group g16) of channel half ph writes chunk (2 ph + g16 / 2 + 4 (g16 & 1)) ^ T; each 8-lane group
+    covers 8 distinct 16-byte slots of a 128-byte bank row."""
+    for ph in range(2):
+        for y0 in range(6):
+            for xi in range(6):
+                addrs = []
+                for lane in range(64):
+                    t, j, g16 = lane & 7, (lane >> 3) & 1, lane >> 4
+                    c = (2 * ph + (g16 >> 1) + 4 * (g16 & 1)) ^ t
+                    addrs.append(((y0 + j + 1) % 6) * C12W_VROW + (xi * 8 + t) * 128 + 16 * c)
+                for grp in WRITE_GROUPS:
+                    assert len({(addrs[l] // 16) % 8 for l in grp}) == 8, (ph, y0, xi, grp[0])
+
+
+def test_c12w_records_cover_each_chunk_once():
+    """Over the 4 P1 waves' channel halves and both swap parities, every (record, chunk) of a V row is written
+    exactly once, and P2 reads exactly the chunk holding its K-group's 8 channels (hi and lo)."""
+    seen = {}
+    for ph in range(2):
+        for lane in range(64):
+            t, g16 = lane & 7, lane >> 4
+            ch0 = 16 * ph + 4 * (g16 & ~1)  # the 8 channels this lane holds after the swap
+            plane = g16 & 1
+            c = (2 * ph + (g16 >> 1) + 4 * plane)
+            key = (t, c ^ t)
+            seen.setdefault(key, set()).add((ch0, plane, (lane >> 3) & 1))
+    for t in range(8):
+        for g in range(4):  # P2: K-group g = channels 8 g .. 8 g + 7
+            for plane in range(2):
+                got = seen[(t, (g + 4 * plane) ^ t)]
+                assert {(c, p) for c, p, _ in got} == {(8 * g, plane)}

@@ -18,14 +18,15 @@ P = 16384  # one sub-chunk = one k_c12 launch
 dev = torch.device("cuda:0")
 nm = NativeModel.from_module(bench.build_model("hardnet"), dev)
 x = bench.synth_input_on_device(P, dev, 5)
-ws = torch.zeros(nm.workspace_bytes(P), dtype=torch.uint8, device=dev)
+nwg, nw = 512, 4
+ws = torch.zeros(nm.workspace_bytes(P) + nwg * nw * 1024, dtype=torch.uint8, device=dev)
 out = torch.empty((P, 128), device=dev)
 for _ in range(2):
     nm.forward(x, out=out, workspace=ws)
 torch.cuda.synchronize()
-per = 32768 * P                      # floats per workspace buffer (ws_floats_per_patch * P)
-off = (2 * per + P * 16384) * 4      # a2 + the launch's c12 output
-nwg, nw = 512, 4
+# the sub-chunked workspace: [a3: P x 16384][a2: P x 16384][a5: P x 8192] floats; k_c12's output is
+# a2, and the stamps go past a5 (out + P * 24576 floats)
+off = (16384 * P + 24576 * P) * 4
 raw = ws[off: off + nwg * nw * 128 * 8].view(torch.int64).cpu().numpy().reshape(nwg, nw, 128)
 t = raw[:, :, :48].reshape(nwg, nw, 8, 6).astype(np.float64)
 ok = (t > 0).all(axis=(1, 2, 3))
