@@ -19,6 +19,8 @@ dev = torch.device("cuda:0")
 nm = NativeModel.from_module(bench.build_model("hardnet"), dev)
 x = bench.synth_input_on_device(P, dev, 5)
 nwg, nw = 512, 4
+if os.environ["HN_C12_CFG"] == "15":
+    nwg, nw = 256, 8  # k_c12s: one 8-wave workgroup per CU
 ws = torch.zeros(nm.workspace_bytes(P) + nwg * nw * 1024, dtype=torch.uint8, device=dev)
 out = torch.empty((P, 128), device=dev)
 for _ in range(2):
@@ -28,6 +30,19 @@ torch.cuda.synchronize()
 # a2, and the stamps go past a5 (out + P * 24576 floats)
 off = (16384 * P + 24576 * P) * 4
 raw = ws[off: off + nwg * nw * 128 * 8].view(torch.int64).cpu().numpy().reshape(nwg, nw, 128)
+if nw == 8:  # k_c12s: per step, A-waves (start, P2 end, past the barrier), B-waves (start, flush, P3, P1, norm, barrier)
+    t = raw[:, :, :48].reshape(nwg, nw, 8, 6).astype(np.float64)
+    ok = (t[:, :4, :, :3] > 0).all(axis=(1, 2, 3)) & (t[:, 4:] > 0).all(axis=(1, 2, 3))
+    t = t[ok]
+    a, b = t[:, :4], t[:, 4:]
+    step = np.median(b[:, :, 1:, 0] - b[:, :, :-1, 0])
+    print(f"{ok.sum()} workgroups; median cycles per step: {step:.0f}")
+    da = np.diff(a[..., :3], axis=3)
+    print(f"  A: P2 {np.median(da[..., 0]):.0f}  barrier wait {np.median(da[..., 1]):.0f}")
+    db = np.diff(b, axis=3)
+    for i, n in enumerate(["flush", "P3", "P1", "norm", "barrier wait"]):
+        print(f"  B: {n:14s} {np.median(db[..., i]):8.0f}  (p90 {np.percentile(db[..., i], 90):8.0f})")
+    sys.exit(0)
 t = raw[:, :, :48].reshape(nwg, nw, 8, 6).astype(np.float64)
 ok = (t > 0).all(axis=(1, 2, 3))
 t = t[ok]
