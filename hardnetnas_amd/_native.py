@@ -380,7 +380,9 @@ class HardNetLossFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, anchor, positive, anchor_swap, margin, loss_type):
         lib = load_library()
-        a, p = anchor.detach().contiguous(), positive.detach().contiguous()
+        # the C ABI takes 16-byte aligned rows: a contiguous view at an odd storage offset is copied
+        a, p = (x if x.data_ptr() % 16 == 0 else x.clone() for x in
+                (anchor.detach().contiguous(), positive.detach().contiguous()))
         b = a.shape[0]
         n = ctypes.c_size_t()
         _check(lib.hn_hardnet_loss_train_workspace_bytes(b, ctypes.byref(n)), "hn_hardnet_loss_train_workspace_bytes")
@@ -397,6 +399,7 @@ class HardNetLossFunction(torch.autograd.Function):
         return loss
 
     @staticmethod
+    @torch.autograd.function.once_differentiable  # the fused backward records no graph (no double backward)
     def backward(ctx, dloss):
         lib = load_library()
         a, p, saved = ctx.saved_tensors

@@ -10,7 +10,9 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));  // arithmetic on it em
 #define HN_DEV __device__ __forceinline__
 
 // ReLU as one integer max: every float with the sign bit set (negative, -0, -NaN) is a negative int, so
-// max_i32(bits, 0) = max(x, +0) for each non-NaN x (a +NaN passes through, as torch.relu's does).
+// max_i32(bits, 0) = max(x, +0) for each non-NaN x (a +NaN passes through, as torch.relu's does; a NaN
+// with the sign bit set becomes +0 where torch.relu would propagate it -- a divergence only for -NaN
+// activations, which the eval path's finite weights and inputs do not produce).
 // fmaxf(x, 0.f) costs two v_max_f32 when x comes from an MFMA or a load: the compiler first quiets a
 // possible signalling NaN (v_max_f32 x, x, x), which was 5-8 % of the fused kernels' instructions.
 HN_DEV float relu0(float x) { return __builtin_bit_cast(float, __builtin_elementwise_max(__builtin_bit_cast(int, x), 0)); }

@@ -18,7 +18,10 @@
 // sqrt(u) passes g / (2 sqrt(u)) to u = |a_i|^2 + |p_j|^2 - 2 a_i.p_j + 1e-6, i.e.
 // 2 a_i - 2 p_j to a_i and 2 p_j - 2 a_i to p_j.  Row i's hardest negative (i, r_i) feeds p_{r_i},
 // the column minimum (c_i, i) feeds a_{c_i}: the gather kernel gives each target row the terms
-// of every source that selected it, in increasing source order (deterministic, no atomics).
+// of every source that selected it, in increasing source order (deterministic: the per-target source
+// lists are built by a counting pass, a scan and an unordered fill, and each target's wave orders its
+// list before summing -- O(B) work for any selection pattern but a target with > 64 sources, which
+// scans all sources in order).
 #include "hn_common.h"
 #include "hn_internal.h"
 
@@ -39,15 +42,27 @@ __global__ __launch_bounds__(256) void k_lmin_init(unsigned long long* __restric
   for (int i = blockIdx.x * 256 + threadIdx.x; i < B; i += gridDim.x * 256) colbest[i] = ~0ull;
 }
 
-// |v|^2 of every row (a then p), one wave per row
+// |v|^2 of every row (a then p), one wave per row; for w < B also the positive distance d_ii from
+// |a_i - p_i|^2 directly: the expanded |a|^2 + |p|^2 - 2 a.p of the distance matrix cancels for the
+// close pairs of a training batch (the reference's fp32 loss carries that error: 2e-6 on a mean of
+// distances), the difference form keeps d_ii at fp32 accuracy
+HN_DEV float diff_sq(const float* a, const float* p, int lane) {
+  const float2 u = reinterpret_cast<const float2*>(a)[lane], v = reinterpret_cast<const float2*>(p)[lane];
+  const float dx = u.x - v.x, dy = u.y - v.y;
+  return wave_sum(fmaf(dx, dx, dy * dy));
+}
 __global__ __launch_bounds__(256) void k_lmin_sq(const float* __restrict__ a, const float* __restrict__ p, int B,
-                                                 float* __restrict__ sq) {
+                                                 float* __restrict__ sq, float* __restrict__ pos) {
   const int w = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (w >= 2 * B) return;
   const float* r = (w < B ? a + (size_t)w * D : p + (size_t)(w - B) * D);
   const float2 v = reinterpret_cast<const float2*>(r)[lane];
   const float s = wave_sum(v.x * v.x + v.y * v.y);
   if (lane == 0) sq[w] = s;
+  if (w < B) {
+    const float x = diff_sq(a + (size_t)w * D, p + (size_t)w * D, lane);
+    if (lane == 0) pos[w] = sqrtf(x + 1e-6f) + 1e-8f;
+  }
 }
 
 // One workgroup per 64 anchors, all positives in 64-column tiles.  Thread (ty, tx) computes the
@@ -114,10 +129,7 @@ __global__ __launch_bounds__(256) void k_lmin_tiles(const float* __restrict__ a,
         const float x = (asq[r] + psq) - 2.0f * acc[r][c];
         const float d = sqrtf(x + 1e-6f) + 1e-8f;
         float dn = d;
-        if (i == j) {
-          pos[i] = d;
-          dn = d + 10.0f;
-        }
+        if (i == j) dn = d + 10.0f;  // (pos[i] comes from k_lmin_sq's difference form)
         if (dn < 0.008f) dn += 10.0f;
         best[r] = umin64(best[r], key_of(dn, j));
         if (swap) cb[c] = umin64(cb[c], key_of(dn, i));
@@ -174,21 +186,24 @@ __global__ __launch_bounds__(1024) void k_lmin_finish(const unsigned long long* 
                                                       const unsigned long long* __restrict__ colbest,
                                                       const float* __restrict__ pos, int B, int swap, float margin,
                                                       int type, float* __restrict__ loss) {
-  __shared__ float part[16];
-  float s = 0.f;
+  // the per-row losses in fp32 (as the reference computes them), their sum in fp64 in a fixed order,
+  // so the mean carries no summation error of its own (the reference's fp32 torch.mean does)
+  __shared__ double part[16];
+  double s = 0.0;
   for (int i = threadIdx.x; i < B; i += 1024) {
     const float vr = key_val(rowbest[i]);
     const float mn = swap ? fminf(vr, key_val(colbest[i])) : vr;
     float dp, dm;
-    s += loss_of(type, margin, pos[i], mn, &dp, &dm);
+    s += (double)loss_of(type, margin, pos[i], mn, &dp, &dm);
   }
-  s = wave_sum(s);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
   if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
   __syncthreads();
   if (threadIdx.x == 0) {
-    float t = 0.f;
+    double t = 0.0;
     for (int w = 0; w < 16; ++w) t += part[w];
-    loss[0] = t * (1.0f / (float)B);
+    loss[0] = (float)(t / (double)B);
   }
 }
 
@@ -233,11 +248,69 @@ __global__ __launch_bounds__(256) void k_lmin_bwd_src(const float* __restrict__ 
   const int r = key_idx(rowbest[i]);
   const int c = swap ? key_idx(colbest[i]) : 0;
   const float gp = g * dp, gn = g * dm;
-  coef[3 * i + 0] = gp != 0.f ? gp * half_rsq(a, p, sq, B, i, i) : 0.f;
+  // the positive entry: sqrt's backward at the difference form of k_lmin_sq (the forward's d_ii)
+  float cp = 0.f;
+  if (gp != 0.f) {
+    const float* ai = a + (size_t)i * D;
+    const float* pi = p + (size_t)i * D;
+    float x = 0.f;
+    for (int k = 0; k < D; ++k) {
+      const float dd = ai[k] - pi[k];
+      x = fmaf(dd, dd, x);
+    }
+    cp = gp * (0.5f / sqrtf(x + 1e-6f));
+  }
+  coef[3 * i + 0] = cp;
   coef[3 * i + 1] = gn * fr != 0.f ? gn * fr * half_rsq(a, p, sq, B, i, r) : 0.f;
   coef[3 * i + 2] = gn * (1.f - fr) != 0.f ? gn * (1.f - fr) * half_rsq(a, p, sq, B, c, i) : 0.f;
   idx[2 * i + 0] = r;
   idx[2 * i + 1] = c;
+}
+
+// Per-target source lists.  Target t < B is anchor t (sources k with a column negative c_k = t, coef
+// slot 2; only with anchor_swap), t >= B positive t - B (sources with a row negative r_k = t - B, slot 1).
+HN_DEV int src_target(const float* coef, const int* idx, int k, int slot, int B) {  // -1: no term
+  if (coef[3 * k + 1 + slot] == 0.f) return -1;
+  return slot ? idx[2 * k + 1] : B + idx[2 * k];
+}
+__global__ __launch_bounds__(256) void k_lmin_bwd_count(const float* __restrict__ coef, const int* __restrict__ idx,
+                                                        int B, int swap, int* __restrict__ cnt) {
+  for (int k = blockIdx.x * 256 + threadIdx.x; k < B; k += gridDim.x * 256)
+    for (int slot = 0; slot < 1 + swap; ++slot) {
+      const int tg = src_target(coef, idx, k, slot, B);
+      if (tg >= 0) atomicAdd(cnt + tg, 1);
+    }
+}
+// exclusive scan of cnt[n] -> off[n] in one workgroup (contiguous chunk per thread); fill[] := 0
+__global__ __launch_bounds__(1024) void k_lmin_bwd_scan(const int* __restrict__ cnt, int n, int* __restrict__ off,
+                                                        int* __restrict__ fill) {
+  __shared__ int tot[1024];
+  const int tid = threadIdx.x, per = (n + 1023) / 1024, b0 = min(n, tid * per), b1 = min(n, b0 + per);
+  int s = 0;
+  for (int i = b0; i < b1; ++i) s += cnt[i];
+  tot[tid] = s;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {  // inclusive scan of the thread totals
+    const int v = tid >= o ? tot[tid - o] : 0;
+    __syncthreads();
+    tot[tid] += v;
+    __syncthreads();
+  }
+  int run = tot[tid] - s;
+  for (int i = b0; i < b1; ++i) {
+    off[i] = run;
+    run += cnt[i];
+    fill[i] = 0;
+  }
+}
+__global__ __launch_bounds__(256) void k_lmin_bwd_fill(const float* __restrict__ coef, const int* __restrict__ idx,
+                                                       int B, int swap, const int* __restrict__ off,
+                                                       int* __restrict__ fill, int* __restrict__ list) {
+  for (int k = blockIdx.x * 256 + threadIdx.x; k < B; k += gridDim.x * 256)
+    for (int slot = 0; slot < 1 + swap; ++slot) {
+      const int tg = src_target(coef, idx, k, slot, B);
+      if (tg >= 0) list[off[tg] + atomicAdd(fill + tg, 1)] = k;  // unordered; the gather orders it
+    }
 }
 
 // one wave per target row: t < B the anchor gradient of row t, else the positive gradient of row
@@ -245,8 +318,9 @@ __global__ __launch_bounds__(256) void k_lmin_bwd_src(const float* __restrict__ 
 // whose selected negative lies in the target's row / column, in increasing source order.
 __global__ __launch_bounds__(256) void k_lmin_bwd_gather(const float* __restrict__ a, const float* __restrict__ p,
                                                          int B, int swap, const float* __restrict__ coef,
-                                                         const int* __restrict__ idx, float* __restrict__ ga,
-                                                         float* __restrict__ gp) {
+                                                         const int* __restrict__ idx, const int* __restrict__ cnt,
+                                                         const int* __restrict__ off, const int* __restrict__ list,
+                                                         float* __restrict__ ga, float* __restrict__ gp) {
   const int t = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (t >= 2 * B) return;
   const bool anc = t < B;
@@ -268,7 +342,18 @@ __global__ __launch_bounds__(256) void k_lmin_bwd_gather(const float* __restrict
   if (cown != 0.f) add(cown, other(idx[2 * i + (anc ? 0 : 1)]));
   // scattered terms: anchor i collects column negatives with c_k = i; positive j row negatives with r_k = j
   const int slot = anc ? 1 : 0;
-  if (!anc || swap) {
+  const int n = cnt[t];  // sources that selected an entry of this target (wave-uniform)
+  if (n > 0 && n <= 64) {
+    // the list in increasing source order: lane j holds source s_j, its rank = #{sources < s_j}
+    const int sj = lane < n ? list[off[t] + lane] : 0x7fffffff;
+    int rank = 0;
+    for (int o = 0; o < n; ++o) rank += __shfl(sj, o, 64) < sj ? 1 : 0;
+    for (int r = 0; r < n; ++r) {
+      const unsigned long long m = __ballot(lane < n && rank == r);
+      const int kk = __shfl(sj, __ffsll((unsigned long long)m) - 1, 64);
+      add(coef[3 * kk + 1 + slot], other(kk));
+    }
+  } else if (n > 64) {  // a heavily selected target: every source, in order
     for (int k0 = 0; k0 < B; k0 += 64) {
       const int k = k0 + lane;
       const bool hit = k < B && idx[2 * k + slot] == i && coef[3 * k + 1 + slot] != 0.f;
@@ -287,10 +372,10 @@ __global__ __launch_bounds__(256) void k_lmin_bwd_gather(const float* __restrict
 }  // namespace
 
 // saved layout (hn_loss_train_saved_bytes): sq [2B] f32 | rowbest [B] u64 | colbest [B] u64 |
-// pos [B] f32 | coef [3B] f32 | idx [2B] i32
+// pos [B] f32 | coef [3B] f32 | idx [2B] i32 | cnt, off, fill, list [2B] i32 (the backward's source lists)
 size_t hn_loss_train_saved_bytes(long B) {
   auto al = [](size_t n) { return (n + 255) / 256 * 256; };
-  return al(2 * B * 4) + 2 * al(B * 8) + al(B * 4) + al(3 * B * 4) + al(2 * B * 4);
+  return al(2 * B * 4) + 2 * al(B * 8) + al(B * 4) + al(3 * B * 4) + 5 * al(2 * B * 4);
 }
 
 namespace {
@@ -300,6 +385,7 @@ struct LossSaved {
   float* pos;
   float* coef;
   int* idx;
+  int *cnt, *off, *fill, *list;
 };
 LossSaved loss_saved(void* ws, long B) {
   auto al = [](size_t n) { return (n + 255) / 256 * 256; };
@@ -316,6 +402,14 @@ LossSaved loss_saved(void* ws, long B) {
   s.coef = reinterpret_cast<float*>(c);
   c += al(3 * B * 4);
   s.idx = reinterpret_cast<int*>(c);
+  c += al(2 * B * 4);
+  s.cnt = reinterpret_cast<int*>(c);
+  c += al(2 * B * 4);
+  s.off = reinterpret_cast<int*>(c);
+  c += al(2 * B * 4);
+  s.fill = reinterpret_cast<int*>(c);
+  c += al(2 * B * 4);
+  s.list = reinterpret_cast<int*>(c);
   return s;
 }
 }  // namespace
@@ -323,7 +417,7 @@ LossSaved loss_saved(void* ws, long B) {
 hipError_t hn_launch_loss_train_fwd(const float* a, const float* p, int B, int swap, float margin, int type,
                                     float* loss, void* saved, hipStream_t st) {
   const LossSaved s = loss_saved(saved, B);
-  hipLaunchKernelGGL(k_lmin_sq, dim3((2 * B + 3) / 4), dim3(256), 0, st, a, p, B, s.sq);
+  hipLaunchKernelGGL(k_lmin_sq, dim3((2 * B + 3) / 4), dim3(256), 0, st, a, p, B, s.sq, s.pos);
   if (swap) hipLaunchKernelGGL(k_lmin_init, dim3(std::min((B + 255) / 256, 1024)), dim3(256), 0, st, s.colbest, B);
   hipLaunchKernelGGL(k_lmin_tiles, dim3((B + TM - 1) / TM), dim3(256), 0, st, a, p, s.sq, B, swap, s.rowbest,
                      s.colbest, s.pos);
@@ -337,7 +431,12 @@ hipError_t hn_launch_loss_train_bwd(const float* a, const float* p, int B, int s
   const LossSaved s = loss_saved(saved, B);
   hipLaunchKernelGGL(k_lmin_bwd_src, dim3((B + 255) / 256), dim3(256), 0, st, a, p, s.sq, s.rowbest, s.colbest,
                      s.pos, B, swap, margin, type, dloss, s.coef, s.idx);
-  hipLaunchKernelGGL(k_lmin_bwd_gather, dim3((2 * B + 3) / 4), dim3(256), 0, st, a, p, B, swap, s.coef, s.idx, ga,
-                     gp);
+  const int g = std::min((B + 255) / 256, 2048);
+  if (hipError_t e = hipMemsetAsync(s.cnt, 0, sizeof(int) * 2 * (size_t)B, st)) return e;
+  hipLaunchKernelGGL(k_lmin_bwd_count, dim3(g), dim3(256), 0, st, s.coef, s.idx, B, swap, s.cnt);
+  hipLaunchKernelGGL(k_lmin_bwd_scan, dim3(1), dim3(1024), 0, st, s.cnt, 2 * B, s.off, s.fill);
+  hipLaunchKernelGGL(k_lmin_bwd_fill, dim3(g), dim3(256), 0, st, s.coef, s.idx, B, swap, s.off, s.fill, s.list);
+  hipLaunchKernelGGL(k_lmin_bwd_gather, dim3((2 * B + 3) / 4), dim3(256), 0, st, a, p, B, swap, s.coef, s.idx, s.cnt,
+                     s.off, s.list, ga, gp);
   return hipGetLastError();
 }

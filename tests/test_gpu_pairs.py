@@ -132,7 +132,8 @@ def test_fused_train_loss_matches_reference_backward(swap, loss_type, cuda_devic
     """loss_HardNet 'min' on HIP tensors runs hn_hardnet_loss_train_forward / hn_hardnet_loss_backward
     (no B x B matrix): loss and d loss / d (anchor, positive) against the reference's fp64 step
     (tests/golden/loss_modes.npz: a masked near-duplicate and a zero positive distance included);
-    loss <= 1e-6 and gradients L2-relative <= 1e-5 (or 3x the reference's own fp32 error on each).  Run twice:
+    loss <= max(1e-6, the reference's own fp32 error) and gradients L2-relative <= 1e-5 (or 3x the
+    reference's own fp32 error).  Run twice:
     bit-identical (no atomics in the backward)."""
     from fixtures import load
     from hardnetnas_amd.losses import loss_HardNet
@@ -151,8 +152,10 @@ def test_fused_train_loss_matches_reference_backward(swap, loss_type, cuda_devic
     ref = fx[f"g_{tag}"].astype(np.float64)
     eg = np.linalg.norm(res[0][1] - ref) / np.linalg.norm(ref)
     print(f"{tag}: loss {el:.2e}, grad L2-rel {eg:.2e} (reference fp32: {float(fx[f'g32err_{tag}']):.2e})")
-    # the reference's own fp32 loss is 2e-6 off its fp64 value for 'contrastive' (a mean of distances)
-    assert el <= max(1e-6, 3 * abs(float(fx[f"min_{tag}_32"]) - float(fx[f"min_{tag}_64"])))
+    # the per-row losses are fp32 as the reference's, their mean is summed in fp64: the loss must be as
+    # close to the fp64 reference as the reference's own fp32 step is (2e-6 for 'contrastive', a mean of
+    # distances)
+    assert el <= max(1e-6, 1.0 * abs(float(fx[f"min_{tag}_32"]) - float(fx[f"min_{tag}_64"])))
     assert eg <= max(1e-5, 3 * float(fx[f"g32err_{tag}"]))
 
 
@@ -174,3 +177,39 @@ def test_fused_train_loss_matches_autograd_on_gpu(b, cuda_device):
     eg = ((out[True][1] - out[False][1]).norm() / out[False][1].norm()).item()
     print(f"B={b}: loss rel {el:.2e}, grad L2-rel {eg:.2e}")
     assert el <= 1e-5 and eg <= 1e-4
+
+
+@pytest.mark.parametrize("swap", [True, False])
+@pytest.mark.parametrize("loss_type", ["triplet_margin", "contrastive"])
+def test_fused_train_loss_ties(swap, loss_type, cuda_device):
+    """Hand-built ties: duplicated positives make two columns of a row exactly equal, and
+    duplicated anchors make a column's minimum appear in two rows of different 64-row workgroups (B = 200),
+    so the first-index rule of the u64 atomicMin keys is exercised across workgroups; duplicated pairs also
+    make the row and the column minimum of a row equal (anchor_swap's 0.5 / 0.5 split).  Loss and
+    gradients against the module formulation in fp64 (hardnetnas_amd.losses, fused=False); a heavily
+    selected target (one positive picked by every row) exercises the gather's long-list path."""
+    from hardnetnas_amd.losses import loss_HardNet
+    g = torch.Generator().manual_seed(7)
+    b = 200
+    unit = lambda v: torch.nn.functional.normalize(v, dim=-1)  # noqa: E731
+    c = unit(torch.randn(128, generator=g))
+    a = unit(c + 0.5 * unit(torch.randn(b, 128, generator=g)))   # anchors clustered around c
+    p = unit(a + 0.3 * unit(torch.randn(b, 128, generator=g)))
+    p[150] = p[20]          # equal columns 20 / 150 for every row (tie across column tiles)
+    a[130] = a[10]          # equal rows 10 / 130 (different 64-row workgroups)
+    a[77], p[77] = a[5].clone(), p[5].clone()  # a duplicated pair: row / column minima tie
+    a2, p2 = a.clone(), p.clone()
+    p2[3] = c               # case 2: the cluster centre is every anchor's hardest negative (long list)
+    for aa, pp in ((a, p), (a2, p2)):
+        x = aa.to(cuda_device).requires_grad_(True)
+        y = pp.to(cuda_device).requires_grad_(True)
+        loss = loss_HardNet(x, y, anchor_swap=swap, loss_type=loss_type)
+        loss.backward()
+        x64 = aa.double().requires_grad_(True)
+        y64 = pp.double().requires_grad_(True)
+        ref = loss_HardNet(x64, y64, anchor_swap=swap, loss_type=loss_type, fused=False)
+        ref.backward()
+        assert abs(loss.item() - ref.item()) <= 1e-5
+        gr = torch.cat([x64.grad, y64.grad]).float()
+        gg = torch.cat([x.grad, y.grad]).cpu()
+        assert (gg - gr).norm() / gr.norm() <= 1e-4, float((gg - gr).norm() / gr.norm())
