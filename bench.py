@@ -608,6 +608,10 @@ def run(opts, world, rank, local, dev, on_gpu, backend):
                 else:
                     roof = {"bound": "mfma", "kernel": dom, "achieved": round(mfma_tf, 2),
                             "peak": round(PEAK_BF16X3, 1), "unit": "TFLOP/s", "frac": round(mfma_frac, 4)}
+                fracs = {"mfma": mfma_frac, "hbm": hbm_frac, "valu_issue": valu_frac or 0.0}
+                top = max(fracs, key=fracs.get)
+                # what binds the stage: the resource nearest its roof, or latency when none is at half of it
+                roof["binding_counter"] = top if fracs[top] >= 0.5 else "latency (MFMA, HBM and VALU issue all < 0.5)"
                 roof.update({"mfma_tflops": round(mfma_tf, 2), "mfma_frac": round(mfma_frac, 4),
                              "hbm_gbps": round(hbm_gbps, 1), "hbm_frac": round(hbm_frac, 4),
                              "hbm_bytes_basis": "PMC" if traffic else "algorithmic",
@@ -680,6 +684,111 @@ def run(opts, world, rank, local, dev, on_gpu, backend):
             result["check"] = check
     del nm, ws, out, x
     return result
+
+
+TRAIN_PAIRS = 512  # the reference training loop's --batch-size (hardnet/HardNet.py:98)
+PEAK_F32 = 157.3   # TFLOP/s, the f32-input MFMA (= the f32 vector peak): the train kernels' exact fp32 products
+
+
+def cpu_baseline_train(seconds: float = 6.0, pairs: int = 64):
+    """The oracle's train step on the host cores (the cgroup quota's thread count): hardnet_train_forward
+    of anchors and positives (batch statistics, running-stat update), the oracle loss_hardnet
+    (anchor_swap, triplet margin), autograd backward and the reference's SGD step, on a bounded batch of
+    ``pairs`` pairs; patches/s = 2 pairs / step time (median over the runs)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from oracle import hardnet_oracle as O
+    torch.manual_seed(0)
+    m = HardNet()
+    p = {k: v.detach().clone().requires_grad_(k.endswith("weight")) for k, v in m.state_dict().items()}
+    run = {k: v for k, v in p.items() if "running" in k}
+    opt = torch.optim.SGD([v for k, v in p.items() if v.requires_grad], lr=1.0, momentum=0.9, dampening=0.9,
+                          weight_decay=1e-4)
+    xa = torch.from_numpy(synth.synth_patches(pairs, seed=21))
+    xp = xa + 0.3 * torch.from_numpy(synth.synth_patches(pairs, seed=22))
+    quota = _cpu_quota()
+    nproc = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    threads = max(1, int(quota)) if 0 < quota < nproc else nproc
+    torch.set_num_threads(threads)
+
+    def step():
+        out_a = O.hardnet_train_forward(p, xa, run)
+        out_p = O.hardnet_train_forward(p, xp, run)
+        loss = O.loss_hardnet(out_a, out_p, anchor_swap=True)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+
+    step()
+    rates, t_start = [], time.perf_counter()
+    while time.perf_counter() - t_start < seconds or len(rates) < 3:
+        t0 = time.perf_counter()
+        step()
+        rates.append(2 * pairs / (time.perf_counter() - t0))
+    return {"value": round(statistics.median(rates), 1), "unit": "patches/s", "cores": threads, "kind": "port",
+            "model": _cpu_model_string(),
+            "sample": f"oracle/hardnet_oracle.py train step (hardnet_train_forward x2 + loss_hardnet + autograd "
+                      f"backward + SGD) at {pairs} pairs, {len(rates)} steps over ~{seconds:.0f} s, median"}
+
+
+def run_train(opts, dev, with_cpu: bool):
+    """The reference training loop's step (hardnet/HardNet.py:379-441) on the HIP train path: model.train()
+    forward of anchors and of positives (two calls, batch statistics), loss_HardNet (anchor_swap, triplet
+    margin, batch_reduce min: the fused hn_loss.hip kernels), backward, SGD (lr 1, momentum 0.9, dampening
+    0.9, weight decay 1e-4: create_optimizer, :492-504), at the reference's batch of 512 pairs."""
+    from hardnetnas_amd.losses import loss_HardNet
+    torch.manual_seed(0)
+    m = HardNet().to(dev).train()
+    opt = torch.optim.SGD(m.features.parameters(), lr=1.0, momentum=0.9, dampening=0.9, weight_decay=1e-4)
+    b = TRAIN_PAIRS
+    xa = synth_input_on_device(b, dev, seed=31)
+    xp = xa + 0.3 * synth_input_on_device(b, dev, seed=32)
+    last = {}
+
+    def step():
+        out_a = m(xa)
+        out_p = m(xp)
+        loss = loss_HardNet(out_a, out_p, anchor_swap=True)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        last["loss"] = loss
+
+    steps, warmup = max(10, opts.steps), max(2, opts.warmup)
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    t0 = time.perf_counter()
+    ev[0].record()
+    for _ in range(steps):
+        step()
+    ev[1].record()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    ms = elapsed / steps * 1e3
+    # algorithmic work: forward + data gradient + weight gradient of every conv = 3 x the forward MACs
+    flop = 3 * flop_per_patch("hardnet") * 2 * b
+    achieved = flop / (ev[0].elapsed_time(ev[1]) / steps * 1e-3) / 1e12
+    res = {"value": round(2 * b * steps / elapsed / 1e6, 4), "unit": "Mpatches/s", "ms_per_step": round(ms, 3),
+           "steps": steps, "warmup": warmup, "dtype": "f32",
+           "config": {"workload": f"Stock HardNet train step (HardNet.py:379-441): 2 x {b} patches, model.train() "
+                                  "forward x2, fused loss_HardNet (anchor_swap, triplet margin, min), backward, "
+                                  "SGD; orthogonal init (weights_init), synthetic pairs",
+                      "model": "hardnet", "global_batch": 2 * b, "pairs": b, "parallelism": "dp1",
+                      "precision": "exact fp32 products (f32-input MFMA), fp64 BatchNorm / split-K sums"},
+           "loss": float(last["loss"].item()),
+           "roofline": {"bound": "mfma", "kernel": "whole train step (forward, backward, BN, loss, SGD)",
+                        "achieved": round(achieved, 2), "peak": PEAK_F32, "unit": "TFLOP/s",
+                        "frac": round(achieved / PEAK_F32, 4), "traffic": None,
+                        "peak_basis": "f32 MFMA 157.3 TFLOP/s (the train kernels' exact fp32 products); "
+                                      "algorithmic FLOP = 3 x the forward's 2 x MAC per patch"},
+           "cpu_baseline": None}
+    if with_cpu:
+        cb = cpu_baseline_train()
+        res["cpu_baseline"] = cb
+        res["gpu_vs_cpu"] = round(res["value"] * 1e6 / cb["value"], 1)
+    del m, opt, xa, xp
+    return res
 
 
 # the other BASELINE configurations measured after the headline one on a default 1-GPU run
@@ -755,6 +864,8 @@ def main():
             torch.cuda.empty_cache()
             r = run(o, world, rank, local, dev, on_gpu, backend)
             result["extra_configs"][key] = {k: r[k] for k in EXTRA_KEYS if k in r}
+        torch.cuda.empty_cache()
+        result["extra_configs"]["train"] = run_train(args, dev, with_cpu=not args.no_cpu_baseline)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
