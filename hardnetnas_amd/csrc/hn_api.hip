@@ -43,7 +43,7 @@ void hn_read_knobs(HnKnobs* k) {
   k->train_splitk = std::max(32, env_int("HN_TRAIN_SPLITK", 1024)) / 32 * 32;
   k->train_f32 = env_int("HN_TRAIN_F32", 1) & 255;
 #ifdef HN_EXPERIMENTS
-  k->c12_abl = env_int("HN_C12_ABL", 0) & 255;
+  k->c12_abl = env_int("HN_C12_ABL", 0) & 4095;  // (65: k_c12s stamps with P1 on the A-waves)
   k->c12w_pd = env_int("HN_C12W_PD", 11);
   k->dbg = env_int("HN_DEBUG", 0);
 #endif
@@ -1134,7 +1134,7 @@ static bool u8_fused(const hn_model* m, int resize) {
   if (m->desc.kind == HN_KIND_FDL_NASNET || m->desc.kind == HN_KIND_FDL_NASNET01) return !m->knobs.fdl_valu;
   if (m->desc.kind == HN_KIND_NAS)  // the fused front's patch load (hn_front.hip): no input_norm, not PIL
     return resize != HN_RESIZE_PIL_BILINEAR && m->front && m->desc.input_norm_eps < 0.f && !m->knobs.front_fold;
-  return m->desc.kind == HN_KIND_HARDNET && m->c12 && !m->unfused_stem && (m->knobs.c12_cfg == 12 || m->knobs.c12_cfg == 13 || m->knobs.c12_cfg == kC12Wino) &&
+  return m->desc.kind == HN_KIND_HARDNET && m->c12 && !m->unfused_stem && (m->knobs.c12_cfg == 12 || m->knobs.c12_cfg == 13 || m->knobs.c12_cfg == kC12Wino || m->knobs.c12_cfg == kC12Split) &&
          !m->knobs.c12_abl;
 }
 

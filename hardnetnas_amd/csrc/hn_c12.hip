@@ -939,6 +939,14 @@ constexpr int kC12Cfgs = 13;
 #endif  // (P1, P3) at priority (2, 1) / (1, 2) / (2, 2): within the box noise of 12, removed
 
 bool hn_c12_cfg_ok(int cfg, int abl) {
+  if (cfg == kC12Split) {  // k_c12s (hn_c12w.hip)
+#ifdef HN_EXPERIMENTS
+    return abl == 0 || abl == 1 || abl == 2 || abl == 4 || abl == 6 || abl == 64 || abl == 65 || abl == 66 || abl == 72 ||
+           abl == 80 || abl == 84 || abl == 88 || abl == 116 || abl == 340 || abl == 576 || abl == 1088;
+#else
+    return abl == 0;
+#endif
+  }
   if (cfg == kC12Wino) {  // k_c12w (hn_c12w.hip)
 #ifdef HN_EXPERIMENTS
     return abl == 0 || abl == 1 || abl == 2 || abl == 4 || abl == 6 || abl == 64 || abl == 192;
@@ -966,6 +974,7 @@ hipError_t hn_launch_c12(const float* in, float* out, const HardnetDev& d, int P
   const int abl = hn_knobs().c12_abl;
   if (!hn_c12_cfg_ok(cfg, abl)) return hipErrorInvalidValue;
   if (cfg == kC12Wino) return hn_launch_c12w(in, out, d, P, eps, st, u8, abl);
+  if (cfg == kC12Split) return hn_launch_c12s(in, out, d, P, eps, st, u8);
   if (u8 && ((cfg != 12 && cfg != 13) || abl)) return hipErrorInvalidValue;  // the uint8 loads: production builds only
   static const void* const fns[kC12Cfgs] = {
 #define HN_C12_FN(C, W, R, E, I, A, Q, PR) reinterpret_cast<const void*>(&k_c12<0, W, R, E, I, A, Q, PR>),

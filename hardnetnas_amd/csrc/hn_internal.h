@@ -75,6 +75,10 @@ bool hn_hardnet_variant_ok(int layer, int variant);
 bool hn_c12_cfg_ok(int cfg, int abl);
 // HN_C12_CFG 14: k_c12w (hn_c12w.hip), conv1 as a 1-D Winograd F(4,3)
 constexpr int kC12Wino = 14;
+// HN_C12_CFG 15: k_c12s (hn_c12w.hip), k_c12w's arithmetic with conv1 / conv2+stem waves per SIMD
+constexpr int kC12Split = 15;
+hipError_t hn_launch_c12s(const float* in, float* out, const HardnetDev& d, int P, float eps, hipStream_t st,
+                          const HnU8In* u8);
 hipError_t hn_launch_c12w(const float* in, float* out, const HardnetDev& d, int P, float eps, hipStream_t st,
                           const HnU8In* u8, int abl);
 hipError_t hn_launch_hardnet_conv(int layer, int variant, const HardnetDev& d, const float* in,

@@ -178,8 +178,10 @@ def test_c12_variants_match(cuda_device, monkeypatch, cfg):
     assert np.abs(nm(xr).cpu().numpy() - np.tile(y0, (12, 1))[:3001]).max() <= 2e-5
 
 
-def test_c12_winograd_conv1_matches_reference(cuda_device, monkeypatch):
-    """HN_C12_CFG=14: k_c12w, conv1 as a 1-D Winograd F(4,3) (hn_c12w.hip): against the reference
+@pytest.mark.parametrize("cfg", ["14", "15"])
+def test_c12_winograd_conv1_matches_reference(cuda_device, monkeypatch, cfg):
+    """HN_C12_CFG=14: k_c12w, conv1 as a 1-D Winograd F(4,3) (hn_c12w.hip); 15: k_c12s, the same
+    arithmetic with conv1 and conv2 + stem waves per SIMD, bands software-pipelined: against the reference
     vectors (edge patches included) at the 1e-4 bar, and within 5e-5 of the direct k_c12 on ragged
     batches and a persistent run of several patches per workgroup (the transform changes the
     rounding: tests/precision/wino1d_precision.py puts it at 1.7e-5 from fp64 vs 1.0e-5 direct)."""
@@ -187,7 +189,7 @@ def test_c12_winograd_conv1_matches_reference(cuda_device, monkeypatch):
     m, fx, _ = build_module("hardnet")
     x = torch.from_numpy(golden_inputs(fx)).to(cuda_device)
     y0 = NativeModel.from_module(m, cuda_device)(x).cpu().numpy()
-    monkeypatch.setenv("HN_C12_CFG", "14")
+    monkeypatch.setenv("HN_C12_CFG", cfg)
     nm = NativeModel.from_module(m, cuda_device)
     y = nm(x).cpu().numpy()
     err, err64 = np.abs(y - fx["y"]).max(), np.abs(y - fx["y64"]).max()
