@@ -29,7 +29,7 @@ static int env_int(const char* name, int dflt) {
 
 void hn_read_knobs(HnKnobs* k) {
   *k = HnKnobs{};
-  k->c12_cfg = env_int("HN_C12_CFG", 12);
+  k->c12_cfg = env_int("HN_C12_CFG", 15);
   k->head = std::getenv("HN_HEAD_V1") ? 1 : env_int("HN_HEAD", 4);
   k->fdl_valu = std::getenv("HN_FDL_VALU") != nullptr;
   k->naive_pw = std::getenv("HN_NAIVE_PW") != nullptr;

@@ -10,7 +10,7 @@
 // Every switch selects a parity-tested alternative kernel; the ablation switches (c12_abl,
 // dbg: timing-only builds with wrong results) exist only in the HN_EXPERIMENTS library.
 struct HnKnobs {
-  int c12_cfg = 12;            // HN_C12_CFG: k_c12 configuration (0..12, all exact)
+  int c12_cfg = 15;            // HN_C12_CFG: k_c12 configuration (0..15, all within the parity bar; 15 = k_c12s)
   int head = 4;                // HN_HEAD: head GEMM form (1 k_head, 2 k_head2, 3 k_head3 LDS-DMA rings, 4 k_head4 256-patch rings)
   bool fdl_valu = false;       // HN_FDL_VALU: FDLNet front as fp32 VALU
   bool naive_pw = false;       // HN_NAIVE_PW: untiled 1x1 conv kernel
