@@ -564,6 +564,43 @@ static std::vector<uint16_t> pack_wino1(const std::vector<float>& w, int cin, in
   return out;
 }
 
+// stride-1 3x3 conv (BN folded) as 1-D Winograd F(4,3) along x (hn_wino1.hip k_conv_w4): U_xi[ky] =
+// sum_kx G[xi][kx] W[ky][kx] in fp64, bf16 hi / lo A fragments of the 16x16x32 MFMA
+// [cin/32][kx 18][cout/16][plane][lane][8] in the kernel's K-step order kx = 3 xo + ky, xi = w4_xi(xo)
+// (lane: output channel 16 nt + (lane & 15), input channels 32 cc + 8 (lane >> 4) + j)
+static std::vector<uint16_t> pack_wino4(const std::vector<float>& w, int cin, int cout) {
+  static const double G[6][3] = {{4, 0, 0},
+                                 {2.0 / 3, 2.0 / 3, 2.0 / 3},
+                                 {2.0 / 3, -2.0 / 3, 2.0 / 3},
+                                 {-8.0 / 3, -4.0 / 3, -2.0 / 3},
+                                 {-8.0 / 3, 4.0 / 3, -2.0 / 3},
+                                 {0, 0, 1}};
+  static const int XO[6] = {0, 5, 1, 2, 3, 4};
+  const int ncc = cin / 32, ntot = cout / 16;
+  std::vector<uint16_t> out((size_t)ncc * 18 * ntot * 2 * 64 * 8);
+  size_t o = 0;
+  for (int cc = 0; cc < ncc; ++cc)
+    for (int kx = 0; kx < 18; ++kx)
+      for (int nt = 0; nt < ntot; ++nt) {
+        const int xi = XO[kx / 3], ky = kx % 3;
+        uint16_t* hi = &out[o];
+        uint16_t* lo = &out[o + 64 * 8];
+        for (int lane = 0; lane < 64; ++lane)
+          for (int j = 0; j < 8; ++j) {
+            const int n = nt * 16 + (lane & 15);
+            const int c = cc * 32 + (lane >> 4) * 8 + j;
+            double u = 0;
+            for (int t = 0; t < 3; ++t) u += G[xi][t] * (double)w[((size_t)n * cin + c) * 9 + ky * 3 + t];
+            const float v = (float)u;
+            const uint16_t hv = f2bf(v);
+            hi[lane * 8 + j] = hv;
+            lo[lane * 8 + j] = f2bf(v - bf2f(hv));
+          }
+        o += 2 * 64 * 8;
+      }
+  return out;
+}
+
 #ifdef HN_EXPERIMENTS
 // stride-1 3x3 conv (BN folded) as Winograd F(2x2,3x3) U = G g G^T (fp64, then bf16 hi/lo),
 // packed as the B operand of hn_wino.hip's 32x32x16 MFMAs: [cout/32][cin/16][xi 16][plane][lane
@@ -623,6 +660,11 @@ static int build_hardnet(hn_model* m, Cursor& cur) {
       uint16_t* c = nullptr;
       if ((rc = m->upload(pack_wino1(f.w, cin[l], cout[l]), &c))) return rc;
       m->hd.wino1[l] = c;
+    }
+    if (l == 3) {  // 1-D Winograd F(4,3) U fragments (hn_wino1.hip k_conv_w4)
+      uint16_t* c = nullptr;
+      if ((rc = m->upload(pack_wino4(f.w, cin[l], cout[l]), &c))) return rc;
+      m->hd.wino4[l] = c;
     }
 #ifdef HN_EXPERIMENTS
     if (l == 3 || l == 5) {  // Winograd U fragments (experiments library only)

@@ -1865,8 +1865,9 @@ bool hn_hardnet_variant_ok(int layer, int v) {
   if (v == 15 || v == 18) return layer == 4;  // 18: outputs stored by the producer waves
   if (v >= 19 && v <= 21) return layer == 3 || layer == 5;  // 1-D Winograd F(2,3) (hn_wino1.hip), weight ring 3 / 4 / 6
   if (v == 26) return layer == 3 || layer == 5;              // the same, weight ring 8 (digit q)
+  if (v == 32 || v == 33) return layer == 3;                 // F(4,3) (k_conv_w4), weight ring 6 / 9 (digits w / x)
 #ifdef HN_EXPERIMENTS
-  if ((v >= 22 && v <= 25) || v == 29) return layer == 3 || layer == 5;  // its timing-only ablations (ABL 1 / 2 / 4 / 8; t: 16)
+  if ((v >= 22 && v <= 25) || v == 29 || v == 30 || v == 31) return layer == 3 || layer == 5;  // its timing-only ablations (ABL 1 / 2 / 4 / 8; t: 16; u: 32, v: 34)
 #endif
   if (v == 16) return layer == 3 || layer == 5;
   if (v == 0 || v == 5 || v == 6) return true;  // (layer 1 always runs conv1_launch)
@@ -1912,9 +1913,11 @@ hipError_t hn_launch_hardnet_conv(int layer, int variant, const HardnetDev& d, c
 #endif
   if (variant >= 19 && variant <= 21) return hn_launch_wino1(layer, variant == 19 ? 3 : variant == 20 ? 4 : 6, d, in, out, P, st);
   if (variant == 26) return hn_launch_wino1(layer, 8, d, in, out, P, st);
+  if (variant == 32 || variant == 33) return hn_launch_wino4(layer, variant == 32 ? 6 : 9, d, in, out, P, st);
 #ifdef HN_EXPERIMENTS
   if (variant >= 22 && variant <= 25) return hn_launch_wino1(layer, 100 + (1 << (variant - 22)), d, in, out, P, st);
   if (variant == 29) return hn_launch_wino1(layer, 116, d, in, out, P, st);
+  if (variant == 30 || variant == 31) return hn_launch_wino1(layer, variant == 30 ? 132 : 134, d, in, out, P, st);
 #endif
   if (variant == 16) {  // coalesced epilogue stores
     switch (layer) {

@@ -56,6 +56,7 @@ struct HardnetDev {
   void* c12_w1w = nullptr;   // conv1 as 1-D Winograd F(4,3) U fragments for k_c12w
   void* wino[7] = {};        // conv3 / conv5: Winograd F(2x2,3x3) U fragments (hn_wino.hip)
   void* wino1[7] = {};       // conv3 / conv5: 1-D Winograd F(2,3) U fragments (hn_wino1.hip)
+  void* wino4[7] = {};       // conv3: 1-D Winograd F(4,3) U fragments (hn_wino1.hip k_conv_w4)
 };
 // uint8 patches for the fused preprocessing load (hn_forward_u8)
 struct HnU8In {
@@ -94,6 +95,9 @@ hipError_t hn_launch_conv_raw(int layer, const void* wp, const float* zero_bias,
 hipError_t hn_launch_wino1(int layer, int wd, const HardnetDev& d, const float* in, float* out, int P,
                            hipStream_t st);
 int hn_wino1_lds_bytes(int layer);
+// conv3 as 1-D Winograd F(4,3) (hn_wino1.hip k_conv_w4; HN_VARIANT digits w / x)
+hipError_t hn_launch_wino4(int layer, int wd, const HardnetDev& d, const float* in, float* out, int P,
+                           hipStream_t st);
 // Winograd F(2x2,3x3) conv3 / conv5 (hn_wino.hip; HN_VARIANT digit h)
 hipError_t hn_launch_wino(int layer, const HardnetDev& d, const float* in, float* out, int P, hipStream_t st);
 

@@ -22,6 +22,8 @@
 // 64 bytes per position, 16-byte chunk q at q ^ (wr & 3): a 32x32x16 operand read (one M tile =
 // 32 / NTX consecutive rows x NTX column pairs) and a producer's 8-lane store group are
 // bank-conflict free (tests/test_lds_banks.py).
+#include <cstdlib>
+
 #include "hn_common.h"
 #include "hn_internal.h"
 
@@ -64,7 +66,7 @@ struct W1Cfg {
 
 // ABL (timing-only ablation builds, HN_EXPERIMENTS library only; wrong results): bit 0 idle producers
 // (barriers only), bit 1 no MFMAs (operands still loaded), bit 2 no weight loads (K-step 0's fragments
-// reused), bit 3 no epilogue stores, bit 4 idle MFMA waves
+// reused), bit 3 no epilogue stores, bit 4 idle MFMA waves, bit 5 no weight loads after the prologue
 template <int CIN, int COUT, int H, int NP, int WM, int WN, bool CST, int WD = 3, int ABL = 0>
 __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_w1(const float* __restrict__ in, float* __restrict__ out,
                                                                 const uint4* __restrict__ wp,
@@ -272,7 +274,8 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_w1(const float* __r
     load_a(0, aq[0]);
 #pragma unroll
     for (int kx = 0; kx < C::NKS; ++kx) {
-      if (kx + WD - 1 < C::NKS)
+      if constexpr ((ABL & 32) != 0) {  // timing only: no weight loads after the prologue
+      } else if (kx + WD - 1 < C::NKS)
         load_b(cc, kx + WD - 1, bq[(kx + WD - 1) % WD]);
       else  // the next stage's first fragments, unconditionally (valid weights even after the last
             // stage): a branch here made the compiler's vmcnt merge wait vmcnt(0) at the stage's end
@@ -385,6 +388,361 @@ hipError_t launch_w1(const float* in, float* out, const void* wp, const float* b
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------------------
+// F(4,3) along x (k_conv_w4): per output row y and column quad (4t .. 4t+3), d_k = x[y + ky - 1][4t - 1 + k]
+// (k = 0..5, zero outside the patch), Toom-Cook points 0, 1, -1, 1/2, -1/2, infinity:
+//   V = B^T d:  V0 = d0/4 - 5 d2/4 + d4            V1 = -(d1 + d2)/4 + d3 + d4
+//               V2 = (d1 - d2)/4 - d3 + d4          V3 = d4 - d2 - (d1 - d3)/2
+//               V4 = d4 - d2 + (d1 - d3)/2          V5 = d1/4 - 5 d3/4 + d5
+//   U_xi[ky] = sum_kx G[xi][kx] W[ky][kx],  G = [4 0 0; 2/3 2/3 2/3; 2/3 -2/3 2/3; -8/3 -4/3 -2/3; -8/3 4/3 -2/3; 0 0 1]
+//   y0 = m0 + m1 + m2 + m3 + m4,  y1 = m1 - m2 + (m3 - m4)/2,  y2 = m1 + m2 + (m3 + m4)/4,
+//   y3 = m1 - m2 + (m3 - m4)/8 + m5                                                   (A^T m)
+// 18 multiplies per output quad and input channel instead of 36 (F(2,3): 24): the layer's MFMA work is
+// 3/4 of the F(2,3) kernel's and so is the weight stream per patch (precision: tests/precision/
+// wino1d_precision.py "1:4 3:4 5:2", 1.9e-5 from fp64 against 1.7e-5 for the F(2,3) form).
+// Same producer / MFMA wave split as k_conv_w1, but the MFMAs are 16x16x32 with the weights as the A
+// operand (16 output channels x 32 input channels) and the transformed positions as B: each MFMA wave
+// owns 16 output channels of every position of the tile (M = 64 positions = 4 B tiles), so a weight
+// fragment is used by 4 MFMAs (k_conv_w1: 2) -- the weight stream that bounds k_conv_w1 drops to half
+// per MFMA -- and the result lanes hold 4 consecutive channels of one pixel (16-byte stores, no LDS
+// transpose).  Operand image per plane: [patch][xi][row -1 .. H][quad][32 channels bf16], zero rows -1
+// and H inside every (patch, xi) block, 256-byte rows, 16-byte chunk c of row r at c ^ 2 (r & 1):
+// the B-operand reads (lane l: position l & 15, chunk l >> 4) and the producers' 8-lane store groups
+// are bank-conflict free (tests/test_lds_banks.py).
+// Accumulation: m0 into Y0, m5 into Y3 (xi order 0, 5, 1, 2, 3, 4), m1..m4 each into one of two
+// temporaries that is folded into Y0..Y3 (A^T coefficients) over the next xi's three K-steps, so that
+// no fold waits on the MFMA that produced its temporary.
+template <int CIN, int COUT, int H, int NP, int WN>
+struct W4Cfg {
+  static constexpr int NTX = H / 4;           // column quads per row
+  static constexpr int POS = NP * H * NTX;    // positions per xi and work tile
+  static constexpr int MT = POS / 16;         // 16-position B tiles
+  static constexpr int NCC = CIN / 32;        // 32-channel stages
+  static constexpr int NT = COUT / 16 / WN;   // 16-channel output tiles per MFMA wave
+  static constexpr int RB = NTX * 64;         // bytes per image row
+  static constexpr int HR = H + 2;            // image rows per (patch, xi) block
+  static constexpr int XB = HR * RB;          // bytes per (patch, xi) block
+  static constexpr int PLANE = NP * 6 * XB;
+  static constexpr int BUF = 2 * PLANE;
+  static constexpr int NWC = WN, NWP = 4, NTHR = (NWC + NWP) * 64, PTHR = NWP * 64;
+  static constexpr int UNITS = NP * H * NTX * 4;  // (patch, row, quad, 8-channel group)
+  static constexpr int UPT = UNITS / PTHR;
+  static constexpr bool DEEP = UPT <= 2;
+  static constexpr int SMEM = 2 * BUF;
+  static constexpr int NKS = 18;  // K-steps per stage: 6 xi x 3 ky, K = the stage's 32 channels
+  static constexpr unsigned KSTEP_BYTES = (COUT / 16) * 2 * 64 * 16;  // every output tile's hi + lo fragments
+  static constexpr unsigned CHUNK_BYTES = NKS * KSTEP_BYTES;
+  static_assert(RB == 256, "the bank-conflict argument assumes 256-byte image rows");
+  static_assert(UNITS % PTHR == 0 && UPT >= 1, "whole units per producer thread");
+  static_assert(POS % 16 == 0 && NT >= 1 && NT * WN * 16 == COUT, "tiling");
+  static_assert(SMEM <= 160 * 1024, "LDS");
+};
+
+// the K-step order's xi sequence (m0 and m5 straight into their outputs first)
+__host__ __device__ constexpr int w4_xi(int xo) { return xo == 0 ? 0 : xo == 1 ? 5 : xo - 1; }
+
+// ABL (timing-only builds, HN_EXPERIMENTS library, HN_W4_ABL): as k_conv_w1's bits 0 (idle producers),
+// 1 (no MFMAs), 4 (idle MFMA waves), 5 (no weight loads after the prologue)
+template <int CIN, int COUT, int H, int NP, int WN, int WD, int ABL = 0>
+__global__ __launch_bounds__((WN + 4) * 64) void k_conv_w4(const float* __restrict__ in, float* __restrict__ out,
+                                                           const uint4* __restrict__ wp,
+                                                           const float* __restrict__ bias, int P) {
+  using C = W4Cfg<CIN, COUT, H, NP, WN>;
+  constexpr int NTX = C::NTX;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool producer = wave >= C::NWC;
+  const int nwg = gridDim.x, rb = xcd_remap(blockIdx.x, nwg);
+  const int ntiles = (P + NP - 1) / NP;
+  const int my_tiles = rb < ntiles ? (ntiles - 1 - rb) / nwg + 1 : 0;
+  const int NS = my_tiles * C::NCC;
+  if (NS == 0) return;
+  char* const buf0 = smem;
+  char* const buf1 = smem + C::BUF;
+  auto tile_of = [&](int s) { return (rb + (s / C::NCC) * nwg) * NP; };
+
+  // the zero rows -1 and H of every (patch, xi) block, both buffers and planes
+  constexpr int ZCH = C::RB / 16, NZ = 2 * 2 * NP * 6 * 2 * ZCH;
+  for (int i = tid; i < NZ; i += C::NTHR) {
+    const int q = i % ZCH, rest = i / ZCH;
+    const int row = (rest & 1) ? C::HR - 1 : 0, blk = (rest >> 1) % (NP * 6), bp = (rest >> 1) / (NP * 6);
+    *reinterpret_cast<uint4*>(smem + bp * C::PLANE + blk * C::XB + row * C::RB + q * 16) = make_uint4(0, 0, 0, 0);
+  }
+
+  if (producer) {
+    if constexpr ((ABL & 1) != 0) {
+#pragma unroll 1
+      for (int s = 0; s <= NS; ++s) __syncthreads();
+      return;
+    }
+    // a unit (patch, row y, quad t, 8-channel group g) loads input columns 4t - 1 .. 4t + 2 (the last quad
+    // also column H - 1); d4 / d5 are the next quad's first two columns, taken from lane + 4
+    const int ptid = tid - C::NWC * 64;
+    float4 pf[C::UPT][10], pf2[C::UPT][10];
+    constexpr unsigned PATCH_BYTES = (unsigned)H * H * CIN * 4, OOB = 0x80000000u;
+    auto produce_loads = [&](int s, float4 (&d)[C::UPT][10]) {
+      const bool live = s < NS;
+      const int p0 = live ? tile_of(s) : 0;
+      const int cc = s % C::NCC;
+      const int nval = !live ? 0 : P - p0 < NP ? P - p0 : NP;
+      const __amdgpu_buffer_rsrc_t rs = make_rsrc(in + (size_t)p0 * H * H * CIN, (unsigned)nval * PATCH_BYTES);
+#pragma unroll
+      for (int k = 0; k < C::UPT; ++k) {
+        const int u = ptid + k * C::PTHR;
+        const int g = u & 3, t = (u >> 2) % NTX, rest = (u >> 2) / NTX;
+        const int y = rest % H, np = rest / H;
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+          const int x = 4 * t - 1 + j;
+          const bool ok = (j < 4 || t == NTX - 1) && (unsigned)x < (unsigned)H;
+          const unsigned vo = ok ? (unsigned)(((np * H + y) * H + x) * CIN + cc * 32 + g * 8) * 4u : OOB;
+          d[k][2 * j] = __builtin_bit_cast(float4, buf_load16(rs, vo, 0));
+          d[k][2 * j + 1] = __builtin_bit_cast(float4, buf_load16(rs, vo, 16));
+        }
+      }
+    };
+    auto shfl4 = [&](const float4& v) {
+      return make_float4(__shfl_down(v.x, 4, 64), __shfl_down(v.y, 4, 64), __shfl_down(v.z, 4, 64),
+                         __shfl_down(v.w, 4, 64));
+    };
+    auto produce_write = [&](char* dst, const float4 (&d)[C::UPT][10]) {
+#pragma unroll
+      for (int k = 0; k < C::UPT; ++k) {
+        const int u = ptid + k * C::PTHR;
+        const int g = u & 3, t = (u >> 2) % NTX, rest = (u >> 2) / NTX;
+        const int y = rest % H, np = rest / H;
+        const bool last = t == NTX - 1;
+        float4 dd[6][2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const float4 n0 = shfl4(d[k][i]), n1 = shfl4(d[k][2 + i]);  // every lane joins the shuffles
+          dd[0][i] = d[k][i];
+          dd[1][i] = d[k][2 + i];
+          dd[2][i] = d[k][4 + i];
+          dd[3][i] = d[k][6 + i];
+          dd[4][i] = last ? d[k][8 + i] : n0;
+          dd[5][i] = last ? make_float4(0.f, 0.f, 0.f, 0.f) : n1;
+        }
+        const int off = np * 6 * C::XB + (y + 1) * C::RB + t * 64 + 16 * (g ^ (2 * (y & 1)));
+#pragma unroll
+        for (int xi = 0; xi < 6; ++xi) {
+          float4 v[2];
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            auto tr = [&](float d0, float d1, float d2, float d3, float d4, float d5) {
+              switch (xi) {
+                case 0: return fmaf(0.25f, d0, fmaf(-1.25f, d2, d4));
+                case 1: return fmaf(-0.25f, d1 + d2, d3 + d4);
+                case 2: return fmaf(0.25f, d1 - d2, d4 - d3);
+                case 3: return fmaf(-0.5f, d1 - d3, d4 - d2);
+                case 4: return fmaf(0.5f, d1 - d3, d4 - d2);
+                default: return fmaf(0.25f, d1, fmaf(-1.25f, d3, d5));
+              }
+            };
+            v[i] = make_float4(tr(dd[0][i].x, dd[1][i].x, dd[2][i].x, dd[3][i].x, dd[4][i].x, dd[5][i].x),
+                               tr(dd[0][i].y, dd[1][i].y, dd[2][i].y, dd[3][i].y, dd[4][i].y, dd[5][i].y),
+                               tr(dd[0][i].z, dd[1][i].z, dd[2][i].z, dd[3][i].z, dd[4][i].z, dd[5][i].z),
+                               tr(dd[0][i].w, dd[1][i].w, dd[2][i].w, dd[3][i].w, dd[4][i].w, dd[5][i].w));
+          }
+          uint4 hi, lo;
+          split8(v[0], v[1], hi, lo);
+          *reinterpret_cast<uint4*>(dst + off + xi * C::XB) = hi;
+          *reinterpret_cast<uint4*>(dst + C::PLANE + off + xi * C::XB) = lo;
+        }
+      }
+    };
+    produce_loads(0, pf);
+    produce_write(buf0, pf);
+    produce_loads(1, pf);
+    __syncthreads();
+    if constexpr (!C::DEEP) {
+#pragma unroll 1
+      for (int s = 0; s < NS; ++s) {
+        produce_write((s & 1) ? buf0 : buf1, pf);
+        produce_loads(s + 2, pf);
+        __syncthreads();
+      }
+    } else {
+#pragma unroll 1
+      for (int s = 0; s < NS; s += 2) {
+        produce_loads(s + 2, pf2);
+        produce_write(buf1, pf);
+        __syncthreads();
+        if (s + 1 >= NS) break;
+        produce_loads(s + 3, pf);
+        produce_write(buf0, pf2);
+        __syncthreads();
+      }
+    }
+    return;
+  }
+
+  // ---- MFMA side ----
+  __syncthreads();
+  if constexpr ((ABL & 16) != 0) {
+#pragma unroll 1
+    for (int s = 0; s < NS; ++s) __syncthreads();
+    return;
+  }
+  const int h4 = lane >> 4;
+  // per-lane part of a B-operand (position) address for M tile mt and kernel row ky; xi is an immediate
+  int vo[C::MT][3];
+#pragma unroll
+  for (int mt = 0; mt < C::MT; ++mt) {
+    const int pos = mt * 16 + (lane & 15);
+    const int np = pos / (H * NTX), rem = pos % (H * NTX), y = rem / NTX, t = rem % NTX;
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+      const int r = y + ky - 1;  // input row; -1 and H are the block's zero rows
+      vo[mt][ky] = np * 6 * C::XB + (r + 1) * C::RB + t * 64 + 16 * (h4 ^ (2 * (r & 1)));
+      asm volatile("" : "+v"(vo[mt][ky]));
+    }
+  }
+  const __amdgpu_buffer_rsrc_t wr_ = make_rsrc(wp, C::NCC * C::CHUNK_BYTES);
+  const unsigned wvoff = (wave * C::NT * 2 * 64 + lane) * 16;
+  float4 bv[C::NT];
+#pragma unroll
+  for (int nt = 0; nt < C::NT; ++nt)
+    bv[nt] = *reinterpret_cast<const float4*>(bias + (wave * C::NT + nt) * 16 + 4 * h4);
+  f32x4_t Y[4][C::MT][C::NT], T[2][C::MT][C::NT];
+#pragma unroll
+  for (int mt = 0; mt < C::MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < C::NT; ++nt) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) Y[q][mt][nt] = f32x4_t{};
+      T[0][mt][nt] = T[1][mt][nt] = f32x4_t{};
+    }
+  // fold piece `part` (0: Y0, 1: Y1, 2: Y2, 3: Y3) of temporary T[ti] holding m_xi
+  auto fold = [&](int ti, int xi, int part) {
+    constexpr float cf[5][4] = {{0, 0, 0, 0}, {1, 1, 1, 1}, {1, -1, 1, -1}, {1, 0.5f, 0.25f, 0.125f},
+                                {1, -0.5f, 0.25f, -0.125f}};
+    const float c = cf[xi][part];
+#pragma unroll
+    for (int mt = 0; mt < C::MT; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < C::NT; ++nt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (c == 1.f) Y[part][mt][nt][j] += T[ti][mt][nt][j];
+          else if (c == -1.f) Y[part][mt][nt][j] -= T[ti][mt][nt][j];
+          else Y[part][mt][nt][j] = fmaf(c, T[ti][mt][nt][j], Y[part][mt][nt][j]);
+        }
+  };
+  auto load_b = [&](int cc, int kx, uint4 (&dst)[C::NT][2]) {
+#pragma unroll
+    for (int nt = 0; nt < C::NT; ++nt) {
+      const unsigned k = cc * C::CHUNK_BYTES + kx * C::KSTEP_BYTES + nt * 2 * 64 * 16;
+      dst[nt][0] = buf_load16(wr_, wvoff, k);
+      dst[nt][1] = buf_load16(wr_, wvoff, k + 64 * 16);
+    }
+  };
+  static_assert(C::NKS % WD == 0, "the weight ring runs on across stages");
+  uint4 bq[WD][C::NT][2];
+#pragma unroll
+  for (int k = 0; k + 1 < WD; ++k) load_b(0, k, bq[k]);
+#pragma unroll 1
+  for (int s = 0; s < NS; ++s) {
+    const char* cur = (s & 1) ? buf1 : buf0;
+    const int cc = s % C::NCC, ccn = (s + 1) % C::NCC;
+    const bool pend = cc != 0;  // xi 4's temporary (T[1]) of the previous stage still to fold
+    // one B fragment pair per M tile, reloaded for the next K-step right behind its own three MFMAs
+    // (12 MFMAs of cover; a second set of 32 registers went to the weight ring instead)
+    uint4 aq[C::MT][2];
+    auto load_a = [&](int kx, int mt) {
+      const int xi = w4_xi(kx / 3), ky = kx % 3;
+      const char* pa = cur + vo[mt][ky];
+      aq[mt][0] = *reinterpret_cast<const uint4*>(pa + xi * C::XB);
+      aq[mt][1] = *reinterpret_cast<const uint4*>(pa + (C::PLANE + xi * C::XB));
+    };
+#pragma unroll
+    for (int mt = 0; mt < C::MT; ++mt) load_a(0, mt);
+#pragma unroll
+    for (int kx = 0; kx < C::NKS; ++kx) {
+      if constexpr ((ABL & 32) != 0) {
+      } else if (kx + WD - 1 < C::NKS)
+        load_b(cc, kx + WD - 1, bq[(kx + WD - 1) % WD]);
+      else
+        load_b(ccn, kx + WD - 1 - C::NKS, bq[(kx + WD - 1) % WD]);
+      __builtin_amdgcn_sched_barrier(0);
+      const int xo = kx / 3, ky = kx % 3, xi = w4_xi(xo);
+#pragma unroll
+      for (int mt = 0; mt < C::MT; ++mt) {
+        const uint4 xh = aq[mt][0], xl = aq[mt][1];
+#pragma unroll
+        for (int nt = 0; nt < C::NT; ++nt) {
+          const uint4 wh = bq[kx % WD][nt][0], wl = bq[kx % WD][nt][1];
+          f32x4_t& acc = xi == 0 ? Y[0][mt][nt] : xi == 5 ? Y[3][mt][nt] : T[xo & 1][mt][nt];
+          f32x4_t a = (xo >= 2 && ky == 0) ? f32x4_t{} : acc;
+          if constexpr ((ABL & 2) != 0) {
+            acc[0] += __builtin_bit_cast(float, xh.x ^ xl.y ^ wh.z ^ wl.w);
+            continue;
+          }
+          a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(wh), as_bf16x8(xh), a, 0, 0, 0);
+          a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(wh), as_bf16x8(xl), a, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(wl), as_bf16x8(xh), a, 0, 0, 0);
+        }
+        if (kx + 1 < C::NKS) load_a(kx + 1, mt);
+      }
+      // folds, behind this K-step's MFMAs: the previous xi's temporary over this xi's three K-steps
+      if (xo >= 3) {
+        const int pxi = w4_xi(xo - 1), ti = (xo - 1) & 1;
+        if (ky == 0) { fold(ti, pxi, 0); fold(ti, pxi, 1); }
+        if (ky == 1) fold(ti, pxi, 2);
+        if (ky == 2) fold(ti, pxi, 3);
+      } else if (pend && kx < 4) {  // xi 4 of the previous stage: Y1, Y2, Y3, then Y0 (after m0's MFMAs)
+        fold(1, 4, kx == 3 ? 0 : kx + 1);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (cc == C::NCC - 1) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) fold(1, 4, q);
+      const int p0 = tile_of(s);
+#pragma unroll
+      for (int mt = 0; mt < C::MT; ++mt) {
+        const int pos = mt * 16 + (lane & 15);
+        const int np = pos / (H * NTX), rem = pos % (H * NTX), y = rem / NTX, t = rem % NTX;
+        if (NP == 1 || p0 + np < P) {
+          float* const ob = out + (((size_t)p0 + np) * H + y) * H * COUT + (size_t)(4 * t) * COUT + 4 * h4;
+#pragma unroll
+          for (int nt = 0; nt < C::NT; ++nt)
+#pragma unroll
+            for (int par = 0; par < 4; ++par) {
+              const f32x4_t& yv = Y[par][mt][nt];
+              *reinterpret_cast<float4*>(ob + par * COUT + (wave * C::NT + nt) * 16) =
+                  make_float4(relu0(yv[0] + bv[nt].x), relu0(yv[1] + bv[nt].y), relu0(yv[2] + bv[nt].z),
+                              relu0(yv[3] + bv[nt].w));
+            }
+        }
+#pragma unroll
+        for (int nt = 0; nt < C::NT; ++nt)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) Y[q][mt][nt] = f32x4_t{};
+      }
+    }
+    __syncthreads();
+  }
+}
+
+template <int CIN, int COUT, int H, int NP, int WN, int WD, int ABL = 0>
+hipError_t launch_w4(const float* in, float* out, const void* wp, const float* bias, int P, hipStream_t st) {
+  using C = W4Cfg<CIN, COUT, H, NP, WN>;
+  const void* fn = reinterpret_cast<const void*>(&k_conv_w4<CIN, COUT, H, NP, WN, WD, ABL>);
+  int resident = 0;
+  const hipError_t e = hn_resident_blocks(fn, C::NTHR, C::SMEM, &resident);
+  if (e != hipSuccess) return e;
+  const int tiles = (P + NP - 1) / NP;
+  const int grid = std::min(tiles, resident);
+  if (grid <= 0) return hipSuccess;
+  hipLaunchKernelGGL((k_conv_w4<CIN, COUT, H, NP, WN, WD, ABL>), dim3(grid), dim3(C::NTHR), C::SMEM, st, in, out,
+                     static_cast<const uint4*>(wp), bias, P);
+  return hipGetLastError();
+}
+
+using W4Conv3 = W4Cfg<64, 64, 16, 1, 4>;
+
 using W1Conv3 = W1Cfg<64, 64, 16, 1, 2, 2, true>;
 using W1Conv5 = W1Cfg<128, 128, 8, 2, 1, 4, true>;
 
@@ -402,7 +760,9 @@ hipError_t hn_launch_wino1(int layer, int wd, const HardnetDev& d, const float* 
   if (wd == 102) return launch_w1<CI, CO, HH, NPP, WMM, WNN, true, 8, 2>(in, out, d.wino1[L], d.bias[L], P, st); \
   if (wd == 104) return launch_w1<CI, CO, HH, NPP, WMM, WNN, true, 8, 4>(in, out, d.wino1[L], d.bias[L], P, st); \
   if (wd == 108) return launch_w1<CI, CO, HH, NPP, WMM, WNN, true, 8, 8>(in, out, d.wino1[L], d.bias[L], P, st); \
-  if (wd == 116) return launch_w1<CI, CO, HH, NPP, WMM, WNN, true, 8, 16>(in, out, d.wino1[L], d.bias[L], P, st);
+  if (wd == 116) return launch_w1<CI, CO, HH, NPP, WMM, WNN, true, 8, 16>(in, out, d.wino1[L], d.bias[L], P, st); \
+  if (wd == 132) return launch_w1<CI, CO, HH, NPP, WMM, WNN, true, 8, 32>(in, out, d.wino1[L], d.bias[L], P, st); \
+  if (wd == 134) return launch_w1<CI, CO, HH, NPP, WMM, WNN, true, 8, 34>(in, out, d.wino1[L], d.bias[L], P, st);
 #else
 #define HN_W1_ABL(CI, CO, HH, NPP, WMM, WNN, L)
 #endif
@@ -418,6 +778,27 @@ hipError_t hn_launch_wino1(int layer, int wd, const HardnetDev& d, const float* 
   HN_W1(5, 128, 128, 8, 2, 1, 4)
 #undef HN_W1
 #undef HN_W1_ABL
+  return hipErrorInvalidValue;
+}
+
+// conv3 as F(4,3) (k_conv_w4); wd: the weight ring depth (HN_VARIANT digit w = 6, x = 9)
+hipError_t hn_launch_wino4(int layer, int wd, const HardnetDev& d, const float* in, float* out, int P,
+                           hipStream_t st) {
+  if (P <= 0) return hipSuccess;
+  if (layer != 3 || !d.wino4[layer]) return hipErrorInvalidValue;
+#ifdef HN_EXPERIMENTS
+  if (const char* e = std::getenv("HN_W4_ABL")) {
+    switch (std::atoi(e)) {
+      case 1: return launch_w4<64, 64, 16, 1, 4, 6, 1>(in, out, d.wino4[3], d.bias[3], P, st);
+      case 2: return launch_w4<64, 64, 16, 1, 4, 6, 2>(in, out, d.wino4[3], d.bias[3], P, st);
+      case 16: return launch_w4<64, 64, 16, 1, 4, 6, 16>(in, out, d.wino4[3], d.bias[3], P, st);
+      case 32: return launch_w4<64, 64, 16, 1, 4, 6, 32>(in, out, d.wino4[3], d.bias[3], P, st);
+      case 34: return launch_w4<64, 64, 16, 1, 4, 6, 34>(in, out, d.wino4[3], d.bias[3], P, st);
+    }
+  }
+#endif
+  if (wd == 6) return launch_w4<64, 64, 16, 1, 4, 6>(in, out, d.wino4[3], d.bias[3], P, st);
+  if (wd == 9) return launch_w4<64, 64, 16, 1, 4, 9>(in, out, d.wino4[3], d.bias[3], P, st);
   return hipErrorInvalidValue;
 }
 

@@ -93,7 +93,8 @@ def test_tiling_variants_match_reference(variant, cuda_device, monkeypatch):
     assert np.abs(y - fx["y"]).max() <= TOL["hardnet"]
 
 
-@pytest.mark.parametrize("variant", ["605jig", "605gij", "605jij", "605kik", "605lil", "605qiq", "605qil"])
+@pytest.mark.parametrize("variant", ["605jig", "605gij", "605jij", "605kik", "605lil", "605qiq", "605qil",
+                                     "605wil", "605xil"])
 def test_winograd_1d_conv3_conv5_match_reference(variant, cuda_device, monkeypatch):
     """conv3 / conv5 as 1-D Winograd F(2,3) (hn_wino1.hip, HN_VARIANT digits j / k / l / q = weight
     ring depth 3 / 4 / 6 / 8) against the reference's fp32 and fp64 vectors (edge patches included) and

@@ -475,6 +475,63 @@ def test_wino1_producer_writes_conflict_free(layer):
                     assert len(slots) == 8, (layer, k, wave, xi, grp[0])
 
 
+# hn_wino1.hip k_conv_w4 (conv3 as F(4,3)): (CIN, COUT, H, NP, WN); image [patch][xi][row -1 .. H][quad]
+# [32 channels bf16], 256-byte rows, chunk c of input row r at c ^ 2 (r & 1)
+W4_CONFIGS = {"3": (64, 64, 16, 1, 4)}
+
+
+def w4_geometry(cin, cout, h, np_, wn):
+    ntx = h // 4
+    rb = ntx * 64
+    xb = (h + 2) * rb
+    return dict(ntx=ntx, h=h, rb=rb, xb=xb, mt=np_ * h * ntx // 16, units=np_ * h * ntx * 4)
+
+
+def w4_xi(xo):
+    return 0 if xo == 0 else 5 if xo == 1 else xo - 1
+
+
+@pytest.mark.parametrize("layer", sorted(W4_CONFIGS))
+def test_wino4_operand_reads_conflict_free(layer):
+    """Every 16x16x32 B-operand read of k_conv_w4 (lane: position l & 15 of M tile mt, 16-byte chunk
+    l >> 4; input row r = y + ky - 1, rows -1 / H being the (patch, xi) block's zero rows)."""
+    g = w4_geometry(*W4_CONFIGS[layer])
+    for mt in range(g["mt"]):
+        for kx in range(18):
+            xi, ky = w4_xi(kx // 3), kx % 3
+            for plane in range(2):
+                addrs = []
+                for lane in range(64):
+                    pos = mt * 16 + (lane & 15)
+                    npi, rem = divmod(pos, g["h"] * g["ntx"])
+                    y, t = divmod(rem, g["ntx"])
+                    r = y + ky - 1
+                    addrs.append(plane * 10 ** 6 + (npi * 6 + xi) * g["xb"] + (r + 1) * g["rb"] + t * 64
+                                 + 16 * ((lane >> 4) ^ (2 * (r & 1))))
+                for grp in GROUPS:
+                    distinct = {addrs[l] for l in grp}
+                    assert len(distinct) == 16
+                    assert len({(a // 16) % 16 for a in distinct}) == 16, (layer, mt, kx, grp[0])
+
+
+@pytest.mark.parametrize("layer", sorted(W4_CONFIGS))
+def test_wino4_producer_writes_conflict_free(layer):
+    """The producers' ds_write_b128 of one xi: unit u = (patch, row y, quad t, 8-channel group g) ->
+    chunk g ^ 2 (y & 1) of position t of row y; each 8-lane group covers 128 distinct bytes."""
+    g = w4_geometry(*W4_CONFIGS[layer])
+    for k in range(g["units"] // 256):
+        for wave in range(4):
+            for xi in range(6):
+                addrs = []
+                for lane in range(64):
+                    u = wave * 64 + lane + k * 256
+                    gg, t, rest = u & 3, (u >> 2) % g["ntx"], (u >> 2) // g["ntx"]
+                    y, npi = rest % g["h"], rest // g["h"]
+                    addrs.append((npi * 6 + xi) * g["xb"] + (y + 1) * g["rb"] + t * 64 + 16 * (gg ^ (2 * (y & 1))))
+                for grp in WRITE_GROUPS:
+                    assert len({(addrs[l] // 16) % 16 for l in grp}) == 8, (layer, k, wave, xi, grp[0])
+
+
 # ---- k_c12w (hn_c12w.hip): conv1 as a 1-D Winograd F(4,3) inside the fused stem+conv1+conv2 kernel ----
 C12W_VROW = 6 * 8 * 128  # W0 ring bytes per a0 row: V records (xi, tile T), 128 B, chunk c at c ^ T
 
