@@ -236,7 +236,8 @@ struct hn_model {
   int chunk = 32768;
   bool unfused_stem = false;  // HN_UNFUSED_STEM=1: separate stem kernel (A/B, debugging)
   bool c12 = true;            // fused stem+conv1+conv2 (k_c12); HN_NO_C12=1 -> separate kernels
-  int subchunk = 16384;       // HardNet conv stages per sub-chunk (HN_SUBCHUNK; same-box A/B: 16384 +0.9 % over 8192)
+  int subchunk = 65536;       // HardNet conv3..conv5 patches per launch (HN_SUBCHUNK)
+  int c12group = 65536;       // HardNet k_c12 patches per launch (HN_C12_GROUP; >= the sub-chunk)
   uint16_t* front_spack = nullptr;  // fused front: stem as MFMA A operand
   int front = 0;  // NAS: 1 = stem + layer-0 IRF pw/dw fused, 2 = stem + layer-0 maxpool fused
   bool no_front = false;  // HN_NO_FRONT=1: unfused NAS stem/layer 0 (A/B, debugging)
@@ -895,6 +896,7 @@ extern "C" int hn_create(const hn_arch_desc* desc, const float* host_params, siz
   if (const char* e = std::getenv("HN_NO_FRONT")) m->no_front = std::atoi(e) != 0;
   if (const char* e = std::getenv("HN_NO_C12")) m->c12 = std::atoi(e) == 0;
   if (const char* e = std::getenv("HN_SUBCHUNK")) m->subchunk = std::max(64, std::atoi(e));
+  if (const char* e = std::getenv("HN_C12_GROUP")) m->c12group = std::max(64, std::atoi(e));
   if (const char* e = std::getenv("HN_NO_IRF")) m->no_irf = std::atoi(e) != 0;
   if (const char* e = std::getenv("HN_NO_IRF2")) m->no_irf2 = std::atoi(e) != 0;
   if (const char* e = std::getenv("HN_VARIANT")) {
@@ -940,18 +942,22 @@ extern "C" int hn_create(const hn_arch_desc* desc, const float* host_params, siz
   return HN_OK;
 }
 
-// HardNet on k_c12: the conv stages run per sub-chunk, so only the head's input (a5, 32 KiB per
-// patch) spans the whole chunk; a2 / a3 (64 KiB per patch each) span one sub-chunk
+// HardNet on k_c12: k_c12 runs per group (HN_C12_GROUP patches, its output a2 spanning the group) and
+// conv3..conv5 per sub-chunk of it, so a3 spans one sub-chunk and the head's input (a5, 32 KiB per
+// patch) the chunk
 static bool hardnet_subchunked(const hn_model* m) {
   return m->desc.kind == HN_KIND_HARDNET && m->c12 && !m->unfused_stem;
+}
+static int64_t hardnet_sub(const hn_model* m, int64_t p) { return std::max<int64_t>(1, std::min<int64_t>(p, m->subchunk)); }
+static int64_t hardnet_group(const hn_model* m, int64_t p) {
+  return std::max(hardnet_sub(m, p), std::min<int64_t>(p, m->c12group));
 }
 
 extern "C" int hn_workspace_bytes(const hn_model* m, int64_t batch, size_t* bytes_out) {
   if (!m || !bytes_out || batch < 0) return fail(HN_ERR_ARG, "bad argument");
   const int64_t p = batch < m->chunk ? batch : m->chunk;
   if (hardnet_subchunked(m)) {
-    const int64_t sub = std::max<int64_t>(1, std::min<int64_t>(p, m->subchunk));
-    *bytes_out = ((size_t)sub * 2 * 16384 + (size_t)p * 8192) * sizeof(float);
+    *bytes_out = ((size_t)(hardnet_sub(m, p) + hardnet_group(m, p)) * 16384 + (size_t)p * 8192) * sizeof(float);
   } else {
     *bytes_out = (size_t)p * m->ws_floats_per_patch * m->n_bufs * sizeof(float);
   }
@@ -984,29 +990,33 @@ static int forward_hardnet(hn_model* m, const float* in, int P, int pmax, float*
   float* a2 = ws + 2 * per;
   const float ineps = m->desc.input_norm_eps;
   if (hardnet_subchunked(m)) {
-    // conv stages in sub-chunks (HN_SUBCHUNK, default 16384 patches): a sub-chunk's a2..a4
-    // (1 GiB for a2) partly stays in the 256 MiB Infinity Cache between its kernels; the
-    // head GEMM, which needs many patches per launch to fill the GPU, runs once per chunk
-    // over the a5 of all sub-chunks.  Workspace (hn_workspace_bytes): [a3: sub x 64 KiB]
-    // [a2 / a4: sub x 64 KiB] [a5: pmax x 32 KiB]
-    const int sub = std::max(1, std::min(P, m->subchunk));
-    const size_t subper = (size_t)16384 * std::max(1, std::min(pmax, m->subchunk));
+    // k_c12 over groups (HN_C12_GROUP) and the conv stages over sub-chunks of a group (HN_SUBCHUNK);
+    // both default to 65,536 patches, one launch of each per chunk (same box: 5.46 against 5.24
+    // Mpatches/s for 16,384-patch launches; k_c12s 20.9 -> 18.5 ms per 262,144-patch step, conv4 7.3 ->
+    // 8.2; a 65,536 group over 16,384 sub-chunks measured 5.26-5.29).  The head GEMM runs
+    // once per chunk over the a5 of all sub-chunks.  conv4 writes its output over the sub-chunk's a2 slots,
+    // which conv3 has consumed.  Workspace (hn_workspace_bytes): [a3: sub x 64 KiB] [a2 / a4: group x 64 KiB]
+    // [a5: pmax x 32 KiB]
+    const int sub = (int)hardnet_sub(m, P), grp = (int)hardnet_group(m, P);
     a0 = ws;
-    a2 = ws + subper;
-    a1 = ws + 2 * subper;
-    for (int s0 = 0; s0 < P; s0 += sub) {
-      const int n = std::min(sub, P - s0);
-      float* a5 = a1 + (size_t)s0 * 8192;
+    a2 = ws + (size_t)16384 * hardnet_sub(m, pmax);
+    a1 = a2 + (size_t)16384 * hardnet_group(m, pmax);
+    for (int g0 = 0; g0 < P; g0 += grp) {
+      const int ng = std::min(grp, P - g0);
       if (u8) {
-        HnU8In sub = *u8;
-        sub.in += (size_t)s0 * (u8->resize == HN_RESIZE_NONE ? 1024 : 4096);
-        STAGE("stem+conv1+conv2", hn_launch_c12(nullptr, a2, m->hd, n, ineps, st, &sub));
+        HnU8In gin = *u8;
+        gin.in += (size_t)g0 * (u8->resize == HN_RESIZE_NONE ? 1024 : 4096);
+        STAGE("stem+conv1+conv2", hn_launch_c12(nullptr, a2, m->hd, ng, ineps, st, &gin));
       } else {
-        STAGE("stem+conv1+conv2", hn_launch_c12(in + (size_t)s0 * 1024, a2, m->hd, n, ineps, st));
+        STAGE("stem+conv1+conv2", hn_launch_c12(in + (size_t)g0 * 1024, a2, m->hd, ng, ineps, st));
       }
-      STAGE("conv3", hn_launch_hardnet_conv(3, m->variant[3], m->hd, a2, a0, n, 0.f, st));
-      STAGE("conv4", hn_launch_hardnet_conv(4, m->variant[4], m->hd, a0, a2, n, 0.f, st));
-      STAGE("conv5", hn_launch_hardnet_conv(5, m->variant[5], m->hd, a2, a5, n, 0.f, st));
+      for (int s0 = g0; s0 < g0 + ng; s0 += sub) {
+        const int n = std::min(sub, g0 + ng - s0);
+        float* const a2s = a2 + (size_t)(s0 - g0) * 16384;
+        STAGE("conv3", hn_launch_hardnet_conv(3, m->variant[3], m->hd, a2s, a0, n, 0.f, st));
+        STAGE("conv4", hn_launch_hardnet_conv(4, m->variant[4], m->hd, a0, a2s, n, 0.f, st));
+        STAGE("conv5", hn_launch_hardnet_conv(5, m->variant[5], m->hd, a2s, a1 + (size_t)s0 * 8192, n, 0.f, st));
+      }
     }
     STAGE("head", hn_launch_head(a1, out, m->hd.wpack[6], m->hd.bias[6], P, 8192, m->desc.l2_eps, st));
     return HN_OK;

@@ -280,6 +280,29 @@ def test_persistent_kernels_past_one_round(name, cuda_device):
     assert (y[idx.to(cuda_device)].cpu() - ref).abs().max().item() <= _tol(name)
 
 
+@pytest.mark.parametrize("u8", [False, True])
+def test_c12_group_and_subchunk_sizes_are_bitwise_neutral(u8, cuda_device, monkeypatch):
+    """k_c12 over groups (HN_C12_GROUP) and conv3..conv5 over sub-chunks of them (HN_SUBCHUNK): odd
+    group / sub-chunk sizes that leave ragged tails give the same descriptors, bit for bit, as one
+    launch per chunk (every patch's arithmetic is the same; only the launch boundaries move)."""
+    from hardnetnas_amd._native import NativeModel
+    m, fx, _ = build_module("hardnet")
+    b = 2 * 16384 + 77
+    g = torch.Generator().manual_seed(7)
+    if u8:
+        x = torch.randint(0, 256, (b, 32, 32), generator=g, dtype=torch.uint8).to(cuda_device)
+    else:
+        x = torch.from_numpy(golden_inputs(fx)).repeat(b // 129 + 1, 1, 1, 1)[:b].to(cuda_device)
+        x = x + 0.01 * torch.randn(x.shape, generator=g).to(cuda_device)
+    out = {}
+    for tag, grp, sub in (("one", 65536, 65536), ("odd", 20000, 7000)):
+        monkeypatch.setenv("HN_C12_GROUP", str(grp))
+        monkeypatch.setenv("HN_SUBCHUNK", str(sub))
+        nm = NativeModel.from_module(m, cuda_device)
+        out[tag] = nm.forward_u8(x, resize="none") if u8 else nm(x)
+    assert torch.equal(out["one"], out["odd"])
+
+
 def test_hardnet_at_the_timed_size(cuda_device):
     """BASELINE config 2's exact launch (262,144 patches, the bench's chunking and grids): a
     strided 1,024-row sample equals the oracle to 1e-4 and every row has unit norm."""

@@ -77,8 +77,9 @@ def test_rccl_world1_matches_single_calls(cuda_device):
 
 def test_module_workspace_footprint(cuda_device):
     """A 65,536-patch module call under no_grad (the reference eval loop's form, HardNet.py:454)
-    allocates at most 8 GiB beyond its input and output: the conv stages' buffers span one
-    16,384-patch sub-chunk, only the head's input spans the chunk (hn_workspace_bytes)."""
+    allocates at most 11 GiB beyond its input and output: k_c12's and conv3's outputs span one
+    65,536-patch launch each, the head's input the chunk (hn_workspace_bytes: 10 GiB, 3.5 % of the
+    288 GB of HBM; HN_C12_GROUP / HN_SUBCHUNK bound it)."""
     m, _, _ = build_module("hardnet")
     m = m.to(cuda_device)
     x = _synth_on_device(65536, cuda_device, 3)
@@ -93,6 +94,6 @@ def test_module_workspace_footprint(cuda_device):
     torch.cuda.synchronize()
     extra = torch.cuda.max_memory_allocated(cuda_device) - base - y.numel() * 4
     print(f"B=65536: {extra / 2**30:.2f} GiB beyond input and output")
-    assert extra <= 8 * 2**30
+    assert extra <= 11 * 2**30
     nm = m._hn_handle
-    assert nm.workspace_bytes(65536) == (2 * 16384 * 16384 + 65536 * 8192) * 4
+    assert nm.workspace_bytes(65536) == ((65536 + 65536) * 16384 + 65536 * 8192) * 4
