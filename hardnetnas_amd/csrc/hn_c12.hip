@@ -942,7 +942,7 @@ bool hn_c12_cfg_ok(int cfg, int abl) {
   if (cfg == kC12Split) {  // k_c12s (hn_c12w.hip)
 #ifdef HN_EXPERIMENTS
     return abl == 0 || abl == 1 || abl == 2 || abl == 4 || abl == 6 || abl == 64 || abl == 65 || abl == 66 || abl == 72 ||
-           abl == 80 || abl == 84 || abl == 88 || abl == 116 || abl == 340 || abl == 576 || abl == 1088;
+           abl == 80 || abl == 84 || abl == 88 || abl == 116 || abl == 86 || abl == 340 || abl == 576 || abl == 1088;
 #else
     return abl == 0;
 #endif

@@ -572,6 +572,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   if constexpr ((ABL & 64) != 0) {                                                                           \
     if (g >= 16 && g < 24 && lane == 0) dbg[(g - 16) * 6 + (K)] = (long long)__builtin_amdgcn_s_memtime();   \
   }
+  // ABL & 64: every wave's start / end in the 100 MHz clock (slots 120 / 121), for the launch's tail
+#define HN_S_RT(K)                                                                                           \
+  if constexpr ((ABL & 64) != 0) {                                                                           \
+    if (lane == 0) dbg[120 + (K)] = (long long)__builtin_amdgcn_s_memrealtime();                             \
+  }
+  HN_S_RT(0);
 
   // P1 of band gq (k_c12w's): a0 rows -> V records, slot (32 p + y) % 10; the padding rows are not
   // stored (the zero row stands for them).  p1_front: the window reads, the B operands and the 6 stem
@@ -791,6 +797,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       __syncthreads();
       HN_S_TS(2);
     }
+    HN_S_RT(1);
     return;
   }
 
@@ -1011,7 +1018,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     HN_S_TS(5);
   }
   flush(G - 1);
+  HN_S_RT(1);
 #undef HN_S_TS
+#undef HN_S_RT
 }
 
 }  // namespace
@@ -1102,6 +1111,7 @@ hipError_t hn_launch_c12s(const float* in, float* out, const HardnetDev& d, int 
       case 64 + 20: HN_C12S_GO(-1, 1, 1, 1, 64 + 20); break;  // timing: P3 without MFMAs, no P1
       case 64 + 20 + 32: HN_C12S_GO(-1, 1, 1, 1, 64 + 20 + 32); break;  // + P2 without its LDS stream
       case 64 + 20 + 256: HN_C12S_GO(-1, 1, 1, 1, 64 + 20, false, false, true); break;  // 84, interleaved
+      case 64 + 20 + 2: HN_C12S_GO(-1, 1, 1, 1, 64 + 20 + 2); break;  // 84 without the conv1 MFMAs
       case 64 + 512: HN_C12S_GO(-1, 1, 1, 1, 64, false, false, true); break;  // stamps, interleaved
       case 64 + 1024: HN_C12S_GO(-1, 1, 1, 1, 64, false, true, true); break;  // stamps, interleaved + P1 in P3
       case 64 + 20 + 1000: HN_C12S_GO(-1, 2, 1, 1, 64 + 20); break;  // the same, P2 two steps ahead

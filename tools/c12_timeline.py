@@ -37,6 +37,11 @@ if nw == 8:  # k_c12s: per step, A-waves (start, P2 end, past the barrier), B-wa
     a, b = t[:, :4], t[:, 4:]
     step = np.median(b[:, :, 1:, 0] - b[:, :, :-1, 0])
     print(f"{ok.sum()} workgroups; median cycles per step: {step:.0f}")
+    rt = raw[:, :, 120:122].astype(np.float64) / 100.0  # 100 MHz -> microseconds
+    st0, en = rt[..., 0].min(axis=1), rt[..., 1].max(axis=1)  # per workgroup
+    t0 = st0.min()
+    print(f"  workgroup start: {np.percentile(st0 - t0, 50):.1f} / max {np.max(st0 - t0):.1f} us after the first;"
+          f" end: min {np.min(en - t0):.1f}, median {np.median(en - t0):.1f}, max {np.max(en - t0):.1f} us")
     da = np.diff(a[..., :3], axis=3)
     print(f"  A: P2 {np.median(da[..., 0]):.0f}  barrier wait {np.median(da[..., 1]):.0f}")
     db = np.diff(b, axis=3)
