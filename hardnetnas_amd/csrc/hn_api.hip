@@ -31,6 +31,7 @@ void hn_read_knobs(HnKnobs* k) {
   *k = HnKnobs{};
   k->c12_cfg = env_int("HN_C12_CFG", 15);
   k->head = std::getenv("HN_HEAD_V1") ? 1 : env_int("HN_HEAD", 4);
+  k->head_pf = env_int("HN_HEAD_PF", 1) != 0;
   k->fdl_valu = std::getenv("HN_FDL_VALU") != nullptr;
   k->naive_pw = std::getenv("HN_NAIVE_PW") != nullptr;
   k->naive_dw = std::getenv("HN_NAIVE_DW") != nullptr;

@@ -1532,7 +1532,12 @@ __global__ __launch_bounds__(512) void k_head3(const float* __restrict__ a, floa
 // B DB x 16 KB.  The DMA schedule, the K-chunk accumulation order and the L2 norm's summation
 // order (two 64-column half sums, then + l2eps) are k_head3's: bit-identical results.
 // ------------------------------------------------------------------------------------
-template <int K, bool F16, int DA, int DB>
+// ABL (timing only, experiments library, HN_HEAD_ABL): bit 0 issues 3 of each wave's 4 A DMA instructions per
+// chunk (24 of the 32 KB: the traffic of a 3-byte activation format), bit 1 streams the weights only into the
+// ring's first DB chunks (no weight traffic after the prologue)
+// PF: the fragments of chunk c + 1 are read from LDS into registers while chunk c's MFMAs run (DMA three
+// chunks ahead, rings of 3): the MFMAs no longer wait for their LDS reads after each barrier
+template <int K, bool F16, int DA, int DB, int ABL = 0, bool PF = false>
 __global__ __launch_bounds__(512) void k_head4(const float* __restrict__ a, float* __restrict__ out,
                                                const uint4* __restrict__ wp,
                                                const float* __restrict__ bias, int P, float l2eps) {
@@ -1573,7 +1578,7 @@ __global__ __launch_bounds__(512) void k_head4(const float* __restrict__ a, floa
   constexpr int J0 = 1 - (DA > DB ? DA : DB);  // first (prologue) iteration
   auto issue = [&](int j) {  // iteration j's DMA: B(j + DB - 1), then A(j + DA - 1)
     const int cb = j + DB - 1, ca = j + DA - 1;
-    if (live(cb)) {
+    if (live(cb) && ((ABL & 2) == 0 || cb < DB)) {
       const unsigned so = (unsigned)(cb % DB) * BBYTES;
 #pragma unroll
       for (int k = 0; k < NB; ++k) dma(bsrc[k] + (size_t)cb * 1024, bdst[k] + so);
@@ -1581,7 +1586,7 @@ __global__ __launch_bounds__(512) void k_head4(const float* __restrict__ a, floa
     if (live(ca)) {
       const unsigned so = (unsigned)(ca % DA) * ABYTES;
 #pragma unroll
-      for (int k = 0; k < NA; ++k) dma(asrc[k] + (size_t)ca * KC, adst[k] + so);
+      for (int k = 0; k < NA - (ABL & 1); ++k) dma(asrc[k] + (size_t)ca * KC, adst[k] + so);
     }
   };
   // this wave's DMA instructions issued after the latest one of A(c) / B(c): walk the issue
@@ -1602,6 +1607,73 @@ __global__ __launch_bounds__(512) void k_head4(const float* __restrict__ a, floa
   };
   const int arow = 32 * wave + r, asw = (arow >> 1) & 7;
   f32x16 acc[4] = {f32x16{}, f32x16{}, f32x16{}, f32x16{}};
+  if constexpr (PF) {
+    static_assert(DA == 3 && DB == 3 && NCH % 2 == 0 && NCH >= 4, "PF: chunk c + 3 refills chunk c's slots");
+    constexpr int PER = NA + NB;  // DMA instructions per wave per chunk
+    auto issue_chunk = [&](int ch) {
+      if (ch >= NCH) return;
+      const unsigned sb = (unsigned)(ch % 3) * BBYTES, sa_ = (unsigned)(ch % 3) * ABYTES;
+#pragma unroll
+      for (int k = 0; k < NB; ++k) dma(bsrc[k] + (size_t)ch * 1024, bdst[k] + sb);
+#pragma unroll
+      for (int k = 0; k < NA; ++k) dma(asrc[k] + (size_t)ch * KC, adst[k] + sa_);
+    };
+    float4 xa[2][2][2];
+    uint4 bq[2][2][4][2];
+    auto read_frags = [&](int ch, int bs) {
+      const char* ast = sa + (ch % 3) * ABYTES + arow * (KC * 4);
+      const char* bst = sbw + (ch % 3) * BBYTES;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int p0 = 4 * ks + 2 * h;
+        xa[bs][ks][0] = *reinterpret_cast<const float4*>(ast + ((p0 ^ asw) << 4));
+        xa[bs][ks][1] = *reinterpret_cast<const float4*>(ast + (((p0 + 1) ^ asw) << 4));
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+          const char* bp = bst + ((((ks * 4 + nt) * 2) * 64 + lane) << 4);
+          bq[bs][ks][nt][0] = *reinterpret_cast<const uint4*>(bp);
+          bq[bs][ks][nt][1] = *reinterpret_cast<const uint4*>(bp + 1024);
+        }
+      }
+    };
+    auto mfmas = [&](int bs) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        uint4 ah, al;
+        if (F16) split8_f16(xa[bs][ks][0], xa[bs][ks][1], ah, al);
+        else split8(xa[bs][ks][0], xa[bs][ks][1], ah, al);
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+          const uint4 bh = bq[bs][ks][nt][0], bl = bq[bs][ks][nt][1];
+          if (F16)
+            acc[nt] = mfma3_f16(as_f16x8(ah), as_f16x8(al), as_f16x8(bh), as_f16x8(bl), acc[nt]);
+          else
+            acc[nt] = mfma3(as_bf16x8(ah), as_bf16x8(al), as_bf16x8(bh), as_bf16x8(bl), acc[nt]);
+        }
+      }
+    };
+    issue_chunk(0);
+    issue_chunk(1);
+    issue_chunk(2);
+    head_wait_vm<2 * PER>();  // chunk 0 landed (1 and 2 in flight)
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    read_frags(0, 0);
+    // iteration c: chunk c + 1 landed (c + 2 may be in flight) and every wave's reads of chunk c done ->
+    // barrier -> refill chunk c's slots with chunk c + 3 -> read chunk c + 1 -> chunk c's MFMAs
+    auto step = [&](int c, int bs) {
+      if (c + 2 < NCH) head_wait_vm<PER>();
+      else head_wait_vm<0>();
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      issue_chunk(c + 3);
+      if (c + 1 < NCH) read_frags(c + 1, bs ^ 1);
+      mfmas(bs);
+    };
+#pragma unroll 1
+    for (int c = 0; c < NCH; c += 2) {
+      step(c, 0);
+      step(c + 1, 1);
+    }
+  } else {
   for (int j = J0; j < 0; ++j) issue(j);
 #pragma unroll 1
   for (int c = 0; c < NCH; ++c) {
@@ -1643,6 +1715,7 @@ __global__ __launch_bounds__(512) void k_head4(const float* __restrict__ a, floa
           acc[nt] = mfma3(as_bf16x8(ah), as_bf16x8(al), as_bf16x8(bh), as_bf16x8(bl), acc[nt]);
       }
     }
+  }
   }
 #pragma unroll
   for (int nt = 0; nt < 4; ++nt) {
@@ -2012,6 +2085,23 @@ hipError_t hn_launch_head(const float* a, float* out, const void* wp, const floa
     return hipGetLastError();                                                                                \
   }
   if (form >= 4 && P >= 240 * 256) {
+    if (hn_knobs().head_pf && K == 8192 && !f16) {
+      hipLaunchKernelGGL((k_head4<8192, false, 3, 3, 0, true>), dim3((P + 255) / 256), dim3(512), 0, st, a, out, w,
+                         bias, P, l2eps);
+      return hipGetLastError();
+    }
+#ifdef HN_EXPERIMENTS
+    if (const char* e = std::getenv("HN_HEAD_ABL")) {
+      const int abl = std::atoi(e);
+      if (K == 8192 && !f16 && (abl == 1 || abl == 2 || abl == 3)) {
+        const dim3 g((P + 255) / 256), b(512);
+        if (abl == 1) hipLaunchKernelGGL((k_head4<8192, false, 3, 3, 1>), g, b, 0, st, a, out, w, bias, P, l2eps);
+        if (abl == 2) hipLaunchKernelGGL((k_head4<8192, false, 3, 3, 2>), g, b, 0, st, a, out, w, bias, P, l2eps);
+        if (abl == 3) hipLaunchKernelGGL((k_head4<8192, false, 3, 3, 3>), g, b, 0, st, a, out, w, bias, P, l2eps);
+        return hipGetLastError();
+      }
+    }
+#endif
     HN_HEAD4(8192, false, 3, 3) HN_HEAD4(2048, true, 3, 3)
   }
   if (form >= 3) {

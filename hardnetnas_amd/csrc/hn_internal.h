@@ -12,6 +12,7 @@
 struct HnKnobs {
   int c12_cfg = 15;            // HN_C12_CFG: k_c12 configuration (0..15, all within the parity bar; 15 = k_c12s)
   int head = 4;                // HN_HEAD: head GEMM form (1 k_head, 2 k_head2, 3 k_head3 LDS-DMA rings, 4 k_head4 256-patch rings)
+  bool head_pf = true;         // HN_HEAD_PF: k_head4 reads chunk c + 1 from LDS while chunk c runs (0: off)
   bool fdl_valu = false;       // HN_FDL_VALU: FDLNet front as fp32 VALU
   bool naive_pw = false;       // HN_NAIVE_PW: untiled 1x1 conv kernel
   bool naive_dw = false;       // HN_NAIVE_DW: untiled depthwise kernel
