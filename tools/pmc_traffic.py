@@ -28,7 +28,7 @@ def stage_of(name: str):
     m = re.search(r"k_conv_w1<(\d+), (\d+), (\d+),", name)  # 1-D Winograd conv3 / conv5 (hn_wino1.hip)
     if m:
         return {(64, 64, 16): "conv3", (128, 128, 8): "conv5"}.get((int(m.group(1)), int(m.group(2)), int(m.group(3))))
-    if "k_c12h<" in name:
+    if "k_c12h<" in name or "k_c12w<" in name or "k_c12s<" in name:
         return "stem+conv1+conv2"
     for k, st in (("k_c12<", "stem+conv1+conv2"), ("k_front<", "front"), ("k_irf<", "irf"),
                   ("k_head<", "head"), ("k_head2<", "head"), ("k_head3<", "head"), ("k_head4<", "head")):
