@@ -40,6 +40,7 @@ void hn_read_knobs(HnKnobs* k) {
   k->pairdist_valu = std::getenv("HN_PAIRDIST_VALU") != nullptr;
   k->pairdist_reg = env_int("HN_PAIRDIST_REG", 0) != 0;
   k->front_fold = env_int("HN_FRONT_FOLD", 0) != 0;
+  k->u8_apart = env_int("HN_U8_APART", 0) != 0;
   k->front_xch3 = env_int("HN_FRONT_XCH3", 0) != 0;
   k->train_splitk = std::max(32, env_int("HN_TRAIN_SPLITK", 1024)) / 32 * 32;
   k->train_f32 = env_int("HN_TRAIN_F32", 1) & 255;
@@ -1179,14 +1180,19 @@ extern "C" int hn_forward(hn_model* m, const float* d_in, int64_t batch, float* 
   return HN_OK;
 }
 
-// uint8 input: the stock HardNet's fused k_c12 and FDLNet's MFMA front (every resize
-// mode) and the NAS models' fused front (NONE / CV2) preprocess in their patch loads; every other
-// model / mode / configuration (NAS PIL, HN_NO_FRONT, HN_FRONT_FOLD, HN_FDL_VALU, the A/B
-// configurations) runs hn_preprocess into the workspace tail first.
+// uint8 input: the stock HardNet's fused k_c12, FDLNet's MFMA front and the NAS
+// models' fused front preprocess in their patch loads in every resize mode; every other model /
+// configuration (HN_NO_FRONT, HN_FRONT_FOLD, HN_FDL_VALU, the A/B configurations) runs hn_preprocess
+// into the workspace tail first.
 static bool u8_fused(const hn_model* m, int resize) {
+  if (m->knobs.u8_apart) return false;
   if (m->desc.kind == HN_KIND_FDL_NASNET || m->desc.kind == HN_KIND_FDL_NASNET01) return !m->knobs.fdl_valu;
-  if (m->desc.kind == HN_KIND_NAS)  // the fused front's patch load (hn_front.hip): no input_norm, not PIL
-    return resize != HN_RESIZE_PIL_BILINEAR && m->front && m->desc.input_norm_eps < 0.f && !m->knobs.front_fold;
+  if (m->desc.kind == HN_KIND_NAS) {  // the fused front's patch load (hn_front.hip): no input_norm
+    // PIL on the k5 front (two workgroups per CU): its staging barrier and LDS window reads cost more
+    // than the separate pass (wang3 23.4-23.6 against 24.4-24.5 Mpatches/s; k3 / max-pool fronts equal)
+    if (resize == HN_RESIZE_PIL_BILINEAR && m->front == 1 && !m->layers.empty() && m->layers[0].k == 5) return false;
+    return m->front && m->desc.input_norm_eps < 0.f && !m->knobs.front_fold;
+  }
   return m->desc.kind == HN_KIND_HARDNET && m->c12 && !m->unfused_stem && (m->knobs.c12_cfg == 12 || m->knobs.c12_cfg == 13 || m->knobs.c12_cfg == kC12Wino || m->knobs.c12_cfg == kC12Split) &&
          !m->knobs.c12_abl;
 }

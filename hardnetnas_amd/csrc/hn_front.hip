@@ -59,9 +59,9 @@ __constant__ unsigned char kDwLane[64] = {
 // U8 (preprocessing fused into the patch load, as k_c12): -1 = fp32 [P,1,32,32]
 // input; HN_RESIZE_NONE / _CV2_LINEAR = uint8 patches (32x32 / 64x64) resized, /255'd and
 // Normalize'd in the load by hn_preproc.h (the arithmetic of hn_preprocess), so the input costs
-// 1 / 4 KiB of HBM per patch and no intermediate fp32 tensor exists.  (PIL mode stays unfused:
-// its 12 prefetched byte registers took the k3 front from three workgroups per CU to two, wang2
-// front 5.7 -> 7.2 ms, against 0.46 ms for the separate hn_preprocess.)
+// 1 / 4 KiB of HBM per patch and no intermediate fp32 tensor exists.  HN_RESIZE_PIL_BILINEAR: the raw
+// 4 KiB are prefetched coalesced and staged in the free pw ring (one extra barrier per patch): its
+// 12-register per-thread window fetched ahead took the k3 front from three workgroups per CU to two.
 template <int K, int MID, int MODE, bool NORM, bool NF, int U8 = -1, bool P5 = false, bool X3 = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRONT_IRF && K == 3 && MID == 32 ? 3 : MODE == FRONT_IRF && MID == 32 ? 2 : 1))) void k_front(const void* __restrict__ in_,
                                                float* __restrict__ out,
@@ -231,12 +231,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRO
   constexpr int INB = U8 == HN_RESIZE_NONE ? 1024 : 4096;  // bytes per uint8 patch
   const int iy = t >> 3, ix = 4 * (t & 7);                  // this thread's 4 pixels (iy, ix ..)
   // the next patch's pixels are fetched one patch ahead (U8: its raw bytes -- 1 / 4 registers for
-  // NONE / CV2, as many as the fp32 form -- resized at use)
-  static_assert(U8 != HN_RESIZE_PIL_BILINEAR, "PIL's 12 prefetch registers cost the k3 front its third workgroup");
+  // NONE / CV2, as many as the fp32 form -- resized at use).  PIL: the 4 KiB patch is fetched ahead
+  // coalesced (16 bytes per thread, 4 registers), staged in the pw ring once the previous patch is
+  // done with it, and every thread reads its 4 x 10-byte window from there (its 12-register window
+  // fetched ahead cost the k3 front its third workgroup per CU)
+  constexpr bool PILS = U8 == HN_RESIZE_PIL_BILINEAR;
+  static_assert(!PILS || (!NORM && IR * RS * 4 >= 4096), "PIL staging: no input_norm, a ring of >= 4 KiB");
   float4 vnext;
-  hnpre::U8Px<U8 < 0 ? HN_RESIZE_NONE : U8, 4> rnext;
+  hnpre::U8Px<U8 < 0 || PILS ? HN_RESIZE_NONE : U8, 4> rnext;
+  uint4 rawnext;
   if constexpr (U8 < 0)
     vnext = reinterpret_cast<const float4*>(in + pb * 1024)[t];
+  else if constexpr (PILS)
+    rawnext = reinterpret_cast<const uint4*>(in8 + pb * INB)[t];
   else
     rnext.load(in8 + pb * INB, iy, ix);
 #pragma unroll 1
@@ -246,6 +253,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == FRO
     if constexpr (U8 < 0) {
       v = vnext;
       if (patch + 1 < pe) vnext = reinterpret_cast<const float4*>(in + (patch + 1) * 1024)[t];
+    } else if constexpr (PILS) {
+      __syncthreads();  // the previous patch is done with the ring
+      reinterpret_cast<uint4*>(s_pw)[t] = rawnext;
+      if (patch + 1 < pe) rawnext = reinterpret_cast<const uint4*>(in8 + (patch + 1) * INB)[t];
+      __syncthreads();
+      hnpre::U8Px<HN_RESIZE_PIL_BILINEAR, 4> wpx;
+      wpx.load(reinterpret_cast<const uint8_t*>(s_pw), iy, ix);
+      int q[4];
+      wpx.resized(iy, ix, q);
+      v = make_float4(hnpre::to_input(q[0], pmean, pstd, pnorm), hnpre::to_input(q[1], pmean, pstd, pnorm),
+                      hnpre::to_input(q[2], pmean, pstd, pnorm), hnpre::to_input(q[3], pmean, pstd, pnorm));
     } else {
       int q[4];
       rnext.resized(iy, ix, q);
@@ -596,7 +614,7 @@ hipError_t front_launch_t(const HnFrontArgs& a, int P, float eps, hipStream_t st
   // wang2 front k3 6.12 -> 5.59 ms without it; the k5 front without the fold alone was 6 % slower, with
   // the paired stem rows 9 % faster than the fold form)
   const bool nf = front_nf<K, MID, MODE>() && !hn_knobs().front_fold && a.pwl_a16;
-  if (u8) {  // uint8 loads (NONE / CV2): the production form without input_norm only (hn_api.hip u8_fused)
+  if (u8) {  // uint8 loads (every resize mode): the production form without input_norm only (hn_api.hip u8_fused)
     if constexpr (NORM) {
       return hipErrorInvalidValue;
     } else {
@@ -606,6 +624,8 @@ hipError_t front_launch_t(const HnFrontArgs& a, int P, float eps, hipStream_t st
         case HN_RESIZE_NONE: return front_launch_nf<K, MID, MODE, false, NFD, HN_RESIZE_NONE, P5D>(a, P, eps, st, u8);
         case HN_RESIZE_CV2_LINEAR:
           return front_launch_nf<K, MID, MODE, false, NFD, HN_RESIZE_CV2_LINEAR, P5D>(a, P, eps, st, u8);
+        case HN_RESIZE_PIL_BILINEAR:
+          return front_launch_nf<K, MID, MODE, false, NFD, HN_RESIZE_PIL_BILINEAR, P5D>(a, P, eps, st, u8);
       }
       return hipErrorInvalidValue;
     }

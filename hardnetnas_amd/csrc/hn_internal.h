@@ -21,6 +21,7 @@ struct HnKnobs {
   bool pairdist_valu = false;  // HN_PAIRDIST_VALU: fp32 VALU pair-distance kernel
   bool pairdist_reg = false;   // HN_PAIRDIST_REG: register-staged positives instead of the LDS-DMA ring
   bool front_fold = false;     // HN_FRONT_FOLD: the NAS front's pwl with the LDS partial-sum fold
+  bool u8_apart = false;       // HN_U8_APART: uint8 input preprocessed into the workspace first (A/B)
   bool front_xch3 = false;     // HN_FRONT_XCH3: the k3 front's dw per channel group (SGPR weights, s_x; two
                                // workgroups per CU instead of three: wang2 front 5.05 -> 5.57 ms, not the default)
   int train_splitk = 1024;     // HN_TRAIN_SPLITK: K per split-K slice of the train GEMMs

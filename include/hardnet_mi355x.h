@@ -178,10 +178,11 @@ int hn_preprocess(const uint8_t* d_in, int64_t n, int32_t in_hw, int32_t resize,
 /* Descriptor forward from uint8 patches (the loader transforms of
  * hardnet/HardNet.py:333-337 / 345-349 + Utils.py:10-11 fused into the network's patch load):
  * d_in [B, in_hw, in_hw] uint8; resize / normalize / mean / std as hn_preprocess.  Equals
- * hn_preprocess followed by hn_forward bit for bit.  For the stock HardNet (every resize mode)
- * and the hardnetNAS descriptors (NONE / CV2) the preprocessing runs inside the first fused kernel
- * (k_c12 / the NAS front: 4 / 1 KiB of input HBM per patch and no fp32 copy); FDLNet, NAS in PIL
- * mode and the A/B configurations preprocess each chunk into the workspace tail first.
+ * hn_preprocess followed by hn_forward bit for bit.  For the stock HardNet, FDLNet and the
+ * hardnetNAS descriptors (every resize mode) the preprocessing runs inside the first fused kernel
+ * (k_c12 / the FDLNet and NAS fronts: 4 / 1 KiB of input HBM per patch and no fp32 copy); the k5
+ * NAS front in PIL mode (measured faster apart) and the A/B configurations (HN_NO_FRONT,
+ * HN_FRONT_FOLD, HN_FDL_VALU, HN_U8_APART) preprocess each chunk into the workspace tail first.
  * Workspace: hn_workspace_bytes_u8. */
 int hn_workspace_bytes_u8(const hn_model* m, int64_t batch, size_t* bytes_out);
 int hn_forward_u8(hn_model* m, const uint8_t* d_in, int64_t batch, int32_t in_hw, int32_t resize,
