@@ -442,7 +442,9 @@ HN_DEV void wait_vm() {  // s_waitcnt vmcnt(N), lgkmcnt / expcnt untouched
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
-template <bool SWAP, int NW>
+// ABL (timing only, experiments library, HN_PAIRDIST_ABL): bit 0 no epilogue (the distance / minimum VALU and
+// the masked path), bit 1 no positive-tile DMA after the prologue (stale tiles), bit 2 no MFMAs
+template <bool SWAP, int NW, int ABL = 0>
 __global__ __launch_bounds__(NW * 64) void k_pairdist_ring(
     const float* __restrict__ a, int NA, int row0, const uint16_t* __restrict__ ph, const uint16_t* __restrict__ pl,
     int B, const float* __restrict__ asq, const float* __restrict__ psq, float xthr, float* __restrict__ rowmin,
@@ -493,6 +495,9 @@ __global__ __launch_bounds__(NW * 64) void k_pairdist_ring(
   // otherwise wait vmcnt(0) before LDS reads of the other buffers; the waits here are explicit.
   const unsigned wv = __builtin_amdgcn_readfirstlane(wave);
   auto issue = [&](char* buf, int j0) {
+    if constexpr ((ABL & 2) != 0) {
+      if (j0 >= 2 * TN) return;
+    }
 #pragma unroll
     for (int k = 0; k < G; ++k) {
       const int gi = wave * G + k, plane = gi >> 4, r4 = (gi & 15) * 4;
@@ -571,7 +576,17 @@ __global__ __launch_bounds__(NW * 64) void k_pairdist_ring(
         nh = *reinterpret_cast<const uint4*>(base + off);
         nl = *reinterpret_cast<const uint4*>(base + PLANE + off);
       }
-      acc = mfma3(ah[ks], al[ks], as_bf16x8(bh), as_bf16x8(bl), acc);
+      if constexpr ((ABL & 4) != 0)
+        acc[ks] += __builtin_bit_cast(float, bh.x ^ bl.y);
+      else
+        acc = mfma3(ah[ks], al[ks], as_bf16x8(bh), as_bf16x8(bl), acc);
+      if constexpr ((ABL & 1) != 0) {
+        if (ks + 1 < 8) {
+          bh = nh;
+          bl = nl;
+        }
+        continue;
+      }
       accp[2 * ks] = fmaf(-2.0f, accp[2 * ks], pj);
       accp[2 * ks + 1] = fmaf(-2.0f, accp[2 * ks + 1], pj);
       lm = fminf(lm, fminf(accp[2 * ks], accp[2 * ks + 1]));
@@ -580,7 +595,8 @@ __global__ __launch_bounds__(NW * 64) void k_pairdist_ring(
         bl = nl;
       }
     }
-    epi_finish(accp, lm, dsel, cslot);
+    if constexpr ((ABL & 1) == 0) epi_finish(accp, lm, dsel, cslot);
+    else xu[0] = fminf(xu[0], accp[0]);
     return acc;
   };
   auto reduce_cols = [&](int t) {
@@ -741,6 +757,19 @@ hipError_t hn_launch_pairdist_rows(const float* a, int NA, int row0, const float
     constexpr int NW = decltype(nw)::value;
     const dim3 grid((NA + 32 * NW - 1) / (32 * NW)), block(64 * NW);
     unsigned* cm = reinterpret_cast<unsigned*>(colmin);
+#ifdef HN_EXPERIMENTS
+    const char* abl_e = std::getenv("HN_PAIRDIST_ABL");
+    const int abl = abl_e ? std::atoi(abl_e) : 0;
+    if (ring && colmin && abl > 0) {
+      switch (abl) {
+        case 1: hipLaunchKernelGGL((k_pairdist_ring<true, NW, 1>), grid, block, 0, st, a, NA, row0, ph, pl, B, asq, psq, xthr, rowmin, cm); break;
+        case 2: hipLaunchKernelGGL((k_pairdist_ring<true, NW, 2>), grid, block, 0, st, a, NA, row0, ph, pl, B, asq, psq, xthr, rowmin, cm); break;
+        case 3: hipLaunchKernelGGL((k_pairdist_ring<true, NW, 3>), grid, block, 0, st, a, NA, row0, ph, pl, B, asq, psq, xthr, rowmin, cm); break;
+        case 4: hipLaunchKernelGGL((k_pairdist_ring<true, NW, 4>), grid, block, 0, st, a, NA, row0, ph, pl, B, asq, psq, xthr, rowmin, cm); break;
+        case 6: hipLaunchKernelGGL((k_pairdist_ring<true, NW, 6>), grid, block, 0, st, a, NA, row0, ph, pl, B, asq, psq, xthr, rowmin, cm); break;
+      }
+    } else
+#endif
     if (ring && colmin)
       hipLaunchKernelGGL((k_pairdist_ring<true, NW>), grid, block, 0, st, a, NA, row0, ph, pl, B, asq, psq, xthr,
                          rowmin, cm);
