@@ -39,6 +39,7 @@ void hn_read_knobs(HnKnobs* k) {
   k->no_irfskip = std::getenv("HN_NO_IRFSKIP") != nullptr;
   k->pairdist_valu = std::getenv("HN_PAIRDIST_VALU") != nullptr;
   k->pairdist_reg = env_int("HN_PAIRDIST_REG", 0) != 0;
+  k->pairdist_spread = env_int("HN_PAIRDIST_SPREAD", 1) != 0;
   k->front_fold = env_int("HN_FRONT_FOLD", 0) != 0;
   k->u8_apart = env_int("HN_U8_APART", 0) != 0;
   k->front_xch3 = env_int("HN_FRONT_XCH3", 0) != 0;

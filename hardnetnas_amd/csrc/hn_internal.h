@@ -20,6 +20,7 @@ struct HnKnobs {
   bool no_irfskip = false;     // HN_NO_IRFSKIP: k_irf + k_skip_s2 instead of k_irf_skip
   bool pairdist_valu = false;  // HN_PAIRDIST_VALU: fp32 VALU pair-distance kernel
   bool pairdist_reg = false;   // HN_PAIRDIST_REG: register-staged positives instead of the LDS-DMA ring
+  bool pairdist_spread = true;  // HN_PAIRDIST_SPREAD: the ring's DMA issued inside the MFMA chain (0: before it)
   bool front_fold = false;     // HN_FRONT_FOLD: the NAS front's pwl with the LDS partial-sum fold
   bool u8_apart = false;       // HN_U8_APART: uint8 input preprocessed into the workspace first (A/B)
   bool front_xch3 = false;     // HN_FRONT_XCH3: the k3 front's dw per channel group (SGPR weights, s_x; two

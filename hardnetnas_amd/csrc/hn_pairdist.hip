@@ -444,7 +444,8 @@ HN_DEV void wait_vm() {  // s_waitcnt vmcnt(N), lgkmcnt / expcnt untouched
 
 // ABL (timing only, experiments library, HN_PAIRDIST_ABL): bit 0 no epilogue (the distance / minimum VALU and
 // the masked path), bit 1 no positive-tile DMA after the prologue (stale tiles), bit 2 no MFMAs
-template <bool SWAP, int NW, int ABL = 0>
+// SPREAD: the next-but-one tile's DMA issued inside the first sub-tile's MFMA chain instead of before it
+template <bool SWAP, int NW, int ABL = 0, bool SPREAD = false>
 __global__ __launch_bounds__(NW * 64) void k_pairdist_ring(
     const float* __restrict__ a, int NA, int row0, const uint16_t* __restrict__ ph, const uint16_t* __restrict__ pl,
     int B, const float* __restrict__ asq, const float* __restrict__ psq, float xthr, float* __restrict__ rowmin,
@@ -494,6 +495,33 @@ __global__ __launch_bounds__(NW * 64) void k_pairdist_ring(
   // statement), so hipcc does not track it as a pending LDS write: its alias analysis would
   // otherwise wait vmcnt(0) before LDS reads of the other buffers; the waits here are explicit.
   const unsigned wv = __builtin_amdgcn_readfirstlane(wave);
+  // DMA instruction k of this wave's share of tile j0 (k = G: wave 0's |p|^2 piece)
+  auto issue_piece = [&](char* buf, int j0, int k) {
+    if constexpr ((ABL & 2) != 0) {
+      if (j0 >= 2 * TN) return;
+    }
+    if (k == G) {
+      if (wv == 0) {
+        const float* src = psq + min(j0 + lane, B - 1);
+        const unsigned dst = (unsigned)(uintptr_t)(lds_ptr_t)(buf + 2 * PLANE);
+        unsigned keep;
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
+      }
+      return;
+    }
+    {
+      const int gi = wave * G + k, plane = gi >> 4, r4 = (gi & 15) * 4;
+      const int row = r4 + (lane >> 4), d = lane & 15;
+      const int jr = min(j0 + row, B - 1);
+      const uint16_t* src = (plane ? pl : ph) + (size_t)jr * 128 + ((d ^ (row & 15)) << 3);
+      const int gu = (int)wv * G + k;
+      const unsigned dst = (unsigned)(uintptr_t)(lds_ptr_t)(buf + (gu >> 4) * PLANE + (gu & 15) * 4 * ROWB);
+      unsigned keep;
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
+    }
+  };
   auto issue = [&](char* buf, int j0) {
     if constexpr ((ABL & 2) != 0) {
       if (j0 >= 2 * TN) return;
@@ -561,7 +589,7 @@ __global__ __launch_bounds__(NW * 64) void k_pairdist_ring(
     }
   };
   // one 32-column sub-tile's bf16x3 chain (K = 128) with the previous sub-tile's epilogue woven in
-  auto chain_epi = [&](const char* cur, int nt, f32x16 accp, float pj, int dsel, int cslot) {
+  auto chain_epi = [&](const char* cur, int nt, f32x16 accp, float pj, int dsel, int cslot, auto hook) {
     f32x16 acc = areg;
     float lm = INFINITY;
     const int row = nt * 32 + r, sw = row & 15;
@@ -580,6 +608,7 @@ __global__ __launch_bounds__(NW * 64) void k_pairdist_ring(
         acc[ks] += __builtin_bit_cast(float, bh.x ^ bl.y);
       else
         acc = mfma3(ah[ks], al[ks], as_bf16x8(bh), as_bf16x8(bl), acc);
+      hook(ks);
       if constexpr ((ABL & 1) != 0) {
         if (ks + 1 < 8) {
           bh = nh;
@@ -635,12 +664,26 @@ __global__ __launch_bounds__(NW * 64) void k_pairdist_ring(
     const int j0 = t * TN;
     if (SWAP && t >= 2 && wave == (t - 2) % NW) reduce_cols(t - 2);
     const bool more2 = t + 2 < ntile;
-    if (more2) issue(nxt2, j0 + 2 * TN);
     const float* ps = reinterpret_cast<const float*>(cur + 2 * PLANE);
+    if constexpr (SPREAD) {
+      // tile t + 2's DMA spread over the first sub-tile's MFMA chain (the G pieces evenly behind its 8
+      // mfma3, |p|^2 last), so the issue stalls of the two waves of a SIMD do not meet after the barrier
+      accp = chain_epi(cur, 0, accp, pjp, dselp, cslotp, [&](int ks) {
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt) {
-      accp = chain_epi(cur, nt, accp, pjp, dselp, cslotp);
-      sub_meta(ps, j0, nt, pjp, dselp, cslotp, t);
+        for (int k = 0; k < G; ++k)
+          if (more2 && (k * 8) / G == ks) issue_piece(nxt2, j0 + 2 * TN, k);
+      });
+      if (more2) issue_piece(nxt2, j0 + 2 * TN, G);
+      sub_meta(ps, j0, 0, pjp, dselp, cslotp, t);
+      accp = chain_epi(cur, 1, accp, pjp, dselp, cslotp, [](int) {});
+      sub_meta(ps, j0, 1, pjp, dselp, cslotp, t);
+    } else {
+      if (more2) issue(nxt2, j0 + 2 * TN);
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        accp = chain_epi(cur, nt, accp, pjp, dselp, cslotp, [](int) {});
+        sub_meta(ps, j0, nt, pjp, dselp, cslotp, t);
+      }
     }
     sync_tile(more2);  // retire tile t + 1's DMA, leaving tile t + 2's in flight
   };
@@ -770,7 +813,14 @@ hipError_t hn_launch_pairdist_rows(const float* a, int NA, int row0, const float
       }
     } else
 #endif
-    if (ring && colmin)
+    const bool spread = hn_knobs().pairdist_spread;
+    if (ring && colmin && spread)
+      hipLaunchKernelGGL((k_pairdist_ring<true, NW, 0, true>), grid, block, 0, st, a, NA, row0, ph, pl, B, asq, psq,
+                         xthr, rowmin, cm);
+    else if (ring && spread)
+      hipLaunchKernelGGL((k_pairdist_ring<false, NW, 0, true>), grid, block, 0, st, a, NA, row0, ph, pl, B, asq, psq,
+                         xthr, rowmin, nullptr);
+    else if (ring && colmin)
       hipLaunchKernelGGL((k_pairdist_ring<true, NW>), grid, block, 0, st, a, NA, row0, ph, pl, B, asq, psq, xthr,
                          rowmin, cm);
     else if (ring)
