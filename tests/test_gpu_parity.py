@@ -280,6 +280,25 @@ def test_persistent_kernels_past_one_round(name, cuda_device):
     assert (y[idx.to(cuda_device)].cpu() - ref).abs().max().item() <= _tol(name)
 
 
+@pytest.mark.parametrize("name", ["wang2", "wang3", "wang4"])
+def test_nas_at_the_timed_size(name, cuda_device):
+    """BASELINE config 3's exact launch (262,144 patches: four 65,536-patch chunks, the bench's grids)
+    for each searched net: a strided 1,024-row sample (away from the chunk starts, plus the last row)
+    equals the oracle to 2e-5 and every row has unit norm."""
+    from hardnetnas_amd import synth
+    m, fx, p = build_module(name)
+    m = m.to(cuda_device)
+    b = 262144
+    x = torch.from_numpy(synth.synth_patches(b, seed=1003)).to(cuda_device)
+    with torch.no_grad():
+        y = m(x)
+    assert torch.isfinite(y).all()
+    assert (y.norm(dim=1) - 1).abs().max().item() < 1e-5
+    idx = torch.cat([torch.arange(0, b, b // 1023)[:1023] + 127, torch.tensor([b - 1])])
+    ref = _oracle_rows(name, p, x[idx.to(cuda_device)].cpu())
+    assert (y[idx.to(cuda_device)].cpu() - ref).abs().max().item() <= _tol(name)
+
+
 @pytest.mark.parametrize("u8", [False, True])
 def test_c12_group_and_subchunk_sizes_are_bitwise_neutral(u8, cuda_device, monkeypatch):
     """k_c12 over groups (HN_C12_GROUP) and conv3..conv5 over sub-chunks of them (HN_SUBCHUNK): odd
