@@ -1941,6 +1941,7 @@ bool hn_hardnet_variant_ok(int layer, int v) {
   if (v == 32 || v == 33) return layer == 3;                 // F(4,3) (k_conv_w4), weight ring 6 / 9 (digits w / x)
 #ifdef HN_EXPERIMENTS
   if ((v >= 22 && v <= 25) || v == 29 || v == 30 || v == 31) return layer == 3 || layer == 5;  // its timing-only ablations (ABL 1 / 2 / 4 / 8; t: 16; u: 32, v: 34)
+  if (v == 34 || v == 35) return layer == 3 || layer == 5;  // wave-priority A/B (y: MFMA waves first, z: producers first)
 #endif
   if (v == 16) return layer == 3 || layer == 5;
   if (v == 0 || v == 5 || v == 6) return true;  // (layer 1 always runs conv1_launch)
@@ -1991,6 +1992,7 @@ hipError_t hn_launch_hardnet_conv(int layer, int variant, const HardnetDev& d, c
   if (variant >= 22 && variant <= 25) return hn_launch_wino1(layer, 100 + (1 << (variant - 22)), d, in, out, P, st);
   if (variant == 29) return hn_launch_wino1(layer, 116, d, in, out, P, st);
   if (variant == 30 || variant == 31) return hn_launch_wino1(layer, variant == 30 ? 132 : 134, d, in, out, P, st);
+  if (variant == 34 || variant == 35) return hn_launch_wino1(layer, variant == 34 ? 164 : 228, d, in, out, P, st);
 #endif
   if (variant == 16) {  // coalesced epilogue stores
     switch (layer) {

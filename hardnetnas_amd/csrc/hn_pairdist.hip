@@ -800,6 +800,7 @@ hipError_t hn_launch_pairdist_rows(const float* a, int NA, int row0, const float
     constexpr int NW = decltype(nw)::value;
     const dim3 grid((NA + 32 * NW - 1) / (32 * NW)), block(64 * NW);
     unsigned* cm = reinterpret_cast<unsigned*>(colmin);
+    const bool spread = hn_knobs().pairdist_spread;
 #ifdef HN_EXPERIMENTS
     const char* abl_e = std::getenv("HN_PAIRDIST_ABL");
     const int abl = abl_e ? std::atoi(abl_e) : 0;
@@ -813,7 +814,6 @@ hipError_t hn_launch_pairdist_rows(const float* a, int NA, int row0, const float
       }
     } else
 #endif
-    const bool spread = hn_knobs().pairdist_spread;
     if (ring && colmin && spread)
       hipLaunchKernelGGL((k_pairdist_ring<true, NW, 0, true>), grid, block, 0, st, a, NA, row0, ph, pl, B, asq, psq,
                          xthr, rowmin, cm);

@@ -170,6 +170,12 @@ __global__ __launch_bounds__((WM * WN + 4) * 64) void k_conv_w1(const float* __r
     *reinterpret_cast<uint4*>(smem + (q >> 1) * C::BUF + (q & 1) * C::PLANE + C::ZROW + o) = make_uint4(0, 0, 0, 0);
   }
   // the two roles split here and share no value: each matches the other's barriers one for one
+  if constexpr ((ABL & 64) != 0) {  // A/B: the MFMA waves issue ahead of the producers
+    if (!producer) __builtin_amdgcn_s_setprio(1);
+  }
+  if constexpr ((ABL & 128) != 0) {  // A/B: the producers issue ahead of the MFMA waves
+    if (producer) __builtin_amdgcn_s_setprio(1);
+  }
   if (producer) {
     if constexpr ((ABL & 1) != 0) {  // timing only: idle producers
 #pragma unroll 1
@@ -762,7 +768,9 @@ hipError_t hn_launch_wino1(int layer, int wd, const HardnetDev& d, const float* 
   if (wd == 108) return launch_w1<CI, CO, HH, NPP, WMM, WNN, true, 8, 8>(in, out, d.wino1[L], d.bias[L], P, st); \
   if (wd == 116) return launch_w1<CI, CO, HH, NPP, WMM, WNN, true, 8, 16>(in, out, d.wino1[L], d.bias[L], P, st); \
   if (wd == 132) return launch_w1<CI, CO, HH, NPP, WMM, WNN, true, 8, 32>(in, out, d.wino1[L], d.bias[L], P, st); \
-  if (wd == 134) return launch_w1<CI, CO, HH, NPP, WMM, WNN, true, 8, 34>(in, out, d.wino1[L], d.bias[L], P, st);
+  if (wd == 134) return launch_w1<CI, CO, HH, NPP, WMM, WNN, true, 8, 34>(in, out, d.wino1[L], d.bias[L], P, st); \
+  if (wd == 164) return launch_w1<CI, CO, HH, NPP, WMM, WNN, true, 8, 64>(in, out, d.wino1[L], d.bias[L], P, st); \
+  if (wd == 228) return launch_w1<CI, CO, HH, NPP, WMM, WNN, true, 8, 128>(in, out, d.wino1[L], d.bias[L], P, st);
 #else
 #define HN_W1_ABL(CI, CO, HH, NPP, WMM, WNN, L)
 #endif
