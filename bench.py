@@ -610,8 +610,14 @@ def run(opts, world, rank, local, dev, on_gpu, backend):
                             "peak": round(PEAK_BF16X3, 1), "unit": "TFLOP/s", "frac": round(mfma_frac, 4)}
                 fracs = {"mfma": mfma_frac, "hbm": hbm_frac, "valu_issue": valu_frac or 0.0}
                 top = max(fracs, key=fracs.get)
-                # what binds the stage: the resource nearest its roof, or latency when none is at half of it
-                roof["binding_counter"] = top if fracs[top] >= 0.5 else "latency (MFMA, HBM and VALU issue all < 0.5)"
+                # what binds the stage: the resource nearest its roof, or latency when none is at half of it;
+                # "bound" then says latency too, and "frac_roof" names the roof achieved / peak / frac refer to
+                roof["frac_roof"] = roof["bound"]
+                if fracs[top] >= 0.5:
+                    roof["binding_counter"] = top
+                else:
+                    roof["binding_counter"] = "latency (MFMA, HBM and VALU issue all < 0.5)"
+                    roof["bound"] = "latency"
                 roof.update({"mfma_tflops": round(mfma_tf, 2), "mfma_frac": round(mfma_frac, 4),
                              "hbm_gbps": round(hbm_gbps, 1), "hbm_frac": round(hbm_frac, 4),
                              "hbm_bytes_basis": "PMC" if traffic else "algorithmic",
@@ -690,11 +696,12 @@ TRAIN_PAIRS = 512  # the reference training loop's --batch-size (hardnet/HardNet
 PEAK_F32 = 157.3   # TFLOP/s, the f32-input MFMA (= the f32 vector peak): the train kernels' exact fp32 products
 
 
-def cpu_baseline_train(seconds: float = 6.0, pairs: int = 64):
+def cpu_baseline_train(seconds: float = 10.0, pairs: int = TRAIN_PAIRS):
     """The oracle's train step on the host cores (the cgroup quota's thread count): hardnet_train_forward
     of anchors and positives (batch statistics, running-stat update), the oracle loss_hardnet
     (anchor_swap, triplet margin), autograd backward and the reference's SGD step, on a bounded batch of
-    ``pairs`` pairs; patches/s = 2 pairs / step time (median over the runs)."""
+    ``pairs`` pairs (default: the GPU leg's 512, so the two rates are like for like); patches/s =
+    2 pairs / step time (median over the runs)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from oracle import hardnet_oracle as O
     torch.manual_seed(0)
@@ -791,6 +798,119 @@ def run_train(opts, dev, with_cpu: bool):
     return res
 
 
+EVAL_BATCH = 512  # the reference eval loop's --test-batch-size (hardnet/HardNet.py:100)
+
+
+def cpu_baseline_eval(model, seconds: float = 6.0, b: int = EVAL_BATCH):
+    """The eval batch on the host cores (the cgroup quota's thread count): the oracle's forward of b anchors
+    and b positives and the per-pair distance of HardNet.py:456-458; pairs/s and patches/s (median)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from oracle import hardnet_oracle as O
+    p = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    xa = torch.from_numpy(synth.synth_patches(b, seed=41))
+    xp = xa + 0.3 * torch.from_numpy(synth.synth_patches(b, seed=42))
+    quota = _cpu_quota()
+    nproc = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    threads = max(1, int(quota)) if 0 < quota < nproc else nproc
+    torch.set_num_threads(threads)
+
+    def batch():
+        with torch.no_grad():
+            oa, op = O.hardnet_forward(p, xa), O.hardnet_forward(p, xp)
+            return torch.sqrt(torch.sum((oa - op) ** 2, 1))
+
+    batch()
+    times, t_start = [], time.perf_counter()
+    while time.perf_counter() - t_start < seconds or len(times) < 3:
+        t0 = time.perf_counter()
+        batch()
+        times.append(time.perf_counter() - t0)
+    t = statistics.median(times)
+    return {"value": round(2 * b / t, 1), "unit": "patches/s", "ms_per_batch": round(t * 1e3, 2), "cores": threads,
+            "kind": "port", "model": _cpu_model_string(),
+            "sample": f"oracle/hardnet_oracle.py hardnet_forward of {b} anchors + {b} positives and the pair "
+                      f"distance, {len(times)} batches over ~{seconds:.0f} s, median"}
+
+
+def run_eval512(opts, dev, with_cpu: bool):
+    """The drop-in caller's own batch: the reference eval loop (hardnet/HardNet.py:443-459) runs, per batch,
+    ``out_a = model(data_a); out_p = model(data_p)`` under torch.no_grad() at --test-batch-size 512 and
+    ``dists = torch.sqrt(torch.sum((out_a - out_p) ** 2, 1))``.  Here the same three lines on the module
+    (hardnetnas_amd.HardNet, eval mode: the native op through torch.ops.hardnet_mi355x.forward), over 64
+    resident batch pairs in turn (inputs already in HBM; the loader's host->device copy is not timed).
+    Reports hipEvent ms per batch (device time, launch stream = torch's current stream), wall ms per batch
+    (includes the Python / ctypes / allocator path), caching-allocator allocations and device mallocs per
+    batch, and the kernel launches of one 512-patch forward."""
+    model = build_model("hardnet").to(dev)
+    b, nb = EVAL_BATCH, 64
+    g = torch.Generator(device=dev).manual_seed(51)
+    xa = synth_input_on_device(b * nb, dev, seed=52).view(nb, b, 1, 32, 32)
+    xp = xa + 0.3 * torch.randn(xa.shape, device=dev, generator=g)
+    steps, warmup = max(200, 10 * opts.steps), 10
+    with torch.no_grad():
+        def batch(i):
+            out_a = model(xa[i % nb])
+            out_p = model(xp[i % nb])
+            return torch.sqrt(torch.sum((out_a - out_p) ** 2, 1))
+        for i in range(warmup):
+            batch(i)
+        torch.cuda.synchronize()
+        m0 = torch.cuda.memory_stats(dev)
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        t0 = time.perf_counter()
+        for i in range(steps):
+            evs[i][0].record()
+            d = batch(i)
+            evs[i][1].record()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        m1 = torch.cuda.memory_stats(dev)
+        gpu_ms = sorted(e[0].elapsed_time(e[1]) for e in evs)
+        # kernel launches and stage times of one 512-patch forward (the library's own hipEvent records)
+        nm = NativeModel.from_module(model, dev)
+        out = torch.empty((b, 128), device=dev)
+        ws = torch.empty(nm.workspace_bytes(b), device=dev, dtype=torch.uint8)
+        nm.forward(xa[0], out=out, workspace=ws)
+        torch.cuda.synchronize()
+        nm.stage_times()
+        nm.set_profiling(True)
+        nm.forward(xa[0], out=out, workspace=ws)
+        torch.cuda.synchronize()
+        nm.set_profiling(False)
+        st = nm.stage_times()
+        ref_d = None
+        if with_cpu:
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            from oracle import hardnet_oracle as O
+            p = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+            i = (steps - 1) % nb
+            ref_d = torch.sqrt(torch.sum((O.hardnet_forward(p, xa[i].cpu()) - O.hardnet_forward(p, xp[i].cpu())) ** 2, 1))
+    n_alloc = (m1["allocation.all.allocated"] - m0["allocation.all.allocated"]) / steps
+    n_seg = m1["segment.all.allocated"] - m0["segment.all.allocated"]
+    res = {"value": round(2 * b * steps / elapsed / 1e6, 4), "unit": "Mpatches/s",
+           "ms_per_batch": round(elapsed / steps * 1e3, 4), "steps": steps, "warmup": warmup, "dtype": "bf16x3",
+           "gpu_ms_per_batch": {"median": round(gpu_ms[len(gpu_ms) // 2], 4), "min": round(gpu_ms[0], 4),
+                                "mean": round(sum(gpu_ms) / steps, 4)},
+           "pairs_per_s": round(b * steps / elapsed, 1),
+           "config": {"workload": f"reference eval loop batch (HardNet.py:454-458): model(data_a), model(data_p) "
+                                  f"on {b}-patch batches under torch.no_grad() through the drop-in module, then "
+                                  "the per-pair L2 distance; 64 resident synthetic batch pairs in turn",
+                      "model": "hardnet", "batch": b, "parallelism": "dp1"},
+           "module_path": {"allocator_allocations_per_batch": n_alloc,
+                           "device_mallocs_during_timed_batches": int(n_seg),
+                           "workspace_bytes_per_forward": int(nm.workspace_bytes(b)),
+                           "kernel_launches_per_forward": int(sum(v[1] for v in st.values())),
+                           "stage_ms_per_forward": {k: round(v[0], 4) for k, v in st.items()}},
+           "cpu_baseline": None}
+    if ref_d is not None:
+        res["check"] = {"pairs": b, "max_abs_err_dist_vs_oracle": float((d.cpu() - ref_d).abs().max())}
+        cb = cpu_baseline_eval(model)
+        res["cpu_baseline"] = cb
+        res["gpu_vs_cpu"] = round(res["value"] * 1e6 / cb["value"], 1)
+    del model, xa, xp, nm, ws, out
+    return res
+
+
 # the other BASELINE configurations measured after the headline one on a default 1-GPU run
 EXTRA_CONFIGS = [("3:wang2", "wang2", None), ("3:wang3", "wang3", None), ("3:wang4", "wang4", None),
                  ("5", "hardnet", 5)]
@@ -866,6 +986,8 @@ def main():
             result["extra_configs"][key] = {k: r[k] for k in EXTRA_KEYS if k in r}
         torch.cuda.empty_cache()
         result["extra_configs"]["train"] = run_train(args, dev, with_cpu=not args.no_cpu_baseline)
+        torch.cuda.empty_cache()
+        result["extra_configs"]["eval512"] = run_eval512(args, dev, with_cpu=not args.no_cpu_baseline)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

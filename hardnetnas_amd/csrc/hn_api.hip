@@ -665,12 +665,12 @@ static int build_hardnet(hn_model* m, Cursor& cur) {
       if ((rc = m->upload(pack_wino1(f.w, cin[l], cout[l]), &c))) return rc;
       m->hd.wino1[l] = c;
     }
-    if (l == 3) {  // 1-D Winograd F(4,3) U fragments (hn_wino1.hip k_conv_w4)
+#ifdef HN_EXPERIMENTS
+    if (l == 3) {  // 1-D Winograd F(4,3) U fragments (hn_wino1.hip k_conv_w4, experiments library only)
       uint16_t* c = nullptr;
       if ((rc = m->upload(pack_wino4(f.w, cin[l], cout[l]), &c))) return rc;
       m->hd.wino4[l] = c;
     }
-#ifdef HN_EXPERIMENTS
     if (l == 3 || l == 5) {  // Winograd U fragments (experiments library only)
       uint16_t* c = nullptr;
       if ((rc = m->upload(pack_wino(f.w, cin[l], cout[l]), &c))) return rc;
@@ -1021,7 +1021,10 @@ static int forward_hardnet(hn_model* m, const float* in, int P, int pmax, float*
         STAGE("conv5", hn_launch_hardnet_conv(5, m->variant[5], m->hd, a2s, a1 + (size_t)s0 * 8192, n, 0.f, st));
       }
     }
-    STAGE("head", hn_launch_head(a1, out, m->hd.wpack[6], m->hd.bias[6], P, 8192, m->desc.l2_eps, st));
+    // a0 -- conv3's output, consumed -- holds the small-batch head's split-K partials (8,192 floats per patch
+    // against its 16,384 per sub-chunk patch)
+    float* const hs = (size_t)16384 * hardnet_sub(m, pmax) >= (size_t)8192 * P ? a0 : nullptr;
+    STAGE("head", hn_launch_head(a1, out, m->hd.wpack[6], m->hd.bias[6], P, 8192, m->desc.l2_eps, st, false, hs));
     return HN_OK;
   } else {
     if (m->unfused_stem) {
@@ -1035,7 +1038,7 @@ static int forward_hardnet(hn_model* m, const float* in, int P, int pmax, float*
   STAGE("conv3", hn_launch_hardnet_conv(3, m->variant[3], m->hd, a2, a1, P, 0.f, st));
   STAGE("conv4", hn_launch_hardnet_conv(4, m->variant[4], m->hd, a1, a2, P, 0.f, st));
   STAGE("conv5", hn_launch_hardnet_conv(5, m->variant[5], m->hd, a2, a1, P, 0.f, st));
-  STAGE("head", hn_launch_head(a1, out, m->hd.wpack[6], m->hd.bias[6], P, 8192, m->desc.l2_eps, st));
+  STAGE("head", hn_launch_head(a1, out, m->hd.wpack[6], m->hd.bias[6], P, 8192, m->desc.l2_eps, st, false, a2));
   return HN_OK;
 }
 
@@ -1146,9 +1149,11 @@ static int forward_nas(hn_model* m, const float* in, int P, int pmax, float* out
                                L.semid, st));
     std::swap(x, y);
   }
-  if (m->head_pack)
-    STAGE("head", hn_launch_head(x, out, m->head_pack, m->head_b, P, m->head_k, m->desc.l2_eps, st, true));
-  else
+  if (m->head_pack) {
+    // (any of the four buffers but the head's input holds the small-batch split-K partials)
+    float* const hs = m->ws_floats_per_patch >= (size_t)head_split(m->head_k) * 128 ? (x == ws ? ws + per : ws) : nullptr;
+    STAGE("head", hn_launch_head(x, out, m->head_pack, m->head_b, P, m->head_k, m->desc.l2_eps, st, true, hs));
+  } else
     STAGE("head", hn_launch_nas_head(x, out, m->head_w, m->head_b, P, m->head_k, m->desc.l2_eps, st));
   return HN_OK;
 }

@@ -920,22 +920,23 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 
 }  // namespace
 
-// HN_C12_CFG variants (A/B and ablation builds; 12 is production):
+// HN_C12_CFG variants of the direct k_c12 (12 is the product library's direct-conv1 fallback; the default is
+// 15 = k_c12s, hn_c12w.hip).  The experiments library also has the measured-slower forms:
 //   0 <8 waves, 4-row bands, 2 waves/SIMD>   1 <4, 4, 1> (512-register file)
 //   2 <4 waves, 2-row bands, 2 workgroups/CU>
 //   3 / 4: 0 with tap-interleaved P3, conv2 fragments 2 / 3 taps ahead;  5 / 6: the same for 2
 //   7 / 8: 2 / 5 with the tap-interleaved P2 (both halves' chains MFMA by MFMA);  9: 0 with it
 //   10 / 11: 7 with the P1 wave priority raised to 1 / 3;  12: 7 with P3 and P1 at priority 1
+//   13: k_c12h (MFMA / helper waves split per SIMD);  14: k_c12w (conv1 as F(4,3), hn_c12w.hip)
+#ifdef HN_EXPERIMENTS
 #define HN_C12_CFGS(X)                                                                   \
   X(0, 8, 4, 2, false, 2, false, 0) X(1, 4, 4, 1, false, 2, false, 0) X(2, 4, 2, 2, false, 2, false, 0) \
   X(3, 8, 4, 2, true, 2, false, 0) X(4, 8, 4, 2, true, 3, false, 0) X(5, 4, 2, 2, true, 2, false, 0)     \
   X(6, 4, 2, 2, true, 3, false, 0) X(7, 4, 2, 2, false, 2, true, 0) X(8, 4, 2, 2, true, 2, true, 0)      \
   X(9, 8, 4, 2, false, 2, true, 0) X(10, 4, 2, 2, false, 2, true, 1) X(11, 4, 2, 2, false, 2, true, 3) \
   X(12, 4, 2, 2, false, 2, true, 5)
-#ifdef HN_EXPERIMENTS
-constexpr int kC12Cfgs = 14;  // 13: k_c12h (MFMA / helper waves split per SIMD), not in HN_C12_CFGS
 #else
-constexpr int kC12Cfgs = 13;
+#define HN_C12_CFGS(X) X(12, 4, 2, 2, false, 2, true, 5)
 #endif  // (P1, P3) at priority (2, 1) / (1, 2) / (2, 2): within the box noise of 12, removed
 
 bool hn_c12_cfg_ok(int cfg, int abl) {
@@ -947,14 +948,13 @@ bool hn_c12_cfg_ok(int cfg, int abl) {
     return abl == 0;
 #endif
   }
-  if (cfg == kC12Wino) {  // k_c12w (hn_c12w.hip)
 #ifdef HN_EXPERIMENTS
+  if (cfg == kC12Wino)  // k_c12w (hn_c12w.hip)
     return abl == 0 || abl == 1 || abl == 2 || abl == 4 || abl == 6 || abl == 64 || abl == 192;
+  if (cfg < 0 || cfg > 13) return false;
 #else
-    return abl == 0;
+  if (cfg != 12) return false;
 #endif
-  }
-  if (cfg < 0 || cfg >= kC12Cfgs) return false;
   if (!abl) return true;
 #ifdef HN_EXPERIMENTS
   switch (cfg) {
@@ -973,28 +973,31 @@ hipError_t hn_launch_c12(const float* in, float* out, const HardnetDev& d, int P
   const int cfg = hn_knobs().c12_cfg;  // same-box A/Bs: 12 2-4 % < 7 1.5 % < 2 4.5 % < 0
   const int abl = hn_knobs().c12_abl;
   if (!hn_c12_cfg_ok(cfg, abl)) return hipErrorInvalidValue;
+#ifdef HN_EXPERIMENTS
   if (cfg == kC12Wino) return hn_launch_c12w(in, out, d, P, eps, st, u8, abl);
+#endif
   if (cfg == kC12Split) return hn_launch_c12s(in, out, d, P, eps, st, u8);
   if (u8 && ((cfg != 12 && cfg != 13) || abl)) return hipErrorInvalidValue;  // the uint8 loads: production builds only
-  static const void* const fns[kC12Cfgs] = {
-#define HN_C12_FN(C, W, R, E, I, A, Q, PR) reinterpret_cast<const void*>(&k_c12<0, W, R, E, I, A, Q, PR>),
-      HN_C12_CFGS(HN_C12_FN)
+  const void* fn = nullptr;
+  int nw = 0;
+  switch (cfg) {
+#define HN_C12_FN(C, W, R, E, I, A, Q, PR)                               \
+  case C:                                                                \
+    fn = reinterpret_cast<const void*>(&k_c12<0, W, R, E, I, A, Q, PR>); \
+    nw = W;                                                              \
+    break;
+    HN_C12_CFGS(HN_C12_FN)
 #undef HN_C12_FN
 #ifdef HN_EXPERIMENTS
-      reinterpret_cast<const void*>(&k_c12h<-1>)
+    case 13:
+      fn = reinterpret_cast<const void*>(&k_c12h<-1>);
+      nw = 8;
+      break;
 #endif
-  };
-  static const int nws[kC12Cfgs] = {
-#define HN_C12_NWS(C, W, R, E, I, A, Q, PR) W,
-      HN_C12_CFGS(HN_C12_NWS)
-#undef HN_C12_NWS
-#ifdef HN_EXPERIMENTS
-      8
-#endif
-  };
-  const int nw = nws[cfg];
+  }
+  if (!fn) return hipErrorInvalidValue;
   int resident = 0;
-  const hipError_t e = hn_resident_blocks(fns[cfg], nw * 64, 0, &resident);
+  const hipError_t e = hn_resident_blocks(fn, nw * 64, 0, &resident);
   if (e != hipSuccess) return e;
   const int grid = (int)std::min<long>((long)P, resident);
   const void* src = u8 ? u8->in : static_cast<const void*>(in);

@@ -33,9 +33,11 @@ namespace {
 
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 
-constexpr int NW = 4;                   // waves per workgroup
+#ifdef HN_EXPERIMENTS
+constexpr int NW = 4;                   // k_c12w: waves per workgroup
+constexpr int NA0 = 6, NA1 = 5;         // k_c12w: ring rows (a band's conv1 reads 6 a0 rows, conv2 5 a1 rows)
+#endif
 constexpr int VROW = 6 * 8 * 128;       // W0 ring: bytes per a0 row (6 xi x 8 tiles x 128 B)
-constexpr int NA0 = 6, NA1 = 5;         // ring rows (a band's conv1 reads 6 a0 rows, conv2 5 a1 rows)
 constexpr int PXB = 160, W1C = 33;      // W1: bytes per pixel, column slots (x = -1 .. 31)
 constexpr int W1ROW = W1C * PXB;
 constexpr int IRS = 72, IPL = 35 * IRS; // normalised patch planes: bytes per row (36 bf16) / plane
@@ -70,6 +72,7 @@ HN_DEV uint4 swap_hilo(uint2 hi, uint2 lo) {
 // W1 column slot of a1 column x (x = -1 .. 31): even (x + 1) -> (x + 1) / 2, odd -> 17 + x / 2
 HN_DEV int w1_slot(int x) { return ((x + 1) & 1) ? 17 + (x >> 1) : (x + 1) >> 1; }
 
+#ifdef HN_EXPERIMENTS  // k_c12w (HN_C12_CFG=14): measured slower than k_c12s, experiments library only
 // U8: -1 = fp32 [P,1,32,32] input; HN_RESIZE_* = uint8 patches preprocessed in the load (hn_preproc.h)
 // ABL (timing builds of the experiments library only; 0 in production): bit 0 / 1 / 2 skip the stem /
 // conv1 / conv2 MFMAs, bit 6 stamps s_memtime at the phase boundaries of every band of each
@@ -484,6 +487,8 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
 #undef HN_W_TS2
 }
 
+#endif  // HN_EXPERIMENTS
+
 // ----------------------------------------------------------------------------------------------------
 // k_c12s: k_c12w's arithmetic (the K-packed stem, conv1 as F(4,3), direct conv2 -- bit-identical to it)
 // with the roles split per SIMD and the bands software-pipelined.  In k_c12 / k_c12w every wave runs
@@ -497,10 +502,18 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
 //                spread over bands 2-6, the input_norm of the next patch (s_in double-buffered).
 // So every SIMD has one conv1 and one conv2 MFMA stream in flight at once and the stem's latency chain
 // runs beside them.  Rings over the workgroup's whole patch range (row G = 32 patch + y): W0 10 a0 rows
-// (P2 of band g reads 6 while P1 of band g + 1 writes 4), W1 9 a1 rows (P3 of band g - 1 reads 5 while
+// (P2 of band g reads 6 while P1 of band g + 1 writes 4), W1 10 a1 rows (P3 of band g - 1 reads 5 while
 // P2 of band g writes 4), each with one more all-zero row that the padding rows (-1, 32) read.  LDS
-// 148.9 KB, one workgroup per CU.
-constexpr int SNA0 = 10, SNA1 = 9;
+// 152.5 KB, one workgroup per CU.
+//
+// P2's N index n stands for tile n >> 1 of a1 row n & 1 (k_c12w: tile n & 7, row n >> 3), so each 8-lane group
+// of its epilogue's ds_write_b128 holds 4 tiles x 2 rows: 2-way at the 160-byte W1 pixel instead of 8 tiles of one
+// row on 2 distinct 16-byte positions (4-way).  Its V-record reads stay conflict-free because W0 rows are padded
+// to VROW + 128 (adjacent rows in opposite halves of the 256-byte bank row; only reads of the zero row collide),
+// and the W1 ring has 10 rows so that the ring's wrap (-9 rows) keeps row pairs apart as +1 does
+// (tests/test_lds_banks.py::test_c12s_*).  P3's reads are k_c12w's (conflict-free, immediate offsets).
+constexpr int SNA0 = 10, SNA1 = 10;
+constexpr int SVROW = VROW + 128;
 
 // PRB: the B-waves' wave priority (1: their VALU-heavy stem chain and conv2 issue ahead of conv1)
 // ABL (experiments library only): bit 0 / 1 / 2 skip the stem / conv1 / conv2 MFMAs, bit 3 / 4 the B-waves'
@@ -516,7 +529,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const float* __restrict__ stem_b, const uint4* __restrict__ w1u, const float* __restrict__ b1,
     const uint4* __restrict__ w2p, const float* __restrict__ b2, int P, float eps, float pmean,
     float pstd, int pnorm) {
-  __shared__ __attribute__((aligned(16))) char s_w0[(SNA0 + 1) * VROW];
+  __shared__ __attribute__((aligned(16))) char s_w0[(SNA0 + 1) * SVROW];
   __shared__ __attribute__((aligned(16))) char s_w1[(SNA1 + 1) * W1ROW];
   __shared__ __attribute__((aligned(16))) char s_in[2][2 * IPL];
   __shared__ __attribute__((aligned(16))) float s_st[2][2 * 16 * 64];  // a2 staging, by band parity
@@ -535,7 +548,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   if (pb >= pe) return;  // workgroup-uniform
   const int np = (int)(pe - pb), G = 8 * np;
 
-  for (int i = t; i < (SNA0 + 1) * VROW / 16; i += 512) reinterpret_cast<uint4*>(s_w0)[i] = make_uint4(0, 0, 0, 0);
+  for (int i = t; i < (SNA0 + 1) * SVROW / 16; i += 512) reinterpret_cast<uint4*>(s_w0)[i] = make_uint4(0, 0, 0, 0);
   for (int i = t; i < (SNA1 + 1) * W1ROW / 16; i += 512) reinterpret_cast<uint4*>(s_w1)[i] = make_uint4(0, 0, 0, 0);
   for (int i = t; i < 4 * IPL / 16; i += 512) reinterpret_cast<uint4*>(&s_in[0][0])[i] = make_uint4(0, 0, 0, 0);
   if (t < 128) {  // stem A (16x16x32) of channel half t >> 6, K-packed as k_c12w's without the bias slots
@@ -617,7 +630,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     {
       const int p = gq >> 3, band = gq & 7, y = y0 + pj;
       const int pchunk = ((2 * ph + (g16 >> 1)) + 4 * (g16 & 1)) ^ pT;
-      c.S = s_w0 + ((32 * p + y) % SNA0) * VROW + pT * 128 + 16 * pchunk;
+      c.S = s_w0 + ((32 * p + y) % SNA0) * SVROW + pT * 128 + 16 * pchunk;
       // row 5 belongs to band 1; row 32 is padding; a band past the range stores nothing
       c.wr = gq < G && y <= 31 && !(band == 0 && y == 5);
     }
@@ -706,7 +719,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       HN_S_TS(0);
       if (g < G) {
         const int p = g >> 3, band = g & 7;
-        const int ln = opaque_lane(), g16 = ln >> 4, tj = (ln >> 3) & 1, tt = ln & 7;
+        const int ln = opaque_lane(), g16 = ln >> 4, tj = ln & 1, tt = (ln >> 1) & 7;
         f32x4v acc[6];
 #pragma unroll
         for (int xi = 0; xi < 6; ++xi) acc[xi] = f32x4v{};
@@ -716,7 +729,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         for (int ky = 0; ky < 3; ++ky) {
           const int r = 4 * band + 2 * rp + tj - 1 + ky;
           const int slot = (r < 0 || r > 31) ? SNA0 : (32 * p + r) % SNA0;
-          vrow[ky] = s_w0 + slot * VROW + tt * 128;
+          vrow[ky] = s_w0 + slot * SVROW + tt * 128;
         }
         const int ohi = 16 * (g16 ^ tt), olo = 16 * ((4 + g16) ^ tt);
         constexpr int R2 = PD2 + 1;
@@ -875,7 +888,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const int ln = opaque_lane(), c16 = ln & 15, g16 = ln >> 4;
     f32x4v acc[2];
     acc[0] = acc[1] = *reinterpret_cast<const f32x4v*>(s_b2 + 16 * aw + 4 * g16);
-    const char* srow[2][3];  // a1 row r = 4 band + 2 ry - 1 + dy: slot (32 p + r) % 9, row -1 -> 9
+    const char* srow[2][3];  // a1 row r = 4 band + 2 ry - 1 + dy: slot (32 p + r) % 10, row -1 -> 10
 #pragma unroll
     for (int ry = 0; ry < 2; ++ry)
 #pragma unroll
@@ -1025,6 +1038,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 
 }  // namespace
 
+#ifdef HN_EXPERIMENTS
 hipError_t hn_launch_c12w(const float* in, float* out, const HardnetDev& d, int P, float eps, hipStream_t st,
                           const HnU8In* u8, int abl) {
   if (P <= 0) return hipSuccess;
@@ -1077,6 +1091,8 @@ hipError_t hn_launch_c12w(const float* in, float* out, const HardnetDev& d, int 
   return hipGetLastError();
 }
 
+#endif  // HN_EXPERIMENTS
+
 hipError_t hn_launch_c12s(const float* in, float* out, const HardnetDev& d, int P, float eps, hipStream_t st,
                           const HnU8In* u8) {
   if (P <= 0) return hipSuccess;
@@ -1092,10 +1108,10 @@ hipError_t hn_launch_c12s(const float* in, float* out, const HardnetDev& d, int 
   hipLaunchKernelGGL((k_c12s<U, ##__VA_ARGS__>), dim3(grid), dim3(512), 0, st, src, out, d.stem_w, d.stem_b, \
                      static_cast<const uint4*>(d.c12_w1w), d.bias[1], static_cast<const uint4*>(d.c12_w2),   \
                      d.bias[2], P, eps, pm, ps, pn)
+#ifdef HN_EXPERIMENTS
   const int pd = hn_knobs().c12w_pd;
   const int abl = hn_knobs().c12_abl + (hn_knobs().c12w_pd == 21 && hn_knobs().c12_abl == 84 ? 1000 : 0);
   if (abl) {
-#ifdef HN_EXPERIMENTS
     if (u8) return hipErrorInvalidValue;
     switch (abl) {
       case 1: HN_C12S_GO(-1, 1, 1, 1, 1); break;
@@ -1118,9 +1134,6 @@ hipError_t hn_launch_c12s(const float* in, float* out, const HardnetDev& d, int 
       default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
-#else
-    return hipErrorInvalidValue;
-#endif
   }
   if (!u8 && pd != 11) {
     switch (pd) {
@@ -1136,7 +1149,10 @@ hipError_t hn_launch_c12s(const float* in, float* out, const HardnetDev& d, int 
       case 7: HN_C12S_GO(-1, 1, 1, 0, 0, false, true, true); break;   // + B-waves at priority 0
       default: return hipErrorInvalidValue;
     }
-  } else if (!u8) HN_C12S_GO(-1);
+    return hipGetLastError();
+  }
+#endif  // HN_EXPERIMENTS
+  if (!u8) HN_C12S_GO(-1);
   else if (u8->resize == HN_RESIZE_NONE) HN_C12S_GO(HN_RESIZE_NONE);
   else if (u8->resize == HN_RESIZE_CV2_LINEAR) HN_C12S_GO(HN_RESIZE_CV2_LINEAR);
   else if (u8->resize == HN_RESIZE_PIL_BILINEAR) HN_C12S_GO(HN_RESIZE_PIL_BILINEAR);

@@ -1391,6 +1391,12 @@ __global__ __launch_bounds__(256) void k_head2(const float* __restrict__ a, floa
 // flight -- then lgkmcnt(0) + s_barrier (every wave's chunk c landed; chunk c - 1's slots free
 // for the refills).  The DMA is inline asm (M0 set and restored in the same statement) so hipcc
 // does not track it as an LDS write.  Accumulation order = k_head2's (bit-identical results).
+//
+// SPLIT > 1 (small batches, hn_launch_head): workgroup (block, s) runs only K-chunks s NCH / SPLIT ..
+// (s + 1) NCH / SPLIT - 1 and writes its raw accumulators to part[s][P][128]; k_head_fin sums the SPLIT
+// partials in order s = 0, 1, .. and adds the bias and the L2 norm.  At the reference eval loop's 512
+// patches one unsplit workgroup per 128 patches would leave 252 of 256 CUs idle while each streams all
+// 8,192 K (its 4 MB of weights and 4 MB of activations through one CU's LDS-DMA path: ~0.2 ms).
 // ------------------------------------------------------------------------------------
 template <int N>
 HN_DEV void head_wait_vm() {  // s_waitcnt vmcnt(N), lgkmcnt / expcnt untouched
@@ -1398,11 +1404,13 @@ HN_DEV void head_wait_vm() {  // s_waitcnt vmcnt(N), lgkmcnt / expcnt untouched
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
-template <int K, bool F16, int DA, int DB>
+template <int K, bool F16, int DA, int DB, int SPLIT = 1>
 __global__ __launch_bounds__(512) void k_head3(const float* __restrict__ a, float* __restrict__ out,
                                                const uint4* __restrict__ wp,
-                                               const float* __restrict__ bias, int P, float l2eps) {
-  constexpr int KC = 32, NCH = K / KC, M = 128;
+                                               const float* __restrict__ bias, int P, float l2eps,
+                                               float* __restrict__ part = nullptr) {
+  constexpr int KC = 32, NCH = K / KC / SPLIT, M = 128;  // NCH: this workgroup's K-chunks
+  static_assert((K / KC) % SPLIT == 0, "split");
   constexpr int ABYTES = M * KC * 4;           // 16 KB per A chunk
   constexpr int BBYTES = 2 * 4 * 2 * 64 * 16;  // 16 KB per B chunk
   static_assert(ABYTES == 16 * 1024 && BBYTES == 16 * 1024, "two DMA instructions per wave each");
@@ -1416,6 +1424,7 @@ __global__ __launch_bounds__(512) void k_head3(const float* __restrict__ a, floa
   const int wm = wave >> 1, wn = wave & 1;
   const int r = lane & 31, h = lane >> 5;
   const int pbase = blockIdx.x * M;
+  const int kc0 = SPLIT > 1 ? (int)blockIdx.y * NCH : 0;  // the first K-chunk of this workgroup
 
   // this wave's DMA instructions 2 wave + k (k = 0, 1) of each chunk; chunk c adds c * KC floats
   // (A) / c * 1024 uint4 (B) to the source
@@ -1425,8 +1434,8 @@ __global__ __launch_bounds__(512) void k_head3(const float* __restrict__ a, floa
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
     const int gi = 2 * wave + k, s = gi * 64 + lane, row = s >> 3, c = (s & 7) ^ ((row >> 1) & 7);
-    asrc[k] = a + (size_t)min(pbase + row, P - 1) * K + c * 4;
-    bsrc[k] = wp + gi * 64 + lane;
+    asrc[k] = a + (size_t)min(pbase + row, P - 1) * K + c * 4 + (size_t)kc0 * KC;
+    bsrc[k] = wp + gi * 64 + lane + (size_t)kc0 * 1024;
     adst[k] = (unsigned)(uintptr_t)(lds_ptr_t)(sa + gi * 1024);
     bdst[k] = (unsigned)(uintptr_t)(lds_ptr_t)(sbw + gi * 1024);
   }
@@ -1496,17 +1505,29 @@ __global__ __launch_bounds__(512) void k_head3(const float* __restrict__ a, floa
       }
     }
   }
+  if constexpr (SPLIT > 1) {  // raw partial sums of this K range (k_head_fin finishes)
+    float* pp = part + (size_t)blockIdx.y * P * 128;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int p = pbase + wm * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+      if (p < P) {
+        pp[(size_t)p * 128 + wn * 64 + r] = acc[0][i];
+        pp[(size_t)p * 128 + wn * 64 + 32 + r] = acc[1][i];
+      }
+    }
+    return;
+  }
   const float b0 = bias[wn * 64 + r], b1 = bias[wn * 64 + 32 + r];
-  float part[16];
+  float part_ss[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     acc[0][i] += b0;
     acc[1][i] += b1;
-    part[i] = half_sum(acc[0][i] * acc[0][i] + acc[1][i] * acc[1][i]);
+    part_ss[i] = half_sum(acc[0][i] * acc[0][i] + acc[1][i] * acc[1][i]);
   }
   if (r == 0) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) ssq[wn][wm * 32 + (i & 3) + 8 * (i >> 2) + 4 * h] = part[i];
+    for (int i = 0; i < 16; ++i) ssq[wn][wm * 32 + (i & 3) + 8 * (i >> 2) + 4 * h] = part_ss[i];
   }
   __syncthreads();
 #pragma unroll
@@ -1519,6 +1540,32 @@ __global__ __launch_bounds__(512) void k_head3(const float* __restrict__ a, floa
       out[(size_t)p * 128 + wn * 64 + 32 + r] = acc[1][i] / norm;
     }
   }
+}
+
+// k_head3's SPLIT partials [SPLIT][P][128] summed in split order + bias, then y / sqrt(sum y^2 + l2eps) (the
+// two 64-column halves summed apart, then added, as k_head3).  32 lanes per patch, 4 columns each.
+template <int SPLIT>
+__global__ __launch_bounds__(256) void k_head_fin(const float* __restrict__ part, float* __restrict__ out,
+                                                  const float* __restrict__ bias, int P, float l2eps) {
+  const int t = threadIdx.x;
+  const int p = blockIdx.x * 8 + (t >> 5);
+  const int n = (t & 31) * 4;
+  if (p >= P) return;  // (a whole 32-lane half-wave: the shuffles below stay inside it)
+  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 8
+  for (int s = 0; s < SPLIT; ++s) {
+    const float4 q = *reinterpret_cast<const float4*>(part + ((size_t)s * P + p) * 128 + n);
+    v.x += q.x; v.y += q.y; v.z += q.z; v.w += q.w;
+  }
+  const float4 b = *reinterpret_cast<const float4*>(bias + n);
+  v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
+  float ss = v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) ss += __shfl_xor(ss, o);  // each 64-column half (16 lanes)
+  ss += __shfl_xor(ss, 16);                                  // the two halves
+  const float norm = sqrtf(ss + l2eps);
+  v.x /= norm; v.y /= norm; v.z /= norm; v.w /= norm;
+  *reinterpret_cast<float4*>(out + (size_t)p * 128 + n) = v;
 }
 
 // ------------------------------------------------------------------------------------
@@ -1862,12 +1909,14 @@ HN_WS_S(ws1s, true, 32, 32, 32, 1, 1, 4, 4, 1)
 HN_WS_S(ws1s_t8, true, 32, 32, 32, 1, 1, 8, 4, 1)
 HN_WS(ws2, 32, 64, 32, 2, 1, 4, 2, 2)
 HN_WS(ws2_t2, 32, 64, 32, 2, 1, 2, 1, 2)
+#ifdef HN_EXPERIMENTS  // conv3..conv5's generic warp-specialised tilings, superseded by their defaults
 HN_WS(ws3, 64, 64, 16, 1, 1, 8, 2, 2)
 HN_WS(ws3_t16, 64, 64, 16, 1, 1, 16, 2, 2)
 HN_WS(ws4, 64, 128, 16, 2, 1, 4, 1, 4)
 HN_WS(ws4_t8, 64, 128, 16, 2, 1, 8, 1, 4)
 HN_WS(ws5, 128, 128, 8, 1, 1, 8, 1, 4)
 HN_WS(ws5_np2, 128, 128, 8, 1, 2, 8, 1, 4)
+#endif
 // conv4 with the 64-byte swizzled window: two patches per stage (twice the weight reuse of ws4_t8)
 // -- HN_VARIANT digit d -- and the same layout at one patch (digit e)
 #ifdef HN_EXPERIMENTS  // superseded tiling (experiments library only)
@@ -1922,10 +1971,13 @@ hipError_t hn_launch_stem(const float* in, float* out, const float* w, const flo
 // 1 = conv1 alone, 2..5 = conv2..conv5); mirrors the dispatch below.  Digits 4 / 8 / 9 are the
 // timing-only ablation builds of conv3..conv5 (HN_EXPERIMENTS library only).
 bool hn_hardnet_variant_ok(int layer, int v) {
-  // the product library: 0 (k_conv3x3), 5 / 6 (warp-specialised, smaller / larger tile), 15 (conv4
-  // on the 64-byte swizzled window, two patches per stage, 2 x 2 waves), 16 (conv3 / conv5 with
-  // epilogue stores through LDS).  The superseded tilings (1, 2, 3, 7, 13, 14), the Winograd
-  // kernels (17) and the timing-only ablations (4, 8, 9) exist only with -DHN_EXPERIMENTS.
+  // the product library: the defaults (digits 6 0 5 q i l) and one fallback per stage -- 0 (k_conv3x3)
+  // everywhere, 5 / 6 (warp-specialised, smaller / larger tile) for the HN_NO_C12 stem+conv1 and conv2,
+  // 15 (conv4 on the 64-byte swizzled window with the MFMA waves' own stores, digit f), 16 (direct conv3 /
+  // conv5 with epilogue stores through LDS, digit g), 21 / 26 (1-D Winograd F(2,3), weight ring 6 / 8).
+  // The measured-slower tilings (1, 2, 3, 7, 13, 14, 5 / 6 on conv3..conv5), the Winograd kernels 17 (2-D),
+  // 19 / 20 (shallower rings), 32 / 33 (F(4,3) conv3) and the timing-only ablations exist only with
+  // -DHN_EXPERIMENTS.
   if (layer < 0 || layer > 5) return false;
 #ifdef HN_EXPERIMENTS
   if (v == 18 && layer == 3) return true;
@@ -1934,17 +1986,17 @@ bool hn_hardnet_variant_ok(int layer, int v) {
   if (v == 17) return layer == 3 || layer == 5;  // Winograd F(2x2,3x3), hn_wino.hip
   if (v == 7) return layer >= 3;
   if (v == 1 || v == 2 || v == 3) return true;
-#endif
-  if (v == 15 || v == 18) return layer == 4;  // 18: outputs stored by the producer waves
-  if (v >= 19 && v <= 21) return layer == 3 || layer == 5;  // 1-D Winograd F(2,3) (hn_wino1.hip), weight ring 3 / 4 / 6
-  if (v == 26) return layer == 3 || layer == 5;              // the same, weight ring 8 (digit q)
+  if (v == 5 || v == 6) return true;
+  if (v == 19 || v == 20) return layer == 3 || layer == 5;  // 1-D Winograd F(2,3), weight ring 3 / 4
   if (v == 32 || v == 33) return layer == 3;                 // F(4,3) (k_conv_w4), weight ring 6 / 9 (digits w / x)
-#ifdef HN_EXPERIMENTS
   if ((v >= 22 && v <= 25) || v == 29 || v == 30 || v == 31) return layer == 3 || layer == 5;  // its timing-only ablations (ABL 1 / 2 / 4 / 8; t: 16; u: 32, v: 34)
   if (v == 34 || v == 35) return layer == 3 || layer == 5;  // wave-priority A/B (y: MFMA waves first, z: producers first)
 #endif
+  if (v == 15 || v == 18) return layer == 4;  // 18: outputs stored by the producer waves
+  if (v == 21 || v == 26) return layer == 3 || layer == 5;  // 1-D Winograd F(2,3) (hn_wino1.hip), weight ring 6 / 8
   if (v == 16) return layer == 3 || layer == 5;
-  if (v == 0 || v == 5 || v == 6) return true;  // (layer 1 always runs conv1_launch)
+  if (v == 5 || v == 6) return layer <= 2;  // (layer 1 always runs conv1_launch)
+  if (v == 0) return true;
   return false;
 }
 
@@ -1985,10 +2037,11 @@ hipError_t hn_launch_hardnet_conv(int layer, int variant, const HardnetDev& d, c
     return hipErrorInvalidValue;
   }
 #endif
-  if (variant >= 19 && variant <= 21) return hn_launch_wino1(layer, variant == 19 ? 3 : variant == 20 ? 4 : 6, d, in, out, P, st);
+  if (variant == 21) return hn_launch_wino1(layer, 6, d, in, out, P, st);
   if (variant == 26) return hn_launch_wino1(layer, 8, d, in, out, P, st);
-  if (variant == 32 || variant == 33) return hn_launch_wino4(layer, variant == 32 ? 6 : 9, d, in, out, P, st);
 #ifdef HN_EXPERIMENTS
+  if (variant == 19 || variant == 20) return hn_launch_wino1(layer, variant == 19 ? 3 : 4, d, in, out, P, st);
+  if (variant == 32 || variant == 33) return hn_launch_wino4(layer, variant == 32 ? 6 : 9, d, in, out, P, st);
   if (variant >= 22 && variant <= 25) return hn_launch_wino1(layer, 100 + (1 << (variant - 22)), d, in, out, P, st);
   if (variant == 29) return hn_launch_wino1(layer, 116, d, in, out, P, st);
   if (variant == 30 || variant == 31) return hn_launch_wino1(layer, variant == 30 ? 132 : 134, d, in, out, P, st);
@@ -2007,9 +2060,11 @@ hipError_t hn_launch_hardnet_conv(int layer, int variant, const HardnetDev& d, c
       case 0:
         return (big ? ws1s_t8 : ws1s)(in, out, d.wpack[1], d.bias[1], P, d.stem_w, d.stem_b, eps, st);
       case 2: return (big ? ws2_t2 : ws2)(in, out, d.wpack[2], d.bias[2], P, nullptr, nullptr, 0.f, st);
+#ifdef HN_EXPERIMENTS
       case 3: return (big ? ws3_t16 : ws3)(in, out, d.wpack[3], d.bias[3], P, nullptr, nullptr, 0.f, st);
       case 4: return (big ? ws4_t8 : ws4)(in, out, d.wpack[4], d.bias[4], P, nullptr, nullptr, 0.f, st);
       case 5: return (big ? ws5_np2 : ws5)(in, out, d.wpack[5], d.bias[5], P, nullptr, nullptr, 0.f, st);
+#endif
     }
     return hipErrorInvalidValue;
   }
@@ -2067,10 +2122,29 @@ hipError_t hn_launch_conv_raw(int layer, const void* wp, const float* zero_bias,
 }
 
 hipError_t hn_launch_head(const float* a, float* out, const void* wp, const float* bias, int P,
-                          int K, float l2eps, hipStream_t st, bool f16) {
+                          int K, float l2eps, hipStream_t st, bool f16, float* part) {
   const int grid = (P + 63) / 64;
-  const int form = hn_knobs().head;  // HN_HEAD: 1 k_head, 2 k_head2, 3 k_head3, 4 k_head4 (default; k_head3 below 61,440 patches)
+  // HN_HEAD: 1 k_head, 2 k_head2, 3 k_head3, 4 (default) k_head4 from 61,440 patches, the split-K k_head3 up to
+  // kHeadSplitMaxP patches (when the caller passes the scratch), k_head3 in between
+  const int form = hn_knobs().head;
   const uint4* w = static_cast<const uint4*>(wp);
+  if (form >= 4 && part && P <= kHeadSplitMaxP && ((K == 8192 && !f16) || (K == 2048 && f16))) {
+    // every batch up to kHeadSplitMaxP patches sums the same K ranges in the same order: its descriptors do
+    // not depend on the batch they come in (bit for bit); the unsplit forms reassociate the K sum
+    const dim3 g((P + 127) / 128, head_split(K));
+    if (K == 8192)
+      hipLaunchKernelGGL((k_head3<8192, false, 4, 4, head_split(8192)>), g, dim3(512), 0, st, a, out, w, bias, P,
+                         l2eps, part);
+    else
+      hipLaunchKernelGGL((k_head3<2048, true, 4, 4, head_split(2048)>), g, dim3(512), 0, st, a, out, w, bias, P,
+                         l2eps, part);
+    if (const hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+    if (K == 8192)
+      hipLaunchKernelGGL(k_head_fin<head_split(8192)>, dim3((P + 7) / 8), dim3(256), 0, st, part, out, bias, P, l2eps);
+    else
+      hipLaunchKernelGGL(k_head_fin<head_split(2048)>, dim3((P + 7) / 8), dim3(256), 0, st, part, out, bias, P, l2eps);
+    return hipGetLastError();
+  }
 #define HN_HEAD3(KK, F, DA, DB)                                                                              \
   if (K == KK && f16 == F) {                                                                                 \
     hipLaunchKernelGGL((k_head3<KK, F, DA, DB>), dim3((P + 127) / 128), dim3(512), 0, st, a, out, w, bias, P, \
@@ -2087,12 +2161,7 @@ hipError_t hn_launch_head(const float* a, float* out, const void* wp, const floa
     return hipGetLastError();                                                                                \
   }
   if (form >= 4 && P >= 240 * 256) {
-    if (hn_knobs().head_pf && K == 8192 && !f16) {
-      hipLaunchKernelGGL((k_head4<8192, false, 3, 3, 0, true>), dim3((P + 255) / 256), dim3(512), 0, st, a, out, w,
-                         bias, P, l2eps);
-      return hipGetLastError();
-    }
-#ifdef HN_EXPERIMENTS
+#ifdef HN_EXPERIMENTS  // (ahead of the prefetching form, which has no ablation builds)
     if (const char* e = std::getenv("HN_HEAD_ABL")) {
       const int abl = std::atoi(e);
       if (K == 8192 && !f16 && (abl == 1 || abl == 2 || abl == 3)) {
@@ -2104,6 +2173,11 @@ hipError_t hn_launch_head(const float* a, float* out, const void* wp, const floa
       }
     }
 #endif
+    if (hn_knobs().head_pf && K == 8192 && !f16) {
+      hipLaunchKernelGGL((k_head4<8192, false, 3, 3, 0, true>), dim3((P + 255) / 256), dim3(512), 0, st, a, out, w,
+                         bias, P, l2eps);
+      return hipGetLastError();
+    }
     HN_HEAD4(8192, false, 3, 3) HN_HEAD4(2048, true, 3, 3)
   }
   if (form >= 3) {

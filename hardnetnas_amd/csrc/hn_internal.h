@@ -87,8 +87,12 @@ hipError_t hn_launch_c12w(const float* in, float* out, const HardnetDev& d, int 
                           const HnU8In* u8, int abl);
 hipError_t hn_launch_hardnet_conv(int layer, int variant, const HardnetDev& d, const float* in,
                                   float* out, int P, float eps, hipStream_t st);
+// part: scratch for the split-K partials of small batches (P <= kHeadSplitMaxP: head_split(K) x P x 128
+// floats), or null for the unsplit forms
+constexpr int kHeadSplitMaxP = 16384;
+constexpr int head_split(int K) { return K / 128; }  // 64 (HardNet, K = 8,192) / 16 (NAS, K = 2,048): 4 K-chunks each
 hipError_t hn_launch_head(const float* a, float* out, const void* wp, const float* bias, int P,
-                          int K, float l2eps, hipStream_t st, bool f16 = false);
+                          int K, float l2eps, hipStream_t st, bool f16 = false, float* part = nullptr);
 int hn_conv_lds_bytes(int layer);
 // train mode: conv layer 1..5 as a plain NHWC convolution (no bias, no ReLU), bf16x3 fragments
 // in the pack_conv3x3 layout

@@ -394,6 +394,7 @@ hipError_t launch_w1(const float* in, float* out, const void* wp, const float* b
   return hipGetLastError();
 }
 
+#ifdef HN_EXPERIMENTS  // F(4,3) conv3 (k_conv_w4): measured slower than k_conv_w1 (11.2 vs 9.9 ms), experiments library only
 // ---------------------------------------------------------------------------------------
 // F(4,3) along x (k_conv_w4): per output row y and column quad (4t .. 4t+3), d_k = x[y + ky - 1][4t - 1 + k]
 // (k = 0..5, zero outside the patch), Toom-Cook points 0, 1, -1, 1/2, -1/2, infinity:
@@ -748,6 +749,7 @@ hipError_t launch_w4(const float* in, float* out, const void* wp, const float* b
 }
 
 using W4Conv3 = W4Cfg<64, 64, 16, 1, 4>;
+#endif  // HN_EXPERIMENTS
 
 using W1Conv3 = W1Cfg<64, 64, 16, 1, 2, 2, true>;
 using W1Conv5 = W1Cfg<128, 128, 8, 2, 1, 4, true>;
@@ -771,13 +773,17 @@ hipError_t hn_launch_wino1(int layer, int wd, const HardnetDev& d, const float* 
   if (wd == 134) return launch_w1<CI, CO, HH, NPP, WMM, WNN, true, 8, 34>(in, out, d.wino1[L], d.bias[L], P, st); \
   if (wd == 164) return launch_w1<CI, CO, HH, NPP, WMM, WNN, true, 8, 64>(in, out, d.wino1[L], d.bias[L], P, st); \
   if (wd == 228) return launch_w1<CI, CO, HH, NPP, WMM, WNN, true, 8, 128>(in, out, d.wino1[L], d.bias[L], P, st);
+// weight rings 3 / 4 (digits j / k): measured slower than 6 / 8
+#define HN_W1_SHALLOW(CI, CO, HH, NPP, WMM, WNN, L)                                                          \
+  if (wd == 3) return launch_w1<CI, CO, HH, NPP, WMM, WNN, true, 3>(in, out, d.wino1[L], d.bias[L], P, st); \
+  if (wd == 4) return launch_w1<CI, CO, HH, NPP, WMM, WNN, true, 4>(in, out, d.wino1[L], d.bias[L], P, st);
 #else
 #define HN_W1_ABL(CI, CO, HH, NPP, WMM, WNN, L)
+#define HN_W1_SHALLOW(CI, CO, HH, NPP, WMM, WNN, L)
 #endif
 #define HN_W1(L, CI, CO, HH, NPP, WMM, WNN)                                                                      \
   if (layer == L) {                                                                                             \
-    if (wd == 3) return launch_w1<CI, CO, HH, NPP, WMM, WNN, true, 3>(in, out, d.wino1[L], d.bias[L], P, st); \
-    if (wd == 4) return launch_w1<CI, CO, HH, NPP, WMM, WNN, true, 4>(in, out, d.wino1[L], d.bias[L], P, st); \
+    HN_W1_SHALLOW(CI, CO, HH, NPP, WMM, WNN, L)                                                                 \
     if (wd == 6) return launch_w1<CI, CO, HH, NPP, WMM, WNN, true, 6>(in, out, d.wino1[L], d.bias[L], P, st); \
     if (wd == 8) return launch_w1<CI, CO, HH, NPP, WMM, WNN, true, 8>(in, out, d.wino1[L], d.bias[L], P, st); \
     HN_W1_ABL(CI, CO, HH, NPP, WMM, WNN, L)                                                                     \
@@ -786,9 +792,11 @@ hipError_t hn_launch_wino1(int layer, int wd, const HardnetDev& d, const float* 
   HN_W1(5, 128, 128, 8, 2, 1, 4)
 #undef HN_W1
 #undef HN_W1_ABL
+#undef HN_W1_SHALLOW
   return hipErrorInvalidValue;
 }
 
+#ifdef HN_EXPERIMENTS
 // conv3 as F(4,3) (k_conv_w4); wd: the weight ring depth (HN_VARIANT digit w = 6, x = 9)
 hipError_t hn_launch_wino4(int layer, int wd, const HardnetDev& d, const float* in, float* out, int P,
                            hipStream_t st) {
@@ -809,6 +817,7 @@ hipError_t hn_launch_wino4(int layer, int wd, const HardnetDev& d, const float* 
   if (wd == 9) return launch_w4<64, 64, 16, 1, 4, 9>(in, out, d.wino4[3], d.bias[3], P, st);
   return hipErrorInvalidValue;
 }
+#endif  // HN_EXPERIMENTS
 
 // LDS bytes of the layer's configuration (tests / DESIGN.md)
 int hn_wino1_lds_bytes(int layer) {

@@ -177,7 +177,8 @@ def test_product_library_has_one_tiling_per_layer_plus_fallbacks():
 @pytest.mark.parametrize("env,val", [("HN_VARIANT", "888888"), ("HN_VARIANT", "004000"),
                                      ("HN_VARIANT", "00000z"), ("HN_VARIANT", "000h00"),
                                      ("HN_VARIANT", "111111"), ("HN_C12_CFG", "13"),
-                                     ("HN_HEAD", "5")])
+                                     ("HN_C12_CFG", "14"), ("HN_C12_CFG", "7"), ("HN_VARIANT", "605wil"),
+                                     ("HN_VARIANT", "605jij"), ("HN_VARIANT", "605565"), ("HN_HEAD", "5")])
 def test_create_rejects_ablation_and_unknown_builds(env, val, monkeypatch):
     """hn_create validates the A/B switches before touching the GPU: an ablation tiling or an
     unknown k_c12 configuration is HN_ERR_ARG, never a silently wrong model."""

@@ -105,22 +105,25 @@ def test_lds_dma_ring_equals_register_staged_form(tmp_path, cuda_device):
     """The LDS-DMA ring pair kernel (default) and the register-staged one (HN_PAIRDIST_REG=1, read
     once per process: a child process) stage the same bf16 hi / lo values and run the same MFMA
     chains: pos, row minima and column minima agree bit for bit, including a batch that is not a
-    multiple of the 64-column tile and the 8-wave (>= 65,536 anchors) form."""
+    multiple of the 64-column tile and the 8-wave (>= 65,536 anchors) form.  The same for the ring kernel
+    with the next-but-one tile's DMA issued at once instead of spread over the first sub-tile's chain
+    (HN_PAIRDIST_SPREAD=0)."""
     import os
     import subprocess
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     res = {}
-    for tag, env in (("ring", {}), ("reg", {"HN_PAIRDIST_REG": "1"})):
+    for tag, env in (("ring", {}), ("reg", {"HN_PAIRDIST_REG": "1"}), ("nospread", {"HN_PAIRDIST_SPREAD": "0"})):
         f = str(tmp_path / f"{tag}.pt")
         r = subprocess.run([sys.executable, "-c", _REG_CHILD, here, f], env=dict(os.environ, **env),
                            capture_output=True, text=True, timeout=110)
         assert r.returncode == 0, r.stderr[-3000:]
         res[tag] = torch.load(f, weights_only=True)
-    for k in res["ring"]:
-        for x, y in zip(res["ring"][k], res["reg"][k]):
-            if x is not None:
-                assert torch.equal(x, y), k
+    for other in ("reg", "nospread"):  # nospread: the ring kernel without the spread next-but-one tile DMA
+        for k in res["ring"]:
+            for x, y in zip(res["ring"][k], res[other][k]):
+                if x is not None:
+                    assert torch.equal(x, y), (other, k)
 
 
 LOSS_TYPES = ["triplet_margin", "softmax", "contrastive"]
@@ -133,8 +136,9 @@ def test_fused_train_loss_matches_reference_backward(swap, loss_type, cuda_devic
     (no B x B matrix): loss and d loss / d (anchor, positive) against the reference's fp64 step
     (tests/golden/loss_modes.npz: a masked near-duplicate and a zero positive distance included);
     loss <= max(1e-6, the reference's own fp32 error) and gradients L2-relative <= 1e-5 (or 3x the
-    reference's own fp32 error).  Run twice:
-    bit-identical (no atomics in the backward)."""
+    reference's own fp32 error).  Run twice: bit-identical -- the backward's atomicAdds only count each
+    target's sources (k_lmin_bwd_count / _fill); the gather sorts every target's source list before it
+    sums, so the summation order does not depend on the order the atomics land in."""
     from fixtures import load
     from hardnetnas_amd.losses import loss_HardNet
     fx = load("loss_modes")

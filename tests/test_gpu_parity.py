@@ -81,9 +81,11 @@ def test_chunked_forward_equals_unchunked(name, cuda_device, monkeypatch):
     assert torch.equal(full, chunked)
 
 
-@pytest.mark.parametrize("variant", ["000000", "005555", "006666", "505000", "605000", "6050f0", "605g0g",
-                                     "505gfg", "605gfg", "6056f6", "605gig"])
+@pytest.mark.parametrize("variant", ["000000", "505000", "606000", "6050f0", "605g0g", "605gfg", "605gig"])
 def test_tiling_variants_match_reference(variant, cuda_device, monkeypatch):
+    """The product library's fallback tilings (HN_VARIANT digits per conv layer; the defaults are 6 0 5 q i l):
+    0 = k_conv3x3 everywhere, 5 / 6 = warp-specialised stem+conv1 / conv2, f / i = conv4 on the 64-byte window
+    (MFMA-wave / producer-wave stores), g = direct conv3 / conv5 -- against the reference vectors."""
     from hardnetnas_amd._native import NativeModel
     m, fx, _ = build_module("hardnet")
     monkeypatch.setenv("HN_VARIANT", variant)
@@ -93,13 +95,12 @@ def test_tiling_variants_match_reference(variant, cuda_device, monkeypatch):
     assert np.abs(y - fx["y"]).max() <= TOL["hardnet"]
 
 
-@pytest.mark.parametrize("variant", ["605jig", "605gij", "605jij", "605kik", "605lil", "605qiq", "605qil",
-                                     "605wil", "605xil"])
+@pytest.mark.parametrize("variant", ["605lil", "605qiq", "605qil", "605gil", "605qig"])
 def test_winograd_1d_conv3_conv5_match_reference(variant, cuda_device, monkeypatch):
-    """conv3 / conv5 as 1-D Winograd F(2,3) (hn_wino1.hip, HN_VARIANT digits j / k / l / q = weight
-    ring depth 3 / 4 / 6 / 8) against the reference's fp32 and fp64 vectors (edge patches included) and
-    against the direct kernels on ragged batches whose last two-patch conv5 tile is half empty.  605qil
-    is the default."""
+    """conv3 / conv5 as 1-D Winograd F(2,3) (hn_wino1.hip, HN_VARIANT digits l / q = weight ring depth 6 / 8;
+    the shallower rings j / k and the F(4,3) conv3 w / x are experiments-library only) against the reference's
+    fp32 and fp64 vectors (edge patches included) and against the direct kernels on ragged batches whose last
+    two-patch conv5 tile is half empty.  605qil is the default."""
     from hardnetnas_amd._native import NativeModel
     m, fx, _ = build_module("hardnet")
     x = torch.from_numpy(golden_inputs(fx)).to(cuda_device)
@@ -154,55 +155,36 @@ def test_fused_c12_is_default_and_matches_layerwise(cuda_device, monkeypatch):
         assert np.abs(nm(x[:b]).cpu().numpy() - lw(x[:b]).cpu().numpy()).max() <= 2e-5
 
 
-@pytest.mark.parametrize("cfg", ["0", "1", "2", "3", "5", "7", "8", "9", "10", "11", "12"])
-def test_c12_variants_match(cuda_device, monkeypatch, cfg):
-    """HN_C12_CFG=0: 8-wave workgroups with 4-row bands; 1: one wave per SIMD (512-register
-    file); 2: 4-wave workgroups with 2-row bands, two per CU; 3 / 5: tap-interleaved P3; 7 / 8 / 9:
-    tap-interleaved P2; 10 / 11: raised P1 priority; 12: 2 with the tap-interleaved P2 and P3 + P1 at
-    raised wave priority (the default) -- against the default build.  Both agree with the default build to the split-precision level (the 4-wave builds sum
-    input_norm's mean/std in a different order; the MFMA order per output is the same)."""
+def test_c12_winograd_conv1_matches_reference(cuda_device, monkeypatch):
+    """The default k_c12s (HN_C12_CFG=15: conv1 as a 1-D Winograd F(4,3), conv1 and conv2 + stem waves per SIMD,
+    bands software-pipelined, hn_c12w.hip) against the reference vectors (edge patches included) at the 1e-4 bar,
+    and within 5e-5 of the direct k_c12 (HN_C12_CFG=12, the product library's fallback) -- the transform changes
+    the rounding: tests/precision/wino1d_precision.py puts it at 1.7e-5 from fp64 vs 1.0e-5 direct; bit-identical
+    to itself on ragged batches and on a persistent run of several patches per workgroup."""
     from hardnetnas_amd._native import NativeModel
     m, fx, _ = build_module("hardnet")
     x = torch.from_numpy(golden_inputs(fx)).to(cuda_device)
-    y0 = NativeModel.from_module(m, cuda_device)(x).cpu().numpy()
-    monkeypatch.setenv("HN_C12_CFG", cfg)  # read once, by hn_create
-    nm = NativeModel.from_module(m, cuda_device)
-    y = nm(x).cpu().numpy()
-    assert np.abs(y - fx["y"]).max() <= TOL["hardnet"]
-    assert np.abs(y - y0).max() <= 2e-5
     xe = torch.from_numpy(fx["x_edge"]).to(cuda_device)
-    assert np.abs(nm(xe).cpu().numpy() - fx["y_edge"]).max() <= TOL["hardnet"]
-    for b in (1, 3, 130):
-        assert np.abs(nm(x[:b]).cpu().numpy() - y0[:b]).max() <= 2e-5
-    # several patches per persistent workgroup, a ragged last range
-    xr = x.repeat(12, 1, 1, 1)[:3001]
-    assert np.abs(nm(xr).cpu().numpy() - np.tile(y0, (12, 1))[:3001]).max() <= 2e-5
-
-
-@pytest.mark.parametrize("cfg", ["14", "15"])
-def test_c12_winograd_conv1_matches_reference(cuda_device, monkeypatch, cfg):
-    """HN_C12_CFG=14: k_c12w, conv1 as a 1-D Winograd F(4,3) (hn_c12w.hip); 15: k_c12s, the same
-    arithmetic with conv1 and conv2 + stem waves per SIMD, bands software-pipelined: against the reference
-    vectors (edge patches included) at the 1e-4 bar, and within 5e-5 of the direct k_c12 on ragged
-    batches and a persistent run of several patches per workgroup (the transform changes the
-    rounding: tests/precision/wino1d_precision.py puts it at 1.7e-5 from fp64 vs 1.0e-5 direct)."""
-    from hardnetnas_amd._native import NativeModel
-    m, fx, _ = build_module("hardnet")
-    x = torch.from_numpy(golden_inputs(fx)).to(cuda_device)
-    y0 = NativeModel.from_module(m, cuda_device)(x).cpu().numpy()
-    monkeypatch.setenv("HN_C12_CFG", cfg)
+    monkeypatch.setenv("HN_C12_CFG", "12")  # read once, by hn_create
+    direct = NativeModel.from_module(m, cuda_device)
+    y0 = direct(x).cpu().numpy()
+    assert np.abs(y0 - fx["y"]).max() <= TOL["hardnet"]
+    assert np.abs(direct(xe).cpu().numpy() - fx["y_edge"]).max() <= TOL["hardnet"]
+    monkeypatch.setenv("HN_C12_CFG", "15")
     nm = NativeModel.from_module(m, cuda_device)
     y = nm(x).cpu().numpy()
     err, err64 = np.abs(y - fx["y"]).max(), np.abs(y - fx["y64"]).max()
-    print(f"k_c12w: max|hip - ref32| = {err:.3e}, max|hip - ref64| = {err64:.3e}, vs direct {np.abs(y - y0).max():.3e}")
+    print(f"k_c12s: max|hip - ref32| = {err:.3e}, max|hip - ref64| = {err64:.3e}, vs direct {np.abs(y - y0).max():.3e}")
     assert err <= TOL["hardnet"]
     assert np.abs(y - y0).max() <= 5e-5
-    xe = torch.from_numpy(fx["x_edge"]).to(cuda_device)
     assert np.abs(nm(xe).cpu().numpy() - fx["y_edge"]).max() <= TOL["hardnet"]
     for b in (1, 3, 130):
         assert np.abs(nm(x[:b]).cpu().numpy() - y[:b]).max() == 0.0
+        assert np.abs(nm(x[:b]).cpu().numpy() - direct(x[:b]).cpu().numpy()).max() <= 5e-5
     xr = x.repeat(12, 1, 1, 1)[:3001]
-    assert np.abs(nm(xr).cpu().numpy() - np.tile(y, (12, 1))[:3001]).max() == 0.0
+    yr = nm(xr).cpu().numpy()
+    assert np.abs(yr - np.tile(y, (12, 1))[:3001]).max() == 0.0
+    assert np.abs(yr - direct(xr).cpu().numpy()).max() <= 5e-5
 
 
 def test_unfused_stem_matches(cuda_device, monkeypatch):
@@ -499,6 +481,7 @@ def test_head_forms_are_bit_identical(name, cuda_device, monkeypatch):
     m, fx, _ = build_module(name)
     x = torch.from_numpy(golden_inputs(fx)).to(cuda_device)
     xr = torch.from_numpy(np.concatenate([golden_inputs(fx)] * 40)[:301]).to(cuda_device)
+    monkeypatch.setenv("HN_HEAD", "3")  # k_head3 unsplit (the default splits K at these batch sizes)
     nm = NativeModel.from_module(m, cuda_device)
     y, yr = nm(x), nm(xr)
     for form in ("2", "1"):  # k_head2; k_head (no LDS staging)
@@ -507,6 +490,34 @@ def test_head_forms_are_bit_identical(name, cuda_device, monkeypatch):
         assert torch.equal(y, nm2(x)), form
         assert torch.equal(yr, nm2(xr)), form
     assert np.abs(y.cpu().numpy() - fx["y"]).max() <= _tol(name)
+
+
+@pytest.mark.parametrize("name", ["hardnet", "wang2"])
+def test_split_k_head_for_small_batches(name, cuda_device, monkeypatch):
+    """Batches of up to 16,384 patches run the head as split-K k_head3 (64 / 16 K ranges, one workgroup per
+    128 patches x range) + k_head_fin (the partials summed in range order, bias, L2): against the reference
+    vectors; within 2e-6 of the unsplit k_head3 (a reassociated K sum); bit for bit the same descriptors for a
+    patch whatever batch of <= 16,384 it comes in (the reference eval loop's 512, a ragged 37, the largest
+    split batch); and the first unsplit batch size (16,385) stays within 2e-6 of it."""
+    from hardnetnas_amd._native import NativeModel
+    m, fx, _ = build_module(name)
+    g = golden_inputs(fx)
+    xb = torch.from_numpy(np.concatenate([g] * (16_385 // len(g) + 1))[:16_385]).to(cuda_device)
+    xb = xb + 0.01 * torch.randn(xb.shape, generator=torch.Generator().manual_seed(3)).to(cuda_device)
+    nm = NativeModel.from_module(m, cuda_device)
+    nm.set_profiling(True)
+    y512, y37, y16k = nm(xb[:512]), nm(xb[:37]), nm(xb[:16_384])
+    launches = nm.stage_times()["head"][1]
+    assert launches == 3, launches  # three split-K heads (stage records count the calls)
+    assert torch.equal(y37, y512[:37]) and torch.equal(y512, y16k[:512])
+    assert torch.equal(nm(xb[100:612]), y16k[100:612])
+    y_unsplit = nm(xb)  # 16,385: k_head3
+    assert (y_unsplit[:16_384] - y16k).abs().max().item() <= 2e-6
+    monkeypatch.setenv("HN_HEAD", "3")
+    n3 = NativeModel.from_module(m, cuda_device)
+    assert (n3(xb[:512]) - y512).abs().max().item() <= 2e-6
+    x = torch.from_numpy(g).to(cuda_device)
+    assert np.abs(nm(x).cpu().numpy() - fx["y"]).max() <= _tol(name)
 
 
 @pytest.mark.parametrize("name", ["hardnet", "wang2"])
@@ -527,6 +538,9 @@ def test_head4_is_bit_identical(name, cuda_device, monkeypatch):
     assert torch.equal(yb, nm4(xb))
     assert torch.equal(ys, nm4(xs))
     assert np.abs(yb[: len(g)].cpu().numpy() - fx["y"]).max() <= _tol(name)
+    if name == "hardnet":  # the prefetching head form (HN_HEAD_PF, default on) against the plain k_head4
+        monkeypatch.setenv("HN_HEAD_PF", "0")
+        assert torch.equal(yb, NativeModel.from_module(m, cuda_device)(xb))
 
 
 @pytest.mark.parametrize("name", ["wang2", "wang4"])

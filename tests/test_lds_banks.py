@@ -587,3 +587,72 @@ def test_c12w_records_cover_each_chunk_once():
             for plane in range(2):
                 got = seen[(t, (g + 4 * plane) ^ t)]
                 assert {(c, p) for c, p, _ in got} == {(8 * g, plane)}
+
+
+
+# ---- k_c12s (hn_c12w.hip): P2's N index = tile n >> 1 of row n & 1, W0 rows padded to VROW + 128, W1 ring of 10 ----
+C12S_VROW = C12W_VROW + 128
+C12S_W1ROW = 33 * 160
+
+
+def _w1_slot(x):  # even (x + 1) -> (x + 1) / 2, odd -> 17 + x / 2
+    return 17 + (x >> 1) if (x + 1) & 1 else (x + 1) >> 1
+
+
+def test_c12s_conv1_operand_reads_conflict_free():
+    """P2's ds_read_b128 of V_xi in k_c12s (lane n = 2 tt + tj: tile tt of a0 row 4 band + 2 rp + tj - 1 + ky,
+    ring slot (32 p + r) % 10, rows -1 / 32 -> the zero row 10): conflict-free for every real row pair; only a
+    pair that includes the zero row may collide (2 of 8 bands, one ky)."""
+    for p in range(10):
+        for band in range(8):
+            for rp in range(2):
+                for ky in range(3):
+                    for xi in range(6):
+                        for plane in range(2):
+                            addrs, pad = [], False
+                            for lane in range(64):
+                                n, g16 = lane & 15, lane >> 4
+                                tt, tj = n >> 1, n & 1
+                                r = 4 * band + 2 * rp + tj - 1 + ky
+                                pad |= not 0 <= r <= 31
+                                slot = 10 if not 0 <= r <= 31 else (32 * p + r) % 10
+                                addrs.append(slot * C12S_VROW + xi * 1024 + tt * 128 + 16 * ((g16 + 4 * plane) ^ tt))
+                            if pad:
+                                continue
+                            for grp in GROUPS:
+                                assert len({(addrs[l] // 16) % 16 for l in grp}) == 16, (p, band, rp, ky, xi, plane)
+
+
+def test_c12s_p2_epilogue_writes_two_way_at_most():
+    """P2's epilogue ds_write_b128 into W1 (160-byte pixels, column 4 tt + i of a1 row (32 p + 4 band + 2 rp + tj)
+    % 10, the 16-byte chunk 32 g1 + 16 (g16 / 2) + 64 (g16 & 1)): each 8-lane group holds 4 tiles x 2 rows on at
+    least 4 distinct 16-byte positions (k_c12w's mapping: 2 positions, 4-way) -- including the ring's wrap."""
+    for p in range(10):
+        for band in range(8):
+            for rp in range(2):
+                for g1 in range(2):
+                    for i in range(4):
+                        addrs = []
+                        for lane in range(64):
+                            n, g16 = lane & 15, lane >> 4
+                            tt, tj = n >> 1, n & 1
+                            row = (32 * p + 4 * band + 2 * rp + tj) % 10
+                            addrs.append(row * C12S_W1ROW + _w1_slot(4 * tt + i) * 160 + 32 * g1 + 16 * (g16 >> 1)
+                                         + 64 * (g16 & 1))
+                        for grp in WRITE_GROUPS:
+                            pos = [(addrs[l] // 16) % 8 for l in grp]
+                            assert max(pos.count(v) for v in pos) <= 2, (p, band, rp, g1, i, grp[0])
+
+
+def test_c12s_p1_writes_conflict_free_on_padded_rows():
+    """P1's V-record stores (k_c12w's lane map) stay conflict-free with the padded W0 row stride."""
+    for ph in range(2):
+        for y0 in range(10):
+            for xi in range(6):
+                addrs = []
+                for lane in range(64):
+                    t, j, g16 = lane & 7, (lane >> 3) & 1, lane >> 4
+                    c = (2 * ph + (g16 >> 1) + 4 * (g16 & 1)) ^ t
+                    addrs.append(((y0 + j) % 10) * C12S_VROW + (xi * 8 + t) * 128 + 16 * c)
+                for grp in WRITE_GROUPS:
+                    assert len({(addrs[l] // 16) % 8 for l in grp}) == 8, (ph, y0, xi, grp[0])
