@@ -241,6 +241,7 @@ struct hn_model {
   bool c12 = true;            // fused stem+conv1+conv2 (k_c12); HN_NO_C12=1 -> separate kernels
   int subchunk = 65536;       // HardNet conv3..conv5 patches per launch (HN_SUBCHUNK)
   int c12group = 65536;       // HardNet k_c12 patches per launch (HN_C12_GROUP; >= the sub-chunk)
+  int c4sub = 0;              // HardNet conv4 patches per launch inside a sub-chunk (HN_C4_SUB; 0: the sub-chunk)
   uint16_t* front_spack = nullptr;  // fused front: stem as MFMA A operand
   int front = 0;  // NAS: 1 = stem + layer-0 IRF pw/dw fused, 2 = stem + layer-0 maxpool fused
   bool no_front = false;  // HN_NO_FRONT=1: unfused NAS stem/layer 0 (A/B, debugging)
@@ -900,6 +901,7 @@ extern "C" int hn_create(const hn_arch_desc* desc, const float* host_params, siz
   if (const char* e = std::getenv("HN_NO_C12")) m->c12 = std::atoi(e) == 0;
   if (const char* e = std::getenv("HN_SUBCHUNK")) m->subchunk = std::max(64, std::atoi(e));
   if (const char* e = std::getenv("HN_C12_GROUP")) m->c12group = std::max(64, std::atoi(e));
+  if (const char* e = std::getenv("HN_C4_SUB")) m->c4sub = std::max(0, std::atoi(e));
   if (const char* e = std::getenv("HN_NO_IRF")) m->no_irf = std::atoi(e) != 0;
   if (const char* e = std::getenv("HN_NO_IRF2")) m->no_irf2 = std::atoi(e) != 0;
   if (const char* e = std::getenv("HN_VARIANT")) {
@@ -1017,7 +1019,10 @@ static int forward_hardnet(hn_model* m, const float* in, int P, int pmax, float*
         const int n = std::min(sub, g0 + ng - s0);
         float* const a2s = a2 + (size_t)(s0 - g0) * 16384;
         STAGE("conv3", hn_launch_hardnet_conv(3, m->variant[3], m->hd, a2s, a0, n, 0.f, st));
-        STAGE("conv4", hn_launch_hardnet_conv(4, m->variant[4], m->hd, a0, a2s, n, 0.f, st));
+        const int c4 = m->c4sub > 0 ? m->c4sub : n;
+        for (int q = 0; q < n; q += c4)  // (a3 is 16,384 floats per patch, a4 8,192)
+          STAGE("conv4", hn_launch_hardnet_conv(4, m->variant[4], m->hd, a0 + (size_t)q * 16384, a2s + (size_t)q * 8192,
+                                                std::min(c4, n - q), 0.f, st));
         STAGE("conv5", hn_launch_hardnet_conv(5, m->variant[5], m->hd, a2s, a1 + (size_t)s0 * 8192, n, 0.f, st));
       }
     }
