@@ -87,6 +87,18 @@ def irf2_pairs(ops) -> set:
     return out
 
 
+def mpfront_irf(ops) -> bool:
+    """True when hn_api.hip::forward_nas runs the max-pool front (layer 0 "skip" at stride 2), the identity layer 1
+    and the 16x16 stride-2 32 -> 64 layer-2 block (no SE, mid 32 / 96 / 128) as one k_mpfront_irf, unless
+    HN_NO_MPFRONT / HN_NO_FRONT (float input; the uint8 modes keep the two kernels)."""
+    if any(os.environ.get(k, "0") not in ("", "0") for k in ("HN_NO_MPFRONT", "HN_NO_FRONT")):
+        return False
+    ops = A.arch_ops(ops)
+    spec = A.OP_SPECS[ops[2]]
+    return (ops[0] == "skip" and ops[1] == "skip" and spec.kind != "skip" and not spec.se
+            and A.ir_mid(32, spec.expansion) in (32, 96, 128))
+
+
 def irf_skip_layers(ops) -> dict:
     """{i: n}: the IRF layer i (16x16 stride 2, 32 -> 64, no SE, not in a k_irf2 pair) whose output goes
     -- past identity skips -- into the 8x8 64 -> 128 stride-2 skip of layer n, both in one k_irf_skip
@@ -96,9 +108,10 @@ def irf_skip_layers(ops) -> dict:
     ops = A.arch_ops(ops)
     pairs = irf2_pairs(ops)
     out = {}
+    mpf = mpfront_irf(ops)
     for i in range(1, len(ops)):
         spec, (ci, co, s) = A.OP_SPECS[ops[i]], A.SEARCH_SPACE2[i]
-        if (spec.kind == "skip" or spec.se or i in pairs or i - 1 in pairs or (ci, co, s) != (32, 64, 2)
+        if (spec.kind == "skip" or spec.se or i in pairs or i - 1 in pairs or (ci, co, s) != (32, 64, 2) or mpf
                 or A.ir_mid(ci, spec.expansion) not in (32, 96, 128)):
             continue
         n = i + 1
@@ -118,14 +131,19 @@ def nas_stage_bytes(ops) -> dict:
     front = os.environ.get("HN_NO_FRONT", "0") in ("", "0")
     irf = os.environ.get("HN_NO_IRF", "0") in ("", "0")
     out = {"stem": 0 if front else 4096 + 32 * 32 * 32 * 4, "front": 0, "irf": 0, "irf2": 0, "skip": 0, "pw": 0,
-           "dw": 0, "pwl": 0, "maxpool": 0, "se": 0, "head": 0, "irf+skip": 0}
+           "dw": 0, "pwl": 0, "maxpool": 0, "se": 0, "head": 0, "irf+skip": 0, "front+irf": 0}
     pairs = irf2_pairs(ops)
     fused_skip = irf_skip_layers(ops)
     skipped = {n for n in fused_skip.values()}
+    mpf = mpfront_irf(ops)
     hw = 32
     for i, (op, (ci, co, s)) in enumerate(zip(A.arch_ops(ops), A.SEARCH_SPACE2)):
         spec = A.OP_SPECS[op]
         ho = hw // s
+        if mpf and i < 3:  # k_mpfront_irf: the patch in, layer 2's 8x8x64 out
+            out["front+irf"] += 4096 + 4 * 64 * 8 * 8 if i == 0 else 0
+            hw = ho
+            continue
         if i in fused_skip:  # k_irf_skip: the block's input in, the skip's 4x4x128 output out
             out["irf+skip"] += 4 * ci * hw * hw + 4 * 128 * 4 * 4
             hw = ho
@@ -330,14 +348,18 @@ def nas_stage_flop(name: str) -> dict:
             hw //= st
         return {"front": 2 * front, "irf": 2 * irf, "head": 2 * 128 * 128 * 16}
     ops = A.arch_ops(name)
-    out = {"front": 0, "irf": 0, "irf2": 0, "skip": 0, "irf+skip": 0, "head": 2 * A.SEARCH_SPACE2[-1][1] * 128 * 16}
+    out = {"front": 0, "irf": 0, "irf2": 0, "skip": 0, "irf+skip": 0, "front+irf": 0,
+           "head": 2 * A.SEARCH_SPACE2[-1][1] * 128 * 16}
     pairs = irf2_pairs(ops)
     fused_skip = irf_skip_layers(ops)
     skipped = set(fused_skip.values())
+    mpf = mpfront_irf(ops)
     hw = 32
     for i, (op, (ci, co, st)) in enumerate(zip(ops, A.SEARCH_SPACE2)):
         macs = A.layer_macs(ci, co, st, op, hw)
-        if i in fused_skip or i in skipped:
+        if mpf and i < 3:
+            out["front+irf"] += 2 * (macs + (9 * 32 * 32 * 32 if i == 0 else 0))
+        elif i in fused_skip or i in skipped:
             out["irf+skip"] += 2 * macs
         elif i in pairs or i - 1 in pairs:
             out["irf2"] += 2 * macs

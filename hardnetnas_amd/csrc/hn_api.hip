@@ -43,6 +43,7 @@ void hn_read_knobs(HnKnobs* k) {
   k->front_fold = env_int("HN_FRONT_FOLD", 0) != 0;
   k->u8_apart = env_int("HN_U8_APART", 0) != 0;
   k->front_xch3 = env_int("HN_FRONT_XCH3", 0) != 0;
+  k->no_mpfront = env_int("HN_NO_MPFRONT", 0) != 0;
   k->train_splitk = std::max(32, env_int("HN_TRAIN_SPLITK", 1024)) / 32 * 32;
   k->train_f32 = env_int("HN_TRAIN_F32", 1) & 255;
 #ifdef HN_EXPERIMENTS
@@ -1059,6 +1060,19 @@ static int forward_nas(hn_model* m, const float* in, int P, int pmax, float* out
   if (m->desc.kind != HN_KIND_NAS) {  // FDLNet front (des.py) -> 8x8x64
     const HnFdlFrontArgs fa{in, x, m->stem_w, m->stem_b, m->fdl_w1, m->fdl_b1, m->fdl_w2, m->fdl_b2};
     STAGE("front", hn_launch_fdl_front(fa, P, m->desc.kind == HN_KIND_FDL_NASNET ? 0 : 1, ineps, st, u8));
+  } else if (m->front == 2 && !u8 && ineps < 0.f && !m->knobs.no_mpfront && m->layers.size() > 2 &&
+             m->layers[1].skip && !m->layers[1].skip_conv && m->layers[1].stride == 1 && m->layers[2].irf_pwl_a &&
+             !m->layers[2].se &&
+             hn_mpfront_irf_supported(m->layers[2].cin, m->layers[2].cout, m->layers[2].hin, m->layers[2].stride,
+                                      m->layers[2].k, m->layers[2].mid)) {
+    // the max-pool front, the identity layer 1 and the 16x16 stride-2 layer-2 block in one kernel
+    // (k_mpfront_irf): the 16x16x32 front output never reaches HBM
+    const NasLayer& L = m->layers[2];
+    const HnIrfArgs ia{nullptr, x, reinterpret_cast<const uint4*>(L.irf_pw_a), L.irf_pw_b, L.dw_w, L.dw_b,
+                       reinterpret_cast<const uint4*>(L.irf_pwl_a), L.pwl_b};
+    STAGE("front+irf", hn_launch_mpfront_irf(in, reinterpret_cast<const uint4*>(m->front_spack), m->stem_b, ia, P, L.k,
+                                             L.mid, false, ineps, st));
+    first = 3;
   } else if (m->front) {
     const NasLayer& L = m->layers[0];
     const bool mp = m->front == 2;

@@ -25,6 +25,7 @@ struct HnKnobs {
   bool u8_apart = false;       // HN_U8_APART: uint8 input preprocessed into the workspace first (A/B)
   bool front_xch3 = false;     // HN_FRONT_XCH3: the k3 front's dw per channel group (SGPR weights, s_x; two
                                // workgroups per CU instead of three: wang2 front 5.05 -> 5.57 ms, not the default)
+  bool no_mpfront = false;     // HN_NO_MPFRONT: k_front (max-pool) + k_irf instead of k_mpfront_irf
   int train_splitk = 1024;     // HN_TRAIN_SPLITK: K per split-K slice of the train GEMMs
   int train_f32 = 1;           // HN_TRAIN_F32: bit 0 train forward convs, bit 1 stride-1 dgrads as f32-MFMA
                                // GEMMs (else the bf16x3 conv kernels); default 1 = every product f32;
@@ -185,6 +186,10 @@ hipError_t hn_launch_irf(const HnIrfArgs& a, int P, int cin, int cout, int hin, 
 // a 16x16 stride-2 32 -> 64 block and the 8x8 64 -> 128 stride-2 skip that follows it (after identity
 // skips) in one kernel (hn_irf.hip k_irf_skip); a.y receives the skip's [P,4,4,128] output
 bool hn_irf_skip_supported(int cin, int cout, int hin, int s, int k, int mid);
+// the max-pool front + the first (16x16 stride-2 32 -> 64) IRF block in one kernel (hn_irf.hip k_mpfront_irf)
+bool hn_mpfront_irf_supported(int cin, int cout, int hin, int s, int k, int mid);
+hipError_t hn_launch_mpfront_irf(const float* in, const uint4* spack, const float* stem_b, const HnIrfArgs& a, int P,
+                                 int k, int mid, bool norm, float eps, hipStream_t st);
 hipError_t hn_launch_irf_skip(const HnIrfArgs& a, const uint4* skip_a, const float* skip_b, int P, int k, int mid,
                               hipStream_t st);
 hipError_t hn_launch_preprocess(const uint8_t* in, int64_t n, int resize, int norm, float mean,

@@ -567,6 +567,175 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
   }
 }
 
+// The max-pool NAS front (layer 0 = the strided "skip": stem ConvBNRelu 1 -> 32 then MaxPool2d(3, 2, 1),
+// model_supernet.py:57-58, fbnet_builder.py:202-228; k_front's FRONT_MAXPOOL form, hn_front.hip) and -- past an
+// identity skip at layer 1 -- the first IRF block, the 16x16 stride-2 32 -> COUT one (SEARCH_SPACE2 layer 2,
+// wang4's ir_k5_s2; fbnet_builder.py:455-570), in one persistent kernel: the 16x16x32 front output (32 KB per
+// patch written by k_front and read back by k_irf, the 8x8 net's largest HBM stream) never leaves the workgroup.
+// Per patch: the front's 4 bands (stem rows on the MFMA into the 9-row ring, the 3x3 / 2 max-pool of each band's
+// 4 output rows) keep their pooled float4s in registers (8 per thread); after the last band they go to an LDS
+// tile [256 pixels][36 floats] over the then dead ring, the block's pw B operands are read from it (k_irf2's
+// A -> B hand-off), and irf_core / irf_store run as in k_irf.  s_in stays apart (4.6 KB), the ring (44 KB) and
+// the block's buffers (46 KB) share one region: 50.7 KB, three workgroups per CU as both kernels it replaces.
+// Every value takes the arithmetic of k_front + k_irf in the same order: bit-identical to the two-kernel path
+// (tests/test_gpu_parity.py::test_maxpool_front_irf_kernel_is_bit_identical).
+namespace mpf {
+// k_front's dw/maxpool read lane map (hn_front.hip kDwLane; tests/test_lds_banks.py::test_front_dw_lane_map)
+__constant__ unsigned char kLane[64] = {
+    0,  1,  2,  3,  46, 47, 8,  9,  10, 11, 12, 13, 4,  5,  6,  7,  20, 21, 28, 29, 14, 15,
+    22, 23, 30, 31, 38, 39, 36, 37, 44, 45, 52, 53, 54, 55, 58, 59, 60, 61, 62, 63, 24, 25,
+    16, 17, 18, 19, 32, 33, 40, 41, 26, 27, 34, 35, 42, 43, 50, 51, 48, 49, 56, 57};
+constexpr int IR = 9, PC = 34, RS = PC * PS;  // ring rows (2 (RB - 1) + 3), padded columns, row stride (floats)
+}  // namespace mpf
+
+template <int K, int MID, bool NORM>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_mpfront_irf(
+    const float* __restrict__ in, float* __restrict__ y, const uint4* __restrict__ spack,
+    const float* __restrict__ stem_b, HnIrfArgs A, int P, float eps) {
+  constexpr int CIN = 32, COUT = 64, HIN = 16, S = 2;
+  using Sh = IrfShape<CIN, COUT, HIN, S, K, MID>;
+  constexpr int TI = Sh::TI, KS = Sh::KS, TW = Sh::TW, MODE = irf_mode<CIN, S>();
+  static_assert(Sh::NPB == 1 && MODE == IRF_WPAD, "one 16x16 patch per tile, dw weights in the pad slots");
+  constexpr int XS = CIN + 4;                         // the front output tile: [256 pixels][36 floats]
+  constexpr int RING = mpf::IR * mpf::RS;             // floats
+  constexpr int BLK = irf_smem_floats<CIN, COUT, HIN, S, K, MID>();
+  constexpr int REG = RING > BLK ? RING : BLK;
+  static_assert(256 * XS <= REG, "the tile fits the shared region");
+  static_assert(3 * (REG + 34 * 34 + 8) * 4 <= 160 * 1024, "three workgroups per CU");
+  __shared__ __attribute__((aligned(16))) float s_reg[REG];  // ring | front output tile | block buffers
+  __shared__ float s_in[34 * 34];
+  __shared__ float red[8];
+  __shared__ __attribute__((aligned(16))) float s_sb[32];  // the stem bias, read where used (registers: the block)
+  float* const s_pw = s_reg;
+
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int px = lane & 31, h = lane >> 5;
+  const long per = ((long)P + gridDim.x - 1) / gridDim.x;
+  const long pb = (long)xcd_remap(blockIdx.x, gridDim.x) * per;
+  const long pe = min((long)P, pb + per);
+  if (pb >= pe) return;  // workgroup-uniform
+
+  for (int i = t; i < 34 * 34; i += 256) s_in[i] = 0.f;  // the frame stays zero (only 32 x 32 rewritten)
+  if (t < 32) s_sb[t] = stem_b[t];
+  const int lm = mpf::kLane[lane], dq = lm & 7, dox = lm >> 3;
+  auto slot_of = [](int yy) { return (yy + 1 + mpf::IR) % mpf::IR; };  // ring slot of stem row yy (PAD 1)
+  float4 vnext = reinterpret_cast<const float4*>(in + pb * 1024)[t];
+#pragma unroll 1
+  for (long patch = pb; patch < pe; ++patch) {
+    float4 v = vnext;
+    if (patch + 1 < pe) vnext = reinterpret_cast<const float4*>(in + (patch + 1) * 1024)[t];
+    float mean = 0.f, sd = 1.f;
+    if (NORM) {  // (x - mean) / (std_unbiased + eps), as k_front
+      const float s0 = wave_sum(v.x + v.y + v.z + v.w);
+      if (lane == 0) red[w] = s0;
+      __syncthreads();
+      mean = (red[0] + red[1] + red[2] + red[3]) * (1.f / 1024.f);
+      const float d0 = v.x - mean, d1 = v.y - mean, d2 = v.z - mean, d3 = v.w - mean;
+      const float q = wave_sum(d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3);
+      if (lane == 0) red[4 + w] = q;
+      __syncthreads();
+      sd = sqrtf((red[4] + red[5] + red[6] + red[7]) * (1.f / 1023.f)) + eps;
+    }
+    __syncthreads();  // the previous patch is done with s_in and the shared region
+    {
+      const int q = 4 * t, yy = q >> 5, xx = q & 31;
+      float* d = s_in + (yy + 1) * 34 + xx + 1;
+      if (NORM) {
+        d[0] = (v.x - mean) / sd; d[1] = (v.y - mean) / sd;
+        d[2] = (v.z - mean) / sd; d[3] = (v.w - mean) / sd;
+      } else {
+        d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+      }
+    }
+    // the ring's left pad column (x = -1; the block's buffers overwrote it): zero, as k_front's one-time init
+    for (int i = t; i < mpf::IR * (PS / 4); i += 256)
+      reinterpret_cast<float4*>(s_pw)[(i / (PS / 4)) * (mpf::RS / 4) + i % (PS / 4)] = make_float4(0.f, 0.f, 0.f, 0.f);
+    __syncthreads();
+    // the stem A operand (L2-resident) per patch: not held in registers through the block's phase
+    const f16x8 sah = as_f16x8(spack[lane]), sal = as_f16x8(spack[64 + lane]);
+    // the pooled output, band b, j -> pixel (4 b + orr, ox), channels 4 dq .. + 3, in mp[b][j] after the
+    // band loop (a register FIFO shifted once per band: the loop stays rolled)
+    float4 mp[4][2];
+#pragma unroll 1
+    for (int band = 0; band < 4; ++band) {
+      const int r0 = band * 4;
+      const int ylast = 2 * r0 + 7, ybeg = band > 0 ? ylast - 7 : -1;  // the ring's new rows
+      const int nreal = ylast + 1 - ybeg;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {  // stem row tiles w + 4 i (k_front's non-PAIR phase A)
+        const int ri = w + 4 * i, yy = ybeg + ri;
+        if (ri >= nreal) continue;  // wave-uniform
+        if (yy < 0 || yy >= 32) {   // padding row of the stem output
+          float4* d = reinterpret_cast<float4*>(s_pw + slot_of(yy) * mpf::RS);
+          for (int j = lane; j < mpf::RS / 4; j += 64) d[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+          continue;
+        }
+        float tp[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int tap = 8 * h + j;  // h = 1 holds tap 8 and zeros
+          tp[j] = tap < 9 ? s_in[(yy + tap / 3) * 34 + px + tap % 3] : 0.f;
+        }
+        uint4 xh, xl;
+        split8_f16(make_float4(tp[0], tp[1], tp[2], tp[3]), make_float4(tp[4], tp[5], tp[6], tp[7]), xh, xl);
+        f32x16 sbr;  // the stem bias in the accumulator order (lane (px, h): acc[4q + r] = channel 4h + 8q + r)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float4 b = *reinterpret_cast<const float4*>(s_sb + 8 * q + 4 * h);
+          sbr[4 * q] = b.x; sbr[4 * q + 1] = b.y; sbr[4 * q + 2] = b.z; sbr[4 * q + 3] = b.w;
+        }
+        const f32x16 c = mfma3_f16(sah, sal, as_f16x8(xh), as_f16x8(xl), sbr);
+        float4* d = reinterpret_cast<float4*>(s_pw + slot_of(yy) * mpf::RS + (1 + px) * PS);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          d[2 * q + h] = make_float4(relu0(c[4 * q]), relu0(c[4 * q + 1]), relu0(c[4 * q + 2]), relu0(c[4 * q + 3]));
+      }
+      __syncthreads();
+      // MaxPool2d(3, 2, 1): padding never wins since every window holds a ReLU output >= 0
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int pp = 8 * (w + 4 * j) + dox, orr = pp >> 4, ox = pp & 15;
+        float4 m = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int dy = 0; dy < 3; ++dy) {
+          const float* rp = s_pw + slot_of(2 * (r0 + orr) - 1 + dy) * mpf::RS;
+#pragma unroll
+          for (int dx = 0; dx < 3; ++dx) {
+            const float4 a = *reinterpret_cast<const float4*>(rp + (2 * ox + dx) * PS + 4 * dq);
+            m.x = fmaxf(m.x, a.x); m.y = fmaxf(m.y, a.y); m.z = fmaxf(m.z, a.z); m.w = fmaxf(m.w, a.w);
+          }
+        }
+#pragma unroll
+        for (int b = 0; b < 3; ++b) mp[b][j] = mp[b + 1][j];
+        mp[3][j] = m;
+      }
+      __syncthreads();  // reads done before the next band's rows (or the output tile) overwrite ring slots
+    }
+    // the front output tile -> LDS [pixel][XS] over the dead ring; the block's pw B operands from it
+#pragma unroll
+    for (int band = 0; band < 4; ++band)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int pp = 8 * (w + 4 * j) + dox;
+        *reinterpret_cast<float4*>(s_reg + (band * 64 + pp) * XS + 4 * dq) = mp[band][j];
+      }
+    __syncthreads();
+    uint4 bh[TI][KS], bl[TI][KS];
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const float4* src = reinterpret_cast<const float4*>(s_reg + ((4 * i + w) * 32 + px) * XS + 16 * s + 8 * h);
+        split8_f16(src[0], src[1], bh[i][s], bl[i][s]);
+      }
+    __syncthreads();  // the region is the block's pw / dw buffers from here
+    f32x16 acc[TW];
+    irf_core<CIN, COUT, HIN, S, K, MID, MODE>(bh, bl, acc, A.pw_a, A.pw_b, A.dw_w, A.dw_b, A.pwl_a, A.pwl_b, s_reg,
+                                             s_reg + Sh::LDS_PW, s_reg + Sh::LDS_PW + Sh::LDS_DW);
+    irf_store<CIN, COUT, HIN, S, K, MID>(acc, y, patch, 1, s_reg);
+  }
+}
+
 template <int CIN, int COUT, int HIN, int S, int K, int MID>
 hipError_t irf_launch(const HnIrfArgs& a, int P, hipStream_t st) {
   constexpr int NPB = IrfTile<CIN, HIN, MID>::NPB;
@@ -625,6 +794,29 @@ hipError_t hn_launch_irf_skip(const HnIrfArgs& a, const uint4* skip_a, const flo
   }
   HN_IRFSK_GO(3, 32) HN_IRFSK_GO(3, 96) HN_IRFSK_GO(3, 128) HN_IRFSK_GO(5, 32) HN_IRFSK_GO(5, 96) HN_IRFSK_GO(5, 128)
 #undef HN_IRFSK_GO
+  return hipErrorInvalidValue;
+}
+
+// max-pool front + the 16x16 stride-2 32 -> 64 block (k_mpfront_irf): k3 / k5, e1 / e3 / e4 (mid 32 / 96 / 128)
+bool hn_mpfront_irf_supported(int cin, int cout, int hin, int s, int k, int mid) {
+  return hn_irf_skip_supported(cin, cout, hin, s, k, mid);
+}
+
+hipError_t hn_launch_mpfront_irf(const float* in, const uint4* spack, const float* stem_b, const HnIrfArgs& a, int P,
+                                 int k, int mid, bool norm, float eps, hipStream_t st) {
+  if (P <= 0) return hipSuccess;
+#define HN_MPF_GO(KK, MM, NN)                                                                                      \
+  if (k == KK && mid == MM && norm == NN) {                                                                        \
+    int resident = 0; /* persistent grid: every workgroup resident at once */                                      \
+    const hipError_t e = hn_resident_blocks(reinterpret_cast<const void*>(&k_mpfront_irf<KK, MM, NN>), 256, 0, &resident); \
+    if (e != hipSuccess) return e;                                                                                 \
+    hipLaunchKernelGGL((k_mpfront_irf<KK, MM, NN>), dim3(std::min(P, resident)), dim3(256), 0, st, in, a.y, spack, \
+                       stem_b, a, P, eps);                                                                         \
+    return hipGetLastError();                                                                                      \
+  }
+  HN_MPF_GO(3, 32, false) HN_MPF_GO(3, 96, false) HN_MPF_GO(3, 128, false)
+  HN_MPF_GO(5, 32, false) HN_MPF_GO(5, 96, false) HN_MPF_GO(5, 128, false)
+#undef HN_MPF_GO
   return hipErrorInvalidValue;
 }
 

@@ -88,7 +88,14 @@ int hn_param_count(const hn_arch_desc* desc, size_t* n_out);
 int hn_create(const hn_arch_desc* desc, const float* host_params, size_t n_params,
               hn_model** out);
 
-/* Bytes of device workspace hn_forward needs for a batch of B patches. */
+/* Bytes of device workspace hn_forward needs for a batch of B patches.  The forward walks the batch in
+ * chunks of min(B, 65,536) patches and sizes the workspace for one chunk; for the stock HardNet at the
+ * defaults that is 160 KiB per patch: 10 GiB from 65,536 patches up, 80 MiB at the reference eval loop's
+ * 512.  Two environment knobs, read by hn_create, bound it for the stock HardNet (both default 65,536; any
+ * values give bit-identical descriptors): HN_C12_GROUP (patches per fused stem+conv1+conv2 launch) and
+ * HN_SUBCHUNK (patches per conv3..conv5 launch); the footprint is (HN_SUBCHUNK + HN_C12_GROUP) x 64 KiB +
+ * chunk x 32 KiB, e.g. 4 GiB per 65,536-patch chunk at 16,384 / 16,384 (about 4 % slower end to end).
+ * NAS / FDL descriptors need four buffers of their largest per-patch activation. */
 int hn_workspace_bytes(const hn_model* m, int64_t batch, size_t* bytes_out);
 
 /* d_in: [B,1,32,32] fp32 contiguous (device); d_out: [B,128] fp32 (device).

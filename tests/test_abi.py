@@ -139,6 +139,22 @@ def test_bench_knows_every_nas_stage(monkeypatch):
     assert b["irf+skip"] == 0 and b["irf"] > 0 and b["skip"] > 0 and sum(f.values()) == 2 * A.nas_macs("wang3")
 
 
+def test_bench_knows_the_maxpool_front_fusion(monkeypatch):
+    """bench.py's mirror of forward_nas's k_mpfront_irf dispatch: wang4 (layers 0 / 1 "skip", layer 2 ir_k5_s2)
+    runs its front, the identity and layer 2 as one "front+irf" stage (the patch in, 8x8x64 out, all three
+    layers' FLOP), and a layer-2 block with SE, or HN_NO_MPFRONT, keeps the separate kernels."""
+    import bench
+    from hardnetnas_amd import arch as A
+    assert bench.mpfront_irf("wang4") and not bench.mpfront_irf("wang2") and not bench.mpfront_irf("wang3")
+    assert not bench.mpfront_irf(["skip", "skip", "ir_k5_e1_se", "skip", "skip", "skip"])
+    b, f = bench.nas_stage_bytes("wang4"), bench.nas_stage_flop("wang4")
+    assert b["front+irf"] == 4096 + 4 * 64 * 8 * 8 and b["front"] == 0
+    assert f["front"] == 0 and sum(f.values()) == 2 * A.nas_macs("wang4")
+    monkeypatch.setenv("HN_NO_MPFRONT", "1")
+    b, f = bench.nas_stage_bytes("wang4"), bench.nas_stage_flop("wang4")
+    assert b["front+irf"] == 0 and b["front"] > 0 and sum(f.values()) == 2 * A.nas_macs("wang4")
+
+
 def _kernel_template_args(kernel: str):
     """Template argument lists of every `kernel<...>` symbol in the product library (nm -C)."""
     import subprocess

@@ -318,7 +318,12 @@ def test_hardnet_at_the_timed_size(cuda_device):
     assert (y.norm(dim=1) - 1).abs().max().item() < 1e-5
     idx = torch.arange(0, b, b // 1024) + 255  # offset: rows away from chunk starts too
     ref = _oracle_rows("hardnet", p, x[idx.to(cuda_device)].cpu())
-    assert (y[idx.to(cuda_device)].cpu() - ref).abs().max().item() <= TOL["hardnet"]
+    err = (y[idx.to(cuda_device)].cpu() - ref).abs().max().item()
+    assert err <= TOL["hardnet"]
+    # the precision margin: bf16x3 products with conv1, conv3 and conv5 in 1-D Winograd
+    # form measure 1.9e-5 here (tests/precision/wino1d_precision.py predicts 1.7-2.0e-5); a further transformed
+    # or narrower layer that eats more than half of the 1e-4 bar fails this guard before it can fail the bar
+    assert err <= 5e-5, err
 
 
 def test_weights_update_triggers_repack(cuda_device):
@@ -700,6 +705,42 @@ def test_irf_skip_kernel_is_bit_identical(op, cuda_device, monkeypatch):
     assert "irf+skip" not in n2.stage_times() and "skip" in n2.stage_times()
     for b in (1, 37):
         assert torch.equal(nm(x[:b].to(cuda_device)), n2(x[:b].to(cuda_device)))
+
+
+@pytest.mark.parametrize("op", ["ir_k3_e1", "ir_k3_e3", "ir_k3_s4", "ir_k5_e1", "ir_k5_e3", "ir_k5_s4", "ir_k3_s2",
+                                "wang4"])
+def test_maxpool_front_irf_kernel_is_bit_identical(op, cuda_device, monkeypatch):
+    """k_mpfront_irf: the max-pool front (layer 0 "skip" at stride 2), the identity layer 1 and the 16x16 stride-2
+    layer-2 block in one persistent kernel, the 16x16x32 front output kept on chip.  It repeats k_front's stem /
+    max-pool and k_irf's block arithmetic step for step, so its descriptors equal the two-kernel path
+    (HN_NO_MPFRONT=1) bit for bit -- every MID (e1 / e3 / e4, groups + shuffle) and kernel size, ragged batches,
+    several patches per persistent workgroup -- and match the reference restatement (wang4: the golden vectors)."""
+    from hardnetnas_amd import synth
+    from hardnetnas_amd._native import NativeModel
+    if op == "wang4":
+        m, fx, _ = build_module("wang4")
+        x = torch.from_numpy(golden_inputs(fx))
+        ref = fx["y"]
+    else:
+        ops = ["skip", "skip", op, "ir_k3_e1", "ir_k5_e1", "skip"]
+        m, p = _synth_nas(ops, seed=19)
+        x = torch.from_numpy(synth.synth_patches(301, seed=23))
+        ref = O.nas_forward(p, ops, x).numpy()
+    nm = NativeModel.from_module(m, cuda_device)
+    nm.set_profiling(True)
+    y = nm(x.to(cuda_device))
+    st = nm.stage_times()
+    assert "front+irf" in st and "front" not in st, st
+    assert np.abs(y.cpu().numpy() - ref).max() <= NAS_TOL
+    monkeypatch.setenv("HN_NO_MPFRONT", "1")
+    n2 = NativeModel.from_module(m, cuda_device)
+    n2.set_profiling(True)
+    assert torch.equal(y, n2(x.to(cuda_device)))
+    assert "front+irf" not in n2.stage_times() and "front" in n2.stage_times()
+    for b in (1, 37):
+        assert torch.equal(nm(x[:b].to(cuda_device)), n2(x[:b].to(cuda_device)))
+    xr = x.repeat(7, 1, 1, 1)[:2001].to(cuda_device)  # more patches than resident workgroups: several each
+    assert torch.equal(nm(xr), n2(xr))
 
 
 @pytest.mark.parametrize("name", ["wang2", "cov_c"])
