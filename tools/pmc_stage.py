@@ -28,6 +28,10 @@ def stage(name: str):
         return "irf2"
     if "k_irf_skip<" in name:
         return "irf+skip"
+    if "k_mpfront_irf<" in name:
+        return "front+irf"
+    if "k_head_fin<" in name:
+        return "head"
     if "k_skip_s2<" in name or "k_skip_s2(" in name:
         return "skip"
     if "k_fdl_front" in name:
