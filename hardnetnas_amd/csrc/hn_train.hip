@@ -257,18 +257,24 @@ struct Fw3Cfg {
   static_assert(32 % H == 0 && (G * CIN * H) % 64 == 0, "geometry");
 };
 
-template <int CIN, int COUT, int H>
+// NS: each patch's H output rows in NS segments of H / NS, one wave each (its own ring, primed with the
+// segment's halo rows) -- small train batches (the reference's 512 pairs: 512 waves for 1,024 SIMDs at NS = 1)
+// get NS times the waves; every output keeps its K order, so the result is the same bit for bit
+template <int CIN, int COUT, int H, int NS = 1>
 __global__ __launch_bounds__(256) void k_fwd3(const float* __restrict__ zx, int relu, const float* __restrict__ W,
                                               long B, float* __restrict__ z) {
   using C = Fw3Cfg<CIN, COUT, H>;
-  constexpr int G = C::G;
+  constexpr int G = C::G, HS = H / NS;
+  static_assert(HS % G == 0, "whole steps per segment");
   __shared__ float smem[4 * C::WAVE_F];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
   float* sx = smem + w * C::WAVE_F;  // [CIN][R slots][XW] (+pad)
   for (int i = lane; i < C::WAVE_F; i += 64) sx[i] = 0.f;
   __builtin_amdgcn_wave_barrier();
   constexpr int HH = H * H;
-  const long b = (long)blockIdx.x * 4 + w;  // one patch per wave
+  const long u = (long)blockIdx.x * 4 + w;  // one (patch, row segment) per wave
+  const long b = u / NS;
+  const int ys = (int)(u % NS) * HS, ye = ys + HS;
   if (b >= B) return;
   // input rows y0 .. y0 + G - 1 of all CIN channels (zero outside the patch): lane -> NLD floats
   auto load_rows = [&](int y0, float (&v)[C::NLD]) {
@@ -287,14 +293,14 @@ __global__ __launch_bounds__(256) void k_fwd3(const float* __restrict__ zx, int 
       if (y <= ymax) sx[c * C::RSX + ((y + 1 + C::R) % C::R) * C::XW + 1 + x] = v[i];
     }
   };
-  {  // prologue: rows -1 .. G into the ring
+  {  // prologue: rows ys - 1 .. ys + G into the ring
     float v[C::NLD];
-    load_rows(-1, v);
-    put_rows(-1, v, G);
+    load_rows(ys - 1, v);
+    put_rows(ys - 1, v, ys + G);
 #pragma unroll 1
-    for (int y0 = G - 1; y0 <= G; y0 += G) {
+    for (int y0 = ys + G - 1; y0 <= ys + G; y0 += G) {
       load_rows(y0, v);
-      put_rows(y0, v, G);
+      put_rows(y0, v, ys + G);
     }
   }
   __builtin_amdgcn_wave_barrier();
@@ -312,9 +318,9 @@ __global__ __launch_bounds__(256) void k_fwd3(const float* __restrict__ zx, int 
       for (int t = 0; t < 9; ++t) wr[j][t] = wl[j * 18 + t];
   }
 #pragma unroll 1
-  for (int y = 0; y < H; y += G) {
+  for (int y = ys; y < ye; y += G) {
     float nv[C::NLD];
-    if (y + G < H) load_rows(y + G + 1, nv);  // rows y + G + 1 .. y + 2G (zero past the patch)
+    if (y + G < ye) load_rows(y + G + 1, nv);  // rows y + G + 1 .. y + 2G (zero past the patch)
     f32x16 acc[C::NCO];
 #pragma unroll
     for (int cb = 0; cb < C::NCO; ++cb) acc[cb] = f32x16{};
@@ -372,7 +378,7 @@ __global__ __launch_bounds__(256) void k_fwd3(const float* __restrict__ zx, int 
         }
     __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");
-    if (y + G < H) put_rows(y + G + 1, nv, 1 << 30);
+    if (y + G < ye) put_rows(y + G + 1, nv, 1 << 30);
     __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");
   }
@@ -382,11 +388,13 @@ __global__ __launch_bounds__(256) void k_fwd3(const float* __restrict__ zx, int 
 // (one 32-channel block each) -- 4 / NWP patches per workgroup.  Per patch one ring instead of NWP,
 // so conv3 (NWP 2, 37 KB per workgroup) and conv5 (NWP 4, 31 KB) run 4-5 waves per SIMD instead
 // of one and the MFMA chains of different waves hide each other's ring and weight loads.
-template <int CIN, int COUT, int H, int NWP>
+// NS: as k_fwd3's (row segments of H / NS per (patch, segment) unit, 4 / NWP units per workgroup)
+template <int CIN, int COUT, int H, int NWP, int NS = 1>
 __global__ __launch_bounds__(256) void k_fwd3s(const float* __restrict__ zx, int relu, const float* __restrict__ W,
                                                long B, float* __restrict__ z) {
   using C = Fw3Cfg<CIN, COUT, H>;
-  constexpr int G = C::G, PPB = 4 / NWP, NLDT = C::NLD / NWP, HH = H * H;
+  constexpr int G = C::G, PPB = 4 / NWP, NLDT = C::NLD / NWP, HH = H * H, HS = H / NS;
+  static_assert(HS % G == 0, "whole steps per segment");
   static_assert(C::NCO == NWP && C::NLD % NWP == 0, "one 32-channel block per wave");
   __shared__ float smem[PPB * C::WAVE_F];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
@@ -394,7 +402,9 @@ __global__ __launch_bounds__(256) void k_fwd3s(const float* __restrict__ zx, int
   float* sx = smem + lp * C::WAVE_F;
   for (int i = threadIdx.x; i < PPB * C::WAVE_F; i += 256) smem[i] = 0.f;
   __syncthreads();
-  const long b = (long)blockIdx.x * PPB + lp;
+  const long u = (long)blockIdx.x * PPB + lp;
+  const long b = u / NS;
+  const int ys = (int)(u % NS) * HS, ye = ys + HS;
   const bool valid = b < B;  // no early return: the waves of a workgroup meet at barriers
   auto load_rows = [&](int y0, float (&v)[NLDT]) {  // this wave's share of rows y0 .. y0 + G - 1
 #pragma unroll
@@ -414,21 +424,21 @@ __global__ __launch_bounds__(256) void k_fwd3s(const float* __restrict__ zx, int
   };
   {
     float v[NLDT];
-    load_rows(-1, v);
-    put_rows(-1, v, G);
+    load_rows(ys - 1, v);
+    put_rows(ys - 1, v, ys + G);
 #pragma unroll 1
-    for (int y0 = G - 1; y0 <= G; y0 += G) {
+    for (int y0 = ys + G - 1; y0 <= ys + G; y0 += G) {
       load_rows(y0, v);
-      put_rows(y0, v, G);
+      put_rows(y0, v, ys + G);
     }
   }
   __syncthreads();
   const int rr0 = r / H, x0 = r % H;
   const float* wl = W + (long)(cb * 32 + r) * CIN * 9 + h * 9;  // W[co][ci = 2 j + h][0..8]
 #pragma unroll 1
-  for (int y = 0; y < H; y += G) {
+  for (int y = ys; y < ye; y += G) {
     float nv[NLDT];
-    if (y + G < H) load_rows(y + G + 1, nv);
+    if (y + G < ye) load_rows(y + G + 1, nv);
     f32x16 acc = f32x16{};
     float wc[9], wn[9];
 #pragma unroll
@@ -457,16 +467,37 @@ __global__ __launch_bounds__(256) void k_fwd3s(const float* __restrict__ zx, int
           z[((long)co * B + b) * HH + (y + rr0) * H + x0] = acc[4 * q + e];
         }
     __syncthreads();
-    if (y + G < H) put_rows(y + G + 1, nv, 1 << 30);
+    if (y + G < ye) put_rows(y + G + 1, nv, 1 << 30);
     __syncthreads();
   }
 }
 
+// row segments per patch: enough (patch, segment) waves for two per SIMD (2,048) at small batches
+static int fwd3_ns(long waves) { return waves >= 2048 ? 1 : waves >= 1024 ? 2 : 4; }
+
 template <int CIN, int COUT, int H>
 hipError_t fwd3s(const float* zx, bool relu, const float* W, long B, float* z, hipStream_t st) {
   constexpr int NWP = COUT / 32, PPB = 4 / NWP;
-  hipLaunchKernelGGL((k_fwd3s<CIN, COUT, H, NWP>), dim3((unsigned)((B + PPB - 1) / PPB)), dim3(256), 0, st, zx,
-                     relu ? 1 : 0, W, B, z);
+  const int ns = std::min(fwd3_ns(B * NWP), H / Fw3Cfg<CIN, COUT, H>::G);
+  auto go = [&](auto nsc) {
+    constexpr int NS = decltype(nsc)::value;
+    hipLaunchKernelGGL((k_fwd3s<CIN, COUT, H, NWP, NS>), dim3((unsigned)((B * NS + PPB - 1) / PPB)), dim3(256), 0, st,
+                       zx, relu ? 1 : 0, W, B, z);
+  };
+  constexpr int NSMAX = H / Fw3Cfg<CIN, COUT, H>::G;  // (whole G-row steps per segment)
+  if constexpr (NSMAX >= 4) {
+    if (ns >= 4) {
+      go(std::integral_constant<int, 4>{});
+      return hipGetLastError();
+    }
+  }
+  if constexpr (NSMAX >= 2) {
+    if (ns >= 2) {
+      go(std::integral_constant<int, 2>{});
+      return hipGetLastError();
+    }
+  }
+  go(std::integral_constant<int, 1>{});
   return hipGetLastError();
 }
 
@@ -481,7 +512,26 @@ __global__ __launch_bounds__(256) void k_wflip(const float* __restrict__ w, int 
 
 template <int CIN, int COUT, int H>
 hipError_t fwd3(const float* zx, bool relu, const float* W, long B, float* z, hipStream_t st) {
-  hipLaunchKernelGGL((k_fwd3<CIN, COUT, H>), dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, zx, relu ? 1 : 0, W, B, z);
+  const int ns = std::min(fwd3_ns(B), H / Fw3Cfg<CIN, COUT, H>::G);
+  auto go = [&](auto nsc) {
+    constexpr int NS = decltype(nsc)::value;
+    hipLaunchKernelGGL((k_fwd3<CIN, COUT, H, NS>), dim3((unsigned)((B * NS + 3) / 4)), dim3(256), 0, st, zx,
+                       relu ? 1 : 0, W, B, z);
+  };
+  constexpr int NSMAX = H / Fw3Cfg<CIN, COUT, H>::G;  // (whole G-row steps per segment)
+  if constexpr (NSMAX >= 4) {
+    if (ns >= 4) {
+      go(std::integral_constant<int, 4>{});
+      return hipGetLastError();
+    }
+  }
+  if constexpr (NSMAX >= 2) {
+    if (ns >= 2) {
+      go(std::integral_constant<int, 2>{});
+      return hipGetLastError();
+    }
+  }
+  go(std::integral_constant<int, 1>{});
   return hipGetLastError();
 }
 
