@@ -126,10 +126,13 @@ struct Wg3Cfg {
   static_assert(NPW >= 1 && NPC % 4 == 0, "chunking");
 };
 
-template <int CIN, int COUT, int H>
+// NS: as k_fwd3's row segments -- the chunk's NPC units are (patch, segment of H / NS rows), so a small batch
+// gets NS times the waves (and NS times the split-K slices; each product lands in the same fp64 slice sum)
+template <int CIN, int COUT, int H, int NS = 1>
 __global__ __launch_bounds__(256) void k_wgrad3(const float* __restrict__ zx, const float* __restrict__ dY, long B,
                                                 float* __restrict__ part) {
   using C = Wg3Cfg<CIN, COUT, H>;
+  constexpr int HS = H / NS;
   __shared__ float smem[4 * C::WAVE_F];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
   const int blk = blockIdx.x, co0 = (blk / C::NCI) * 32, ci0 = (blk % C::NCI) * 32;
@@ -171,19 +174,21 @@ __global__ __launch_bounds__(256) void k_wgrad3(const float* __restrict__ zx, co
   };
 #pragma unroll 1
   for (int pi = 0; pi < C::NPW; ++pi) {
-    const long b = chunk * C::NPC + w + 4 * pi;
+    const long u = chunk * C::NPC + w + 4 * pi;
+    const long b = u / NS;
     if (b >= B) break;  // wave-uniform
+    const int ys = (int)(u % NS) * HS, ye = ys + HS;
     float vy[NPR], vx[NPR];
-    // prologue: X rows -1, 0, 1 and dY row 0
-    load_row(zx, ci0, b, -1, vx, true); put_x(vx, -1);
-    load_row(zx, ci0, b, 0, vx, true);  put_x(vx, 0);
-    load_row(zx, ci0, b, 1, vx, true);  put_x(vx, 1);
-    load_row(dY, co0, b, 0, vy, false); put_y(vy);
+    // prologue: X rows ys - 1, ys, ys + 1 and dY row ys (the ring slot of row y is (y + 1) % 3)
+    load_row(zx, ci0, b, ys - 1, vx, true); put_x(vx, ys - 1);
+    load_row(zx, ci0, b, ys, vx, true);     put_x(vx, ys);
+    load_row(zx, ci0, b, ys + 1, vx, true); put_x(vx, ys + 1);
+    load_row(dY, co0, b, ys, vy, false);    put_y(vy);
     __builtin_amdgcn_wave_barrier();
 #pragma unroll 1
-    for (int y = 0; y < H; ++y) {
+    for (int y = ys; y < ye; ++y) {
       // prefetch dY row y + 1 and X row y + 2 while row y's MFMAs run
-      if (y + 1 < H) load_row(dY, co0, b, y + 1, vy, false);
+      if (y + 1 < ye) load_row(dY, co0, b, y + 1, vy, false);
       load_row(zx, ci0, b, y + 2, vx, true);
       const float* xr[3];
 #pragma unroll
@@ -200,7 +205,7 @@ __global__ __launch_bounds__(256) void k_wgrad3(const float* __restrict__ zx, co
       }
       __builtin_amdgcn_wave_barrier();
       asm volatile("" ::: "memory");
-      if (y + 1 < H) put_y(vy);
+      if (y + 1 < ye) put_y(vy);
       put_x(vx, y + 2);
       __builtin_amdgcn_wave_barrier();
       asm volatile("" ::: "memory");
@@ -218,12 +223,21 @@ __global__ __launch_bounds__(256) void k_wgrad3(const float* __restrict__ zx, co
         dst[(long)(co0 + 8 * q + 4 * h + e) * (CIN * 9) + (ci0 + r) * 9 + t] = acc[t][4 * q + e];
 }
 
+static int wgrad3_ns(long B) { return B >= 2048 ? 1 : B >= 1024 ? 2 : 4; }  // (B x NS waves per layer)
+
 template <int CIN, int COUT, int H>
 hipError_t wgrad3(const float* zx, const float* dY, long B, float* dW, float* part, hipStream_t st) {
   using C = Wg3Cfg<CIN, COUT, H>;
-  const long chunks = (B + C::NPC - 1) / C::NPC;
-  hipLaunchKernelGGL((k_wgrad3<CIN, COUT, H>), dim3(C::NCO * C::NCI, (unsigned)chunks), dim3(256), 0, st, zx, dY,
-                     B, part);
+  const int ns = wgrad3_ns(B);
+  const long chunks = (B * ns + C::NPC - 1) / C::NPC;
+  auto go = [&](auto nsc) {
+    constexpr int NS = decltype(nsc)::value;
+    hipLaunchKernelGGL((k_wgrad3<CIN, COUT, H, NS>), dim3(C::NCO * C::NCI, (unsigned)chunks), dim3(256), 0, st, zx,
+                       dY, B, part);
+  };
+  if (ns == 4) go(std::integral_constant<int, 4>{});
+  else if (ns == 2) go(std::integral_constant<int, 2>{});
+  else go(std::integral_constant<int, 1>{});
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   GemmArgs g{nullptr, nullptr, dW, COUT, (long)CIN * 9, 0, 0, 0, 0, 0, (long)CIN * 9, 1, 1.f, 0.f};
@@ -235,7 +249,7 @@ hipError_t wgrad3(const float* zx, const float* dY, long B, float* dW, float* pa
 // slices k_wgrad3 writes for layer l (0 if it does not take that layer)
 static long wgrad3_slices(int l, long B) {
   const int npc = l == 1 ? Wg3Cfg<32, 32, 32>::NPC : l == 3 ? Wg3Cfg<64, 64, 16>::NPC : l == 5 ? Wg3Cfg<128, 128, 8>::NPC : 0;
-  return npc ? 4 * ((B + npc - 1) / npc) : 0;
+  return npc ? 4 * ((B * wgrad3_ns(B) + npc - 1) / npc) : 0;
 }
 
 // ------------------------------------------------------------------------------------------
