@@ -571,11 +571,14 @@ struct Fw2Cfg {
 
 // NWP waves share one patch's ring and split its output-channel blocks (NWP > 1: 4 / NWP patches
 // per workgroup, workgroup barriers; NWP = 1: one patch per wave, wave barriers).
-template <int CIN, int COUT, int HI, int NWP>
+// NS: output rows in NS segments of HO / NS per (patch, segment) unit (k_fwd3's small-batch split)
+template <int CIN, int COUT, int HI, int NWP, int NS = 1>
 __global__ __launch_bounds__(256) void k_fwd2(const float* __restrict__ zx, int relu, const float* __restrict__ W,
                                               long B, float* __restrict__ z) {
   using C = Fw2Cfg<CIN, COUT, HI>;
   constexpr int G = C::G, HO = C::HO, HHI = HI * HI, PPB = 4 / NWP, CPW = C::NCO / NWP, NLDT = C::NLD / NWP;
+  constexpr int HS = HO / NS;
+  static_assert(HS % G == 0, "whole steps per segment");
   static_assert(C::NCO % NWP == 0 && C::NLD % NWP == 0, "split");
   __shared__ float smem[PPB * C::WAVE_F];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
@@ -591,36 +594,41 @@ __global__ __launch_bounds__(256) void k_fwd2(const float* __restrict__ zx, int 
   for (int i = (NWP > 1 ? threadIdx.x : lane); i < (NWP > 1 ? PPB : 1) * C::WAVE_F; i += (NWP > 1 ? 256 : 64))
     (NWP > 1 ? smem : sx)[i] = 0.f;
   sync();
-  const long b = (long)blockIdx.x * PPB + lp;
+  const long u = (long)blockIdx.x * PPB + lp;
+  const long b = u / NS;
+  const int ys = (int)(u % NS) * HS, ye = ys + HS;
   const bool valid = b < B;
   if (NWP == 1 && !valid) return;
   auto load_rows = [&](int y0, float (&v)[NLDT]) {  // this wave's share of input rows y0 .. y0 + 2G - 1
 #pragma unroll
     for (int i = 0; i < NLDT; ++i) {
       const int e = (wp * 64 + lane) * NLDT + i, c = e / (2 * G * HI), rr = (e / HI) % (2 * G), x = e % HI;
-      const float t = valid ? zx[((long)c * B + b) * HHI + (y0 + rr) * HI + x] : 0.f;
+      const int y = y0 + rr;
+      const float t = valid && y >= 0 && y < HI ? zx[((long)c * B + b) * HHI + y * HI + x] : 0.f;
       v[i] = relu ? fmaxf(t, 0.f) : t;
     }
   };
-  auto put_rows = [&](int y0, const float (&v)[NLDT]) {
+  auto put_rows = [&](int y0, const float (&v)[NLDT], int ymax) {
 #pragma unroll
     for (int i = 0; i < NLDT; ++i) {
       const int e = (wp * 64 + lane) * NLDT + i, c = e / (2 * G * HI), rr = (e / HI) % (2 * G), x = e % HI;
-      sx[c * C::RSX + ((y0 + rr + 1) % C::R) * C::XW + 1 + x] = v[i];
+      if (y0 + rr <= ymax) sx[c * C::RSX + ((y0 + rr + 1 + C::R) % C::R) * C::XW + 1 + x] = v[i];
     }
   };
-  {
+  {  // prologue: input rows 2 ys - 1 .. 2 ys + 2G - 1 (row -1: the zero pad)
     float v[NLDT];
-    load_rows(0, v);
-    put_rows(0, v);
+    load_rows(2 * ys - 1, v);
+    put_rows(2 * ys - 1, v, 2 * ys + 2 * G - 1);
+    load_rows(2 * ys + 2 * G - 1, v);
+    put_rows(2 * ys + 2 * G - 1, v, 2 * ys + 2 * G - 1);
   }
   sync();
   const int rr0 = r / HO, x0 = r % HO;
   const float* wl = W + (long)(wp * CPW * 32 + r) * CIN * 9 + h * 9;  // W[co = (wp CPW + cb) 32 + r][ci = 2 j + h]
 #pragma unroll 1
-  for (int y = 0; y < HO; y += G) {
+  for (int y = ys; y < ye; y += G) {
     float nv[NLDT];
-    if (y + G < HO) load_rows(2 * (y + G), nv);
+    if (y + G < ye) load_rows(2 * (y + G), nv);
     f32x16 acc[CPW];
 #pragma unroll
     for (int cb = 0; cb < CPW; ++cb) acc[cb] = f32x16{};
@@ -673,19 +681,36 @@ __global__ __launch_bounds__(256) void k_fwd2(const float* __restrict__ zx, int 
             z[((long)co * B + b) * (HO * HO) + (y + rr0) * HO + x0] = acc[cb][4 * q + e];
           }
     sync();
-    if (y + G < HO) put_rows(2 * (y + G), nv);
+    if (y + G < ye) put_rows(2 * (y + G), nv, 1 << 30);
     sync();
   }
 }
 
+// (patch, row segment) units: B NS waves x NWP (shared rings) reach two per SIMD at small batches
+template <int HS, int G, class F>
+static void launch_ns(int ns, F&& go) {
+  if constexpr (HS / G >= 4) {
+    if (ns >= 4) return go(std::integral_constant<int, 4>{});
+  }
+  if constexpr (HS / G >= 2) {
+    if (ns >= 2) return go(std::integral_constant<int, 2>{});
+  }
+  go(std::integral_constant<int, 1>{});
+}
+
 template <int CIN, int COUT, int HI, int NWP = (COUT / 32 >= 4 ? 4 : COUT / 32)>
 hipError_t fwd2(const float* zx, bool relu, const float* W, long B, float* z, hipStream_t st, bool shared) {
-  if (shared)
-    hipLaunchKernelGGL((k_fwd2<CIN, COUT, HI, NWP>), dim3((unsigned)((B + 4 / NWP - 1) / (4 / NWP))), dim3(256), 0,
-                       st, zx, relu ? 1 : 0, W, B, z);
-  else
-    hipLaunchKernelGGL((k_fwd2<CIN, COUT, HI, 1>), dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, zx, relu ? 1 : 0,
-                       W, B, z);
+  using C = Fw2Cfg<CIN, COUT, HI>;
+  const int nwp = shared ? NWP : 1;
+  launch_ns<C::HO, C::G>(fwd3_ns(B * nwp), [&](auto nsc) {
+    constexpr int NS = decltype(nsc)::value;
+    if (shared)
+      hipLaunchKernelGGL((k_fwd2<CIN, COUT, HI, NWP, NS>), dim3((unsigned)((B * NS + 4 / NWP - 1) / (4 / NWP))),
+                         dim3(256), 0, st, zx, relu ? 1 : 0, W, B, z);
+    else
+      hipLaunchKernelGGL((k_fwd2<CIN, COUT, HI, 1, NS>), dim3((unsigned)((B * NS + 3) / 4)), dim3(256), 0, st, zx,
+                         relu ? 1 : 0, W, B, z);
+  });
   return hipGetLastError();
 }
 
@@ -706,11 +731,13 @@ struct Dg2Cfg {
   static_assert(32 % HO == 0 && (G * CO * HO) % 64 == 0 && HO >= G, "geometry");
 };
 
-template <int CO, int CI, int HO, int NWP>
+template <int CO, int CI, int HO, int NWP, int NS = 1>
 __global__ __launch_bounds__(256) void k_dgrad2(const float* __restrict__ dY, const float* __restrict__ W, long B,
                                                 float* __restrict__ din) {
   using C = Dg2Cfg<CO, CI, HO>;
   constexpr int G = C::G, HI = 2 * HO, HH = HO * HO, PPB = 4 / NWP, CPW = C::NCI / NWP, NLDT = C::NLD / NWP;
+  constexpr int HS = HO / NS;  // cell rows per (patch, segment) unit
+  static_assert(HS % G == 0, "whole steps per segment");
   static_assert(C::NCI % NWP == 0 && C::NLD % NWP == 0, "split");
   __shared__ float smem[PPB * C::WAVE_F];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
@@ -726,7 +753,9 @@ __global__ __launch_bounds__(256) void k_dgrad2(const float* __restrict__ dY, co
   for (int i = (NWP > 1 ? threadIdx.x : lane); i < (NWP > 1 ? PPB : 1) * C::WAVE_F; i += (NWP > 1 ? 256 : 64))
     (NWP > 1 ? smem : sx)[i] = 0.f;
   sync();
-  const long b = (long)blockIdx.x * PPB + lp;
+  const long u = (long)blockIdx.x * PPB + lp;
+  const long b = u / NS;
+  const int ys = (int)(u % NS) * HS, ye = ys + HS;
   const bool valid = b < B;
   if (NWP == 1 && !valid) return;
   auto load_rows = [&](int y0, float (&v)[NLDT]) {  // dY rows y0 .. y0 + G - 1 (zero past the patch)
@@ -743,20 +772,20 @@ __global__ __launch_bounds__(256) void k_dgrad2(const float* __restrict__ dY, co
       if (y <= ymax) sx[c * C::RSX + (y % C::R) * C::XW + x] = v[i];
     }
   };
-  {  // prologue: rows 0 .. G
+  {  // prologue: rows ys .. ys + G
     float v[NLDT];
-    load_rows(0, v);
-    put_rows(0, v, G);
-    load_rows(G, v);
-    put_rows(G, v, G);
+    load_rows(ys, v);
+    put_rows(ys, v, ys + G);
+    load_rows(ys + G, v);
+    put_rows(ys + G, v, ys + G);
   }
   sync();
   const int rr0 = r / HO, n0 = r % HO;
   const float* wl = W + ((long)h * CI + wp * CPW * 32 + r) * 9;  // W[co = 2 j + h][ci = (wp CPW + cb) 32 + r]
 #pragma unroll 1
-  for (int y = 0; y < HO; y += G) {
+  for (int y = ys; y < ye; y += G) {
     float nv[NLDT];
-    if (y + G < HO) load_rows(y + G + 1, nv);
+    if (y + G < ye) load_rows(y + G + 1, nv);
     f32x16 acc[4][CPW];  // [2 py + px][ci block]
 #pragma unroll
     for (int k = 0; k < 4; ++k)
@@ -810,7 +839,7 @@ __global__ __launch_bounds__(256) void k_dgrad2(const float* __restrict__ dY, co
             *reinterpret_cast<float2*>(o + py * HI) = make_float2(acc[2 * py][cb][4 * q + e], acc[2 * py + 1][cb][4 * q + e]);
         }
     sync();
-    if (y + G < HO) put_rows(y + G + 1, nv, 1 << 30);
+    if (y + G < ye) put_rows(y + G + 1, nv, 1 << 30);
     sync();
   }
 }
@@ -818,11 +847,17 @@ __global__ __launch_bounds__(256) void k_dgrad2(const float* __restrict__ dY, co
 template <int CO, int CI, int HO>
 hipError_t dgrad2(const float* dY, const float* W, long B, float* din, hipStream_t st, bool shared) {
   constexpr int NWP = CI / 32 >= 4 ? 4 : CI / 32;
-  if (shared && NWP > 1)
-    hipLaunchKernelGGL((k_dgrad2<CO, CI, HO, NWP>), dim3((unsigned)((B + 4 / NWP - 1) / (4 / NWP))), dim3(256), 0,
-                       st, dY, W, B, din);
-  else
-    hipLaunchKernelGGL((k_dgrad2<CO, CI, HO, 1>), dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, dY, W, B, din);
+  using C = Dg2Cfg<CO, CI, HO>;
+  const bool sh = shared && NWP > 1;
+  launch_ns<HO, C::G>(fwd3_ns(B * (sh ? NWP : 1)), [&](auto nsc) {
+    constexpr int NS = decltype(nsc)::value;
+    if (sh)
+      hipLaunchKernelGGL((k_dgrad2<CO, CI, HO, NWP, NS>), dim3((unsigned)((B * NS + 4 / NWP - 1) / (4 / NWP))),
+                         dim3(256), 0, st, dY, W, B, din);
+    else
+      hipLaunchKernelGGL((k_dgrad2<CO, CI, HO, 1, NS>), dim3((unsigned)((B * NS + 3) / 4)), dim3(256), 0, st, dY, W, B,
+                         din);
+  });
   return hipGetLastError();
 }
 
@@ -843,11 +878,11 @@ struct Wg2Cfg {
   static_assert(NPY >= 1 && NPC % 4 == 0 && HO % 2 == 0, "geometry");
 };
 
-template <int CIN, int COUT, int HO>
+template <int CIN, int COUT, int HO, int NS = 1>
 __global__ __launch_bounds__(256) void k_wgrad2(const float* __restrict__ zx, const float* __restrict__ dY, long B,
                                                 float* __restrict__ part) {
   using C = Wg2Cfg<CIN, COUT, HO>;
-  constexpr int HI = C::HI;
+  constexpr int HI = C::HI, HS = HO / NS;  // (output rows per (patch, segment) unit)
   __shared__ float smem[4 * C::WAVE_F];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
   const int blk = blockIdx.x, co0 = (blk / C::NCI) * 32, ci0 = (blk % C::NCI) * 32;
@@ -890,19 +925,25 @@ __global__ __launch_bounds__(256) void k_wgrad2(const float* __restrict__ zx, co
   };
 #pragma unroll 1
   for (int pi = 0; pi < C::NPW; ++pi) {
-    const long b = chunk * C::NPC + w + 4 * pi;
+    const long u = chunk * C::NPC + w + 4 * pi;
+    const long b = u / NS;
     if (b >= B) break;  // wave-uniform
+    const int ys = (int)(u % NS) * HS, ye = ys + HS;
     float vy[C::NPY], va[C::NPX], vb[C::NPX];
-    // prologue: X row -1 = zeros (slot 0), rows 0 and 1, dY row 0
-    for (int i = 0; i < C::NPX; ++i) va[i] = 0.f;
-    put_x(va, -1);
-    load_x(b, 0, va); put_x(va, 0);
-    load_x(b, 1, va); put_x(va, 1);
-    load_y(b, 0, vy); put_y(vy);
+    // prologue: X row 2 ys - 1 (zeros for ys = 0: the pad), rows 2 ys and 2 ys + 1, dY row ys
+    if (ys == 0) {
+      for (int i = 0; i < C::NPX; ++i) va[i] = 0.f;
+    } else {
+      load_x(b, 2 * ys - 1, va);
+    }
+    put_x(va, 2 * ys - 1);
+    load_x(b, 2 * ys, va); put_x(va, 2 * ys);
+    load_x(b, 2 * ys + 1, va); put_x(va, 2 * ys + 1);
+    load_y(b, ys, vy); put_y(vy);
     __builtin_amdgcn_wave_barrier();
 #pragma unroll 1
-    for (int y = 0; y < HO; ++y) {
-      const bool more = y + 1 < HO;  // prefetch dY row y + 1 and X rows 2y + 2, 2y + 3
+    for (int y = ys; y < ye; ++y) {
+      const bool more = y + 1 < ye;  // prefetch dY row y + 1 and X rows 2y + 2, 2y + 3
       if (more) {
         load_y(b, y + 1, vy);
         load_x(b, 2 * y + 2, va);
@@ -946,9 +987,16 @@ __global__ __launch_bounds__(256) void k_wgrad2(const float* __restrict__ zx, co
 template <int CIN, int COUT, int HO>
 hipError_t wgrad2(const float* zx, const float* dY, long B, float* dW, float* part, hipStream_t st) {
   using C = Wg2Cfg<CIN, COUT, HO>;
-  const long chunks = (B + C::NPC - 1) / C::NPC;
-  hipLaunchKernelGGL((k_wgrad2<CIN, COUT, HO>), dim3(C::NCO * C::NCI, (unsigned)chunks), dim3(256), 0, st, zx, dY,
-                     B, part);
+  const int ns = wgrad3_ns(B);
+  const long chunks = (B * ns + C::NPC - 1) / C::NPC;
+  auto go = [&](auto nsc) {
+    constexpr int NS = decltype(nsc)::value;
+    hipLaunchKernelGGL((k_wgrad2<CIN, COUT, HO, NS>), dim3(C::NCO * C::NCI, (unsigned)chunks), dim3(256), 0, st, zx,
+                       dY, B, part);
+  };
+  if (ns == 4) go(std::integral_constant<int, 4>{});
+  else if (ns == 2) go(std::integral_constant<int, 2>{});
+  else go(std::integral_constant<int, 1>{});
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   GemmArgs g{nullptr, nullptr, dW, COUT, (long)CIN * 9, 0, 0, 0, 0, 0, (long)CIN * 9, 1, 1.f, 0.f};
@@ -960,7 +1008,7 @@ hipError_t wgrad2(const float* zx, const float* dY, long B, float* dW, float* pa
 
 static long wgrad2_slices(int l, long B) {
   const int npc = l == 2 ? Wg2Cfg<32, 64, 16>::NPC : l == 4 ? Wg2Cfg<64, 128, 8>::NPC : 0;
-  return npc ? 4 * ((B + npc - 1) / npc) : 0;
+  return npc ? 4 * ((B * wgrad3_ns(B) + npc - 1) / npc) : 0;
 }
 
 // implicit-im2col convs of one layer (compile-time geometry): the forward Y = W . col and the
