@@ -126,6 +126,29 @@ struct Wg3Cfg {
   static_assert(NPW >= 1 && NPC % 4 == 0, "chunking");
 };
 
+// The workgroup's one split-K slice of dW: its 4 waves' 9 tap accumulators summed in wave order (w0 + w1 + w2
+// + w3, fp32) through LDS, one tap per round (16 KB), wave w adding and storing accumulator rows 4w .. 4w + 3;
+// k_splitk_sum then adds the slices in fp64.  (One slice per wave made the slice sum 4x longer.)
+template <int CIN, int COUT>
+HN_DEV void wgrad_slice_write(const f32x16 (&acc)[9], float* smem, float* __restrict__ dst, int co0, int ci0) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    __syncthreads();  // (the waves are done with their rings / the previous tap's reads)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) smem[(w * 16 + i) * 64 + lane] = acc[t][i];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int i = 4 * w + k;
+      float v = smem[i * 64 + lane];
+#pragma unroll
+      for (int src = 1; src < 4; ++src) v += smem[(src * 16 + i) * 64 + lane];
+      dst[(long)(co0 + 8 * w + 4 * h + k) * (CIN * 9) + (ci0 + r) * 9 + t] = v;  // i = 4q + e: q = w, e = k
+    }
+  }
+}
+
 // NS: as k_fwd3's row segments -- the chunk's NPC units are (patch, segment of H / NS rows), so a small batch
 // gets NS times the waves (and NS times the split-K slices; each product lands in the same fp64 slice sum)
 template <int CIN, int COUT, int H, int NS = 1>
@@ -133,6 +156,7 @@ __global__ __launch_bounds__(256) void k_wgrad3(const float* __restrict__ zx, co
                                                 float* __restrict__ part) {
   using C = Wg3Cfg<CIN, COUT, H>;
   constexpr int HS = H / NS;
+  static_assert(4 * C::WAVE_F >= 4 * 16 * 64, "the slice reduction's round fits the rings");
   __shared__ float smem[4 * C::WAVE_F];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
   const int blk = blockIdx.x, co0 = (blk / C::NCI) * 32, ci0 = (blk % C::NCI) * 32;
@@ -211,16 +235,8 @@ __global__ __launch_bounds__(256) void k_wgrad3(const float* __restrict__ zx, co
       asm volatile("" ::: "memory");
     }
   }
-  // slice write: acc[t][4q + e] = dW row co0 + 8q + 4h + e, column (ci0 + r) * 9 + t
-  const long slice = chunk * 4 + w;
-  float* dst = part + slice * (long)COUT * CIN * 9;
-#pragma unroll
-  for (int t = 0; t < 9; ++t)
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        dst[(long)(co0 + 8 * q + 4 * h + e) * (CIN * 9) + (ci0 + r) * 9 + t] = acc[t][4 * q + e];
+  // acc[t][4q + e] = dW row co0 + 8q + 4h + e, column (ci0 + r) * 9 + t
+  wgrad_slice_write<CIN, COUT>(acc, smem, part + chunk * (long)COUT * CIN * 9, co0, ci0);
 }
 
 static int wgrad3_ns(long B) { return B >= 2048 ? 1 : B >= 1024 ? 2 : 4; }  // (B x NS waves per layer)
@@ -242,14 +258,14 @@ hipError_t wgrad3(const float* zx, const float* dY, long B, float* dW, float* pa
   if (e != hipSuccess) return e;
   GemmArgs g{nullptr, nullptr, dW, COUT, (long)CIN * 9, 0, 0, 0, 0, 0, (long)CIN * 9, 1, 1.f, 0.f};
   hipLaunchKernelGGL(k_splitk_sum, dim3((unsigned)((g.M * g.N + 63) / 64)), dim3(1024), 0, st, g,
-                     (int)(chunks * 4), part);
+                     (int)chunks, part);
   return hipGetLastError();
 }
 
 // slices k_wgrad3 writes for layer l (0 if it does not take that layer)
 static long wgrad3_slices(int l, long B) {
   const int npc = l == 1 ? Wg3Cfg<32, 32, 32>::NPC : l == 3 ? Wg3Cfg<64, 64, 16>::NPC : l == 5 ? Wg3Cfg<128, 128, 8>::NPC : 0;
-  return npc ? 4 * ((B * wgrad3_ns(B) + npc - 1) / npc) : 0;
+  return npc ? (B * wgrad3_ns(B) + npc - 1) / npc : 0;  // one slice per workgroup chunk
 }
 
 // ------------------------------------------------------------------------------------------
@@ -883,6 +899,7 @@ __global__ __launch_bounds__(256) void k_wgrad2(const float* __restrict__ zx, co
                                                 float* __restrict__ part) {
   using C = Wg2Cfg<CIN, COUT, HO>;
   constexpr int HI = C::HI, HS = HO / NS;  // (output rows per (patch, segment) unit)
+  static_assert(4 * C::WAVE_F >= 4 * 16 * 64, "the slice reduction's round fits the rings");
   __shared__ float smem[4 * C::WAVE_F];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
   const int blk = blockIdx.x, co0 = (blk / C::NCI) * 32, ci0 = (blk % C::NCI) * 32;
@@ -973,15 +990,7 @@ __global__ __launch_bounds__(256) void k_wgrad2(const float* __restrict__ zx, co
       asm volatile("" ::: "memory");
     }
   }
-  const long slice = chunk * 4 + w;
-  float* dst = part + slice * (long)COUT * CIN * 9;
-#pragma unroll
-  for (int t = 0; t < 9; ++t)
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        dst[(long)(co0 + 8 * q + 4 * h + e) * (CIN * 9) + (ci0 + r) * 9 + t] = acc[t][4 * q + e];
+  wgrad_slice_write<CIN, COUT>(acc, smem, part + chunk * (long)COUT * CIN * 9, co0, ci0);
 }
 
 template <int CIN, int COUT, int HO>
@@ -1001,14 +1010,14 @@ hipError_t wgrad2(const float* zx, const float* dY, long B, float* dW, float* pa
   if (e != hipSuccess) return e;
   GemmArgs g{nullptr, nullptr, dW, COUT, (long)CIN * 9, 0, 0, 0, 0, 0, (long)CIN * 9, 1, 1.f, 0.f};
   hipLaunchKernelGGL(k_splitk_sum, dim3((unsigned)((g.M * g.N + 63) / 64)), dim3(1024), 0, st, g,
-                     (int)(chunks * 4), part);
+                     (int)chunks, part);
   return hipGetLastError();
 }
 
 
 static long wgrad2_slices(int l, long B) {
   const int npc = l == 2 ? Wg2Cfg<32, 64, 16>::NPC : l == 4 ? Wg2Cfg<64, 128, 8>::NPC : 0;
-  return npc ? 4 * ((B * wgrad3_ns(B) + npc - 1) / npc) : 0;
+  return npc ? (B * wgrad3_ns(B) + npc - 1) / npc : 0;  // one slice per workgroup chunk
 }
 
 // implicit-im2col convs of one layer (compile-time geometry): the forward Y = W . col and the
