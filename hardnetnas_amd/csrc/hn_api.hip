@@ -45,7 +45,7 @@ void hn_read_knobs(HnKnobs* k) {
   k->front_xch3 = env_int("HN_FRONT_XCH3", 0) != 0;
   k->no_mpfront = env_int("HN_NO_MPFRONT", 0) != 0;
   k->train_splitk = std::max(32, env_int("HN_TRAIN_SPLITK", 1024)) / 32 * 32;
-  k->train_f32 = env_int("HN_TRAIN_F32", 1) & 255;
+  k->train_f32 = env_int("HN_TRAIN_F32", 17) & 255;
 #ifdef HN_EXPERIMENTS
   k->c12_abl = env_int("HN_C12_ABL", 0) & 4095;  // (65: k_c12s stamps with P1 on the A-waves)
   k->c12w_pd = env_int("HN_C12W_PD", 11);

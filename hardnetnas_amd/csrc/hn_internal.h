@@ -27,8 +27,9 @@ struct HnKnobs {
                                // workgroups per CU instead of three: wang2 front 5.05 -> 5.57 ms, not the default)
   bool no_mpfront = false;     // HN_NO_MPFRONT: k_front (max-pool) + k_irf instead of k_mpfront_irf
   int train_splitk = 1024;     // HN_TRAIN_SPLITK: K per split-K slice of the train GEMMs
-  int train_f32 = 1;           // HN_TRAIN_F32: bit 0 train forward convs, bit 1 stride-1 dgrads as f32-MFMA
-                               // GEMMs (else the bf16x3 conv kernels); default 1 = every product f32;
+  int train_f32 = 17;          // HN_TRAIN_F32: bit 0 train forward convs, bit 1 stride-1 dgrads as f32-MFMA
+                               // GEMMs (else the bf16x3 conv kernels); 1 = every product f32; default 17 =
+                               // f32 forwards, the stride-1 dgrads on the bf16x3 conv kernels;
                                // bit 2: stride-1 weight gradients as the generic GEMM (else k_wgrad3);
                                // bit 3: stride-1 f32 forwards as the generic GEMM (else k_fwd3);
                                // bit 4: stride-1 dgrads not as k_fwd3 over dY (then bit 1 decides);

@@ -240,13 +240,13 @@ for b in (256, 37):
 """
 
 
-@pytest.mark.parametrize("knobs", ["129", "127", "17"])
+@pytest.mark.parametrize("knobs", ["145", "127", "1"])
 def test_train_kernel_alternatives(knobs, cuda_device):
     """The HN_TRAIN_F32 alternatives (read once per process, so each runs in a child process):
-    129 = the default kernels with the one-ring / shared-ring forms swapped; 127 = the generic
+    145 = the default kernels with the one-ring / shared-ring forms swapped; 127 = the generic
     implicit-GEMM forwards, weight gradients and data gradients (stride-1 col2im gather, stride-2
-    and conv0 through the column GEMM); 17 = the stride-1 data gradients on the bf16x3 eval conv
-    kernels.  Smooth-objective gradients at 256 and 37 patches against fp64, the same bar."""
+    and conv0 through the column GEMM); 1 = every product on f32 MFMA (the stride-1 data gradients
+    as f32 GEMMs; the default 17 runs them on the bf16x3 eval conv kernels).  Smooth-objective gradients at 256 and 37 patches against fp64, the same bar."""
     import os
     import subprocess
     import sys
