@@ -820,6 +820,115 @@ def run_train(opts, dev, with_cpu: bool):
     return res
 
 
+SUPERNET_PAIRS = 128  # the supernet search's batch_size (hardnetNAS/supernet_functions/config_for_supernet.py:17)
+
+
+def _supernet_step(m, opt, crit, xa, xp, lat_dev):
+    """training_functions_supernet.py:93-104, one step of _training_step: outs_X with grad, outs_Y under no_grad
+    (latency accumulated through both), SupernetLoss (target latency 15, config_for_supernet.py:42), backward,
+    the optimizer's step; temperature 5.0 (the initial one, :39)."""
+    opt.zero_grad()
+    lat0 = torch.zeros(1, 1, device=lat_dev, requires_grad=True)
+    ox, lacc, soft, _ = m(xa, 5.0, lat0)
+    with torch.no_grad():
+        oy, _, _, _ = m(xp, 5.0, lacc)
+    loss = crit(ox, oy, lacc, soft, 15.0)[0]
+    loss.backward()
+    opt.step()
+    return loss
+
+
+def _supernet_setup(dev, pairs):
+    from hardnetnas_amd.losses import SupernetLoss
+    from hardnetnas_amd.model import HardNetNASSupernet
+    torch.manual_seed(0)
+    m = HardNetNASSupernet().to(dev).train()
+    # the w_optimizer: SGD over the weights (not the thetas), lr 0.01, momentum 0.9, wd 1e-4 (config :22-24)
+    opt = torch.optim.SGD([p for n, p in m.named_parameters() if not n.endswith("thetas")], lr=0.01,
+                          momentum=0.9, weight_decay=1e-4)
+    xa = torch.from_numpy(synth.synth_patches(pairs, seed=61)).to(dev)
+    xp = xa + 0.3 * torch.from_numpy(synth.synth_patches(pairs, seed=62)).to(dev)
+    return m, opt, SupernetLoss(), xa, xp
+
+
+def supernet_flop_per_patch() -> int:
+    """Forward FLOP (2 x MAC) of one patch through the supernet (every candidate op of every searched layer is
+    evaluated and mixed, model_supernet.py:40-50), counted by torch's FlopCounterMode on the module's torch layers
+    on the CPU at a batch of 2."""
+    from torch.utils.flop_counter import FlopCounterMode
+    from hardnetnas_amd.model import HardNetNASSupernet
+    m = HardNetNASSupernet().eval()
+    x = torch.from_numpy(synth.synth_patches(2, seed=63))
+    with torch.no_grad(), FlopCounterMode(display=False) as fc:
+        m(x, 5.0, torch.zeros(1, 1))
+    return int(fc.get_total_flops()) // 2
+
+
+def cpu_baseline_supernet(seconds: float = 8.0, pairs: int = SUPERNET_PAIRS):
+    """The same supernet search step on the host cores (the cgroup quota's thread count): the module's torch
+    layers (the reference's FBNet_Stochastic_SuperNet structure, model_supernet.py:53-85) in fp32 on the CPU,
+    at the GPU leg's batch; patches/s = 2 x pairs / step time (median)."""
+    quota = _cpu_quota()
+    nproc = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    threads = max(1, int(quota)) if 0 < quota < nproc else nproc
+    torch.set_num_threads(threads)
+    m, opt, crit, xa, xp = _supernet_setup(torch.device("cpu"), pairs)
+    _supernet_step(m, opt, crit, xa, xp, "cpu")
+    rates, t_start = [], time.perf_counter()
+    while time.perf_counter() - t_start < seconds or len(rates) < 3:
+        t0 = time.perf_counter()
+        _supernet_step(m, opt, crit, xa, xp, "cpu")
+        rates.append(2 * pairs / (time.perf_counter() - t0))
+    return {"value": round(statistics.median(rates), 1), "unit": "patches/s", "cores": threads, "kind": "port",
+            "model": _cpu_model_string(),
+            "sample": f"hardnetnas_amd.HardNetNASSupernet torch layers (fp32, CPU) supernet search step at {pairs} "
+                      f"pairs (outs_X + no_grad outs_Y + SupernetLoss + backward + SGD), {len(rates)} steps over "
+                      f"~{seconds:.0f} s, median"}
+
+
+def run_train_supernet(opts, dev, with_cpu: bool):
+    """The supernet search step (hardnetNAS/supernet_functions/training_functions_supernet.py:87-104) on the HIP
+    NAS train path (NasTrainFunction: the supernet's mixed layers, backward to the weights and the thetas) at the
+    reference's batch_size of 128 pairs, with the w_optimizer's SGD."""
+    m, opt, crit, xa, xp = _supernet_setup(dev, SUPERNET_PAIRS)
+    steps, warmup = max(10, opts.steps), max(2, opts.warmup)
+    for _ in range(warmup):
+        loss = _supernet_step(m, opt, crit, xa, xp, dev)
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    t0 = time.perf_counter()
+    ev[0].record()
+    for _ in range(steps):
+        loss = _supernet_step(m, opt, crit, xa, xp, dev)
+    ev[1].record()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    b = SUPERNET_PAIRS
+    # algorithmic work per step: outs_X forward + its data and weight gradients (3 x F) + outs_Y forward (F)
+    flop = 4 * supernet_flop_per_patch() * b
+    achieved = flop / (ev[0].elapsed_time(ev[1]) / steps * 1e-3) / 1e12
+    res = {"value": round(2 * b * steps / elapsed / 1e6, 4), "unit": "Mpatches/s",
+           "ms_per_step": round(elapsed / steps * 1e3, 3), "steps": steps, "warmup": warmup, "dtype": "f32",
+           "config": {"workload": f"hardnetNAS supernet search step (training_functions_supernet.py:93-104): "
+                                  f"outs_X = model(X) with grad, outs_Y under no_grad, SupernetLoss (target "
+                                  f"latency 15, temperature 5), backward, SGD on the weights; 2 x {b} patches, "
+                                  "synthetic pairs",
+                      "model": "hardnetnas_supernet", "global_batch": 2 * b, "pairs": b, "parallelism": "dp1"},
+           "loss": float(loss.item()),
+           "roofline": {"bound": "latency", "kernel": "whole supernet step (every candidate op, backward, loss, SGD)",
+                        "achieved": round(achieved, 3), "peak": PEAK_F32, "unit": "TFLOP/s",
+                        "frac": round(achieved / PEAK_F32, 4), "traffic": None,
+                        "peak_basis": "f32 MFMA 157.3 TFLOP/s; algorithmic FLOP = 4 x the supernet forward's "
+                                      "2 x MAC per patch (FlopCounterMode) x 128 pairs"},
+           "cpu_baseline": None}
+    if with_cpu:
+        cb = cpu_baseline_supernet()
+        res["cpu_baseline"] = cb
+        res["gpu_vs_cpu"] = round(res["value"] * 1e6 / cb["value"], 1)
+    del m, opt, xa, xp
+    return res
+
+
 EVAL_BATCH = 512  # the reference eval loop's --test-batch-size (hardnet/HardNet.py:100)
 
 
@@ -1008,6 +1117,8 @@ def main():
             result["extra_configs"][key] = {k: r[k] for k in EXTRA_KEYS if k in r}
         torch.cuda.empty_cache()
         result["extra_configs"]["train"] = run_train(args, dev, with_cpu=not args.no_cpu_baseline)
+        torch.cuda.empty_cache()
+        result["extra_configs"]["train_supernet"] = run_train_supernet(args, dev, with_cpu=not args.no_cpu_baseline)
         torch.cuda.empty_cache()
         result["extra_configs"]["eval512"] = run_eval512(args, dev, with_cpu=not args.no_cpu_baseline)
     if rank == 0:

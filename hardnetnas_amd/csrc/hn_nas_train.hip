@@ -30,13 +30,37 @@ constexpr int NOPS = 17;  // CANDIDATE_BLOCKS
 // ------------------------------------------------------------------------------------------
 // kernels
 // ------------------------------------------------------------------------------------------
-// BatchNorm apply: y (conv output, in place) -> z = (y - mean) * rstd; a = act(gamma z + beta) [+ res]
-__global__ __launch_bounds__(256) void k_bna_apply(float* __restrict__ y, long L, const float* __restrict__ mean,
-                                                   const float* __restrict__ rstd, const float* __restrict__ gamma,
-                                                   const float* __restrict__ beta, int relu,
-                                                   const float* __restrict__ res, float* __restrict__ a) {
+// BatchNorm apply: y (conv output, in place) -> z = (y - mean) * rstd; a = act(gamma z + beta) [+ res].
+// The channel's statistics come from k_bn_part's slice sums, combined by thread 0 of every workgroup in
+// k_bn_final's order and arithmetic (so mean / rstd are k_bn_final's values); workgroup (c, 0) also
+// writes rstd and the running statistics -- one launch fewer per BatchNorm than part / final / apply
+__global__ __launch_bounds__(256) void k_bna_apply(float* __restrict__ y, long L, const double* __restrict__ part,
+                                                   int NS, float eps, float mom, float* __restrict__ rmean,
+                                                   float* __restrict__ rvar, float* __restrict__ rstd_out,
+                                                   const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                   int relu, const float* __restrict__ res, float* __restrict__ a) {
+  __shared__ float st[2];
   const int c = blockIdx.x;
-  const float mu = mean[c], rs = rstd[c], g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
+  if (threadIdx.x == 0) {
+    double s1 = 0.0, s2 = 0.0;
+    for (int sl = 0; sl < NS; ++sl) {
+      s1 += part[((long)c * NS + sl) * 2];
+      s2 += part[((long)c * NS + sl) * 2 + 1];
+    }
+    const double mean = s1 / (double)L;
+    const double var = fmax(s2 / (double)L - mean * mean, 0.0);
+    st[0] = (float)mean;
+    st[1] = (float)(1.0 / sqrt(var + (double)eps));
+    if (blockIdx.y == 0) {
+      rstd_out[c] = st[1];
+      if (rmean) {
+        rmean[c] = (1.f - mom) * rmean[c] + mom * (float)mean;
+        rvar[c] = (1.f - mom) * rvar[c] + mom * (float)(L > 1 ? var * (double)L / (double)(L - 1) : var);
+      }
+    }
+  }
+  __syncthreads();
+  const float mu = st[0], rs = st[1], g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
   const long base = (long)c * L, step = (long)gridDim.y * 256;
   for (long i = (long)blockIdx.y * 256 + threadIdx.x; i < L; i += step) {
     const float z = (y[base + i] - mu) * rs;
@@ -74,31 +98,32 @@ __global__ __launch_bounds__(256) void k_bna_bwd_part(const float* __restrict__ 
   }
 }
 
-// per channel: d beta = sum g, d gamma = sum g z; m1 = gamma mean(g), m2 = gamma mean(g z)
-__global__ __launch_bounds__(256) void k_bna_bwd_final(const double* __restrict__ part, int C, int NS, long L,
-                                                       const float* __restrict__ gamma, float* __restrict__ dgamma,
-                                                       float* __restrict__ dbeta, float* __restrict__ m12) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= C) return;
-  double s1 = 0.0, s2 = 0.0;
-  for (int sl = 0; sl < NS; ++sl) {
-    s1 += part[((long)c * NS + sl) * 2];
-    s2 += part[((long)c * NS + sl) * 2 + 1];
-  }
-  if (dgamma) dgamma[c] = (float)s2;
-  if (dbeta) dbeta[c] = (float)s1;
-  const double gm = gamma ? (double)gamma[c] : 1.0;
-  m12[2 * c] = (float)(gm * s1 / (double)L);
-  m12[2 * c + 1] = (float)(gm * s2 / (double)L);
-}
-
-// dy = rstd * (gamma g - m1 - z m2); dy may alias da
+// dy = rstd * (gamma g - m1 - z m2); dy may alias da.  m1 / m2 from k_bna_bwd_part's slice sums, combined
+// by thread 0 of every workgroup in k_bna_bwd_final's order; workgroup (c, 0) writes d gamma / d beta
 __global__ __launch_bounds__(256) void k_bna_bwd_apply(const float* da, const float* __restrict__ z, long L,
-                                                       const float* __restrict__ m12, const float* __restrict__ rstd,
+                                                       const double* __restrict__ part, int NS,
+                                                       float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                       const float* __restrict__ rstd,
                                                        const float* __restrict__ gamma, const float* __restrict__ beta,
                                                        int relu, float* dy) {
+  __shared__ float st[2];
   const int c = blockIdx.x;
-  const float m1 = m12[2 * c], m2 = m12[2 * c + 1], rs = rstd[c];
+  if (threadIdx.x == 0) {
+    double s1 = 0.0, s2 = 0.0;
+    for (int sl = 0; sl < NS; ++sl) {
+      s1 += part[((long)c * NS + sl) * 2];
+      s2 += part[((long)c * NS + sl) * 2 + 1];
+    }
+    if (blockIdx.y == 0) {
+      if (dgamma) dgamma[c] = (float)s2;
+      if (dbeta) dbeta[c] = (float)s1;
+    }
+    const double g0 = gamma ? (double)gamma[c] : 1.0;
+    st[0] = (float)(g0 * s1 / (double)L);
+    st[1] = (float)(g0 * s2 / (double)L);
+  }
+  __syncthreads();
+  const float m1 = st[0], m2 = st[1], rs = rstd[c];
   const float gm = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
   const long base = (long)c * L, step = (long)gridDim.y * 256;
   for (long i = (long)blockIdx.y * 256 + threadIdx.x; i < L; i += step) {
@@ -318,11 +343,12 @@ __global__ __launch_bounds__(256) void k_dot_part(const float* __restrict__ a, c
   block_sum2(s, z, sh);
   if (threadIdx.x == 0) part[blockIdx.x] = s;
 }
-__global__ void k_dot_final(const double* __restrict__ part, int n, float* __restrict__ out) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+// one wave: lane l sums partials l, l + 64, ... in order, then a fixed butterfly over the 64 lanes
+__global__ __launch_bounds__(64) void k_dot_final(const double* __restrict__ part, int n, float* __restrict__ out) {
   double s = 0.0;
-  for (int i = 0; i < n; ++i) s += part[i];
-  out[0] = (float)s;
+  for (int i = threadIdx.x; i < n; i += 64) s += part[i];
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if (threadIdx.x == 0) out[0] = (float)s;
 }
 
 // SEModule (fbnet_builder.py:407-421): out = x * sigmoid(W2 relu(W1 avgpool(x) + b1) + b2)
@@ -465,7 +491,7 @@ struct Plan {
   size_t saved = 0;
   // scratch
   size_t maxact = 0;  // floats
-  size_t g0 = 0, g1 = 0, t0 = 0, t1 = 0, t2 = 0, part = 0, bnpart = 0, dwpart = 0, m12 = 0, mean = 0,
+  size_t g0 = 0, g1 = 0, t0 = 0, t1 = 0, t2 = 0, part = 0, bnpart = 0, dwpart = 0,
          se0 = 0, se1 = 0, se2 = 0, hcol = 0, dotpart = 0, scratch = 0;
   size_t part_floats = 0;
 };
@@ -631,8 +657,6 @@ Plan make_plan(const hn_arch_desc& d, long B) {
   P.part = take(part * 4);
   P.bnpart = take((size_t)512 * kBnSlices * 2 * sizeof(double));
   P.dwpart = take((size_t)512 * kBnSlices * 25 * sizeof(double));
-  P.m12 = take((size_t)2 * 512 * sizeof(float));
-  P.mean = take((size_t)512 * sizeof(float));
   P.se0 = take((size_t)512 * B * sizeof(float));
   P.se1 = take((size_t)512 * B * sizeof(float));
   P.se2 = take((size_t)512 * B * sizeof(float));
@@ -662,13 +686,10 @@ hipError_t bn_fwd(const Ctx& c, float* y, int C, long L, int bnt, bool affine, b
                   float* rstd) {
   const int NS = bn_slices(C, L);
   double* part = reinterpret_cast<double*>(c.sc + c.P.bnpart);
-  float* mean = c.s(c.P.mean);
   hipLaunchKernelGGL(k_bn_part, dim3(C, NS), dim3(256), 0, c.st, y, L, NS, part);
   float* rm = c.T[affine ? bnt + 2 : bnt];
   float* rv = c.T[affine ? bnt + 3 : bnt + 1];
-  hipLaunchKernelGGL(k_bn_final, dim3((C + 255) / 256), dim3(256), 0, c.st, part, C, NS, L, 1e-5f, c.mom, rm, rv,
-                     mean, rstd);
-  hipLaunchKernelGGL(k_bna_apply, bn_row_grid(C, L), dim3(256), 0, c.st, y, L, mean, rstd,
+  hipLaunchKernelGGL(k_bna_apply, bn_row_grid(C, L), dim3(256), 0, c.st, y, L, part, NS, 1e-5f, c.mom, rm, rv, rstd,
                      affine ? c.T[bnt] : nullptr, affine ? c.T[bnt + 1] : nullptr, relu ? 1 : 0, res, a);
   return hipGetLastError();
 }
@@ -678,14 +699,11 @@ hipError_t bn_bwd(const Ctx& c, const float* da, const float* z, const float* rs
                   bool relu, float* dy) {
   const int NS = bn_slices(C, L);
   double* part = reinterpret_cast<double*>(c.sc + c.P.bnpart);
-  float* m12 = c.s(c.P.m12);
   const float* gm = affine ? c.T[bnt] : nullptr;
   const float* bt = affine ? c.T[bnt + 1] : nullptr;
   hipLaunchKernelGGL(k_bna_bwd_part, dim3(C, NS), dim3(256), 0, c.st, da, z, L, NS, gm, bt, relu ? 1 : 0, part);
-  hipLaunchKernelGGL(k_bna_bwd_final, dim3((C + 255) / 256), dim3(256), 0, c.st, part, C, NS, L, gm,
-                     affine ? c.G[bnt] : nullptr, affine ? c.G[bnt + 1] : nullptr, m12);
-  hipLaunchKernelGGL(k_bna_bwd_apply, bn_row_grid(C, L), dim3(256), 0, c.st, da, z, L, m12, rstd, gm, bt,
-                     relu ? 1 : 0, dy);
+  hipLaunchKernelGGL(k_bna_bwd_apply, bn_row_grid(C, L), dim3(256), 0, c.st, da, z, L, part, NS,
+                     affine ? c.G[bnt] : nullptr, affine ? c.G[bnt + 1] : nullptr, rstd, gm, bt, relu ? 1 : 0, dy);
   return hipGetLastError();
 }
 

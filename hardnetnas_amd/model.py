@@ -471,8 +471,8 @@ def _nas_train_native_forward(module: nn.Module, x: torch.Tensor, soft):
     _, tensors = N.train_tensors(module)
     params = [t for t in tensors if t.requires_grad]
     y = N.NasTrainFunction.apply(x.contiguous(), soft, desc, tensors, bns[0].momentum, *params)
-    for b in bns:
-        b.num_batches_tracked.add_(1)
+    # one multi-tensor launch for every BatchNorm's counter (the supernet has 584)
+    torch._foreach_add_([b.num_batches_tracked for b in bns], 1)
     return y
 
 

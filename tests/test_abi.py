@@ -257,3 +257,18 @@ def test_train_rejects_fdl_without_input_norm():
     n = ctypes.c_size_t()
     assert N.load_library().hn_nas_train_tensor_count(ctypes.byref(d), ctypes.byref(n)) == 1
     assert b"input_norm" in N.load_library().hn_last_error()
+
+
+def test_bench_supernet_train_leg_flop_count():
+    """bench.py's train_supernet leg prices its roofline with FlopCounterMode over the supernet's torch layers:
+    that count equals the analytic per-patch MACs of the stem, all 17 candidate ops of all six searched
+    layers (arch.layer_macs) and the 4x4 head, x 2 (within the SE modules' pooling / bias terms)."""
+    import bench
+    from hardnetnas_amd import arch as A
+    hw, macs = 32, A.STEM_CHANNELS * 9 * 32 * 32
+    for ci, co, s in A.SEARCH_SPACE2:
+        macs += sum(A.layer_macs(ci, co, s, op, hw) for op in A.CANDIDATE_BLOCKS)
+        hw //= s
+    macs += A.SEARCH_SPACE2[-1][1] * A.DESC_DIM * A.HEAD_KERNEL ** 2
+    assert abs(bench.supernet_flop_per_patch() / (2 * macs) - 1) < 1e-4
+    assert bench.SUPERNET_PAIRS == 128
