@@ -1224,12 +1224,10 @@ hipError_t hn_train_forward(const float* in, long B, const float* const* W, floa
     {
       const int NS = bn_slices(S.cout, B * hw);
       double* part = reinterpret_cast<double*>(sc + L.bnpart);
-      float* mean = reinterpret_cast<float*>(sc + L.bnmean);
       float* rstd = reinterpret_cast<float*>(sv + L.rstd[l]);
       hipLaunchKernelGGL(k_bn_part, dim3(S.cout, NS), dim3(256), 0, st, z, B * hw, NS, part);
-      hipLaunchKernelGGL(k_bn_final, dim3((S.cout + 255) / 256), dim3(256), 0, st, part, S.cout, NS, B * hw, bn_eps,
-                         mom, rmean ? rmean[l] : nullptr, rvar ? rvar[l] : nullptr, mean, rstd);
-      hipLaunchKernelGGL(k_bn_apply, bn_row_grid(S.cout, B * hw), dim3(256), 0, st, z, B * hw, mean, rstd);
+      hipLaunchKernelGGL(k_bn_apply, bn_row_grid(S.cout, B * hw), dim3(256), 0, st, z, B * hw, part, NS, bn_eps, mom,
+                         rmean ? rmean[l] : nullptr, rvar ? rvar[l] : nullptr, rstd);
       HCK(hipGetLastError());
     }
   }
@@ -1256,12 +1254,10 @@ hipError_t hn_train_backward(const float* dout, long B, const float* const* W, f
     {
       const int NS = bn_slices(S.cout, B * hw);
       double* part = reinterpret_cast<double*>(sc + L.bnpart);
-      float* m12 = reinterpret_cast<float*>(sc + L.bnmean);
       const float* zl = reinterpret_cast<const float*>(sv + L.z[l]);
       hipLaunchKernelGGL(k_bn_bwd_part, dim3(S.cout, NS), dim3(256), 0, st, g, zl, B * hw, NS, l < 6 ? 1 : 0,
                          l == 5 ? drop_p : 0.f, seed, part);
-      hipLaunchKernelGGL(k_bn_bwd_final, dim3((S.cout + 255) / 256), dim3(256), 0, st, part, S.cout, NS, B * hw, m12);
-      hipLaunchKernelGGL(k_bn_bwd_apply, bn_row_grid(S.cout, B * hw), dim3(256), 0, st, g, zl, B * hw, m12,
+      hipLaunchKernelGGL(k_bn_bwd_apply, bn_row_grid(S.cout, B * hw), dim3(256), 0, st, g, zl, B * hw, part, NS,
                          reinterpret_cast<const float*>(sv + L.rstd[l]), l < 6 ? 1 : 0, l == 5 ? drop_p : 0.f, seed);
       HCK(hipGetLastError());
     }

@@ -334,12 +334,11 @@ __global__ __launch_bounds__(256) void k_bn_part(const float* __restrict__ y, lo
   }
 }
 
-// one thread per channel: mean, 1/sqrt(var + eps), running statistics (var unbiased)
-__global__ __launch_bounds__(256) void k_bn_final(const double* __restrict__ part, int C, int NS, long L, float eps,
-                                                  float mom, float* __restrict__ rmean, float* __restrict__ rvar,
-                                                  float* __restrict__ mean_out, float* __restrict__ rstd_out) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= C) return;
+// the channel's batch statistics from k_bn_part's slice sums (fixed slice order): mean, 1/sqrt(var + eps);
+// with `upd`, rstd saved and the running statistics updated (var unbiased)
+HN_DEV void bn_stats(const double* __restrict__ part, int c, int NS, long L, float eps, float mom, bool upd,
+                     float* __restrict__ rmean, float* __restrict__ rvar, float* __restrict__ rstd_out, float& mu,
+                     float& rs) {
   double s1 = 0.0, s2 = 0.0;
   for (int sl = 0; sl < NS; ++sl) {
     s1 += part[((long)c * NS + sl) * 2];
@@ -347,20 +346,29 @@ __global__ __launch_bounds__(256) void k_bn_final(const double* __restrict__ par
   }
   const double mean = s1 / (double)L;
   const double var = fmax(s2 / (double)L - mean * mean, 0.0);
-  mean_out[c] = (float)mean;
-  rstd_out[c] = (float)(1.0 / sqrt(var + (double)eps));
-  if (rmean) {
-    rmean[c] = (1.f - mom) * rmean[c] + mom * (float)mean;
-    rvar[c] = (1.f - mom) * rvar[c] + mom * (float)(L > 1 ? var * (double)L / (double)(L - 1) : var);
+  mu = (float)mean;
+  rs = (float)(1.0 / sqrt(var + (double)eps));
+  if (upd) {
+    rstd_out[c] = rs;
+    if (rmean) {
+      rmean[c] = (1.f - mom) * rmean[c] + mom * (float)mean;
+      rvar[c] = (1.f - mom) * rvar[c] + mom * (float)(L > 1 ? var * (double)L / (double)(L - 1) : var);
+    }
   }
 }
 
 // y (in place) -> z = (y - mean) * rstd over [C][L]; grid (C, S): workgroup (c, s) walks row c
-// (no per-element channel division), float4 when rows are 16-byte aligned
-__global__ __launch_bounds__(256) void k_bn_apply(float* __restrict__ y, long L, const float* __restrict__ mean,
-                                                  const float* __restrict__ rstd) {
+// (no per-element channel division), float4 when rows are 16-byte aligned.  Thread 0 of every workgroup
+// combines the channel's slice sums (bn_stats); workgroup (c, 0) also saves rstd and updates the running
+// statistics -- no separate statistics launch between k_bn_part and this one
+__global__ __launch_bounds__(256) void k_bn_apply(float* __restrict__ y, long L, const double* __restrict__ part,
+                                                  int NS, float eps, float mom, float* __restrict__ rmean,
+                                                  float* __restrict__ rvar, float* __restrict__ rstd_out) {
+  __shared__ float st[2];
   const int c = blockIdx.x;
-  const float mu = mean[c], rs = rstd[c];
+  if (threadIdx.x == 0) bn_stats(part, c, NS, L, eps, mom, blockIdx.y == 0, rmean, rvar, rstd_out, st[0], st[1]);
+  __syncthreads();
+  const float mu = st[0], rs = st[1];
   float* row = y + (long)c * L;
   const long step = (long)gridDim.y * 256;
   if ((L & 3) == 0) {
@@ -419,27 +427,26 @@ __global__ __launch_bounds__(256) void k_bn_bwd_part(const float* __restrict__ d
   }
 }
 
-// one thread per channel: m1 = mean(g), m2 = mean(g z)
-__global__ __launch_bounds__(256) void k_bn_bwd_final(const double* __restrict__ part, int C, int NS, long L,
-                                                      float* __restrict__ m12) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= C) return;
-  double s1 = 0.0, s2 = 0.0;
-  for (int sl = 0; sl < NS; ++sl) {
-    s1 += part[((long)c * NS + sl) * 2];
-    s2 += part[((long)c * NS + sl) * 2 + 1];
-  }
-  m12[2 * c] = (float)(s1 / (double)L);
-  m12[2 * c + 1] = (float)(s2 / (double)L);
-}
-
-// dy = rstd * (g - m1 - z m2) with g = da * relu'(z) [* mask] as in k_bn_bwd_part, in place;
-// grid (C, S) as k_bn_apply
+// dy = rstd * (g - m1 - z m2) with g = da * relu'(z) [* mask] as in k_bn_bwd_part, in place; grid (C, S)
+// as k_bn_apply; m1 = mean(g), m2 = mean(g z) combined from k_bn_bwd_part's slice sums by thread 0 of
+// every workgroup (fixed slice order)
 __global__ __launch_bounds__(256) void k_bn_bwd_apply(float* __restrict__ g, const float* __restrict__ z, long L,
-                                                      const float* __restrict__ m12, const float* __restrict__ rstd,
-                                                      int relu, float drop_p, unsigned long long seed) {
+                                                      const double* __restrict__ part, int NS,
+                                                      const float* __restrict__ rstd, int relu, float drop_p,
+                                                      unsigned long long seed) {
+  __shared__ float st[2];
   const int c = blockIdx.x;
-  const float m1 = m12[2 * c], m2 = m12[2 * c + 1], rs = rstd[c];
+  if (threadIdx.x == 0) {
+    double s1 = 0.0, s2 = 0.0;
+    for (int sl = 0; sl < NS; ++sl) {
+      s1 += part[((long)c * NS + sl) * 2];
+      s2 += part[((long)c * NS + sl) * 2 + 1];
+    }
+    st[0] = (float)(s1 / (double)L);
+    st[1] = (float)(s2 / (double)L);
+  }
+  __syncthreads();
+  const float m1 = st[0], m2 = st[1], rs = rstd[c];
   const long base = (long)c * L, step = (long)gridDim.y * 256;
   auto one = [&](float v, float zv, long i) {
     if (relu && zv <= 0.f) v = 0.f;
