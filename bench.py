@@ -87,6 +87,25 @@ def irf2_pairs(ops) -> set:
     return out
 
 
+def irf3_triples(ops) -> set:
+    """First layers i of the k_irf2 pairs that hn_api.hip::forward_nas extends to k_irf3: the 8x8 64-channel pair
+    (i, i + 1), B without SE, then layer i + 2 a 4x4 stride-1 128 -> 128 block of mid 128 (e1 / s2 ops) without SE,
+    kernels 3 / 5 -- only with HN_IRF3=1 on the experiments library (HN_LIB; measured slower)."""
+    if os.environ.get("HN_IRF3", "0") in ("", "0") or "abl" not in os.environ.get("HN_LIB", ""):
+        return set()
+    ops = A.arch_ops(ops)
+    out = set()
+    for i in irf2_pairs(ops):
+        if i + 2 >= len(ops) or A.SEARCH_SPACE2[i][0] != 64:
+            continue
+        b, c = A.OP_SPECS[ops[i + 1]], A.OP_SPECS[ops[i + 2]]
+        ci, co, s = A.SEARCH_SPACE2[i + 2]
+        if (not b.se and c.kind != "skip" and not c.se and s == 1 and ci == co == 128
+                and A.ir_mid(ci, c.expansion) == 128 and c.kernel in (3, 5)):
+            out.add(i)
+    return out
+
+
 def mpfront_irf(ops) -> bool:
     """True when hn_api.hip::forward_nas runs the max-pool front (layer 0 "skip" at stride 2), the identity layer 1
     and the 16x16 stride-2 32 -> 64 layer-2 block (no SE, mid 32 / 96 / 128) as one k_mpfront_irf, unless
@@ -131,8 +150,10 @@ def nas_stage_bytes(ops) -> dict:
     front = os.environ.get("HN_NO_FRONT", "0") in ("", "0")
     irf = os.environ.get("HN_NO_IRF", "0") in ("", "0")
     out = {"stem": 0 if front else 4096 + 32 * 32 * 32 * 4, "front": 0, "irf": 0, "irf2": 0, "skip": 0, "pw": 0,
-           "dw": 0, "pwl": 0, "maxpool": 0, "se": 0, "head": 0, "irf+skip": 0, "front+irf": 0}
+           "dw": 0, "pwl": 0, "maxpool": 0, "se": 0, "head": 0, "irf+skip": 0, "front+irf": 0, "irf3": 0}
     pairs = irf2_pairs(ops)
+    triples = irf3_triples(ops)
+    in3 = {j for i in triples for j in (i, i + 1, i + 2)}
     fused_skip = irf_skip_layers(ops)
     skipped = {n for n in fused_skip.values()}
     mpf = mpfront_irf(ops)
@@ -149,6 +170,10 @@ def nas_stage_bytes(ops) -> dict:
             hw = ho
             continue
         if i in skipped:
+            hw = ho
+            continue
+        if i in in3:  # k_irf3: the pair's input in, layer i + 2's 4x4x128 output out
+            out["irf3"] += 4 * ci * hw * hw + 4 * 128 * 4 * 4 if i in triples else 0
             hw = ho
             continue
         if i in pairs:  # k_irf2: this block's input in, the next block's output out
@@ -348,9 +373,10 @@ def nas_stage_flop(name: str) -> dict:
             hw //= st
         return {"front": 2 * front, "irf": 2 * irf, "head": 2 * 128 * 128 * 16}
     ops = A.arch_ops(name)
-    out = {"front": 0, "irf": 0, "irf2": 0, "skip": 0, "irf+skip": 0, "front+irf": 0,
+    out = {"front": 0, "irf": 0, "irf2": 0, "skip": 0, "irf+skip": 0, "front+irf": 0, "irf3": 0,
            "head": 2 * A.SEARCH_SPACE2[-1][1] * 128 * 16}
     pairs = irf2_pairs(ops)
+    in3 = {j for i in irf3_triples(ops) for j in (i, i + 1, i + 2)}
     fused_skip = irf_skip_layers(ops)
     skipped = set(fused_skip.values())
     mpf = mpfront_irf(ops)
@@ -361,6 +387,8 @@ def nas_stage_flop(name: str) -> dict:
             out["front+irf"] += 2 * (macs + (9 * 32 * 32 * 32 if i == 0 else 0))
         elif i in fused_skip or i in skipped:
             out["irf+skip"] += 2 * macs
+        elif i in in3:
+            out["irf3"] += 2 * macs
         elif i in pairs or i - 1 in pairs:
             out["irf2"] += 2 * macs
         elif i == 0:

@@ -44,12 +44,14 @@ void hn_read_knobs(HnKnobs* k) {
   k->u8_apart = env_int("HN_U8_APART", 0) != 0;
   k->front_xch3 = env_int("HN_FRONT_XCH3", 0) != 0;
   k->no_mpfront = env_int("HN_NO_MPFRONT", 0) != 0;
+
   k->train_splitk = std::max(32, env_int("HN_TRAIN_SPLITK", 1024)) / 32 * 32;
   k->train_f32 = env_int("HN_TRAIN_F32", 17) & 255;
 #ifdef HN_EXPERIMENTS
   k->c12_abl = env_int("HN_C12_ABL", 0) & 4095;  // (65: k_c12s stamps with P1 on the A-waves)
   k->c12w_pd = env_int("HN_C12W_PD", 11);
   k->dbg = env_int("HN_DEBUG", 0);
+  k->irf3 = env_int("HN_IRF3", 0) != 0;
 #endif
 }
 
@@ -1121,6 +1123,21 @@ static int forward_nas(hn_model* m, const float* in, int P, int pmax, float* out
                            reinterpret_cast<const uint4*>(L.irf_pwl_a), L.pwl_b};
         const HnIrfArgs ib{nullptr, y, reinterpret_cast<const uint4*>(N.irf_pw_a), N.irf_pw_b, N.dw_w, N.dw_b,
                            reinterpret_cast<const uint4*>(N.irf_pwl_a), N.pwl_b};
+#ifdef HN_EXPERIMENTS
+        if (li + 2 < m->layers.size() && !N.se && m->knobs.irf3) {
+          // and the 4x4 128 -> 128 stride-1 block after the pair (k_irf3): B's output tile stays in LDS for it
+          const NasLayer& C = m->layers[li + 2];
+          if (C.irf_pwl_a && !C.se && C.stride == 1 && C.cin == N.cout && C.cout == N.cout && C.hin == N.hout &&
+              N.cout == 128 && L.cin == 64 && L.hin == 8 && hn_irf3_supported(L.k, L.mid, N.k, N.mid, C.k, C.mid)) {
+            const HnIrfArgs ic{nullptr, y, reinterpret_cast<const uint4*>(C.irf_pw_a), C.irf_pw_b, C.dw_w, C.dw_b,
+                               reinterpret_cast<const uint4*>(C.irf_pwl_a), C.pwl_b};
+            STAGE("irf3", hn_launch_irf3(ia, ib, ic, P, L.k, N.k, C.k, st));
+            std::swap(x, y);
+            li += 2;
+            continue;
+          }
+        }
+#endif
         STAGE("irf2", hn_launch_irf2(ia, ib, P, L.cin, L.hin, L.k, L.mid, N.cout, N.k, N.mid, st));
         if (N.se)
           STAGE("se", hn_launch_se(y, N.se_w1, N.se_b1, N.se_w2, N.se_b2, P, N.hout * N.hout, N.cout, N.semid, st));

@@ -26,6 +26,7 @@ struct HnKnobs {
   bool front_xch3 = false;     // HN_FRONT_XCH3: the k3 front's dw per channel group (SGPR weights, s_x; two
                                // workgroups per CU instead of three: wang2 front 5.05 -> 5.57 ms, not the default)
   bool no_mpfront = false;     // HN_NO_MPFRONT: k_front (max-pool) + k_irf instead of k_mpfront_irf
+  bool irf3 = false;           // HN_IRF3 (HN_EXPERIMENTS only): k_irf3 for layers 3 -> 4 -> 5 (measured slower)
   int train_splitk = 1024;     // HN_TRAIN_SPLITK: K per split-K slice of the train GEMMs
   int train_f32 = 17;          // HN_TRAIN_F32: bit 0 train forward convs, bit 1 stride-1 dgrads as f32-MFMA
                                // GEMMs (else the bf16x3 conv kernels); 1 = every product f32; default 17 =
@@ -187,6 +188,11 @@ hipError_t hn_launch_irf(const HnIrfArgs& a, int P, int cin, int cout, int hin, 
 // a 16x16 stride-2 32 -> 64 block and the 8x8 64 -> 128 stride-2 skip that follows it (after identity
 // skips) in one kernel (hn_irf.hip k_irf_skip); a.y receives the skip's [P,4,4,128] output
 bool hn_irf_skip_supported(int cin, int cout, int hin, int s, int k, int mid);
+// k_irf2's 8x8 pair (64 -> 64 s1, 64 -> 128 s2, mid 64) and the 4x4 128 -> 128 e1 block in one kernel (k_irf3,
+// experiments library only)
+bool hn_irf3_supported(int ka, int ma, int kb, int mb, int kc, int mc);
+hipError_t hn_launch_irf3(const HnIrfArgs& a, const HnIrfArgs& b, const HnIrfArgs& c, int P, int ka, int kb, int kc,
+                          hipStream_t st);
 // the max-pool front + the first (16x16 stride-2 32 -> 64) IRF block in one kernel (hn_irf.hip k_mpfront_irf)
 bool hn_mpfront_irf_supported(int cin, int cout, int hin, int s, int k, int mid);
 hipError_t hn_launch_mpfront_irf(const float* in, const uint4* spack, const float* stem_b, const HnIrfArgs& a, int P,

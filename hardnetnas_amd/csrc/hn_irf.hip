@@ -455,6 +455,196 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
   }
 }
 
+#ifdef HN_EXPERIMENTS
+// (experiments library, HN_IRF3=1: measured slower -- wang4 irf2 + irf 5.09 -> irf3 5.68 ms per step)
+// Three consecutive blocks on one tile: k_irf2's 8x8 pair (A: 64 -> 64 stride 1, B: 64 -> 128 stride 2;
+// SEARCH_SPACE2 layers 3 -> 4) and C, the 4x4 stride-1 128 -> 128 e1 block after it (layer 5), on B's output
+// tile -- 2 patches = 32 pixels x 128 channels -- so the B -> C activation (8 KB per patch each way) never
+// reaches HBM and C costs no launch of its own.  C's tile is
+// a single 32-pixel MFMA tile, so its work is split by channel chunk instead of by pixel tile: wave w runs
+// C's pw for mid chunk w (all CB / 16 K-steps, its B operands split from an LDS copy of B's output), that
+// chunk's depthwise conv (RUNS x 8 = 64 items: one per lane), and -- after a workgroup barrier -- the pwl for
+// output-channel tile w over the MID chunks in irf_core's order, then the residual as identity-weight
+// K-steps.  Every C output is the same products added in the same order as k_irf's: bit-identical.
+template <int CA, int HI, int KA, int MA, int CB, int KB, int MB, int KC, int MC>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_irf3(
+    const float* __restrict__ x, float* __restrict__ y, HnIrfArgs A, HnIrfArgs Bk, HnIrfArgs Cc, int P) {
+  using SA = IrfShape<CA, CA, HI, 1, KA, MA>;
+  using SB = IrfShape<CA, CB, HI, 2, KB, MB>;
+  constexpr int HC = HI / 2, NC = SB::NO;      // C's resolution and its tile's pixels
+  constexpr int KSC = CB / 16, NCH = MC / 32;  // C's pw K-steps and mid chunks
+  static_assert(SA::NPB == SB::NPB && SA::NO == SB::NI, "A's output tile is B's input tile");
+  static_assert(NC == 32 && SB::TW == 1 && SB::NCT == 4 && NCH == 4, "C: one pixel tile, one mid chunk per wave");
+  static_assert(irf2_mode_a<CA>() == IRF_PLAIN && irf2_mode_b<CA>() == IRF_PLAIN, "the 64-channel pair");
+  constexpr int NPB = SA::NPB, XS = CA + 4, XC = CB + 4;
+  constexpr int CW = KC * KC * 8 + 8;          // C's dw weight + bias float4s per chunk
+  constexpr int LA = irf_lds_floats<CA, CA, HI, 1, KA, MA>(), LB = irf_lds_floats<CA, CB, HI, 2, KB, MB>();
+  constexpr int LX = SA::NO * XS, LCX = NC * XC;
+  constexpr int C_PW = 0, C_W = NCH * NC * PS, C_DW = C_W + NCH * CW * 4, LC = C_DW + NCH * NC * PS;
+  constexpr int L1 = LA > LB ? LA : LB, L2 = LX > LCX ? LX : LCX, L3 = L1 > L2 ? L1 : L2;
+  constexpr int LDS = L3 > LC ? L3 : LC;
+  static_assert(3 * LDS * 4 <= 160 * 1024, "three workgroups per CU");
+  __shared__ __attribute__((aligned(16))) float smem[LDS];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, px = lane & 31, h = lane >> 5;
+  const int tile = (int)blockIdx.x;
+  if (tile * NPB >= P) return;  // workgroup-uniform
+  const long p0 = (long)tile * NPB;
+  const int npv = (int)min<long>(NPB, P - p0);
+  f32x16 accb[1];
+  {
+    float4 pa[SA::TI][SA::KS], pb[SA::TI][SA::KS];
+    irf_load<CA, CA, HI, 1, KA, MA>(&pa[0][0], &pb[0][0], x, tile, P);
+    {
+      uint4 bh[SA::TI][SA::KS], bl[SA::TI][SA::KS];
+#pragma unroll
+      for (int i = 0; i < SA::TI; ++i)
+#pragma unroll
+        for (int s = 0; s < SA::KS; ++s) split8_f16(pa[i][s], pb[i][s], bh[i][s], bl[i][s]);
+      f32x16 acc[SA::TW];
+      irf_core<CA, CA, HI, 1, KA, MA, IRF_PLAIN>(bh, bl, acc, A.pw_a, A.pw_b, A.dw_w, A.dw_b, A.pwl_a, A.pwl_b, smem,
+                                                 smem + SA::LDS_PW, smem + SA::LDS_PW + SA::LDS_DW);
+#pragma unroll
+      for (int i = 0; i < SA::TW; ++i) {
+        const int tl = 4 * i + w, pt = tl % SA::NOT, ct = tl / SA::NOT;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          *reinterpret_cast<float4*>(smem + (pt * 32 + px) * XS + 32 * ct + 8 * q + 4 * h) =
+              make_float4(acc[i][4 * q], acc[i][4 * q + 1], acc[i][4 * q + 2], acc[i][4 * q + 3]);
+      }
+    }
+    __syncthreads();
+    uint4 bh[SB::TI][SB::KS], bl[SB::TI][SB::KS];
+#pragma unroll
+    for (int i = 0; i < SB::TI; ++i)
+#pragma unroll
+      for (int s = 0; s < SB::KS; ++s) {
+        const float4* src = reinterpret_cast<const float4*>(smem + ((4 * i + w) * 32 + px) * XS + 16 * s + 8 * h);
+        split8_f16(src[0], src[1], bh[i][s], bl[i][s]);
+      }
+    __syncthreads();
+    irf_core<CA, CB, HI, 2, KB, MB, IRF_PLAIN>(bh, bl, accb, Bk.pw_a, Bk.pw_b, Bk.dw_w, Bk.dw_b, Bk.pwl_a, Bk.pwl_b,
+                                               smem, smem + SB::LDS_PW, smem + SB::LDS_PW + SB::LDS_DW);
+  }
+  // B's output (wave w: pixels 0..31, channels 32 w ..) -> LDS [pixel][XC]; C's pw B operands from it
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    *reinterpret_cast<float4*>(smem + px * XC + 32 * w + 8 * q + 4 * h) =
+        make_float4(accb[0][4 * q], accb[0][4 * q + 1], accb[0][4 * q + 2], accb[0][4 * q + 3]);
+  __syncthreads();
+  uint4 ch[KSC], cl[KSC];
+#pragma unroll
+  for (int s = 0; s < KSC; ++s) {
+    const float4* src = reinterpret_cast<const float4*>(smem + px * XC + 16 * s + 8 * h);
+    split8_f16(src[0], src[1], ch[s], cl[s]);
+  }
+  __syncthreads();  // the region is C's pw / dw buffers from here
+  // ---- C: pw of mid chunk m = w (bias + ReLU) -> this wave's [32 pixels][PS] ------------------
+  const int m = w;
+  float* s_pwc = smem + C_PW + w * NC * PS;
+  float* s_wc = smem + C_W + w * CW * 4;
+  float* s_dwa = smem + C_DW;
+  for (int i = lane; i < CW; i += 64) {
+    const float* src = i < KC * KC * 8 ? Cc.dw_w + (i >> 3) * MC + 32 * m + 4 * (i & 7)
+                                       : Cc.dw_b + 32 * m + 4 * (i - KC * KC * 8);
+    *reinterpret_cast<float4*>(s_wc + 4 * i) = *reinterpret_cast<const float4*>(src);
+  }
+  {
+    f32x16 c;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 b = *reinterpret_cast<const float4*>(Cc.pw_b + 32 * m + 8 * q + 4 * h);
+      c[4 * q] = b.x; c[4 * q + 1] = b.y; c[4 * q + 2] = b.z; c[4 * q + 3] = b.w;
+    }
+#pragma unroll
+    for (int s = 0; s < KSC; ++s) {
+      const uint4* ap = Cc.pw_a + ((size_t)(m * KSC + s) * 2) * 64 + lane;
+      c = mfma3_f16(as_f16x8(ap[0]), as_f16x8(ap[64]), as_f16x8(ch[s]), as_f16x8(cl[s]), c);
+    }
+    float4* d = reinterpret_cast<float4*>(s_pwc + px * PS);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      d[2 * q + h] = make_float4(relu0(c[4 * q]), relu0(c[4 * q + 1]), relu0(c[4 * q + 2]), relu0(c[4 * q + 3]));
+  }
+  __builtin_amdgcn_wave_barrier();  // (one wave: its LDS accesses execute in order)
+  asm volatile("" ::: "memory");
+  // ---- C: depthwise KC x KC (stride 1, pad KC / 2, BN, ReLU) of chunk m: lane = (4-pixel row run, quad) -----
+  {
+    constexpr int R = 4, PAD = KC / 2, WIN = R - 1 + KC;
+    static_assert(HC == R && NC / R * 8 == 64, "one run (a whole row) per lane");
+    const int q = (lane & 3) | ((lane >> 5) << 2), run = (lane >> 2) & 7;
+    const int o0 = run * R, pl = o0 / (HC * HC), oy = (o0 / HC) % HC;
+    const f32x4 b4 = *reinterpret_cast<const f32x4*>(s_wc + 4 * (KC * KC * 8 + q));
+    f32x4 o[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) o[r] = b4;
+#pragma unroll 1
+    for (int dy = 0; dy < KC; ++dy) {
+      const int iy = oy + dy - PAD;
+      if (iy < 0 || iy >= HC) continue;
+      const float* rowp = s_pwc + ((pl * HC + iy) * HC) * PS + 4 * q;
+      f32x4 win[WIN];
+#pragma unroll
+      for (int c = 0; c < WIN; ++c) {
+        const int ix = c - PAD;
+        win[c] = (ix >= 0 && ix < HC) ? *reinterpret_cast<const f32x4*>(rowp + ix * PS) : f32x4{};
+      }
+#pragma unroll
+      for (int dx = 0; dx < KC; ++dx) {
+        const f32x4 wv = *reinterpret_cast<const f32x4*>(s_wc + 4 * ((dy * KC + dx) * 8 + q));
+#pragma unroll
+        for (int r = 0; r < R; ++r) o[r] = __builtin_elementwise_fma(wv, win[r + dx], o[r]);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+      *reinterpret_cast<f32x4*>(s_dwa + (m * NC + o0 + r) * PS + 4 * q) = relu4(o[r]);
+  }
+  __syncthreads();
+  // ---- C: pwl (output-channel tile ct = w over the MID chunks, irf_core's order) + residual ---------------
+  const int ct = w;
+  f32x16 acc;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float4 b = *reinterpret_cast<const float4*>(Cc.pwl_b + 32 * ct + 8 * q + 4 * h);
+    acc[4 * q] = b.x; acc[4 * q + 1] = b.y; acc[4 * q + 2] = b.z; acc[4 * q + 3] = b.w;
+  }
+#pragma unroll
+  for (int mm = 0; mm < NCH; ++mm)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const float4* src = reinterpret_cast<const float4*>(s_dwa + (mm * NC + px) * PS + 16 * s + 8 * h);
+      uint4 xh, xl;
+      split8_f16(src[0], src[1], xh, xl);
+      const uint4* ap = Cc.pwl_a + ((size_t)(ct * (MC / 16) + 2 * mm + s) * 2) * 64 + lane;
+      acc = mfma3_f16(as_f16x8(ap[0]), as_f16x8(ap[64]), as_f16x8(xh), as_f16x8(xl), acc);
+    }
+#pragma unroll
+  for (int sl = 0; sl < 2; ++sl) {
+    f16x8 id;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) id[j] = (_Float16)((px == 16 * sl + 8 * h + j) ? 1.f : 0.f);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(id, as_f16x8(cl[2 * ct + sl]), acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(id, as_f16x8(ch[2 * ct + sl]), acc, 0, 0, 0);
+  }
+  // ---- C's output tile -> y through this wave's (dead) pw chunk region: 128-byte pixel rows per store ------
+  float* scr = s_pwc;
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    *reinterpret_cast<float4*>(scr + px * PS + 8 * q + 4 * h) =
+        make_float4(acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]);
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int pl = 8 * k + (lane >> 3), c4 = lane & 7;
+    if (pl < npv * HC * HC)
+      *reinterpret_cast<float4*>(y + (p0 * (HC * HC) + pl) * CB + 32 * ct + 4 * c4) =
+          *reinterpret_cast<const float4*>(scr + pl * PS + 4 * c4);
+  }
+}
+
+#endif  // HN_EXPERIMENTS
+
 // A 16x16 stride-2 block (32 -> 64, SEARCH_SPACE2 layer 2) followed -- after any identity skips -- by the
 // channel-changing stride-2 "skip" op at 8x8 (layer 4: MaxPool2d(3, 2, 1) then ConvBNRelu 1x1 64 -> 128,
 // fbnet_builder.py:202-228; wang3's layers 2-4, fbnet_modeldef.py:30-95): the block's 8x8x64 output
@@ -752,7 +942,36 @@ hipError_t irf2_launch(const HnIrfArgs& a, const HnIrfArgs& b, int P, hipStream_
   return hipGetLastError();
 }
 
+#ifdef HN_EXPERIMENTS
+template <int KA, int KB, int KC>
+hipError_t irf3_launch(const HnIrfArgs& a, const HnIrfArgs& b, const HnIrfArgs& c, int P, hipStream_t st) {
+  constexpr int NPB = IrfTile<64, 8, 64>::NPB;
+  hipLaunchKernelGGL((k_irf3<64, 8, KA, 64, 128, KB, 64, KC, 128>), dim3((P + NPB - 1) / NPB), dim3(256), 0, st, a.x,
+                     c.y, a, b, c, P);
+  return hipGetLastError();
+}
+#endif
+
 }  // namespace
+
+#ifdef HN_EXPERIMENTS
+// three consecutive blocks fused (k_irf3): k_irf2's 8x8 pair (64 -> 64 stride 1 mid 64, then 64 -> 128 stride 2
+// mid 64: e1 / s2 ops at SEARCH_SPACE2 layers 3 -> 4) and the 4x4 128 -> 128 e1 block of layer 5, kernels 3 / 5
+bool hn_irf3_supported(int ka, int ma, int kb, int mb, int kc, int mc) {
+  return ma == 64 && mb == 64 && mc == 128 && (ka == 3 || ka == 5) && (kb == 3 || kb == 5) && (kc == 3 || kc == 5);
+}
+
+hipError_t hn_launch_irf3(const HnIrfArgs& a, const HnIrfArgs& b, const HnIrfArgs& c, int P, int ka, int kb, int kc,
+                          hipStream_t st) {
+  if (P <= 0) return hipSuccess;
+#define HN_IRF3_GO(KA, KB, KC) \
+  if (ka == KA && kb == KB && kc == KC) return irf3_launch<KA, KB, KC>(a, b, c, P, st);
+  HN_IRF3_GO(3, 3, 3) HN_IRF3_GO(3, 3, 5) HN_IRF3_GO(3, 5, 3) HN_IRF3_GO(3, 5, 5)
+  HN_IRF3_GO(5, 3, 3) HN_IRF3_GO(5, 3, 5) HN_IRF3_GO(5, 5, 3) HN_IRF3_GO(5, 5, 5)
+#undef HN_IRF3_GO
+  return hipErrorInvalidValue;
+}
+#endif
 
 // two consecutive blocks fused (k_irf2): A = (CA -> CA, stride 1, kernel KA, mid MA) at HI x HI,
 // B = (CA -> CB, stride 2, KB, MB); e = 1 / s2 ops (mid = CA) at SEARCH_SPACE2 layers 1 -> 2 and 3 -> 4

@@ -272,3 +272,19 @@ def test_bench_supernet_train_leg_flop_count():
     macs += A.SEARCH_SPACE2[-1][1] * A.DESC_DIM * A.HEAD_KERNEL ** 2
     assert abs(bench.supernet_flop_per_patch() / (2 * macs) - 1) < 1e-4
     assert bench.SUPERNET_PAIRS == 128
+
+
+def test_bench_three_block_fusion_is_experiments_only(monkeypatch):
+    """k_irf3 (layers 3 -> 4 -> 5 in one kernel) measured slower and lives in the experiments library: bench.py's
+    stage mirror counts an "irf3" stage only for HN_IRF3=1 on that library, else wang4 keeps irf2 + irf."""
+    import bench
+    from hardnetnas_amd import arch as A
+    monkeypatch.setenv("HN_IRF3", "1")
+    assert bench.irf3_triples("wang4") == set()
+    b = bench.nas_stage_bytes("wang4")
+    assert b["irf3"] == 0 and b["irf2"] > 0 and b["irf"] > 0
+    monkeypatch.setenv("HN_LIB", "/x/abl/libhardnet_mi355x.so")
+    assert bench.irf3_triples("wang4") == {3} and bench.irf3_triples("wang2") == set()
+    b, f = bench.nas_stage_bytes("wang4"), bench.nas_stage_flop("wang4")
+    assert b["irf3"] == 4 * 64 * 8 * 8 + 4 * 128 * 16 and b["irf2"] == 0 and b["irf"] == 0
+    assert sum(f.values()) == 2 * A.nas_macs("wang4")

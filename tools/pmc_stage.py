@@ -24,6 +24,8 @@ from pmc_traffic import stage_of  # noqa: E402
 def stage(name: str):
     if "k_pairdist_rows<" in name or "k_pairdist_ring<" in name:
         return "pairdist"
+    if "k_irf3<" in name:
+        return "irf3"
     if "k_irf2<" in name:
         return "irf2"
     if "k_irf_skip<" in name:
