@@ -26,6 +26,8 @@ struct HnKnobs {
   bool front_xch3 = false;     // HN_FRONT_XCH3: the k3 front's dw per channel group (SGPR weights, s_x; two
                                // workgroups per CU instead of three: wang2 front 5.05 -> 5.57 ms, not the default)
   bool no_mpfront = false;     // HN_NO_MPFRONT: k_front (max-pool) + k_irf instead of k_mpfront_irf
+  bool pipeline = false;       // HN_PIPELINE=1: HardNet batches of several chunks overlap chunk k + 1's k_c12s (second
+                               // stream) with chunk k's conv3 .. head (opt-in: measured within noise)
   bool irf3 = false;           // HN_IRF3 (HN_EXPERIMENTS only): k_irf3 for layers 3 -> 4 -> 5 (measured slower)
   int train_splitk = 1024;     // HN_TRAIN_SPLITK: K per split-K slice of the train GEMMs
   int train_f32 = 17;          // HN_TRAIN_F32: bit 0 train forward convs, bit 1 stride-1 dgrads as f32-MFMA

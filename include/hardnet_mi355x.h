@@ -95,6 +95,9 @@ int hn_create(const hn_arch_desc* desc, const float* host_params, size_t n_param
  * values give bit-identical descriptors): HN_C12_GROUP (patches per fused stem+conv1+conv2 launch) and
  * HN_SUBCHUNK (patches per conv3..conv5 launch); the footprint is (HN_SUBCHUNK + HN_C12_GROUP) x 64 KiB +
  * chunk x 32 KiB, e.g. 4 GiB per 65,536-patch chunk at 16,384 / 16,384 (about 4 % slower end to end).
+ * HN_PIPELINE=1 (opt-in) overlaps a multi-chunk HardNet batch's chunks over a second, internally created
+ * stream (forked from and joined back into hip_stream, so graph capture holds) and adds one more
+ * chunk x 64 KiB buffer for batches of more than one chunk.
  * NAS / FDL descriptors need four buffers of their largest per-patch activation. */
 int hn_workspace_bytes(const hn_model* m, int64_t batch, size_t* bytes_out);
 

@@ -650,6 +650,49 @@ def test_forward_is_graph_capturable(cuda_device):
     assert torch.equal(out, ref)
 
 
+def test_chunk_pipeline_is_bit_identical(cuda_device, monkeypatch):
+    """forward_hardnet_pipe (opt-in, HN_PIPELINE=1): a HardNet batch of several chunks runs chunk k + 1's k_c12s on
+    a second stream (into
+    the other of two k_c12 output buffers) beside chunk k's conv3 .. head.  The kernels and their inputs are the
+    sequential path's, so the descriptors are bit-identical to HN_PIPELINE=0 -- here 6 chunks of 4,096 (the
+    buffer alternation and both event waits) with a ragged last one -- the workspace grows by one k_c12 output
+    (64 KiB per chunk patch) only for batches of more than one chunk, and the two-stream forward is captured
+    into a HIP graph (fork and join through events) and replayed."""
+    from hardnetnas_amd import synth
+    from hardnetnas_amd._native import NativeModel
+    m, fx, _ = build_module("hardnet")
+    g = golden_inputs(fx)
+    n = 5 * 4096 + 37
+    x = torch.from_numpy(np.concatenate([g, synth.synth_patches(n - len(g), seed=41)])).to(cuda_device)
+    monkeypatch.setenv("HN_CHUNK", "4096")
+    monkeypatch.setenv("HN_PIPELINE", "1")
+    nm = NativeModel.from_module(m, cuda_device)
+    nm.set_profiling(True)
+    y = nm(x)
+    assert nm.stage_times()["stem+conv1+conv2"][1] == 6
+    assert np.abs(y[: len(g)].cpu().numpy() - fx["y"]).max() <= _tol("hardnet")
+    monkeypatch.setenv("HN_PIPELINE", "0")
+    n0 = NativeModel.from_module(m, cuda_device)
+    assert torch.equal(y, n0(x))
+    assert nm.workspace_bytes(n) == n0.workspace_bytes(n) + 4096 * 16384 * 4
+    assert nm.workspace_bytes(4096) == n0.workspace_bytes(4096)
+    nm.set_profiling(False)
+    static_x = torch.zeros_like(x)
+    out = torch.empty((n, 128), device=cuda_device)
+    ws = torch.empty(nm.workspace_bytes(n), device=cuda_device, dtype=torch.uint8)
+    nm.forward(static_x, out=out, workspace=ws)
+    torch.cuda.synchronize()
+    gr = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream(device=cuda_device)
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(gr, stream=s):
+            nm.forward(static_x, out=out, workspace=ws)
+    static_x.copy_(x)
+    gr.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out, y)
+
+
 @pytest.mark.parametrize("name", ["wang3", "cov_c"])
 def test_nas_fused_skip_s2_matches_unfused(name, cuda_device, monkeypatch):
     """The channel-changing stride-2 "skip" (MaxPool2d(3, 2, 1) + ConvBNRelu 1x1,
