@@ -52,7 +52,8 @@ HN_DEV float diff_sq(const float* a, const float* p, int lane) {
   return wave_sum(fmaf(dx, dx, dy * dy));
 }
 __global__ __launch_bounds__(256) void k_lmin_sq(const float* __restrict__ a, const float* __restrict__ p, int B,
-                                                 float* __restrict__ sq, float* __restrict__ pos) {
+                                                 float* __restrict__ sq, float* __restrict__ pos,
+                                                 float* __restrict__ posx) {
   const int w = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (w >= 2 * B) return;
   const float* r = (w < B ? a + (size_t)w * D : p + (size_t)(w - B) * D);
@@ -61,7 +62,10 @@ __global__ __launch_bounds__(256) void k_lmin_sq(const float* __restrict__ a, co
   if (lane == 0) sq[w] = s;
   if (w < B) {
     const float x = diff_sq(a + (size_t)w * D, p + (size_t)w * D, lane);
-    if (lane == 0) pos[w] = sqrtf(x + 1e-6f) + 1e-8f;
+    if (lane == 0) {
+      pos[w] = sqrtf(x + 1e-6f) + 1e-8f;
+      posx[w] = x;  // (kept for the backward's sqrt derivative)
+    }
   }
 }
 
@@ -232,7 +236,8 @@ __global__ __launch_bounds__(256) void k_lmin_bwd_src(const float* __restrict__ 
                                                       const float* __restrict__ sq,
                                                       const unsigned long long* __restrict__ rowbest,
                                                       const unsigned long long* __restrict__ colbest,
-                                                      const float* __restrict__ pos, int B, int swap, float margin,
+                                                      const float* __restrict__ pos,
+                                                      const float* __restrict__ posx, int B, int swap, float margin,
                                                       int type, const float* __restrict__ dloss,
                                                       float* __restrict__ coef, int* __restrict__ idx) {
   const int i = blockIdx.x * 256 + threadIdx.x;
@@ -248,18 +253,8 @@ __global__ __launch_bounds__(256) void k_lmin_bwd_src(const float* __restrict__ 
   const int r = key_idx(rowbest[i]);
   const int c = swap ? key_idx(colbest[i]) : 0;
   const float gp = g * dp, gn = g * dm;
-  // the positive entry: sqrt's backward at the difference form of k_lmin_sq (the forward's d_ii)
-  float cp = 0.f;
-  if (gp != 0.f) {
-    const float* ai = a + (size_t)i * D;
-    const float* pi = p + (size_t)i * D;
-    float x = 0.f;
-    for (int k = 0; k < D; ++k) {
-      const float dd = ai[k] - pi[k];
-      x = fmaf(dd, dd, x);
-    }
-    cp = gp * (0.5f / sqrtf(x + 1e-6f));
-  }
+  // the positive entry: sqrt's backward at the forward's own |a_i - p_i|^2 (k_lmin_sq's difference form)
+  const float cp = gp != 0.f ? gp * (0.5f / sqrtf(posx[i] + 1e-6f)) : 0.f;
   coef[3 * i + 0] = cp;
   coef[3 * i + 1] = gn * fr != 0.f ? gn * fr * half_rsq(a, p, sq, B, i, r) : 0.f;
   coef[3 * i + 2] = gn * (1.f - fr) != 0.f ? gn * (1.f - fr) * half_rsq(a, p, sq, B, c, i) : 0.f;
@@ -372,10 +367,11 @@ __global__ __launch_bounds__(256) void k_lmin_bwd_gather(const float* __restrict
 }  // namespace
 
 // saved layout (hn_loss_train_saved_bytes): sq [2B] f32 | rowbest [B] u64 | colbest [B] u64 |
-// pos [B] f32 | coef [3B] f32 | idx [2B] i32 | cnt, off, fill, list [2B] i32 (the backward's source lists)
+// pos [B] f32 | posx [B] f32 (|a_i - p_i|^2) | coef [3B] f32 | idx [2B] i32 | cnt, off, fill, list [2B] i32
+// (the backward's source lists)
 size_t hn_loss_train_saved_bytes(long B) {
   auto al = [](size_t n) { return (n + 255) / 256 * 256; };
-  return al(2 * B * 4) + 2 * al(B * 8) + al(B * 4) + al(3 * B * 4) + 5 * al(2 * B * 4);
+  return al(2 * B * 4) + 2 * al(B * 8) + 2 * al(B * 4) + al(3 * B * 4) + 5 * al(2 * B * 4);
 }
 
 namespace {
@@ -383,6 +379,7 @@ struct LossSaved {
   float* sq;
   unsigned long long *rowbest, *colbest;
   float* pos;
+  float* posx;
   float* coef;
   int* idx;
   int *cnt, *off, *fill, *list;
@@ -398,6 +395,8 @@ LossSaved loss_saved(void* ws, long B) {
   s.colbest = reinterpret_cast<unsigned long long*>(c);
   c += al(B * 8);
   s.pos = reinterpret_cast<float*>(c);
+  c += al(B * 4);
+  s.posx = reinterpret_cast<float*>(c);
   c += al(B * 4);
   s.coef = reinterpret_cast<float*>(c);
   c += al(3 * B * 4);
@@ -417,7 +416,7 @@ LossSaved loss_saved(void* ws, long B) {
 hipError_t hn_launch_loss_train_fwd(const float* a, const float* p, int B, int swap, float margin, int type,
                                     float* loss, void* saved, hipStream_t st) {
   const LossSaved s = loss_saved(saved, B);
-  hipLaunchKernelGGL(k_lmin_sq, dim3((2 * B + 3) / 4), dim3(256), 0, st, a, p, B, s.sq, s.pos);
+  hipLaunchKernelGGL(k_lmin_sq, dim3((2 * B + 3) / 4), dim3(256), 0, st, a, p, B, s.sq, s.pos, s.posx);
   if (swap) hipLaunchKernelGGL(k_lmin_init, dim3(std::min((B + 255) / 256, 1024)), dim3(256), 0, st, s.colbest, B);
   hipLaunchKernelGGL(k_lmin_tiles, dim3((B + TM - 1) / TM), dim3(256), 0, st, a, p, s.sq, B, swap, s.rowbest,
                      s.colbest, s.pos);
@@ -430,7 +429,7 @@ hipError_t hn_launch_loss_train_bwd(const float* a, const float* p, int B, int s
                                     const float* dloss, float* ga, float* gp, void* saved, hipStream_t st) {
   const LossSaved s = loss_saved(saved, B);
   hipLaunchKernelGGL(k_lmin_bwd_src, dim3((B + 255) / 256), dim3(256), 0, st, a, p, s.sq, s.rowbest, s.colbest,
-                     s.pos, B, swap, margin, type, dloss, s.coef, s.idx);
+                     s.pos, s.posx, B, swap, margin, type, dloss, s.coef, s.idx);
   const int g = std::min((B + 255) / 256, 2048);
   if (hipError_t e = hipMemsetAsync(s.cnt, 0, sizeof(int) * 2 * (size_t)B, st)) return e;
   hipLaunchKernelGGL(k_lmin_bwd_count, dim3(g), dim3(256), 0, st, s.coef, s.idx, B, swap, s.cnt);
