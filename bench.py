@@ -832,7 +832,9 @@ def run_train(opts, dev, with_cpu: bool):
                                   "forward x2, fused loss_HardNet (anchor_swap, triplet margin, min), backward, "
                                   "SGD; orthogonal init (weights_init), synthetic pairs",
                       "model": "hardnet", "global_batch": 2 * b, "pairs": b, "parallelism": "dp1",
-                      "precision": "exact fp32 products (f32-input MFMA), fp64 BatchNorm / split-K sums"},
+                      "precision": "forwards and weight gradients exact fp32 products (f32-input MFMA); stride-1 "
+                                   "data gradients bf16x3 (HN_TRAIN_F32=17, the default); fp64 BatchNorm / split-K "
+                                   "sums"},
            "loss": float(last["loss"].item()),
            "roofline": {"bound": "mfma", "kernel": "whole train step (forward, backward, BN, loss, SGD)",
                         "achieved": round(achieved, 2), "peak": PEAK_F32, "unit": "TFLOP/s",
