@@ -1005,6 +1005,23 @@ extern "C" int hn_workspace_bytes(const hn_model* m, int64_t batch, size_t* byte
   } while (0)
 #define STAGE(NAME, CALL) STAGE_ON(st, NAME, CALL)
 
+// conv3 .. conv5 of a k_c12 group's n patches (its output a2 [n][16,384 floats]) in sub-chunks of `sub`: conv3 into
+// a0, conv4 back over the sub-chunk's a2 slots (consumed by conv3; in HN_C4_SUB pieces), conv5 into a5 rows
+// a5 + [patch][8,192 floats]
+static int hardnet_convs(hn_model* m, float* a2, int n, int sub, float* a0, float* a5, hipStream_t st) {
+  for (int s0 = 0; s0 < n; s0 += sub) {
+    const int ns = std::min(sub, n - s0);
+    float* const a2s = a2 + (size_t)s0 * 16384;
+    STAGE("conv3", hn_launch_hardnet_conv(3, m->variant[3], m->hd, a2s, a0, ns, 0.f, st));
+    const int c4 = m->c4sub > 0 ? m->c4sub : ns;
+    for (int q = 0; q < ns; q += c4)  // (a3 is 16,384 floats per patch, a4 8,192)
+      STAGE("conv4", hn_launch_hardnet_conv(4, m->variant[4], m->hd, a0 + (size_t)q * 16384, a2s + (size_t)q * 8192,
+                                            std::min(c4, ns - q), 0.f, st));
+    STAGE("conv5", hn_launch_hardnet_conv(5, m->variant[5], m->hd, a2s, a5 + (size_t)s0 * 8192, ns, 0.f, st));
+  }
+  return HN_OK;
+}
+
 // pmax: the largest chunk of this call; the buffers keep the same offsets for every chunk
 static int forward_hardnet(hn_model* m, const float* in, int P, int pmax, float* out, float* ws,
                            hipStream_t st, const HnU8In* u8 = nullptr) {
@@ -1034,16 +1051,7 @@ static int forward_hardnet(hn_model* m, const float* in, int P, int pmax, float*
       } else {
         STAGE("stem+conv1+conv2", hn_launch_c12(in + (size_t)g0 * 1024, a2, m->hd, ng, ineps, st));
       }
-      for (int s0 = g0; s0 < g0 + ng; s0 += sub) {
-        const int n = std::min(sub, g0 + ng - s0);
-        float* const a2s = a2 + (size_t)(s0 - g0) * 16384;
-        STAGE("conv3", hn_launch_hardnet_conv(3, m->variant[3], m->hd, a2s, a0, n, 0.f, st));
-        const int c4 = m->c4sub > 0 ? m->c4sub : n;
-        for (int q = 0; q < n; q += c4)  // (a3 is 16,384 floats per patch, a4 8,192)
-          STAGE("conv4", hn_launch_hardnet_conv(4, m->variant[4], m->hd, a0 + (size_t)q * 16384, a2s + (size_t)q * 8192,
-                                                std::min(c4, n - q), 0.f, st));
-        STAGE("conv5", hn_launch_hardnet_conv(5, m->variant[5], m->hd, a2s, a1 + (size_t)s0 * 8192, n, 0.f, st));
-      }
+      if (int rc = hardnet_convs(m, a2, ng, sub, a0, a1 + (size_t)g0 * 8192, st)) return rc;
     }
     // a0 -- conv3's output, consumed -- holds the small-batch head's split-K partials (8,192 floats per patch
     // against its 16,384 per sub-chunk patch)
@@ -1104,16 +1112,7 @@ static int forward_hardnet_pipe(hn_model* m, const float* in, int64_t batch, flo
     }
     if (k >= 1) HIPCHK(hipStreamWaitEvent(st, m->ev_ready[k & 1], 0));
     float* const a2 = a2b[k & 1];
-    for (int s0 = 0; s0 < P; s0 += sub) {
-      const int ns = std::min(sub, P - s0);
-      float* const a2s = a2 + (size_t)s0 * 16384;
-      STAGE("conv3", hn_launch_hardnet_conv(3, m->variant[3], m->hd, a2s, a0, ns, 0.f, st));
-      const int c4 = m->c4sub > 0 ? m->c4sub : ns;
-      for (int q = 0; q < ns; q += c4)
-        STAGE("conv4", hn_launch_hardnet_conv(4, m->variant[4], m->hd, a0 + (size_t)q * 16384, a2s + (size_t)q * 8192,
-                                              std::min(c4, ns - q), 0.f, st));
-      STAGE("conv5", hn_launch_hardnet_conv(5, m->variant[5], m->hd, a2s, a1 + (size_t)s0 * 8192, ns, 0.f, st));
-    }
+    if (int rc = hardnet_convs(m, a2, P, sub, a0, a1, st)) return rc;
     if (k + 2 < n) HIPCHK(hipEventRecord(m->ev_free[k & 1], st));  // a2b[k & 1] free for c12(k + 2)
     float* const hs = (size_t)16384 * sub >= (size_t)8192 * P ? a0 : nullptr;
     STAGE("head", hn_launch_head(a1, out + (size_t)k * C * 128, m->hd.wpack[6], m->hd.bias[6], P, 8192,
