@@ -657,7 +657,10 @@ class NasTrainFunction(torch.autograd.Function):
     def backward(ctx, dout):
         lib = load_library()
         saved, x, soft_c, *params = ctx.saved_tensors
-        grads = [torch.empty_like(p) for p in params]
+        # one allocation for every parameter's gradient (the supernet has ~2,000), handed out as views
+        # (contiguous, the parameters' shapes: autograd stores them as .grad without a copy)
+        flat = torch.empty(sum(p.numel() for p in params), device=dout.device, dtype=torch.float32)
+        grads = [g.view(p.shape) for g, p in zip(flat.split([p.numel() for p in params]), params)]
         it = iter(grads)
         gptrs = [next(it) if k == 1 else torch.empty_like(t) if k == 2 else None
                  for k, t in zip(ctx.slot, ctx.tensors)]

@@ -371,8 +371,9 @@ class HardNetNeiMask(_NativeMixin, nn.Module):
         y = self._dispatch_native(input)
         if y is not None:
             return y
-        if _nas_train_native_eligible(self, input, A.FDL_LAYERS, A.FDL_LAYERS):
-            return _nas_train_native_forward(self, input, None)
+        walk = _nas_train_native_eligible(self, input, A.FDL_LAYERS, A.FDL_LAYERS)
+        if walk is not None:
+            return _nas_train_native_forward(self, input, None, walk)
         x_features = self.features(self.input_norm(input))
         x = x_features.view(x_features.size(0), -1)
         return x / torch.norm(x, p=2, dim=-1, keepdim=True)
@@ -406,8 +407,9 @@ class HardNetNAS(_NativeMixin, nn.Module):
         y = self._dispatch_native(x)
         if y is not None:
             return y
-        if _nas_train_native_eligible(self, x, self.layers):
-            return _nas_train_native_forward(self, x, None)
+        walk = _nas_train_native_eligible(self, x, self.layers)
+        if walk is not None:
+            return _nas_train_native_forward(self, x, None, walk)
         y = self.first(x)
         for op in self.stages:
             y = op(y)
@@ -435,26 +437,51 @@ class HardNetNAS(_NativeMixin, nn.Module):
         return self.load_state_dict(out, strict=strict)
 
 
-def _nas_train_native_eligible(module: nn.Module, x: torch.Tensor, layers, expect=A.SEARCH_SPACE2) -> bool:
+def _nas_train_native_eligible(module: nn.Module, x: torch.Tensor, layers, expect=A.SEARCH_SPACE2):
     """model.train() of HardNetNAS / HardNetNASSupernet / HardNetNeiMask on a HIP fp32
     [B>=2,1,32,32] batch that needs no input gradient, with the reference's BatchNorm setup (one
     momentum, running statistics tracked, eps 1e-5) and every parameter / buffer fp32 contiguous on
     x's device, runs hn_nas_train_* (SURVEY 8(f) row 4).  Anything else runs the module's torch
-    layers."""
+    layers (returns None).  Eligible: returns (bns, tensors) -- the BatchNorms, and the float state_dict
+    tensors in state_dict order without num_batches_tracked and the supernet's thetas (the train
+    ABI's tensor list, _native.train_tensors) -- gathered in the same single pass over the module tree
+    that checks them (the supernet has ~1,400 modules: one walk instead of five per forward)."""
     if not (getattr(module, "native_train", True) and module.training and x.is_cuda
             and x.dtype == torch.float32 and x.dim() == 4 and tuple(x.shape[1:]) == (1, 32, 32)
             and x.shape[0] >= 2 and not (torch.is_grad_enabled() and x.requires_grad)
             and list(layers) == list(expect)):
-        return False
-    bns = [m for m in module.modules() if isinstance(m, nn.BatchNorm2d)]
-    # the kernels' BatchNorm forms: affine=False for the head's BN (and FDLNet NASNet's BN after
-    # conv0), affine for every other; all of them in train mode (batch statistics)
+        return None
+    return _nas_train_walk(module, x.device)
+
+
+def _nas_train_walk(module: nn.Module, dev: torch.device):
+    """The single pass of _nas_train_native_eligible: None unless every parameter / float buffer is fp32
+    contiguous on `dev` and every BatchNorm has the kernels' form (affine=False for the head's BN and
+    FDLNet NASNet's BN after conv0, affine for every other; train mode, running statistics, one momentum,
+    eps 1e-5); else (bns, tensors) with tensors in _native.train_tensors' order."""
     plain = {id(b) for b in _non_affine_bns(module)}
-    if not all(b.training and b.momentum is not None and b.track_running_stats and b.eps == 1e-5
-               and b.momentum == bns[0].momentum and b.affine == (id(b) not in plain) for b in bns):
-        return False
-    ts = list(module.parameters()) + [b for b in module.buffers() if b.dtype != torch.int64]
-    return all(t.dtype == torch.float32 and t.device == x.device and t.is_contiguous() for t in ts)
+    bns, tensors = [], []
+    for mod in module.modules():  # the DFS pre-order state_dict walks
+        for name, t in mod._parameters.items():
+            if t is None:
+                continue
+            if not (t.dtype == torch.float32 and t.device == dev and t.is_contiguous()):
+                return None
+            if name != "thetas":
+                tensors.append(t)
+        for name, t in mod._buffers.items():
+            if t is None or t.dtype == torch.int64:
+                continue
+            if not (t.dtype == torch.float32 and t.device == dev and t.is_contiguous()):
+                return None
+            if name not in mod._non_persistent_buffers_set:
+                tensors.append(t)
+        if isinstance(mod, nn.BatchNorm2d):
+            if not (mod.training and mod.momentum is not None and mod.track_running_stats and mod.eps == 1e-5
+                    and (not bns or mod.momentum == bns[0].momentum) and mod.affine == (id(mod) not in plain)):
+                return None
+            bns.append(mod)
+    return bns, tensors
 
 
 def _non_affine_bns(module: nn.Module):
@@ -464,11 +491,10 @@ def _non_affine_bns(module: nn.Module):
     return [module.last_stages.batchnorm]
 
 
-def _nas_train_native_forward(module: nn.Module, x: torch.Tensor, soft):
+def _nas_train_native_forward(module: nn.Module, x: torch.Tensor, soft, walk):
     from . import _native as N
-    bns = [m for m in module.modules() if isinstance(m, nn.BatchNorm2d)]
+    bns, tensors = walk
     desc = N.supernet_desc() if soft is not None else N.desc_for_module(module)
-    _, tensors = N.train_tensors(module)
     params = [t for t in tensors if t.requires_grad]
     y = N.NasTrainFunction.apply(x.contiguous(), soft, desc, tensors, bns[0].momentum, *params)
     # one multi-tensor launch for every BatchNorm's counter (the supernet has 584)
@@ -493,7 +519,7 @@ class MixedOperation(nn.Module):
         max_all, _ = maxk.max(dim=-1, keepdim=True)
         exp_maps = torch.exp(strength * (variables - max_all))
         exp_maps_pad = F.pad(exp_maps, [ksize // 2, ksize // 2], mode="replicate")
-        sum_exp = F.conv1d(exp_maps_pad, weight=torch.ones([1, 1, ksize]).to(exp_maps.device), stride=1)
+        sum_exp = F.conv1d(exp_maps_pad, weight=torch.ones([1, 1, ksize], device=exp_maps.device), stride=1)
         return exp_maps / sum_exp
 
     def latency_terms(self, m, latency_to_accumulate):
@@ -546,8 +572,9 @@ class HardNetNASSupernet(nn.Module):
         for i, st in enumerate(self.stages_to_search):
             latency_to_accumulate, s_i, h_i = st.latency_terms(soft_weights[i], latency_to_accumulate)
             soft, hard = soft + s_i, hard + h_i
-        if _nas_train_native_eligible(self, x, self.layers):
-            y = _nas_train_native_forward(self, x, soft_weights.to(device=x.device, dtype=torch.float32))
+        walk = _nas_train_native_eligible(self, x, self.layers)
+        if walk is not None:
+            y = _nas_train_native_forward(self, x, soft_weights.to(device=x.device, dtype=torch.float32), walk)
             return y, latency_to_accumulate, soft, hard
         y = self.first(x)
         for i, st in enumerate(self.stages_to_search):
