@@ -352,12 +352,16 @@ __global__ __launch_bounds__(64) void k_dot_final(const double* __restrict__ par
 }
 
 // SEModule (fbnet_builder.py:407-421): out = x * sigmoid(W2 relu(W1 avgpool(x) + b1) + b2)
+// one wave per (channel, patch) row: lanes stride the HW contiguous values (coalesced), then a butterfly
+// (one thread per row walking it serially read 4-byte pieces HW floats apart across the wave)
 __global__ __launch_bounds__(256) void k_se_pool(const float* __restrict__ x, long CB, int HW, float* __restrict__ pooled) {
-  for (long cb = (long)blockIdx.x * 256 + threadIdx.x; cb < CB; cb += (long)gridDim.x * 256) {
+  const int lane = threadIdx.x & 63;
+  for (long cb = ((long)blockIdx.x * 256 + threadIdx.x) >> 6; cb < CB; cb += (long)gridDim.x * 4) {
     const float* r = x + cb * HW;
     float s = 0.f;
-    for (int i = 0; i < HW; ++i) s += r[i];
-    pooled[cb] = s / (float)HW;
+    for (int i = lane; i < HW; i += 64) s += r[i];
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if (lane == 0) pooled[cb] = s / (float)HW;
   }
 }
 // v[r][j] = act(v[r][j] + bias[r]): act 1 = ReLU, 2 = sigmoid
@@ -375,13 +379,18 @@ __global__ __launch_bounds__(256) void k_se_scale(const float* __restrict__ x, c
   for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < CB * HW; e += (long)gridDim.x * 256) out[e] = x[e] * s[e / HW];
 }
 // dq[cb] = (sum_hw dO x) s (1 - s)   (the gradient at the sigmoid's input)
+// (one wave per row, as k_se_pool)
 __global__ __launch_bounds__(256) void k_se_bwd_ds(const float* __restrict__ dO, const float* __restrict__ x,
                                                    const float* __restrict__ s, long CB, int HW, float* __restrict__ dq) {
-  for (long cb = (long)blockIdx.x * 256 + threadIdx.x; cb < CB; cb += (long)gridDim.x * 256) {
+  const int lane = threadIdx.x & 63;
+  for (long cb = ((long)blockIdx.x * 256 + threadIdx.x) >> 6; cb < CB; cb += (long)gridDim.x * 4) {
     float acc = 0.f;
-    for (int i = 0; i < HW; ++i) acc = fmaf(dO[cb * HW + i], x[cb * HW + i], acc);
-    const float sv = s[cb];
-    dq[cb] = acc * sv * (1.f - sv);
+    for (int i = lane; i < HW; i += 64) acc = fmaf(dO[cb * HW + i], x[cb * HW + i], acc);
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    if (lane == 0) {
+      const float sv = s[cb];
+      dq[cb] = acc * sv * (1.f - sv);
+    }
   }
 }
 __global__ __launch_bounds__(256) void k_relu_mask(float* __restrict__ d, const float* __restrict__ h, long n) {
@@ -805,7 +814,7 @@ hipError_t op_fwd(const Ctx& c, OpPlan& o, const float* x, const float** out) {
     const long CB = (long)o.cout * B;
     const int HW = o.hout * o.hout;
     float* pooled = c.f(o.pooled);
-    hipLaunchKernelGGL(k_se_pool, dim3(grid_of(CB)), dim3(256), 0, c.st, c.f(o.o3), CB, HW, pooled);
+    hipLaunchKernelGGL(k_se_pool, dim3(grid_of(CB * 64)), dim3(256), 0, c.st, c.f(o.o3), CB, HW, pooled);
     GemmArgs a1{c.T[o.se_w1], pooled, c.f(o.hh), o.semid, B, o.cout, o.cout, 1, B, 1, B, 1, 1.f, 0.f};
     HCK(gemm(a1, c.st));
     hipLaunchKernelGGL(k_bias_act, dim3(grid_of((long)o.semid * B)), dim3(256), 0, c.st, c.f(o.hh), o.semid, B,
@@ -854,7 +863,7 @@ hipError_t op_bwd(const Ctx& c, const OpPlan& o, const float* x, float* dO, floa
     float* dh = c.s(c.P.se1);
     float* dp = c.s(c.P.se2);
     float* part = c.s(c.P.part);
-    hipLaunchKernelGGL(k_se_bwd_ds, dim3(grid_of(CB)), dim3(256), 0, c.st, dO, c.f(o.o3), c.f(o.sg), CB, HW, dq);
+    hipLaunchKernelGGL(k_se_bwd_ds, dim3(grid_of(CB * 64)), dim3(256), 0, c.st, dO, c.f(o.o3), c.f(o.sg), CB, HW, dq);
     GemmArgs w2{dq, c.f(o.hh), c.G[o.se_w2], o.cout, o.semid, B, B, 1, 1, B, o.semid, 1, 1.f, 0.f};  // dW2 = dq h^T
     HCK(gemm(w2, c.st, part));
     hipLaunchKernelGGL(k_rowsum, dim3(o.cout), dim3(256), 0, c.st, dq, B, c.G[o.se_b2]);
