@@ -33,12 +33,16 @@ constexpr int NOPS = 17;  // CANDIDATE_BLOCKS
 // BatchNorm apply: y (conv output, in place) -> z = (y - mean) * rstd; a = act(gamma z + beta) [+ res].
 // The channel's statistics come from k_bn_part's slice sums, combined by thread 0 of every workgroup in
 // k_bn_final's order and arithmetic (so mean / rstd are k_bn_final's values); workgroup (c, 0) also
-// writes rstd and the running statistics -- one launch fewer per BatchNorm than part / final / apply
+// writes rstd and the running statistics -- one launch fewer per BatchNorm than part / final / apply.
+// mix (the supernet's MixedOperation, an op's last BatchNorm): also mix = (mixacc ? mix : 0) + mixc[0] a, the
+// FMA k_axpy would run on the stored a, so the layer's weighted sum needs no launch of its own
 __global__ __launch_bounds__(256) void k_bna_apply(float* __restrict__ y, long L, const double* __restrict__ part,
                                                    int NS, float eps, float mom, float* __restrict__ rmean,
                                                    float* __restrict__ rvar, float* __restrict__ rstd_out,
                                                    const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                   int relu, const float* __restrict__ res, float* __restrict__ a) {
+                                                   int relu, const float* __restrict__ res, float* __restrict__ a,
+                                                   const float* __restrict__ mixc, float* __restrict__ mix,
+                                                   int mixacc) {
   __shared__ float st[2];
   const int c = blockIdx.x;
   if (threadIdx.x == 0) {
@@ -61,6 +65,7 @@ __global__ __launch_bounds__(256) void k_bna_apply(float* __restrict__ y, long L
   }
   __syncthreads();
   const float mu = st[0], rs = st[1], g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
+  const float mc = mix ? *mixc : 0.f;
   const long base = (long)c * L, step = (long)gridDim.y * 256;
   for (long i = (long)blockIdx.y * 256 + threadIdx.x; i < L; i += step) {
     const float z = (y[base + i] - mu) * rs;
@@ -70,6 +75,7 @@ __global__ __launch_bounds__(256) void k_bna_apply(float* __restrict__ y, long L
       if (relu) v = fmaxf(v, 0.f);
       if (res) v += res[base + i];
       a[base + i] = v;
+      if (mix) mix[base + i] = mixacc ? fmaf(mc, v, mix[base + i]) : mc * v;
     }
   }
 }
@@ -334,21 +340,27 @@ __global__ __launch_bounds__(256) void k_axpy(long n, const float* __restrict__ 
     y[e] = acc ? fmaf(c, x[e], y[e]) : c * x[e];
 }
 
-// <a, b> over n elements: per-workgroup fp64 partials, then one fixed-order sum
-__global__ __launch_bounds__(256) void k_dot_part(const float* __restrict__ a, const float* __restrict__ b, long n,
+// <a, b_j> over n elements for the NOPS ops j of a supernet layer (blockIdx.y = j): per-workgroup fp64
+// partials, then one fixed-order sum per op
+struct DotSrc {
+  const float* b[NOPS];
+};
+__global__ __launch_bounds__(256) void k_dot_part(const float* __restrict__ a, DotSrc src, long n,
                                                   double* __restrict__ part) {
   __shared__ double sh[8];
+  const float* __restrict__ b = src.b[blockIdx.y];
   double s = 0.0, z = 0.0;
   for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < n; e += (long)gridDim.x * 256) s += (double)a[e] * b[e];
   block_sum2(s, z, sh);
-  if (threadIdx.x == 0) part[blockIdx.x] = s;
+  if (threadIdx.x == 0) part[(long)blockIdx.y * gridDim.x + blockIdx.x] = s;
 }
-// one wave: lane l sums partials l, l + 64, ... in order, then a fixed butterfly over the 64 lanes
+// one wave per op: lane l sums partials l, l + 64, ... in order, then a fixed butterfly over the 64 lanes
 __global__ __launch_bounds__(64) void k_dot_final(const double* __restrict__ part, int n, float* __restrict__ out) {
+  const double* p = part + (long)blockIdx.x * n;
   double s = 0.0;
-  for (int i = threadIdx.x; i < n; i += 64) s += part[i];
+  for (int i = threadIdx.x; i < n; i += 64) s += p[i];
   for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-  if (threadIdx.x == 0) out[0] = (float)s;
+  if (threadIdx.x == 0) out[blockIdx.x] = (float)s;
 }
 
 // SEModule (fbnet_builder.py:407-421): out = x * sigmoid(W2 relu(W1 avgpool(x) + b1) + b2)
@@ -670,7 +682,7 @@ Plan make_plan(const hn_arch_desc& d, long B) {
   P.se1 = take((size_t)512 * B * sizeof(float));
   P.se2 = take((size_t)512 * B * sizeof(float));
   P.hcol = take((size_t)cl * 16 * B * sizeof(float));
-  P.dotpart = take((size_t)kDotParts * sizeof(double));
+  P.dotpart = take((size_t)NOPS * kDotParts * sizeof(double));
   P.scratch = off;
   return P;
 }
@@ -692,14 +704,15 @@ struct Ctx {
 
 // train-mode BN over [C][L] (y in place -> z), rstd saved; a = act(gamma z + beta) [+ res]
 hipError_t bn_fwd(const Ctx& c, float* y, int C, long L, int bnt, bool affine, bool relu, const float* res, float* a,
-                  float* rstd) {
+                  float* rstd, const float* mixc = nullptr, float* mix = nullptr, bool mixacc = false) {
   const int NS = bn_slices(C, L);
   double* part = reinterpret_cast<double*>(c.sc + c.P.bnpart);
   hipLaunchKernelGGL(k_bn_part, dim3(C, NS), dim3(256), 0, c.st, y, L, NS, part);
   float* rm = c.T[affine ? bnt + 2 : bnt];
   float* rv = c.T[affine ? bnt + 3 : bnt + 1];
   hipLaunchKernelGGL(k_bna_apply, bn_row_grid(C, L), dim3(256), 0, c.st, y, L, part, NS, 1e-5f, c.mom, rm, rv, rstd,
-                     affine ? c.T[bnt] : nullptr, affine ? c.T[bnt + 1] : nullptr, relu ? 1 : 0, res, a);
+                     affine ? c.T[bnt] : nullptr, affine ? c.T[bnt + 1] : nullptr, relu ? 1 : 0, res, a, mixc, mix,
+                     mixacc ? 1 : 0);
   return hipGetLastError();
 }
 
@@ -778,7 +791,11 @@ hipError_t dw_bwd(const Ctx& c, const OpPlan& o, const float* dy, const float* a
 // ------------------------------------------------------------------------------------------
 // forward / backward of one op (x: the layer input [cin][B][hin^2])
 // ------------------------------------------------------------------------------------------
-hipError_t op_fwd(const Ctx& c, OpPlan& o, const float* x, const float** out) {
+// mixc / mix / mixacc (the supernet): an IRF op without SE adds mixc[0] x its output into mix inside its last
+// BatchNorm and sets *mixed; the caller mixes the other ops' outputs itself
+hipError_t op_fwd(const Ctx& c, OpPlan& o, const float* x, const float** out, const float* mixc = nullptr,
+                  float* mix = nullptr, bool mixacc = false, bool* mixed = nullptr) {
+  if (mixed) *mixed = false;
   const long B = c.P.B, Li = B * o.hin * o.hin, Lo = B * o.hout * o.hout;
   switch (o.kind) {
     case SKIP_ID:
@@ -809,7 +826,10 @@ hipError_t op_fwd(const Ctx& c, OpPlan& o, const float* x, const float** out) {
   HCK(dw_fwd(c, o, c.f(o.a1), c.f(o.z2)));
   HCK(bn_fwd(c, c.f(o.z2), o.mid, Lo, o.dw_bn, true, true, nullptr, c.f(o.a2), c.f(o.r2)));
   HCK(pw_fwd(c, c.T[o.pwl_w], o.cout, o.mid, o.g, c.f(o.a2), Lo, c.f(o.z3)));
-  HCK(bn_fwd(c, c.f(o.z3), o.cout, Lo, o.pwl_bn, true, false, o.res ? x : nullptr, c.f(o.o3), c.f(o.r3)));
+  const bool mx = mix && !o.se;
+  HCK(bn_fwd(c, c.f(o.z3), o.cout, Lo, o.pwl_bn, true, false, o.res ? x : nullptr, c.f(o.o3), c.f(o.r3),
+             mx ? mixc : nullptr, mx ? mix : nullptr, mixacc));
+  if (mx) *mixed = true;
   if (o.se) {
     const long CB = (long)o.cout * B;
     const int HW = o.hout * o.hout;
@@ -948,9 +968,11 @@ hipError_t nas_fwd(Ctx& c, Plan& P, const float* in, const float* soft, float* o
     const long n = (long)L.cout * B * L.hout * L.hout;
     for (int j = 0; j < NOPS; ++j) {  // MixedOperation: sum_j m_j op_j(x) (model_supernet.py:23-36)
       const float* oj = nullptr;
-      HCK(op_fwd(c, L.ops[j], x, &oj));
-      hipLaunchKernelGGL(k_axpy, dim3(grid_of(n)), dim3(256), 0, c.st, n, soft + i * NOPS + j, oj, c.f(L.sum),
-                         j > 0 ? 1 : 0);
+      bool mixed = false;
+      HCK(op_fwd(c, L.ops[j], x, &oj, soft + i * NOPS + j, c.f(L.sum), j > 0, &mixed));
+      if (!mixed)
+        hipLaunchKernelGGL(k_axpy, dim3(grid_of(n)), dim3(256), 0, c.st, n, soft + i * NOPS + j, oj, c.f(L.sum),
+                           j > 0 ? 1 : 0);
     }
     x = c.f(L.sum);
   }
@@ -1009,15 +1031,15 @@ hipError_t nas_bwd(Ctx& c, Plan& P, const float* in, const float* soft, const fl
     } else {
       float* dOj = c.s(P.t0);
       double* dp = reinterpret_cast<double*>(c.sc + P.dotpart);
+      // d m_j = <d out, op_j(x)> for all 17 ops at once (g is not written by the op backwards below)
+      DotSrc ds;
+      for (int j = 0; j < NOPS; ++j) ds.b[j] = L.ops[j].out_is_input ? xin[i] : c.f(L.ops[j].out);
+      const unsigned np = std::min<unsigned>(kDotParts, grid_of(nout));
+      hipLaunchKernelGGL(k_dot_part, dim3(np, NOPS), dim3(256), 0, c.st, g, ds, nout, dp);
+      hipLaunchKernelGGL(k_dot_final, dim3(NOPS), dim3(64), 0, c.st, dp, (int)np, dsoft + i * NOPS);
       for (int j = 0; j < NOPS; ++j) {
-        const OpPlan& o = L.ops[j];
-        const float* oj = o.out_is_input ? xin[i] : c.f(o.out);
-        // d m_j = <d out, op_j(x)>
-        const unsigned np = std::min<unsigned>(kDotParts, grid_of(nout));
-        hipLaunchKernelGGL(k_dot_part, dim3(np), dim3(256), 0, c.st, g, oj, nout, dp);
-        hipLaunchKernelGGL(k_dot_final, dim3(1), dim3(64), 0, c.st, dp, (int)np, dsoft + i * NOPS + j);
         hipLaunchKernelGGL(k_axpy, dim3(grid_of(nout)), dim3(256), 0, c.st, nout, soft + i * NOPS + j, g, dOj, 0);
-        HCK(op_bwd(c, o, xin[i], dOj, gx));
+        HCK(op_bwd(c, L.ops[j], xin[i], dOj, gx));
       }
     }
     std::swap(g, gx);
