@@ -363,6 +363,35 @@ __global__ __launch_bounds__(64) void k_dot_final(const double* __restrict__ par
   if (threadIdx.x == 0) out[blockIdx.x] = (float)s;
 }
 
+// The supernet's 1x1 convs of one layer phase (every IRF op's pw, or every op's pwl, each group of a grouped
+// conv a problem) in one launch: problem q is pw_fwd's GEMM C [M][N] = A [M][K] . B [K][N] (row strides K, N,
+// N), workgroup t takes tile t - tile0[q] of problem q, and gemm_tile runs the exact k_gemm tile -- so each
+// output equals the separate launch's bit for bit.  One launch per tile height (BM 32 for M <= 32, else 64,
+// gemm()'s choice).
+constexpr int kPwBatch = 40;
+struct PwProb {
+  const float* A;
+  const float* B;
+  float* C;
+  int M, K;
+};
+struct PwBatch {
+  PwProb p[kPwBatch];
+  int tile0[kPwBatch + 1];
+  int n;
+  long N;
+};
+template <int BM>
+__global__ __launch_bounds__(256) void k_gemm_pw_batch(PwBatch b) {
+  const int t = (int)blockIdx.x;
+  int q = 0;
+  while (q + 1 < b.n && b.tile0[q + 1] <= t) ++q;
+  const PwProb& pr = b.p[q];
+  const long nt = (b.N + GBN - 1) / GBN, lt = t - b.tile0[q];
+  const GemmArgs g{pr.A, pr.B, pr.C, pr.M, b.N, pr.K, pr.K, 1, b.N, 1, b.N, 1, 1.f, 0.f};
+  gemm_tile<BM>(g, StridedB{}, (lt / nt) * BM, (lt % nt) * GBN, 0, pr.K, 0, nullptr);
+}
+
 // SEModule (fbnet_builder.py:407-421): out = x * sigmoid(W2 relu(W1 avgpool(x) + b1) + b2)
 // one wave per (channel, patch) row: lanes stride the HW contiguous values (coalesced), then a butterfly
 // (one thread per row walking it serially read 4-byte pieces HW floats apart across the wave)
@@ -760,6 +789,46 @@ hipError_t pw_dgrad(const Ctx& c, const float* w, const float* dy, int cout, int
   return hipSuccess;
 }
 
+// pw_fwd's per-group GEMMs of several ops gathered, then launched as k_gemm_pw_batch (<= 2 launches per flush)
+struct PwBatcher {
+  const Ctx& c;
+  long N;
+  std::vector<PwProb> small, big;  // M <= 32 / M > 32
+  void add(const float* w, int cout, int cin, int g, const float* x, float* y) {
+    const int cog = cout / g, cig = cin / g;
+    for (int gi = 0; gi < g; ++gi) {
+      const PwProb p{w + (long)gi * cog * cig, x + (long)gi * cig * N, y + (long)gi * cog * N, cog, cig};
+      (cog <= 32 ? small : big).push_back(p);
+    }
+  }
+  template <int BM>
+  hipError_t launch(const std::vector<PwProb>& v) {
+    for (size_t q0 = 0; q0 < v.size(); q0 += kPwBatch) {
+      PwBatch b{};
+      b.N = N;
+      b.n = (int)std::min<size_t>(kPwBatch, v.size() - q0);
+      const long nt = (N + GBN - 1) / GBN;
+      int tiles = 0;
+      for (int q = 0; q < b.n; ++q) {
+        b.p[q] = v[q0 + q];
+        b.tile0[q] = tiles;
+        tiles += (int)(nt * ((b.p[q].M + BM - 1) / BM));
+      }
+      b.tile0[b.n] = tiles;
+      hipLaunchKernelGGL((k_gemm_pw_batch<BM>), dim3((unsigned)tiles), dim3(256), 0, c.st, b);
+      HCK(hipGetLastError());
+    }
+    return hipSuccess;
+  }
+  hipError_t flush() {
+    HCK(launch<32>(small));
+    HCK(launch<64>(big));
+    small.clear();
+    big.clear();
+    return hipSuccess;
+  }
+};
+
 hipError_t dw_fwd(const Ctx& c, const OpPlan& o, const float* a, float* y) {
   const long n = (long)o.mid * c.P.B * o.hout * o.hout;
   const float* w = c.T[o.dw_w];
@@ -793,8 +862,11 @@ hipError_t dw_bwd(const Ctx& c, const OpPlan& o, const float* dy, const float* a
 // ------------------------------------------------------------------------------------------
 // mixc / mix / mixacc (the supernet): an IRF op without SE adds mixc[0] x its output into mix inside its last
 // BatchNorm and sets *mixed; the caller mixes the other ops' outputs itself
+// stages (IRF ops; the supernet runs its pw / pwl GEMMs batched across ops in between): 1 the pw GEMM, 2 its
+// BatchNorm + the dw + its BatchNorm, 4 the pwl GEMM, 8 the pwl BatchNorm [+ SE] (the op's output)
+constexpr int kOpAll = 15;
 hipError_t op_fwd(const Ctx& c, OpPlan& o, const float* x, const float** out, const float* mixc = nullptr,
-                  float* mix = nullptr, bool mixacc = false, bool* mixed = nullptr) {
+                  float* mix = nullptr, bool mixacc = false, bool* mixed = nullptr, int stages = kOpAll) {
   if (mixed) *mixed = false;
   const long B = c.P.B, Li = B * o.hin * o.hin, Lo = B * o.hout * o.hout;
   switch (o.kind) {
@@ -821,11 +893,14 @@ hipError_t op_fwd(const Ctx& c, OpPlan& o, const float* x, const float** out, co
     }
   }
   // IRFBlock: pw (+BN+ReLU) -> [shuffle] -> dw (+BN+ReLU) -> pwl (+BN) [+ x] [-> SE]
-  HCK(pw_fwd(c, c.T[o.pw_w], o.mid, o.cin, o.g, x, Li, c.f(o.z1)));
-  HCK(bn_fwd(c, c.f(o.z1), o.mid, Li, o.pw_bn, true, true, nullptr, c.f(o.a1), c.f(o.r1)));
-  HCK(dw_fwd(c, o, c.f(o.a1), c.f(o.z2)));
-  HCK(bn_fwd(c, c.f(o.z2), o.mid, Lo, o.dw_bn, true, true, nullptr, c.f(o.a2), c.f(o.r2)));
-  HCK(pw_fwd(c, c.T[o.pwl_w], o.cout, o.mid, o.g, c.f(o.a2), Lo, c.f(o.z3)));
+  if (stages & 1) HCK(pw_fwd(c, c.T[o.pw_w], o.mid, o.cin, o.g, x, Li, c.f(o.z1)));
+  if (stages & 2) {
+    HCK(bn_fwd(c, c.f(o.z1), o.mid, Li, o.pw_bn, true, true, nullptr, c.f(o.a1), c.f(o.r1)));
+    HCK(dw_fwd(c, o, c.f(o.a1), c.f(o.z2)));
+    HCK(bn_fwd(c, c.f(o.z2), o.mid, Lo, o.dw_bn, true, true, nullptr, c.f(o.a2), c.f(o.r2)));
+  }
+  if (stages & 4) HCK(pw_fwd(c, c.T[o.pwl_w], o.cout, o.mid, o.g, c.f(o.a2), Lo, c.f(o.z3)));
+  if (!(stages & 8)) return hipSuccess;
   const bool mx = mix && !o.se;
   HCK(bn_fwd(c, c.f(o.z3), o.cout, Lo, o.pwl_bn, true, false, o.res ? x : nullptr, c.f(o.o3), c.f(o.r3),
              mx ? mixc : nullptr, mx ? mix : nullptr, mixacc));
@@ -966,10 +1041,26 @@ hipError_t nas_fwd(Ctx& c, Plan& P, const float* in, const float* soft, float* o
       continue;
     }
     const long n = (long)L.cout * B * L.hout * L.hout;
-    for (int j = 0; j < NOPS; ++j) {  // MixedOperation: sum_j m_j op_j(x) (model_supernet.py:23-36)
+    // every IRF op's pw GEMMs in one batched launch per tile height, then each op's BatchNorm / dw / BatchNorm,
+    // then every pwl GEMM batched, then each op's output in op order with the weighted sum
+    // (MixedOperation: sum_j m_j op_j(x), model_supernet.py:23-36)
+    PwBatcher pw{c, B * L.hin * L.hin, {}, {}}, pwl{c, B * L.hout * L.hout, {}, {}};
+    for (int j = 0; j < NOPS; ++j) {
+      OpPlan& o = L.ops[j];
+      if (o.kind == IRF) pw.add(c.T[o.pw_w], o.mid, o.cin, o.g, x, c.f(o.z1));
+    }
+    HCK(pw.flush());
+    for (int j = 0; j < NOPS; ++j) {
+      OpPlan& o = L.ops[j];
+      if (o.kind != IRF) continue;
+      HCK(op_fwd(c, o, x, nullptr, nullptr, nullptr, false, nullptr, 2));
+      pwl.add(c.T[o.pwl_w], o.cout, o.mid, o.g, c.f(o.a2), c.f(o.z3));
+    }
+    HCK(pwl.flush());
+    for (int j = 0; j < NOPS; ++j) {
       const float* oj = nullptr;
       bool mixed = false;
-      HCK(op_fwd(c, L.ops[j], x, &oj, soft + i * NOPS + j, c.f(L.sum), j > 0, &mixed));
+      HCK(op_fwd(c, L.ops[j], x, &oj, soft + i * NOPS + j, c.f(L.sum), j > 0, &mixed, L.ops[j].kind == IRF ? 8 : kOpAll));
       if (!mixed)
         hipLaunchKernelGGL(k_axpy, dim3(grid_of(n)), dim3(256), 0, c.st, n, soft + i * NOPS + j, oj, c.f(L.sum),
                            j > 0 ? 1 : 0);

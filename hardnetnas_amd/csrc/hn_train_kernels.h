@@ -113,15 +113,15 @@ __global__ __launch_bounds__(256) void k_wt(const float* __restrict__ w, int cou
 }
 
 // BM = 64: 2 x 2 waves of 32 x 64; BM = 32 (the 32-output-channel layers): 1 x 4 waves of 32 x 32
+// one workgroup's output tile: rows i0 .., columns j0 .., K range [kb, ke) (split-K slice z into part[z])
 template <int BM, class BL>
-__global__ __launch_bounds__(256) void k_gemm(GemmArgs g, BL bl, long kslice, float* __restrict__ part) {
+HN_DEV void gemm_tile(const GemmArgs& g, const BL& bl, long i0, long j0, long kb, long ke, int z,
+                      float* __restrict__ part) {
   constexpr int GBM = BM, WN = BM == 64 ? 64 : 32;  // M rows per workgroup, N columns per wave
   __shared__ float sA[2][GBK][GBM + 4];   // [k][m]
   __shared__ float sB[2][GBK][GBN + 4];   // [k][n]
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int wm = BM == 64 ? w >> 1 : 0, wn = BM == 64 ? w & 1 : w, r = lane & 31, h = lane >> 5;
-  const long i0 = (long)blockIdx.y * GBM, j0 = (long)blockIdx.x * GBN;
-  const long kb = (long)blockIdx.z * kslice, ke = min(g.K, kb + kslice);
   const bool a_k = g.sak == 1, b_n = g.sbj == 1;  // contiguous index of each operand
   constexpr int AN = GBM * GBK / 256, BNN = GBK * GBN / 256;  // 8 / 16 elements per thread
   float ra[AN], rb[BNN];
@@ -192,7 +192,7 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g, BL bl, long kslice, fl
         const float v = nt ? acc1[4 * q + e] : acc0[4 * q + e];
         if (i < g.M && j < g.N) {
           if (part) {
-            part[((long)blockIdx.z * g.M + i) * g.N + j] = v;
+            part[((long)z * g.M + i) * g.N + j] = v;
           } else {
             float* c = g.C + i * g.sci + j * g.scj;
             *c = g.beta == 0.f ? g.alpha * v : g.alpha * v + g.beta * *c;
@@ -200,6 +200,13 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g, BL bl, long kslice, fl
         }
       }
   }
+}
+
+template <int BM, class BL>
+__global__ __launch_bounds__(256) void k_gemm(GemmArgs g, BL bl, long kslice, float* __restrict__ part) {
+  const long kb = (long)blockIdx.z * kslice;
+  gemm_tile<BM>(g, bl, (long)blockIdx.y * BM, (long)blockIdx.x * GBN, kb, min(g.K, kb + kslice), (int)blockIdx.z,
+                part);
 }
 
 // 64 consecutive outputs x 16 slice groups per workgroup: lane x of group y sums slices y, y + 16,
