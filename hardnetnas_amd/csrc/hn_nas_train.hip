@@ -36,15 +36,13 @@ constexpr int NOPS = 17;  // CANDIDATE_BLOCKS
 // writes rstd and the running statistics -- one launch fewer per BatchNorm than part / final / apply.
 // mix (the supernet's MixedOperation, an op's last BatchNorm): also mix = (mixacc ? mix : 0) + mixc[0] a, the
 // FMA k_axpy would run on the stored a, so the layer's weighted sum needs no launch of its own
-__global__ __launch_bounds__(256) void k_bna_apply(float* __restrict__ y, long L, const double* __restrict__ part,
-                                                   int NS, float eps, float mom, float* __restrict__ rmean,
-                                                   float* __restrict__ rvar, float* __restrict__ rstd_out,
-                                                   const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                   int relu, const float* __restrict__ res, float* __restrict__ a,
-                                                   const float* __restrict__ mixc, float* __restrict__ mix,
-                                                   int mixacc) {
+HN_DEV void bna_apply_body(float* __restrict__ y, long L, const double* __restrict__ part, int NS, float eps,
+                           float mom, float* __restrict__ rmean, float* __restrict__ rvar,
+                           float* __restrict__ rstd_out, const float* __restrict__ gamma,
+                           const float* __restrict__ beta, int relu, const float* __restrict__ res,
+                           float* __restrict__ a, const float* __restrict__ mixc, float* __restrict__ mix, int mixacc,
+                           int c, int by, int gy) {
   __shared__ float st[2];
-  const int c = blockIdx.x;
   if (threadIdx.x == 0) {
     double s1 = 0.0, s2 = 0.0;
     for (int sl = 0; sl < NS; ++sl) {
@@ -55,7 +53,7 @@ __global__ __launch_bounds__(256) void k_bna_apply(float* __restrict__ y, long L
     const double var = fmax(s2 / (double)L - mean * mean, 0.0);
     st[0] = (float)mean;
     st[1] = (float)(1.0 / sqrt(var + (double)eps));
-    if (blockIdx.y == 0) {
+    if (by == 0) {
       rstd_out[c] = st[1];
       if (rmean) {
         rmean[c] = (1.f - mom) * rmean[c] + mom * (float)mean;
@@ -66,8 +64,8 @@ __global__ __launch_bounds__(256) void k_bna_apply(float* __restrict__ y, long L
   __syncthreads();
   const float mu = st[0], rs = st[1], g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
   const float mc = mix ? *mixc : 0.f;
-  const long base = (long)c * L, step = (long)gridDim.y * 256;
-  for (long i = (long)blockIdx.y * 256 + threadIdx.x; i < L; i += step) {
+  const long base = (long)c * L, step = (long)gy * 256;
+  for (long i = (long)by * 256 + threadIdx.x; i < L; i += step) {
     const float z = (y[base + i] - mu) * rs;
     y[base + i] = z;
     if (a) {
@@ -78,6 +76,53 @@ __global__ __launch_bounds__(256) void k_bna_apply(float* __restrict__ y, long L
       if (mix) mix[base + i] = mixacc ? fmaf(mc, v, mix[base + i]) : mc * v;
     }
   }
+}
+__global__ __launch_bounds__(256) void k_bna_apply(float* __restrict__ y, long L, const double* __restrict__ part,
+                                                   int NS, float eps, float mom, float* __restrict__ rmean,
+                                                   float* __restrict__ rvar, float* __restrict__ rstd_out,
+                                                   const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                   int relu, const float* __restrict__ res, float* __restrict__ a,
+                                                   const float* __restrict__ mixc, float* __restrict__ mix,
+                                                   int mixacc) {
+  bna_apply_body(y, L, part, NS, eps, mom, rmean, rvar, rstd_out, gamma, beta, relu, res, a, mixc, mix, mixacc,
+                 blockIdx.x, blockIdx.y, gridDim.y);
+}
+
+// The supernet's BatchNorms of one layer phase (every IRF op's pw BN, or every dw BN: one row length L) in one
+// k_bn_part and one apply launch: entry q owns global channels c0 .. c0 + C - 1 and its own slice count and
+// partial-sum region, and runs the single-BatchNorm bodies (bn_part_body, bna_apply_body) unchanged -- the
+// same statistics and outputs bit for bit
+constexpr int kBnMulti = 17;
+struct BnEntry {
+  float* y;
+  float* a;
+  float* rstd;
+  const float* gamma;
+  const float* beta;
+  float* rm;
+  float* rv;
+  long p0;  // first double of its partial sums
+  int C, NS, c0;
+};
+struct BnMulti {
+  BnEntry e[kBnMulti];
+  int n;
+};
+HN_DEV int bn_entry(const BnMulti& t, int gc) {
+  int q = 0;
+  while (q + 1 < t.n && t.e[q + 1].c0 <= gc) ++q;
+  return q;
+}
+__global__ __launch_bounds__(256) void k_bn_part_multi(BnMulti t, long L, double* __restrict__ part) {
+  const BnEntry& E = t.e[bn_entry(t, blockIdx.x)];
+  if ((int)blockIdx.y >= E.NS) return;  // workgroup-uniform
+  bn_part_body(E.y, L, E.NS, part + E.p0, (int)blockIdx.x - E.c0, blockIdx.y);
+}
+__global__ __launch_bounds__(256) void k_bna_apply_multi(BnMulti t, long L, const double* __restrict__ part, float eps,
+                                                         float mom, int relu) {
+  const BnEntry& E = t.e[bn_entry(t, blockIdx.x)];
+  bna_apply_body(E.y, L, part + E.p0, E.NS, eps, mom, E.rm, E.rv, E.rstd, E.gamma, E.beta, relu, nullptr, E.a,
+                 nullptr, nullptr, 0, (int)blockIdx.x - E.c0, blockIdx.y, gridDim.y);
 }
 
 // backward through [ReLU o] affine BN(train): g = da [* (gamma z + beta > 0)]; slice sums of g and g z
@@ -705,7 +750,8 @@ Plan make_plan(const hn_arch_desc& d, long B) {
   part = std::max(part, (size_t)32 * 9 * wgrad0_slices(B));
   P.part_floats = part;
   P.part = take(part * 4);
-  P.bnpart = take((size_t)512 * kBnSlices * 2 * sizeof(double));
+  // (one BatchNorm of up to 512 channels, or a layer phase of the supernet's: NS <= ceil(2048 / C) per channel)
+  P.bnpart = take(std::max<size_t>((size_t)512 * kBnSlices, (size_t)NOPS * (2048 + 512)) * 2 * sizeof(double));
   P.dwpart = take((size_t)512 * kBnSlices * 25 * sizeof(double));
   P.se0 = take((size_t)512 * B * sizeof(float));
   P.se1 = take((size_t)512 * B * sizeof(float));
@@ -744,6 +790,32 @@ hipError_t bn_fwd(const Ctx& c, float* y, int C, long L, int bnt, bool affine, b
                      mixacc ? 1 : 0);
   return hipGetLastError();
 }
+
+// train-mode affine BN + ReLU over several (y [C][L] -> z in place, a) of one row length, two launches
+struct BnBatcher {
+  const Ctx& c;
+  long L;
+  BnMulti t{};
+  int channels = 0, rows = 1;
+  long doubles = 0;
+  void add(float* y, int C, int bnt, float* a, float* rstd) {
+    BnEntry& E = t.e[t.n++];
+    E = BnEntry{y, a, rstd, c.T[bnt], c.T[bnt + 1], c.T[bnt + 2], c.T[bnt + 3], doubles, C, bn_slices(C, L), channels};
+    channels += C;
+    doubles += (long)C * E.NS * 2;
+    rows = std::max(rows, (int)bn_row_grid(C, L).y);
+  }
+  hipError_t run() {
+    if (!t.n) return hipSuccess;
+    int ns = 1;
+    for (int q = 0; q < t.n; ++q) ns = std::max(ns, t.e[q].NS);
+    double* part = reinterpret_cast<double*>(c.sc + c.P.bnpart);
+    hipLaunchKernelGGL(k_bn_part_multi, dim3((unsigned)channels, (unsigned)ns), dim3(256), 0, c.st, t, L, part);
+    hipLaunchKernelGGL(k_bna_apply_multi, dim3((unsigned)channels, (unsigned)rows), dim3(256), 0, c.st, t, L, part,
+                       1e-5f, c.mom, 1);
+    return hipGetLastError();
+  }
+};
 
 // backward through [ReLU o] BN: da -> dy (may alias), d gamma / d beta written
 hipError_t bn_bwd(const Ctx& c, const float* da, const float* z, const float* rstd, int C, long L, int bnt, bool affine,
@@ -1050,12 +1122,19 @@ hipError_t nas_fwd(Ctx& c, Plan& P, const float* in, const float* soft, float* o
       if (o.kind == IRF) pw.add(c.T[o.pw_w], o.mid, o.cin, o.g, x, c.f(o.z1));
     }
     HCK(pw.flush());
+    // the pw BatchNorms of every op, the dw of each, the dw BatchNorms of every op (op_fwd stage 2, batched)
+    BnBatcher b1{c, B * L.hin * L.hin}, b2{c, B * L.hout * L.hout};
     for (int j = 0; j < NOPS; ++j) {
       OpPlan& o = L.ops[j];
       if (o.kind != IRF) continue;
-      HCK(op_fwd(c, o, x, nullptr, nullptr, nullptr, false, nullptr, 2));
+      b1.add(c.f(o.z1), o.mid, o.pw_bn, c.f(o.a1), c.f(o.r1));
+      b2.add(c.f(o.z2), o.mid, o.dw_bn, c.f(o.a2), c.f(o.r2));
       pwl.add(c.T[o.pwl_w], o.cout, o.mid, o.g, c.f(o.a2), c.f(o.z3));
     }
+    HCK(b1.run());
+    for (int j = 0; j < NOPS; ++j)
+      if (L.ops[j].kind == IRF) HCK(dw_fwd(c, L.ops[j], c.f(L.ops[j].a1), c.f(L.ops[j].z2)));
+    HCK(b2.run());
     HCK(pwl.flush());
     for (int j = 0; j < NOPS; ++j) {
       const float* oj = nullptr;

@@ -314,9 +314,8 @@ int bn_slices(long C, long L) {
 }
 
 // forward stats: part[(c * NS + s) * 2 + {0, 1}] = sum y, sum y^2 over slice s of row c
-__global__ __launch_bounds__(256) void k_bn_part(const float* __restrict__ y, long L, int NS, double* __restrict__ part) {
+HN_DEV void bn_part_body(const float* __restrict__ y, long L, int NS, double* __restrict__ part, int c, int sl) {
   __shared__ double sh[8];
-  const int c = blockIdx.x, sl = blockIdx.y;
   const float* row = y + (long)c * L;
   double s1 = 0.0, s2 = 0.0;
   if ((L & 3) == 0) {  // float4 loads: slices of a multiple of 4 elements (rows start 16-byte aligned)
@@ -339,6 +338,9 @@ __global__ __launch_bounds__(256) void k_bn_part(const float* __restrict__ y, lo
     part[((long)c * NS + sl) * 2] = s1;
     part[((long)c * NS + sl) * 2 + 1] = s2;
   }
+}
+__global__ __launch_bounds__(256) void k_bn_part(const float* __restrict__ y, long L, int NS, double* __restrict__ part) {
+  bn_part_body(y, L, NS, part, blockIdx.x, blockIdx.y);
 }
 
 // the channel's batch statistics from k_bn_part's slice sums (fixed slice order): mean, 1/sqrt(var + eps);
