@@ -217,6 +217,45 @@ __global__ __launch_bounds__(256) void k_dw_fwd(const float* __restrict__ a, int
   }
 }
 
+// k_dw_fwd of several ops of one layer with the same kernel size (blockIdx.y = op): the same per-output sum
+struct DwEntry {
+  const float* a;
+  const float* w;
+  float* y;
+  int C, g;
+};
+struct DwMulti {
+  DwEntry e[NOPS];
+  int n;
+};
+template <int K, int S>
+__global__ __launch_bounds__(256) void k_dw_fwd_multi(DwMulti t, long B, int H) {
+  constexpr int P = K / 2;
+  const DwEntry& E = t.e[blockIdx.y];
+  const int HO = H / S;
+  const long total = (long)E.C * B * HO * HO;
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
+    const int ox = (int)(e % HO), oy = (int)((e / HO) % HO);
+    const long cb = e / ((long)HO * HO);
+    const int c = (int)(cb / B);
+    const long b = cb % B;
+    const float* src = E.a + ((long)shuffle_src(c, E.C, E.g) * B + b) * H * H;
+    const float* wc = E.w + c * K * K;
+    float s = 0.f;
+#pragma unroll
+    for (int dy = 0; dy < K; ++dy) {
+      const int iy = oy * S - P + dy;
+      if (iy < 0 || iy >= H) continue;
+#pragma unroll
+      for (int dx = 0; dx < K; ++dx) {
+        const int ix = ox * S - P + dx;
+        if (ix >= 0 && ix < H) s = fmaf(wc[dy * K + dx], src[iy * H + ix], s);
+      }
+    }
+    E.y[e] = s;
+  }
+}
+
 // data gradient: input pixel (iy, ix) of row src(c) collects the taps that landed on it
 template <int K, int S>
 __global__ __launch_bounds__(256) void k_dw_dgrad(const float* __restrict__ dy, int C, int g, long B, int H,
@@ -1132,8 +1171,23 @@ hipError_t nas_fwd(Ctx& c, Plan& P, const float* in, const float* soft, float* o
       pwl.add(c.T[o.pwl_w], o.cout, o.mid, o.g, c.f(o.a2), c.f(o.z3));
     }
     HCK(b1.run());
-    for (int j = 0; j < NOPS; ++j)
-      if (L.ops[j].kind == IRF) HCK(dw_fwd(c, L.ops[j], c.f(L.ops[j].a1), c.f(L.ops[j].z2)));
+    {  // every op's dw, one launch per kernel size
+      DwMulti d3{}, d5{};
+      long n3 = 0, n5 = 0;
+      for (int j = 0; j < NOPS; ++j) {
+        const OpPlan& o = L.ops[j];
+        if (o.kind != IRF) continue;
+        DwMulti& d = o.k == 3 ? d3 : d5;
+        d.e[d.n++] = DwEntry{c.f(o.a1), c.T[o.dw_w], c.f(o.z2), o.mid, o.g};
+        (o.k == 3 ? n3 : n5) = std::max(o.k == 3 ? n3 : n5, (long)o.mid * B * L.hout * L.hout);
+      }
+#define HN_DWM(KK, SS, D, N)                                                                                       \
+  if (D.n && L.s == SS)                                                                                            \
+    hipLaunchKernelGGL((k_dw_fwd_multi<KK, SS>), dim3(grid_of(N), (unsigned)D.n), dim3(256), 0, c.st, D, B, L.hin);
+      HN_DWM(3, 1, d3, n3) HN_DWM(3, 2, d3, n3) HN_DWM(5, 1, d5, n5) HN_DWM(5, 2, d5, n5)
+#undef HN_DWM
+      HCK(hipGetLastError());
+    }
     HCK(b2.run());
     HCK(pwl.flush());
     for (int j = 0; j < NOPS; ++j) {
