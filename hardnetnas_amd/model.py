@@ -519,15 +519,29 @@ class MixedOperation(nn.Module):
         max_all, _ = maxk.max(dim=-1, keepdim=True)
         exp_maps = torch.exp(strength * (variables - max_all))
         exp_maps_pad = F.pad(exp_maps, [ksize // 2, ksize // 2], mode="replicate")
-        sum_exp = F.conv1d(exp_maps_pad, weight=torch.ones([1, 1, ksize], device=exp_maps.device), stride=1)
+        sum_exp = F.conv1d(exp_maps_pad, weight=self._const("ones", [1.0] * ksize, exp_maps).view(1, 1, ksize),
+                           stride=1)
         return exp_maps / sum_exp
 
-    def latency_terms(self, m, latency_to_accumulate):
-        """model_supernet.py:27-35: the soft latency, its soft-NMS and hard-sample forms."""
-        latency = sum(mj * lat for mj, lat in zip(m, self.latency))
+    def _const(self, name, values, like):
+        """values as a tensor on like's device / dtype, kept between calls (no host copy per step)."""
+        cache = self.__dict__.setdefault("_const_cache", {})
+        key = (name, like.device, like.dtype, tuple(values))
+        t = cache.get(key)
+        if t is None:
+            t = cache[key] = torch.tensor(values, device=like.device, dtype=like.dtype)
+        return t
+
+    def latency_terms(self, m, latency_to_accumulate, hard_idx=None):
+        """model_supernet.py:27-35: the soft latency, its soft-NMS and hard-sample forms.  The two weighted
+        sums are one product and one reduction each (the reference's Python sum over the 17 ops launches 34
+        kernels per term; the fp32 sum order differs at the 1e-7 level).  hard_idx: argmax(m), when the
+        caller already has it (HardNetNASSupernet reads all six layers' in one device sync)."""
+        lat = self._const("latency", self.latency, m)
+        latency = (m * lat).sum()
         nmsprobs = self.softnms(m.unsqueeze(0).unsqueeze(0), len(self.latency), 50)
-        soft = sum(p * lat for p, lat in zip(nmsprobs.squeeze(), self.latency))
-        hard = self.latency[torch.argmax(m).item()]
+        soft = (nmsprobs.squeeze() * lat).sum()
+        hard = self.latency[torch.argmax(m).item() if hard_idx is None else hard_idx]
         return latency_to_accumulate + latency, soft, hard
 
     def forward(self, x, temperature, latency_to_accumulate, m=None):
@@ -569,8 +583,9 @@ class HardNetNASSupernet(nn.Module):
         if soft_weights is None:
             soft_weights = torch.stack([F.gumbel_softmax(st.thetas, temperature) for st in self.stages_to_search])
         soft, hard = 0, 0
+        hard_idx = torch.argmax(soft_weights, dim=1).tolist()  # (one device sync for the six layers)
         for i, st in enumerate(self.stages_to_search):
-            latency_to_accumulate, s_i, h_i = st.latency_terms(soft_weights[i], latency_to_accumulate)
+            latency_to_accumulate, s_i, h_i = st.latency_terms(soft_weights[i], latency_to_accumulate, hard_idx[i])
             soft, hard = soft + s_i, hard + h_i
         walk = _nas_train_native_eligible(self, x, self.layers)
         if walk is not None:
